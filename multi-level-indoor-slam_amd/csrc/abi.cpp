@@ -1,0 +1,296 @@
+// Public C ABI (include/mlgate.h): ViT-B/14 forward orchestration, kNN gate,
+// op-level entry points and HIP-event profiling.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/mlgate.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int PATCH = 14;
+
+inline size_t align_up(size_t v, size_t a = 256) { return (v + a - 1) / a * a; }
+
+struct VitGeom {
+    int B, S, grid, P, T, Tpad;
+    explicit VitGeom(int b, int s) : B(b), S(s), grid(s / PATCH), P(grid * grid), T(grid * grid + 1) {
+        Tpad = (T + 63) / 64 * 64;
+    }
+};
+
+struct VitWorkspace {
+    bf16_t *patches, *xn, *q, *k, *vt, *o, *h;
+    float *x, *partial;
+    size_t vt_bytes;
+};
+
+size_t carve(const VitGeom& g, char* base, VitWorkspace* ws) {
+    size_t off = 0;
+    auto take = [&](size_t bytes) -> char* {
+        char* p = base ? base + off : nullptr;
+        off = align_up(off + bytes);
+        return p;
+    };
+    const size_t rows = (size_t)g.B * g.T;
+    const size_t heads = (size_t)g.B * 12;
+    VitWorkspace w{};
+    w.patches = (bf16_t*)take((size_t)g.B * g.P * MLG_VIT_PATCH_K * 2);
+    w.x = (float*)take(rows * 768 * 4);
+    w.xn = (bf16_t*)take(rows * 768 * 2);
+    w.q = (bf16_t*)take(heads * g.Tpad * 64 * 2);
+    w.k = (bf16_t*)take(heads * g.Tpad * 64 * 2);
+    w.vt_bytes = heads * 64 * g.Tpad * 2;
+    w.vt = (bf16_t*)take(w.vt_bytes);
+    w.o = (bf16_t*)take(rows * 768 * 2);
+    w.h = (bf16_t*)take(rows * 3072 * 2);
+    w.partial = (float*)take(mlg_gem_partial_bytes(g.B));
+    if (ws) *ws = w;
+    return off;
+}
+
+// ------------------------------------------------------------- profiling
+struct Prof {
+    std::mutex mu;
+    unsigned mask = 0;  // slots being recorded
+    std::vector<hipEvent_t> pool;
+    struct Rec { int slot; hipEvent_t a, b; };
+    std::vector<Rec> recs;
+    size_t next = 0;
+    double total[8] = {0};
+    long count[8] = {0};
+} g_prof;
+
+constexpr size_t PROF_POOL = 32768;
+
+struct ProfScope {
+    int slot;
+    hipStream_t s;
+    hipEvent_t a = nullptr, b = nullptr;
+    ProfScope(int slot_, hipStream_t s_) : slot(slot_), s(s_) {
+        if (!(g_prof.mask & (1u << slot))) return;
+        std::lock_guard<std::mutex> lk(g_prof.mu);
+        if (g_prof.next + 2 > g_prof.pool.size()) return;  // pool exhausted: stop recording
+        a = g_prof.pool[g_prof.next++];
+        b = g_prof.pool[g_prof.next++];
+        (void)hipEventRecord(a, s);
+    }
+    ~ProfScope() {
+        if (!a) return;
+        (void)hipEventRecord(b, s);
+        std::lock_guard<std::mutex> lk(g_prof.mu);
+        g_prof.recs.push_back({slot, a, b});
+    }
+};
+
+void prof_collect() {
+    for (auto& r : g_prof.recs) {
+        float ms = 0.f;
+        (void)hipEventSynchronize(r.b);
+        if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            g_prof.total[r.slot] += ms;
+            g_prof.count[r.slot] += 1;
+        }
+    }
+    g_prof.recs.clear();
+    g_prof.next = 0;
+}
+
+#define TRY(x)                     \
+    do {                           \
+        int rc_ = (x);             \
+        if (rc_ != MLG_OK) return rc_; \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int mlg_abi_version(void) { return 1; }
+
+const char* mlg_strerror(int status) {
+    switch (status) {
+        case MLG_OK: return "ok";
+        case MLG_EINVAL: return "invalid argument (shape, alignment or size)";
+        case MLG_EHIP: return "HIP launch error";
+        case MLG_ENOMEM: return "workspace too small";
+        default: return "unknown mlgate status";
+    }
+}
+
+size_t mlg_vit_workspace_bytes(int batch, int image_size) {
+    if (batch <= 0 || image_size <= 0 || image_size % PATCH) return 0;
+    return carve(VitGeom(batch, image_size), nullptr, nullptr);
+}
+
+int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, int H, int W, int C,
+                    long frame_stride, int image_size, int flags, void* workspace, size_t workspace_bytes,
+                    float* desc_out, float* local_out, void* stream) {
+    if (!w || !frames || !workspace || !desc_out || batch <= 0 || image_size % PATCH) return MLG_EINVAL;
+    const VitGeom g(batch, image_size);
+    VitWorkspace ws;
+    if (carve(g, (char*)workspace, &ws) > workspace_bytes) return MLG_ENOMEM;
+    hipStream_t s = (hipStream_t)stream;
+    const int M = g.B * g.T;
+
+    const int swap_rb = (flags & MLG_VIT_KEEP_CHANNELS) ? 0 : 1;
+    const int mean_pool = (flags & MLG_VIT_POOL_MEAN) ? 1 : 0;
+    TRY(mlg_preprocess_patches(frames, g.B, H, W, C, frame_stride, g.S, MLG_VIT_PATCH_K, swap_rb, ws.patches, s));
+    TRY(mlg_gemm_patch(ws.patches, w->patch_w, w->patch_b, w->pos, ws.x, g.B * g.P, g.P, MLG_VIT_PATCH_K, s));
+    TRY(mlg_cls_rows(ws.x, w->cls, w->pos, g.B, g.T, s));
+    // padded key columns of V^T must be finite: masked keys multiply them by p = 0
+    if (hipMemsetAsync(ws.vt, 0, ws.vt_bytes, s) != hipSuccess) return MLG_EHIP;
+
+    for (int l = 0; l < MLG_VIT_DEPTH; ++l) {
+        const mlg_vit_block& bl = w->blocks[l];
+        TRY(mlg_layernorm_bf16(ws.x, bl.norm1_w, bl.norm1_b, ws.xn, M, s));
+        {
+            ProfScope p(2, s);
+            TRY(mlg_gemm_qkv(ws.xn, bl.qkv_w, bl.qkv_b, ws.q, ws.k, ws.vt, M, g.T, g.Tpad, s));
+        }
+        {
+            ProfScope p(4, s);
+            TRY(mlg_attention(ws.q, ws.k, ws.vt, ws.o, g.B, g.T, g.Tpad, s));
+        }
+        {
+            ProfScope p(3, s);
+            TRY(mlg_gemm_residual(ws.o, bl.proj_w, bl.proj_b, bl.ls1, ws.x, M, 768, 768, s));
+        }
+        TRY(mlg_layernorm_bf16(ws.x, bl.norm2_w, bl.norm2_b, ws.xn, M, s));
+        {
+            ProfScope p(0, s);
+            TRY(mlg_gemm_bias_gelu_bf16(ws.xn, bl.fc1_w, bl.fc1_b, ws.h, M, 3072, 768, s));
+        }
+        {
+            ProfScope p(1, s);
+            TRY(mlg_gemm_residual(ws.h, bl.fc2_w, bl.fc2_b, bl.ls2, ws.x, M, 768, 3072, s));
+        }
+    }
+    TRY(mlg_final_norm_gem(ws.x, w->norm_w, w->norm_b, local_out, ws.partial, desc_out, g.B, g.T, mean_pool, s));
+    return MLG_OK;
+}
+
+size_t mlg_knn_workspace_bytes(int N, int D, int Q) {
+    if (N <= 0 || D <= 0 || Q <= 0) return 0;
+    return align_up((size_t)N * D * 4) + align_up((size_t)Q * D * 4) + align_up((size_t)Q * N * 4);
+}
+
+int mlg_knn_gate(const float* desc, int N, int D, const double* t, const int64_t* floor, const uint8_t* has_floor,
+                 double min_gap, float thr, int k, int gating, int q0, int Q, void* workspace,
+                 size_t workspace_bytes, int32_t* idx, float* sim, uint8_t* valid, int32_t* count,
+                 unsigned long long* totals, void* stream) {
+    if (!desc || !t || !workspace || N <= 0 || D <= 0 || Q <= 0 || q0 < 0 || q0 + Q > N) return MLG_EINVAL;
+    if (gating && (!floor || !has_floor)) return MLG_EINVAL;
+    if (mlg_knn_workspace_bytes(N, D, Q) > workspace_bytes) return MLG_ENOMEM;
+    hipStream_t s = (hipStream_t)stream;
+    float* Xn = (float*)workspace;
+    float* S = (float*)((char*)workspace + align_up((size_t)N * D * 4) + align_up((size_t)Q * D * 4));
+    TRY(mlg_row_normalize(desc, Xn, N, D, nullptr, s));
+    TRY(mlg_similarity_f32(Xn + (size_t)q0 * D, Q, Xn, N, D, S, N, s));
+    TRY(mlg_topk_gate(S, N, N, Q, t + q0, t, gating ? floor + q0 : nullptr, gating ? has_floor + q0 : nullptr,
+                      gating ? floor : nullptr, gating ? has_floor : nullptr, min_gap, thr, k, gating, idx, sim,
+                      valid, count, totals, s));
+    return MLG_OK;
+}
+
+int mlg_knn_query(const float* db, int N, int D, const float* qdesc, int Q, const double* t_db,
+                  const double* t_query, double min_gap, int k, void* workspace, size_t workspace_bytes,
+                  int32_t* idx, float* sim, int32_t* count, void* stream) {
+    if (!db || !qdesc || !t_db || !t_query || !workspace || N <= 0 || D <= 0 || Q <= 0) return MLG_EINVAL;
+    if (mlg_knn_workspace_bytes(N, D, Q) > workspace_bytes) return MLG_ENOMEM;
+    hipStream_t s = (hipStream_t)stream;
+    float* Xn = (float*)workspace;
+    float* Qn = (float*)((char*)workspace + align_up((size_t)N * D * 4));
+    float* S = (float*)((char*)Qn + align_up((size_t)Q * D * 4));
+    TRY(mlg_row_normalize(db, Xn, N, D, nullptr, s));
+    TRY(mlg_row_normalize(qdesc, Qn, Q, D, nullptr, s));
+    TRY(mlg_similarity_f32(Qn, Q, Xn, N, D, S, N, s));
+    TRY(mlg_topk_gate(S, N, N, Q, t_query, t_db, nullptr, nullptr, nullptr, nullptr, min_gap, -INFINITY, k, 0, idx,
+                      sim, nullptr, count, nullptr, s));
+    return MLG_OK;
+}
+
+int mlg_row_normalize_f32(const float* X, float* Xn, int N, int D, float* norms_or_null, void* stream) {
+    return mlg_row_normalize(X, Xn, N, D, norms_or_null, (hipStream_t)stream);
+}
+
+int mlg_similarity(const float* A, int Q, const float* B, int N, int D, float* S, void* stream) {
+    return mlg_similarity_f32(A, Q, B, N, D, S, N, (hipStream_t)stream);
+}
+
+size_t mlg_xcorr_workspace_bytes(int n1, int n2, int D) {
+    if (n1 <= 0 || n2 <= 0 || D <= 0) return 0;
+    return align_up((size_t)n1 * D * 4) + align_up((size_t)n2 * D * 4) + align_up((size_t)n1 * n2 * 4);
+}
+
+int mlg_xcorr_score(const float* q, int n1, const float* m, int n2, int D, void* workspace, size_t workspace_bytes,
+                    float* score, void* stream) {
+    if (!q || !m || !workspace || !score || n1 <= 0 || n2 <= 0 || D <= 0) return MLG_EINVAL;
+    if (mlg_xcorr_workspace_bytes(n1, n2, D) > workspace_bytes) return MLG_ENOMEM;
+    hipStream_t s = (hipStream_t)stream;
+    float* qn = (float*)workspace;
+    float* mn = (float*)((char*)workspace + align_up((size_t)n1 * D * 4));
+    float* C = (float*)((char*)mn + align_up((size_t)n2 * D * 4));
+    TRY(mlg_row_normalize(q, qn, n1, D, nullptr, s));
+    TRY(mlg_row_normalize(m, mn, n2, D, nullptr, s));
+    TRY(mlg_similarity_f32(qn, n1, mn, n2, D, C, n2, s));
+    TRY(mlg_xcorr_reduce(C, n1, n2, score, s));
+    return MLG_OK;
+}
+
+int mlg_op_gemm_f32out(const uint16_t* A, const uint16_t* W, float* C, int M, int N, int K, void* stream) {
+    return mlg_gemm_f32out(A, W, C, M, N, K, (hipStream_t)stream);
+}
+int mlg_op_gemm_bias_gelu(const uint16_t* A, const uint16_t* W, const float* bias, uint16_t* C, int M, int N,
+                          int K, void* stream) {
+    return mlg_gemm_bias_gelu_bf16(A, W, bias, C, M, N, K, (hipStream_t)stream);
+}
+int mlg_op_gemm_residual(const uint16_t* A, const uint16_t* W, const float* bias, const float* gamma, float* X,
+                         int M, int N, int K, void* stream) {
+    return mlg_gemm_residual(A, W, bias, gamma, X, M, N, K, (hipStream_t)stream);
+}
+int mlg_op_layernorm_bf16(const float* X, const float* g, const float* b, uint16_t* Y, int M, void* stream) {
+    return mlg_layernorm_bf16(X, g, b, Y, M, (hipStream_t)stream);
+}
+int mlg_op_attention(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, uint16_t* O, int B, int T, int Tpad,
+                     void* stream) {
+    return mlg_attention(Q, K, Vt, O, B, T, Tpad, (hipStream_t)stream);
+}
+int mlg_op_preprocess_patches(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, int S,
+                              uint16_t* patches, void* stream) {
+    return mlg_preprocess_patches(frames, B, H, W, C, frame_stride, S, MLG_VIT_PATCH_K, 1, patches,
+                                  (hipStream_t)stream);
+}
+
+int mlg_prof_enable(int slot_mask) {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    if (slot_mask && g_prof.pool.empty()) {
+        g_prof.pool.resize(PROF_POOL);
+        for (auto& e : g_prof.pool)
+            if (hipEventCreate(&e) != hipSuccess) return MLG_EHIP;
+    }
+    g_prof.mask = (unsigned)slot_mask & 0xffu;
+    return MLG_OK;
+}
+
+int mlg_prof_reset(void) {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    prof_collect();
+    for (int i = 0; i < 8; ++i) { g_prof.total[i] = 0; g_prof.count[i] = 0; }
+    return MLG_OK;
+}
+
+int mlg_prof_read(int slot, double* total_ms, long* launches) {
+    if (slot < 0 || slot >= 8 || !total_ms || !launches) return MLG_EINVAL;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    prof_collect();
+    *total_ms = g_prof.total[slot];
+    *launches = g_prof.count[slot];
+    return MLG_OK;
+}
+
+}  // extern "C"

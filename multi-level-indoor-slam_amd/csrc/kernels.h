@@ -1,0 +1,45 @@
+// Internal (C++ linkage) launchers of the mlgate HIP kernels.  The public C ABI is
+// include/mlgate.h; these are the building blocks behind it.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+typedef uint16_t bf16_t;
+
+// gemm_bf16.hip -- C = epi(A[M,K] . W[N,K]^T), N % 128 == 0, K % 64 == 0
+int mlg_gemm_f32out(const bf16_t* A, const bf16_t* W, float* C, int M, int N, int K, hipStream_t s);
+int mlg_gemm_bias_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,
+                       hipStream_t s);
+int mlg_gemm_bias_gelu_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,
+                            hipStream_t s);
+int mlg_gemm_residual(const bf16_t* A, const bf16_t* W, const float* bias, const float* gamma, float* X, int M,
+                      int N, int K, hipStream_t s);
+int mlg_gemm_qkv(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* Q, bf16_t* K, bf16_t* Vt, int M,
+                 int T, int Tpad, hipStream_t s);
+int mlg_gemm_patch(const bf16_t* A, const bf16_t* W, const float* bias, const float* pos, float* X, int M, int P,
+                   int Kpad, hipStream_t s);
+
+// attention.hip
+int mlg_attention(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int B, int T, int Tpad,
+                  hipStream_t s);
+
+// vit_ops.hip
+int mlg_preprocess_patches(const uint8_t* img, int B, int H, int W, int C, long img_stride, int S, int Kpad,
+                           int swap_rb, bf16_t* out, hipStream_t s);
+int mlg_cls_rows(float* X, const float* cls, const float* pos, int B, int T, hipStream_t s);
+int mlg_layernorm_bf16(const float* X, const float* g, const float* b, bf16_t* Y, int M, hipStream_t s);
+int mlg_final_norm_gem(const float* X, const float* g, const float* b, float* local, float* partial, float* desc,
+                       int B, int T, int mean_pool, hipStream_t s);
+size_t mlg_gem_partial_bytes(int B);
+
+// knn.hip
+int mlg_row_normalize(const float* X, float* Xn, int N, int D, float* norms, hipStream_t s);
+int mlg_similarity_f32(const float* A, int Q, const float* B, int N, int D, float* S, int lds, hipStream_t s);
+int mlg_topk_gate(const float* S, int lds, int N, int Q, const double* tq, const double* tdb, const int64_t* fq,
+                  const uint8_t* hfq, const int64_t* fdb, const uint8_t* hfdb, double min_gap, float thr, int k,
+                  int gating, int32_t* idx, float* sim, uint8_t* valid, int32_t* count, unsigned long long* totals,
+                  hipStream_t s);
+int mlg_xcorr_reduce(const float* C, int n1, int n2, float* out, hipStream_t s);

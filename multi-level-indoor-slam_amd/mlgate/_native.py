@@ -1,0 +1,94 @@
+"""ctypes binding of libmlgate.so -- the C ABI declared in include/mlgate.h.
+
+The library is the only compute path of this package: there is no CPU or eager
+PyTorch fallback.  ``lib()`` raises if the shared object is missing, and
+``require_device()`` raises if no HIP device is visible.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmlgate.so")
+
+c_int, c_long, c_size_t, c_float, c_double, c_void_p = (
+    ctypes.c_int, ctypes.c_long, ctypes.c_size_t, ctypes.c_float, ctypes.c_double, ctypes.c_void_p)
+
+EXPORTS = {
+    "mlg_abi_version": (c_int, []),
+    "mlg_strerror": (ctypes.c_char_p, [c_int]),
+    "mlg_vit_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "mlg_vit_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_long, c_int, c_int, c_void_p,
+                                c_size_t, c_void_p, c_void_p, c_void_p]),
+    "mlg_knn_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mlg_knn_gate": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_float, c_int,
+                             c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_void_p]),
+    "mlg_knn_query": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_double, c_int,
+                              c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mlg_row_normalize_f32": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "mlg_similarity": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "mlg_xcorr_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mlg_xcorr_score": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p,
+                                c_void_p]),
+    "mlg_op_gemm_f32out": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mlg_op_gemm_bias_gelu": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mlg_op_gemm_residual": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                     c_void_p]),
+    "mlg_op_layernorm_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
+    "mlg_op_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mlg_op_preprocess_patches": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_long, c_int, c_void_p,
+                                          c_void_p]),
+    "mlg_prof_enable": (c_int, [c_int]),
+    "mlg_prof_reset": (c_int, []),
+    "mlg_prof_read": (c_int, [c_int, ctypes.POINTER(c_double), ctypes.POINTER(c_long)]),
+}
+
+_lib = None
+
+
+class MlgateError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libmlgate.so (built by __graft_entry__.build / `make -C csrc`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MlgateError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                              "g.build()'` (hipcc --offload-arch=gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().mlg_strerror(rc).decode()
+        raise MlgateError(f"{what} failed: {msg} (status {rc})")
+
+
+def require_device(device="cuda"):
+    """Raise unless a HIP device is usable for `device` (mlgate has no CPU path)."""
+    import torch
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise MlgateError(f"mlgate runs its hot path on MI355X HIP kernels only; got device={device!r}. "
+                          "Use device='cuda' (PyTorch-ROCm's name for the HIP device).")
+    if not torch.cuda.is_available():
+        raise MlgateError("no HIP device visible: mlgate's kernels need an MI355X (gfx950)")
+    lib()
+    return dev
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

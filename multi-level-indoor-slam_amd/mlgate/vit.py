@@ -1,0 +1,120 @@
+"""DINOv2 ViT-B/14 + GeM descriptor engine (CricaVPR path) on the mlgate HIP kernels.
+
+Device-resident replacement for what CricaVPR does per keyframe
+(place_recognition.py:613-667, 759-803): preprocessing, the hub
+``get_intermediate_layers`` forward, GeM pooling and the local-feature cache -- all
+from ONE forward (the reference runs the identical forward twice per add_image, once
+for the descriptor and once for the local features).  Frames go in as uint8
+[B, H, W, C] device tensors; everything up to the float32 descriptors stays in HBM.
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import _native
+from .weights import DEPTH, EMBED, PATCH
+
+PATCH_K = 640  # 3*14*14 = 588 patch inputs zero-padded to a multiple of 64 (include/mlgate.h)
+P = ctypes.c_void_p
+
+
+class _Block(ctypes.Structure):
+    _fields_ = [(n, P) for n in ("norm1_w", "norm1_b", "qkv_w", "qkv_b", "proj_w", "proj_b", "ls1", "norm2_w",
+                                 "norm2_b", "fc1_w", "fc1_b", "fc2_w", "fc2_b", "ls2")]
+
+
+class _Weights(ctypes.Structure):
+    _fields_ = [("patch_w", P), ("patch_b", P), ("cls", P), ("pos", P), ("blocks", _Block * DEPTH),
+                ("norm_w", P), ("norm_b", P)]
+
+
+def resample_pos_embed(pos_embed, grid):
+    """Hub DinoVisionTransformer.interpolate_pos_encoding (square input): bicubic,
+    scale_factor (grid + 0.1) / 37, antialias off.  One-time weight transform."""
+    pos_embed = pos_embed.float()
+    m = int(math.sqrt(pos_embed.shape[1] - 1))
+    if grid == m:
+        return pos_embed
+    s = float(grid + 0.1) / m
+    patch = pos_embed[:, 1:].reshape(1, m, m, -1).permute(0, 3, 1, 2)
+    patch = F.interpolate(patch, mode="bicubic", antialias=False, scale_factor=(s, s))
+    patch = patch.permute(0, 2, 3, 1).reshape(1, grid * grid, -1)
+    return torch.cat((pos_embed[:, :1], patch), dim=1).contiguous()
+
+
+class VitB14:
+    """Packed device weights + workspace for batched CricaVPR descriptor extraction."""
+
+    def __init__(self, state_dict, device="cuda", image_size=322, max_batch=64, pool="gem", swap_rb=True):
+        self.device = _native.require_device(device)
+        if image_size % PATCH:
+            raise ValueError("image_size must be a multiple of 14")
+        self.image_size, self.grid = image_size, image_size // PATCH
+        self.n_patches = self.grid * self.grid
+        self.n_local = self.n_patches - 1  # tokens 2.. of get_intermediate_layers (CLS + patch 0 dropped)
+        self.max_batch = max_batch
+        self.flags = (1 if pool == "mean" else 0) | (0 if swap_rb else 2)  # MLG_VIT_POOL_MEAN / KEEP_CHANNELS
+        self._keep = []
+        self._w = self._pack(state_dict)
+        self._ws_bytes = _native.lib().mlg_vit_workspace_bytes(max_batch, image_size)
+        self._ws = torch.empty(self._ws_bytes, dtype=torch.uint8, device=self.device)
+
+    # ------------------------------------------------------------ weights
+    def _dev(self, a, dtype):
+        t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
+        t = t.to(self.device, torch.float32).to(dtype).contiguous()
+        self._keep.append(t)
+        return ctypes.c_void_p(t.data_ptr())
+
+    def _pack(self, sd):
+        f32, bf = torch.float32, torch.bfloat16
+        w = _Weights()
+        pw = torch.as_tensor(np.asarray(sd["patch_embed.proj.weight"], np.float32)).reshape(EMBED, -1)
+        w.patch_w = self._dev(F.pad(pw, (0, PATCH_K - pw.shape[1])), bf)
+        w.patch_b = self._dev(sd["patch_embed.proj.bias"], f32)
+        w.cls = self._dev(np.asarray(sd["cls_token"], np.float32).reshape(EMBED), f32)
+        pos = torch.as_tensor(np.asarray(sd["pos_embed"], np.float32)).to(self.device)
+        w.pos = self._dev(resample_pos_embed(pos, self.grid).reshape(-1, EMBED), f32)
+        for i in range(DEPTH):
+            p, b = f"blocks.{i}.", w.blocks[i]
+            b.norm1_w, b.norm1_b = self._dev(sd[p + "norm1.weight"], f32), self._dev(sd[p + "norm1.bias"], f32)
+            b.qkv_w, b.qkv_b = self._dev(sd[p + "attn.qkv.weight"], bf), self._dev(sd[p + "attn.qkv.bias"], f32)
+            b.proj_w, b.proj_b = self._dev(sd[p + "attn.proj.weight"], bf), self._dev(sd[p + "attn.proj.bias"], f32)
+            b.ls1 = self._dev(sd[p + "ls1.gamma"], f32)
+            b.norm2_w, b.norm2_b = self._dev(sd[p + "norm2.weight"], f32), self._dev(sd[p + "norm2.bias"], f32)
+            b.fc1_w, b.fc1_b = self._dev(sd[p + "mlp.fc1.weight"], bf), self._dev(sd[p + "mlp.fc1.bias"], f32)
+            b.fc2_w, b.fc2_b = self._dev(sd[p + "mlp.fc2.weight"], bf), self._dev(sd[p + "mlp.fc2.bias"], f32)
+            b.ls2 = self._dev(sd[p + "ls2.gamma"], f32)
+        w.norm_w, w.norm_b = self._dev(sd["norm.weight"], f32), self._dev(sd["norm.bias"], f32)
+        return w
+
+    # ------------------------------------------------------------ forward
+    def forward_into(self, frames, desc_out, local_out=None, stream=None):
+        """frames: uint8 [B, H, W, C] device tensor (C = 1, 3 BGR or 4 BGRA; or [B, H, W]).
+        Writes float32 descriptors [B, 768] (and local features [B, n_local, 768])."""
+        if frames.dim() == 3:
+            frames = frames.unsqueeze(-1)
+        if frames.dtype != torch.uint8 or frames.device.type != "cuda":
+            raise TypeError("frames must be a uint8 tensor on the HIP device")
+        frames = frames.contiguous()
+        B, H, W, C = frames.shape
+        st = stream if stream is not None else _native.stream_of(self.device)
+        L = _native.lib()
+        for b0 in range(0, B, self.max_batch):
+            nb = min(self.max_batch, B - b0)
+            lo = ctypes.c_void_p(local_out[b0].data_ptr()) if local_out is not None else None
+            rc = L.mlg_vit_forward(ctypes.byref(self._w), ctypes.c_void_p(frames[b0].data_ptr()), nb, H, W, C,
+                                   H * W * C, self.image_size, self.flags, _native.ptr(self._ws), self._ws_bytes,
+                                   ctypes.c_void_p(desc_out[b0].data_ptr()), lo, st)
+            _native.check(rc, "mlg_vit_forward")
+
+    def forward(self, frames, with_local=False):
+        B = frames.shape[0]
+        desc = torch.empty(B, EMBED, dtype=torch.float32, device=self.device)
+        local = (torch.empty(B, self.n_local, EMBED, dtype=torch.float32, device=self.device)
+                 if with_local else None)
+        self.forward_into(frames, desc, local)
+        return (desc, local) if with_local else desc

@@ -1,0 +1,65 @@
+"""ctypes loader for oracle/build/liboracle.so (test infrastructure only)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO) or os.path.getmtime(_SO) < os.path.getmtime(
+                os.path.join(_HERE, "csrc", "oracle.c")):
+            build()
+        _lib = ctypes.CDLL(_SO)
+        _lib.orc_resize_linear_u8.restype = ctypes.c_int
+        _lib.orc_resize_vec_end.restype = ctypes.c_int
+        _lib.orc_row_norms_f32.restype = ctypes.c_int
+        _lib.orc_knn_rows.restype = ctypes.c_int
+    return _lib
+
+
+def ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def resize_linear_u8(img, dh, dw):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape[:2]
+    c = 1 if img.ndim == 2 else img.shape[2]
+    out = np.empty((dh, dw) + (() if img.ndim == 2 else (c,)), np.uint8)
+    rc = lib().orc_resize_linear_u8(ptr(img), h, w, c, ptr(out), dh, dw)
+    assert rc == 0
+    return out
+
+
+def row_norms_f32(x):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty(x.shape[0], np.float32)
+    lib().orc_row_norms_f32(ptr(x), ctypes.c_long(x.shape[0]), ctypes.c_long(x.shape[1]), ptr(out))
+    return out
+
+
+def knn_rows(S, q0, t, floor, has_floor, min_gap, thr, k, gating):
+    S = np.ascontiguousarray(S, dtype=np.float32)
+    Q, N = S.shape
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    floor = np.ascontiguousarray(floor, dtype=np.int64)
+    has_floor = np.ascontiguousarray(has_floor, dtype=np.uint8)
+    kk = max(k, 1)
+    idx = np.zeros((Q, kk), np.int32)
+    sim = np.zeros((Q, kk), np.float32)
+    valid = np.zeros((Q, kk), np.uint8)
+    count = np.zeros(Q, np.int32)
+    lib().orc_knn_rows(ptr(S), Q, N, q0, ptr(t), ptr(floor), ptr(has_floor), ctypes.c_double(min_gap),
+                       ctypes.c_float(thr), k, int(gating), ptr(idx), ptr(sim), ptr(valid), ptr(count))
+    return idx, sim, valid, count

@@ -1,0 +1,145 @@
+"""Op-level parity of the HIP kernels (called through the C ABI) against float32
+PyTorch references of the same op and against the CPU oracle.  GPU only."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mlgate import _native
+
+pytestmark = pytest.mark.gpu
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def S(dev):
+    return _native.stream_of(dev)
+
+
+def bf16_bits(x):
+    return x.to(torch.bfloat16).contiguous()
+
+
+def rel_err(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (1060, 256, 768), (530, 3072, 768), (777, 768, 3072)])
+def test_gemm_f32out(dev, M, N, K):
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(dev)
+    W = torch.randn(N, K, generator=g).to(dev)
+    Ab, Wb = bf16_bits(A), bf16_bits(W)
+    C = torch.full((M, N), float("nan"), device=dev)
+    _native.check(_native.lib().mlg_op_gemm_f32out(P(Ab), P(Wb), P(C), M, N, K, S(dev)), "gemm")
+    ref = Ab.float().cpu() @ Wb.float().cpu().T
+    torch.cuda.synchronize()
+    assert torch.isfinite(C).all()
+    assert rel_err(C.cpu(), ref) < 1e-5
+
+
+def test_gemm_asymmetric_identity(dev):
+    """A = I with asymmetric W catches a transposed C-write (guide §3)."""
+    M = N = 128
+    K = 128
+    A = torch.eye(M, K, device=dev)
+    W = (torch.arange(N, device=dev)[:, None] * 1000 + torch.arange(K, device=dev)[None, :]).float() / 256.0
+    Ab, Wb = bf16_bits(A), bf16_bits(W)
+    C = torch.empty(M, N, device=dev)
+    _native.check(_native.lib().mlg_op_gemm_f32out(P(Ab), P(Wb), P(C), M, N, K, S(dev)), "gemm")
+    torch.cuda.synchronize()
+    assert torch.equal(C.cpu(), Wb.float().cpu().T)
+
+
+def test_gemm_gelu_and_residual(dev):
+    M, N, K = 600, 384, 768
+    g = torch.Generator().manual_seed(3)
+    A = bf16_bits(torch.randn(M, K, generator=g).to(dev) * 0.5)
+    W = bf16_bits(torch.randn(N, K, generator=g).to(dev) * 0.05)
+    b = torch.randn(N, generator=g).to(dev) * 0.1
+    gam = torch.rand(N, generator=g).to(dev)
+    H = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    _native.check(_native.lib().mlg_op_gemm_bias_gelu(P(A), P(W), P(b), P(H), M, N, K, S(dev)), "gelu")
+    ref = F.gelu(A.float().cpu() @ W.float().cpu().T + b.cpu())
+    torch.cuda.synchronize()
+    assert rel_err(H.float().cpu(), ref) < 5e-3
+    X0 = torch.randn(M, N, generator=g).to(dev)
+    X = X0.clone()
+    _native.check(_native.lib().mlg_op_gemm_residual(P(A), P(W), P(b), P(gam), P(X), M, N, K, S(dev)), "res")
+    ref = X0.cpu() + gam.cpu() * (A.float().cpu() @ W.float().cpu().T + b.cpu())
+    torch.cuda.synchronize()
+    assert rel_err(X.cpu(), ref) < 1e-5
+
+
+def test_gemm_rejects_bad_shapes(dev):
+    A = torch.zeros(64, 96, dtype=torch.bfloat16, device=dev)
+    W = torch.zeros(128, 96, dtype=torch.bfloat16, device=dev)
+    C = torch.zeros(64, 128, device=dev)
+    assert _native.lib().mlg_op_gemm_f32out(P(A), P(W), P(C), 64, 128, 96, S(dev)) == -1  # K % 64
+    assert _native.lib().mlg_op_gemm_f32out(P(A), P(W), P(C), 64, 100, 64, S(dev)) == -1  # N % 128
+
+
+def test_layernorm(dev):
+    M = 1061
+    g = torch.Generator().manual_seed(5)
+    X = (torch.randn(M, 768, generator=g) * 3 + 1).to(dev)
+    w = (1 + 0.1 * torch.randn(768, generator=g)).to(dev)
+    b = (0.1 * torch.randn(768, generator=g)).to(dev)
+    Y = torch.empty(M, 768, dtype=torch.bfloat16, device=dev)
+    _native.check(_native.lib().mlg_op_layernorm_bf16(P(X), P(w), P(b), P(Y), M, S(dev)), "ln")
+    ref = F.layer_norm(X.cpu(), (768,), w.cpu(), b.cpu(), eps=1e-6)
+    torch.cuda.synchronize()
+    assert rel_err(Y.float().cpu(), ref) < 4e-3
+
+
+@pytest.mark.parametrize("B,T", [(2, 530), (1, 64), (3, 197), (1, 1370)])
+def test_attention(dev, B, T):
+    Tpad = (T + 63) // 64 * 64
+    g = torch.Generator().manual_seed(T)
+    q, k, v = (torch.randn(B, 12, T, 64, generator=g) * 1.5 for _ in range(3))
+    q, k, v = (bf16_bits(x) for x in (q, k, v))
+    Qd = torch.zeros(B, 12, Tpad, 64, dtype=torch.bfloat16)
+    Kd = torch.zeros(B, 12, Tpad, 64, dtype=torch.bfloat16)
+    Vt = torch.zeros(B, 12, 64, Tpad, dtype=torch.bfloat16)
+    Qd[:, :, :T] = q
+    Kd[:, :, :T] = k
+    Vt[:, :, :, :T] = v.transpose(-1, -2)
+    Qd, Kd, Vt = Qd.to(dev), Kd.to(dev), Vt.to(dev)
+    O = torch.empty(B * T, 768, dtype=torch.bfloat16, device=dev)
+    _native.check(_native.lib().mlg_op_attention(P(Qd), P(Kd), P(Vt), P(O), B, T, Tpad, S(dev)), "attn")
+    a = ((q.float() * 0.125) @ k.float().transpose(-1, -2)).softmax(-1)
+    ref = (a @ v.float()).transpose(1, 2).reshape(B * T, 768)
+    torch.cuda.synchronize()
+    assert rel_err(O.float().cpu(), ref) < 1e-2
+
+
+def _patches_ref(img, S_=322):
+    from oracle import vit as ovit
+    x = ovit.preprocess(img, S_)  # [1, 3, S, S] f32
+    g = S_ // 14
+    p = x.reshape(3, g, 14, g, 14).permute(1, 3, 0, 2, 4).reshape(g * g, 588)
+    return p
+
+
+@pytest.mark.parametrize("shape", [(480, 640, 3), (540, 720, 3), (480, 640, 4), (480, 640), (77, 100, 3)])
+def test_preprocess_bit_exact(dev, shape):
+    rng = np.random.default_rng(sum(shape))
+    imgs = rng.integers(0, 256, (2,) + shape, dtype=np.uint8)
+    fr = torch.from_numpy(imgs).to(dev)
+    H, W = shape[:2]
+    C = 1 if len(shape) == 2 else shape[2]
+    out = torch.empty(2 * 529, 640, dtype=torch.bfloat16, device=dev)
+    _native.check(_native.lib().mlg_op_preprocess_patches(P(fr), 2, H, W, C, H * W * C, 322, P(out), S(dev)),
+                  "prep")
+    torch.cuda.synchronize()
+    out = out.cpu()
+    for b in range(2):
+        ref = _patches_ref(imgs[b]).to(torch.bfloat16)
+        got = out[b * 529:(b + 1) * 529]
+        assert torch.equal(got[:, :588].view(torch.int16), ref.view(torch.int16))
+        assert torch.count_nonzero(got[:, 588:].float()) == 0
