@@ -74,6 +74,20 @@ def pairwise_similarities(desc):
     return S
 
 
+def similarity(A, B):
+    """Cosine similarities S[Q, N] between the rows of A [Q, D] and B [N, D] (device, float32)."""
+    Q, D = A.shape
+    N = B.shape[0]
+    L = _native.lib()
+    st = _native.stream_of(A.device)
+    an, bn = torch.empty_like(A), torch.empty_like(B)
+    S = torch.empty(Q, N, dtype=torch.float32, device=A.device)
+    _native.check(L.mlg_row_normalize_f32(_native.ptr(A), _native.ptr(an), Q, D, None, st), "normalize")
+    _native.check(L.mlg_row_normalize_f32(_native.ptr(B), _native.ptr(bn), N, D, None, st), "normalize")
+    _native.check(L.mlg_similarity(_native.ptr(an), Q, _native.ptr(bn), N, D, _native.ptr(S), st), "similarity")
+    return S
+
+
 def flatten_matches(idx, sim, valid, count, q0=0):
     """Host flat arrays (q, m, sim, valid) in emission order from per-row device outputs."""
     idx, sim, valid, count = (x.cpu().numpy() for x in (idx, sim, valid, count))

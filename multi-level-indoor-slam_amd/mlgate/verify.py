@@ -1,0 +1,174 @@
+"""Geometric verification: drop-in mirror of scripts/semantic_gating/geometric_verification.py.
+
+Status (round 1): the dataclasses, the verifier decision rule
+(geometric_verification.py:586-634), the semantic cross-floor skip and its statistics
+(:688-744) are complete.  The matcher back-ends -- SuperPoint + LightGlue attention
+matching, SuperGlue Sinkhorn, LoFTR, and GPU RANSAC (essential / fundamental) with
+recoverPose -- are the next HIP kernels on the roadmap; until they exist,
+``detect_and_match`` / ``verify_geometric_consistency`` raise MlgateError instead of
+silently running on the CPU.
+"""
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+from ._native import MlgateError
+
+
+@dataclass
+class MatchResult:
+    """Outcome of verifying one (query, match) keyframe pair."""
+    query_idx: int
+    match_idx: int
+    num_keypoints_query: int
+    num_keypoints_match: int
+    num_matches: int
+    num_inliers: int
+    inlier_ratio: float
+    relative_pose: Optional[np.ndarray]
+    essential_matrix: Optional[np.ndarray]
+    confidence: float
+    is_valid: bool
+
+
+@dataclass
+class Keypoint:
+    x: float
+    y: float
+    score: float
+    descriptor: Optional[np.ndarray] = None
+
+
+def _rejected(query_idx, match_idx):
+    return MatchResult(query_idx=query_idx, match_idx=match_idx, num_keypoints_query=0, num_keypoints_match=0,
+                       num_matches=0, num_inliers=0, inlier_ratio=0.0, relative_pose=None, essential_matrix=None,
+                       confidence=0.0, is_valid=False)
+
+
+class BaseFeatureMatcher:
+    def __init__(self, device: str = 'cuda'):
+        self.device = device
+        self.model = None
+
+    def detect_and_match(self, image1: np.ndarray, image2: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        raise NotImplementedError
+
+    def verify_geometric_consistency(self, kpts1: np.ndarray, kpts2: np.ndarray, K: Optional[np.ndarray] = None,
+                                     ransac_threshold: float = 3.0) -> Tuple[np.ndarray, np.ndarray, float]:
+        if len(kpts1) < 5:
+            return np.array([]), None, 0.0
+        raise MlgateError("GPU RANSAC (essential / fundamental matrix) is not implemented on MI355X yet")
+
+    def estimate_relative_pose(self, kpts1: np.ndarray, kpts2: np.ndarray, K: np.ndarray, inlier_mask: np.ndarray,
+                               E: np.ndarray) -> Optional[np.ndarray]:
+        if E is None or np.sum(inlier_mask) < 5:
+            return None
+        raise MlgateError("recoverPose is not implemented on MI355X yet")
+
+
+class _PendingMatcher(BaseFeatureMatcher):
+    _what = "feature matcher"
+
+    def detect_and_match(self, image1, image2):
+        raise MlgateError(f"{type(self).__name__}: the {self._what} HIP kernels are not implemented yet")
+
+
+class LightGlue(_PendingMatcher):
+    _what = "SuperPoint + LightGlue"
+
+    def __init__(self, device: str = 'cuda', max_keypoints: int = 2048, detection_threshold: float = 0.001):
+        super().__init__(device)
+        self.max_keypoints = max_keypoints
+        self.detection_threshold = detection_threshold
+        self._model_loaded = False
+
+
+class SuperGlue(_PendingMatcher):
+    _what = "SuperPoint + SuperGlue (Sinkhorn)"
+
+    def __init__(self, device: str = 'cuda', max_keypoints: int = 2048, weights: str = 'indoor'):
+        super().__init__(device)
+        self.max_keypoints = max_keypoints
+        self.weights = weights
+        self._model_loaded = False
+
+
+class LoFTR(_PendingMatcher):
+    _what = "LoFTR"
+
+    def __init__(self, device: str = 'cuda', weights: str = 'indoor'):
+        super().__init__(device)
+        self.weights = weights
+        self._model_loaded = False
+
+
+_MATCHERS = {'lightglue': LightGlue, 'superglue': SuperGlue, 'loftr': LoFTR}
+
+
+class GeometricVerifier:
+    """Matching + RANSAC + the validity / confidence rule of the reference."""
+
+    def __init__(self, matcher_type: str = 'lightglue', device: str = 'cuda', min_inliers: int = 20,
+                 min_inlier_ratio: float = 0.25, ransac_threshold: float = 3.0):
+        self.min_inliers = min_inliers
+        self.min_inlier_ratio = min_inlier_ratio
+        self.ransac_threshold = ransac_threshold
+        cls = _MATCHERS.get(matcher_type.lower())
+        if cls is None:
+            raise ValueError(f"Unknown matcher: {matcher_type}")
+        self.matcher = cls(device=device)
+
+    def decide(self, kpts1, kpts2, inlier_mask, E, inlier_ratio, K=None, query_idx=0, match_idx=0) -> MatchResult:
+        """The decision rule given matches and a RANSAC result (geometric_verification.py:606-634)."""
+        n_in = int(np.sum(inlier_mask)) if len(inlier_mask) > 0 else 0
+        pose = None
+        if K is not None and E is not None and n_in >= 5:
+            pose = self.matcher.estimate_relative_pose(kpts1, kpts2, K, inlier_mask, E)
+        return MatchResult(query_idx=query_idx, match_idx=match_idx, num_keypoints_query=len(kpts1),
+                           num_keypoints_match=len(kpts2), num_matches=len(kpts1), num_inliers=n_in,
+                           inlier_ratio=inlier_ratio, relative_pose=pose, essential_matrix=E,
+                           confidence=min(1.0, inlier_ratio * (n_in / self.min_inliers)),
+                           is_valid=n_in >= self.min_inliers and inlier_ratio >= self.min_inlier_ratio)
+
+    def verify(self, image1: np.ndarray, image2: np.ndarray, K: Optional[np.ndarray] = None, query_idx: int = 0,
+               match_idx: int = 0) -> MatchResult:
+        k1, k2, _ = self.matcher.detect_and_match(image1, image2)
+        if len(k1) < 5:
+            return _rejected(query_idx, match_idx)
+        mask, E, ratio = self.matcher.verify_geometric_consistency(k1, k2, K, self.ransac_threshold)
+        return self.decide(k1, k2, mask, E, ratio, K, query_idx, match_idx)
+
+    def verify_batch(self, image_pairs: List[Tuple[np.ndarray, np.ndarray]], K: Optional[np.ndarray] = None,
+                     indices: Optional[List[Tuple[int, int]]] = None) -> List[MatchResult]:
+        out = []
+        for i, (a, b) in enumerate(image_pairs):
+            q, m = indices[i] if indices is not None else (i, i)
+            out.append(self.verify(a, b, K, q, m))
+        return out
+
+
+class SemanticGeometricVerifier(GeometricVerifier):
+    """Cross-floor pairs are rejected before any matching work is spent on them."""
+
+    def __init__(self, matcher_type: str = 'lightglue', device: str = 'cuda', min_inliers: int = 20,
+                 min_inlier_ratio: float = 0.25, enable_floor_gating: bool = True):
+        super().__init__(matcher_type, device, min_inliers, min_inlier_ratio)
+        self.enable_floor_gating = enable_floor_gating
+        self.stats = {'verified': 0, 'skipped_floor_mismatch': 0, 'valid': 0, 'invalid': 0}
+
+    def verify_with_semantics(self, image1: np.ndarray, image2: np.ndarray, floor1: int, floor2: int,
+                              K: Optional[np.ndarray] = None, query_idx: int = 0, match_idx: int = 0) -> MatchResult:
+        if self.enable_floor_gating and floor1 != floor2:
+            self.stats['skipped_floor_mismatch'] += 1
+            return _rejected(query_idx, match_idx)
+        res = self.verify(image1, image2, K, query_idx, match_idx)
+        self.stats['verified'] += 1
+        self.stats['valid' if res.is_valid else 'invalid'] += 1
+        return res
+
+    def get_statistics(self) -> Dict:
+        total = self.stats['verified'] + self.stats['skipped_floor_mismatch']
+        return {**self.stats, 'total_candidates': total,
+                'skip_rate': self.stats['skipped_floor_mismatch'] / total if total > 0 else 0,
+                'valid_rate': self.stats['valid'] / self.stats['verified'] if self.stats['verified'] > 0 else 0}

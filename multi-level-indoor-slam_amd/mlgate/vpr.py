@@ -1,0 +1,388 @@
+"""Visual place recognition: the drop-in mirror of scripts/semantic_gating/place_recognition.py.
+
+Same class names, constructor signatures, dataclasses, return types and error
+behaviour as the reference; the compute runs on the mlgate HIP kernels:
+
+  * CricaVPR -> DINOv2 ViT-B/14 + GeM on MI355X (mlgate.vit.VitB14); ONE forward per
+    keyframe feeds both the descriptor and the local-feature cache (the reference runs
+    the same forward twice, place_recognition.py:765/777).
+  * AnyLoc   -> the same ViT at 518^2 with mean pooling and unswapped channels
+    (place_recognition.py:467-505).
+  * retrieval (find_loop_closures / query / pairwise similarities / cross-correlation
+    rerank) -> mlg_knn_gate / mlg_knn_query / mlg_xcorr_score.
+  * MixVPR / SALAD -> the reference resolves both to a torchvision ResNet-50 GAP
+    fallback (place_recognition.py:241-306, 370-378); that network is not built on HIP
+    yet, so their extract_descriptor raises.  Descriptors can still be injected into
+    ``.descriptors`` (as the reference's own demo does, :1020) and retrieved on the GPU.
+
+Weights: the hub checkpoint cannot be fetched offline.  ``pretrained_path`` (or
+MLGATE_DINOV2_WEIGHTS) may point at a local hub-format dinov2_vitb14 state_dict;
+otherwise seeded synthetic weights are used and a warning says so.
+"""
+import warnings
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Dict, List, Optional, Tuple, Union
+
+import numpy as np
+
+from . import _native
+
+
+@dataclass
+class PlaceMatch:
+    """A retrieved (query, match) pair; ``is_valid`` is the floor-gate decision."""
+    query_idx: int
+    match_idx: int
+    similarity: float
+    query_timestamp: Optional[float] = None
+    match_timestamp: Optional[float] = None
+    is_valid: bool = True
+
+
+@dataclass
+class PlaceDescriptor:
+    """One database entry: global descriptor plus its timestamp / floor label."""
+    timestamp: float
+    descriptor: np.ndarray
+    image_path: Optional[str] = None
+    floor_label: Optional[int] = None
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _as_frames(images):
+    """List / array of HxW[xC] uint8 images (one size) -> contiguous uint8 [B, H, W, C]."""
+    arrs = [np.asarray(im) for im in images]
+    if not arrs:
+        raise ValueError("no images")
+    if any(a.shape != arrs[0].shape for a in arrs):
+        raise ValueError("all images of a batch must have the same shape")
+    batch = np.stack(arrs).astype(np.uint8, copy=False)
+    if batch.ndim == 3:
+        batch = batch[..., None]
+    return np.ascontiguousarray(batch)
+
+
+class BasePlaceRecognition:
+    """Descriptor database + GPU retrieval shared by every VPR method."""
+
+    def __init__(self, descriptor_dim: int = 4096, device: str = 'cuda'):
+        self.descriptor_dim = descriptor_dim
+        self.device = device
+        self.model = None
+        self.descriptors: List[PlaceDescriptor] = []
+
+    # ---------------------------------------------------------- extraction
+    def extract_descriptor(self, image: np.ndarray) -> np.ndarray:
+        raise NotImplementedError
+
+    def extract_descriptors(self, images) -> np.ndarray:
+        """Batched extraction (mlgate extension): [B, D] float32."""
+        return np.stack([self.extract_descriptor(im) for im in images])
+
+    def add_image(self, image: np.ndarray, timestamp: float, floor_label: Optional[int] = None,
+                  image_path: Optional[str] = None) -> PlaceDescriptor:
+        entry = PlaceDescriptor(timestamp=timestamp, descriptor=self.extract_descriptor(image),
+                                image_path=image_path, floor_label=floor_label)
+        self.descriptors.append(entry)
+        return entry
+
+    def add_images(self, images, timestamps, floor_labels=None, image_paths=None) -> List[PlaceDescriptor]:
+        """Batched add_image (mlgate extension): one device batch instead of N calls."""
+        descs = self.extract_descriptors(images)
+        out = []
+        for i, d in enumerate(descs):
+            out.append(PlaceDescriptor(timestamp=timestamps[i], descriptor=d,
+                                       image_path=None if image_paths is None else image_paths[i],
+                                       floor_label=None if floor_labels is None else floor_labels[i]))
+        self.descriptors.extend(out)
+        return out
+
+    # ---------------------------------------------------------- database
+    def build_descriptor_matrix(self) -> np.ndarray:
+        if not self.descriptors:
+            return np.array([])
+        return np.vstack([d.descriptor for d in self.descriptors])
+
+    def _device_matrix(self):
+        torch = _torch()
+        dev = _native.require_device(self.device)
+        X = np.ascontiguousarray(self.build_descriptor_matrix(), dtype=np.float32)
+        return torch.from_numpy(X).to(dev), dev
+
+    def compute_all_pairwise_similarities(self) -> np.ndarray:
+        """N x N cosine similarities (float32), computed on the device."""
+        if not self.descriptors:
+            return np.array([])
+        from . import retrieval
+        X, _ = self._device_matrix()
+        return retrieval.pairwise_similarities(X).cpu().numpy()
+
+    def _compute_similarity(self, query: np.ndarray, database: np.ndarray) -> np.ndarray:
+        torch = _torch()
+        from . import retrieval
+        dev = _native.require_device(self.device)
+        db = torch.from_numpy(np.ascontiguousarray(database, dtype=np.float32)).to(dev)
+        q = torch.from_numpy(np.ascontiguousarray(np.asarray(query, np.float32).reshape(1, -1))).to(dev)
+        return retrieval.similarity(q, db)[0].cpu().numpy()
+
+    def query(self, image: np.ndarray, timestamp: Optional[float] = None, k: int = 5,
+              min_time_gap: float = 10.0) -> List[PlaceMatch]:
+        """Top-k database entries for a new image (the query is not added)."""
+        if not self.descriptors:
+            return []
+        torch = _torch()
+        from . import retrieval
+        qd = self.extract_descriptor(image)
+        db, dev = self._device_matrix()
+        t_db = torch.tensor([float(d.timestamp) for d in self.descriptors], dtype=torch.float64, device=dev)
+        tq = torch.tensor([float('nan') if timestamp is None else float(timestamp)], dtype=torch.float64,
+                          device=dev)
+        q = torch.from_numpy(np.asarray(qd, np.float32).reshape(1, -1)).to(dev)
+        kk = max(1, min(k, len(self.descriptors), retrieval.MAX_K))
+        idx, sim, cnt = retrieval.knn_query(db, q, t_db, tq, min_time_gap if timestamp is not None else 0.0, kk)
+        c = int(cnt[0]) if k > 0 else 0
+        idx, sim = idx[0, :c].cpu().numpy(), sim[0, :c].cpu().numpy()
+        n = len(self.descriptors)
+        return [PlaceMatch(query_idx=n, match_idx=int(j), similarity=float(s), query_timestamp=timestamp,
+                           match_timestamp=self.descriptors[int(j)].timestamp) for j, s in zip(idx, sim)]
+
+
+class _ResNetFallback(BasePlaceRecognition):
+    """MixVPR / SALAD: what the reference executes is a torchvision ResNet-50 GAP
+    (place_recognition.py:248-306).  Not built on HIP yet."""
+
+    def __init__(self, descriptor_dim, device, pretrained_path=None):
+        super().__init__(descriptor_dim, device)
+        self.pretrained_path = pretrained_path
+        self._model_loaded = False
+
+    def extract_descriptor(self, image: np.ndarray) -> np.ndarray:
+        raise _native.MlgateError(
+            f"{type(self).__name__}: the ResNet-50 descriptor path (the reference's MixVPR/SALAD fallback) is "
+            "not implemented on MI355X yet; use vpr_method='cricavpr' or 'anyloc', or inject descriptors into "
+            ".descriptors")
+
+
+class MixVPR(_ResNetFallback):
+    def __init__(self, backbone: str = 'resnet50', descriptor_dim: int = 4096, device: str = 'cuda',
+                 pretrained_path: Optional[str] = None):
+        super().__init__(descriptor_dim, device, pretrained_path)
+        self.backbone_name = backbone
+
+
+class SALAD(_ResNetFallback):
+    def __init__(self, descriptor_dim: int = 8448, device: str = 'cuda', pretrained_path: Optional[str] = None):
+        super().__init__(descriptor_dim, device, pretrained_path)
+
+
+class _DinoEngineMixin:
+    """Lazy ViT-B/14 engine construction shared by CricaVPR and AnyLoc."""
+
+    _image_size = 322
+    _pool = "gem"
+    _swap_rb = True
+
+    def _engine(self):
+        if getattr(self, '_vit', None) is None:
+            if self.backbone_name != 'dinov2_vitb14':
+                raise ValueError(f"{self.backbone_name}: only the dinov2_vitb14 backbone has MI355X kernels")
+            from .vit import VitB14
+            from .weights import resolve_state_dict
+            sd, source = resolve_state_dict(getattr(self, 'pretrained_path', None))
+            if source.startswith('synthetic'):
+                warnings.warn("DINOv2 hub weights are not available offline; using seeded synthetic "
+                              "dinov2_vitb14 weights (set pretrained_path or MLGATE_DINOV2_WEIGHTS to a local "
+                              "hub checkpoint for real descriptors).")
+            self._vit = VitB14(sd, device=self.device, image_size=self._image_size, pool=self._pool,
+                               swap_rb=self._swap_rb)
+            self.feat_dim = 768
+            self._model_loaded = True
+        return self._vit
+
+    def _forward(self, images, with_local=False):
+        torch = _torch()
+        eng = self._engine()
+        frames = torch.from_numpy(_as_frames(images)).to(eng.device)
+        return eng.forward(frames, with_local=with_local)
+
+    def extract_descriptors(self, images) -> np.ndarray:
+        return self._forward(images).cpu().numpy()
+
+    def extract_descriptor(self, image: np.ndarray) -> np.ndarray:
+        return self._forward([image])[0].cpu().numpy().flatten()
+
+
+class AnyLoc(_DinoEngineMixin, BasePlaceRecognition):
+    _image_size = 518
+    _pool = "mean"
+    _swap_rb = False
+
+    def __init__(self, backbone: str = 'dinov2_vitb14', descriptor_dim: int = 49152, device: str = 'cuda',
+                 num_clusters: int = 64):
+        super().__init__(descriptor_dim, device)
+        self.backbone_name = backbone
+        self.num_clusters = num_clusters
+        self._model_loaded = False
+        self._vit = None
+
+
+class CricaVPR(_DinoEngineMixin, BasePlaceRecognition):
+    def __init__(self, backbone: str = 'dinov2_vitb14', descriptor_dim: int = 10752, device: str = 'cuda',
+                 pretrained_path: Optional[str] = None, use_reranking: bool = True):
+        super().__init__(descriptor_dim, device)
+        self.backbone_name = backbone
+        self.pretrained_path = pretrained_path
+        self.use_reranking = use_reranking
+        self._model_loaded = False
+        self._vit = None
+        self._feature_cache = {}  # idx -> device float32 [1, 528, 768]
+
+    def extract_local_features(self, image: np.ndarray) -> np.ndarray:
+        _, local = self._forward([image], with_local=True)
+        return local.cpu().numpy()
+
+    def _to_device_feats(self, f):
+        torch = _torch()
+        dev = self._engine().device if getattr(self, '_vit', None) is not None else _native.require_device(
+            self.device)
+        t = f if isinstance(f, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(f, dtype=np.float32))
+        t = t.to(dev, torch.float32)
+        if t.dim() == 3:
+            t = t.squeeze(0)
+        return t.contiguous()
+
+    def compute_cross_correlation_score(self, query_features, match_features) -> float:
+        from . import retrieval
+        return float(retrieval.xcorr_score(self._to_device_feats(query_features),
+                                           self._to_device_feats(match_features)).item())
+
+    def rerank_candidates(self, query_idx: int, candidates: List[Tuple[int, float]],
+                          top_k: int = 5) -> List[Tuple[int, float]]:
+        if not self.use_reranking or query_idx not in self._feature_cache:
+            return candidates[:top_k]
+        qf = self._feature_cache[query_idx]
+        scored = []
+        for j, g in candidates:
+            if j in self._feature_cache:
+                scored.append((j, 0.5 * g + 0.5 * self.compute_cross_correlation_score(qf, self._feature_cache[j])))
+            else:
+                scored.append((j, g))
+        scored.sort(key=lambda x: x[1], reverse=True)
+        return scored[:top_k]
+
+    def _append(self, descs, local, timestamps, floor_labels, image_paths):
+        out = []
+        for i in range(len(descs)):
+            entry = PlaceDescriptor(timestamp=timestamps[i], descriptor=descs[i],
+                                    image_path=None if image_paths is None else image_paths[i],
+                                    floor_label=None if floor_labels is None else floor_labels[i])
+            self.descriptors.append(entry)
+            if self.use_reranking:
+                self._feature_cache[len(self.descriptors) - 1] = local[i:i + 1]
+            out.append(entry)
+        return out
+
+    def add_image(self, image: np.ndarray, timestamp: float, floor_label: Optional[int] = None,
+                  image_path: Optional[str] = None) -> PlaceDescriptor:
+        desc, local = self._forward([image], with_local=True)
+        return self._append(desc.cpu().numpy(), local, [timestamp], [floor_label], [image_path])[0]
+
+    def add_images(self, images, timestamps, floor_labels=None, image_paths=None) -> List[PlaceDescriptor]:
+        desc, local = self._forward(images, with_local=True)
+        return self._append(desc.cpu().numpy(), local, timestamps, floor_labels, image_paths)
+
+
+_METHODS = {'mixvpr': MixVPR, 'salad': SALAD, 'anyloc': AnyLoc, 'cricavpr': CricaVPR}
+
+
+class SemanticPlaceRecognition:
+    """VPR database + floor-gated all-keyframes loop-closure retrieval."""
+
+    def __init__(self, vpr_method: str = 'mixvpr', device: str = 'cuda', similarity_threshold: float = 0.5,
+                 min_time_gap: float = 10.0):
+        self.similarity_threshold = similarity_threshold
+        self.min_time_gap = min_time_gap
+        key = vpr_method.lower()
+        if key not in _METHODS:
+            raise ValueError(f"Unknown VPR method: {vpr_method}. Available: mixvpr, salad, anyloc, cricavpr")
+        self.vpr = CricaVPR(device=device, use_reranking=True) if key == 'cricavpr' else _METHODS[key](device=device)
+
+    def add_image(self, image: np.ndarray, timestamp: float, floor_label: int,
+                  image_path: Optional[str] = None) -> PlaceDescriptor:
+        return self.vpr.add_image(image, timestamp, floor_label, image_path)
+
+    def add_images(self, images, timestamps, floor_labels, image_paths=None) -> List[PlaceDescriptor]:
+        """Batched add_image (mlgate extension)."""
+        return self.vpr.add_images(images, timestamps, floor_labels, image_paths)
+
+    def find_loop_closures(self, enable_floor_gating: bool = True, k: int = 10) -> List[PlaceMatch]:
+        descs = self.vpr.descriptors
+        n = len(descs)
+        if n < 2:
+            return []
+        torch = _torch()
+        from . import retrieval
+        X, dev = self.vpr._device_matrix()
+        t = torch.tensor([float(d.timestamp) for d in descs], dtype=torch.float64, device=dev)
+        fl = torch.tensor([0 if d.floor_label is None else int(d.floor_label) for d in descs], dtype=torch.int64,
+                          device=dev)
+        hf = torch.tensor([d.floor_label is not None for d in descs], dtype=torch.uint8, device=dev)
+        if k <= 0:
+            return []
+        kk = min(k, retrieval.MAX_K)
+        if k > retrieval.MAX_K and n - 1 > retrieval.MAX_K:
+            raise ValueError(f"k={k} exceeds the device top-k limit of {retrieval.MAX_K}")
+        out = retrieval.knn_gate(X, t, fl, hf, self.min_time_gap, self.similarity_threshold, kk,
+                                 enable_floor_gating)
+        q, m, sim, valid = retrieval.flatten_matches(*out)
+        return [PlaceMatch(query_idx=int(i), match_idx=int(j), similarity=float(s),
+                           query_timestamp=descs[int(i)].timestamp, match_timestamp=descs[int(j)].timestamp,
+                           is_valid=bool(v)) for i, j, s, v in zip(q, m, sim, valid)]
+
+    def get_statistics(self, matches: List[PlaceMatch]) -> Dict:
+        if not matches:
+            return {'total_matches': 0, 'valid_matches': 0, 'rejected_matches': 0, 'rejection_rate': 0.0}
+        ok = [m.is_valid for m in matches]
+        n_valid = sum(ok)
+        n = len(matches)
+        sims = [m.similarity for m in matches]
+        return {
+            'total_matches': n,
+            'valid_matches': n_valid,
+            'rejected_matches': n - n_valid,
+            'rejection_rate': (n - n_valid) / n,
+            'mean_similarity': np.mean(sims),
+            'mean_valid_similarity': np.mean([s for s, v in zip(sims, ok) if v]) if n_valid > 0 else 0.0,
+        }
+
+
+def process_image_sequence(image_dir: Union[str, Path], timestamps: np.ndarray, floor_labels: np.ndarray,
+                           vpr_method: str = 'mixvpr',
+                           device: str = 'cuda') -> Tuple[SemanticPlaceRecognition, List[PlaceMatch]]:
+    """Sorted *.png then *.jpg of a directory -> database -> floor-gated loop closures."""
+    try:
+        import cv2
+    except ImportError as e:
+        raise ImportError("OpenCV is required for image loading. Install with: pip install opencv-python") from e
+    image_dir = Path(image_dir)
+    spr = SemanticPlaceRecognition(vpr_method=vpr_method, device=device)
+    files = sorted(image_dir.glob('*.png')) + sorted(image_dir.glob('*.jpg'))
+    if len(files) != len(timestamps):
+        warnings.warn(f"Number of images ({len(files)}) != timestamps ({len(timestamps)}). Using minimum of both.")
+    n = min(len(files), len(timestamps), len(floor_labels))
+    print(f"Processing {n} images with {vpr_method}...")
+    for i in range(n):
+        img = cv2.imread(str(files[i]))
+        if img is None:
+            warnings.warn(f"Failed to load image: {files[i]}")
+            continue
+        spr.add_image(image=img, timestamp=timestamps[i], floor_label=int(floor_labels[i]), image_path=str(files[i]))
+        if (i + 1) % 100 == 0:
+            print(f"  Processed {i + 1}/{n} images")
+    print("Finding loop closure candidates...")
+    return spr, spr.find_loop_closures(enable_floor_gating=True)

@@ -31,12 +31,17 @@ STD = np.array([0.229, 0.224, 0.225])
 EMBED, HEADS, DEPTH, PATCH = 768, 12, 12, 14
 
 
-def preprocess(image, size=322):
-    """uint8 HxW / HxWx3 (BGR) / HxWx4 (BGRA) -> float32 [1, 3, size, size]."""
+def preprocess(image, size=322, swap_rb=True):
+    """uint8 HxW / HxWx3 (BGR) / HxWx4 (BGRA) -> float32 [1, 3, size, size].
+
+    swap_rb=False is AnyLoc._preprocess (place_recognition.py:489-505), which only
+    converts gray and feeds 3-channel frames in stored (BGR) order."""
     img = np.asarray(image, dtype=np.uint8)
     r = _lib.resize_linear_u8(img, size, size)
     if r.ndim == 2:
         rgb = np.stack([r, r, r], axis=-1)
+    elif not swap_rb:
+        rgb = r[:, :, :3]
     elif r.shape[2] == 4:
         rgb = r[:, :, [2, 1, 0]]
     else:
@@ -112,3 +117,10 @@ def extract_descriptor(image, sd):
 def extract_local_features(image, sd):
     """CricaVPR.extract_local_features -> float32 [1, 528, 768]."""
     return forward_tokens(preprocess(image), sd)[:, 1:, :].cpu().numpy()
+
+
+@torch.no_grad()
+def anyloc_descriptor(image, sd):
+    """AnyLoc.extract_descriptor (place_recognition.py:467-487): 518^2, patch mean -> (768,)."""
+    f = forward_tokens(preprocess(image, 518, swap_rb=False), sd)
+    return f[:, 1:, :].mean(dim=1).cpu().numpy().flatten()

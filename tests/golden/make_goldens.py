@@ -39,7 +39,7 @@ import numpy as np
 
 REF = "/root/reference"
 OUT = os.path.dirname(os.path.abspath(__file__))
-MARGIN = 1e-6
+MARGIN = 1e-5  # > 2x the float32 summation-order tolerance of the parity tests (4e-6)
 
 
 def _import_reference():
@@ -83,7 +83,7 @@ def margins_ok(sim, t, min_gap, k, thr):
 
 def knn_case(sg, name, seed, n, d, k, thr, gap, gating, none_frac, n_places, spread, dt=0.765):
     from scripts.semantic_gating.place_recognition import PlaceDescriptor, SemanticPlaceRecognition
-    for attempt in range(50):
+    for attempt in range(400):
         rng = np.random.default_rng(seed + 1000 * attempt)
         X, place = clustered_descriptors(rng, n, d, n_places, spread)
         t = np.arange(n, dtype=np.float64) * dt + rng.uniform(0, 0.01, n)
@@ -271,15 +271,49 @@ def traj_case(sg, system):
     return analysis.total_candidates
 
 
+def _params(fn):
+    import inspect
+    return [[p.name, None if p.default is inspect.Parameter.empty else repr(p.default)]
+            for p in inspect.signature(fn).parameters.values()]
+
+
+def api_case(sg):
+    """Public signatures / dataclass fields of the reference API (the drop-in contract)."""
+    import dataclasses
+    import inspect
+    from scripts.semantic_gating import floor_detector, geometric_verification, loop_closure_gate
+    from scripts.semantic_gating import place_recognition
+    out = {}
+    for mod in (floor_detector, loop_closure_gate, place_recognition, geometric_verification):
+        for name, obj in vars(mod).items():
+            if name.startswith('_') or getattr(obj, '__module__', None) != mod.__name__:
+                continue
+            if inspect.isclass(obj):
+                entry = {}
+                if dataclasses.is_dataclass(obj):
+                    entry['__fields__'] = [(f.name, repr(f.default) if f.default is not dataclasses.MISSING
+                                            else None) for f in dataclasses.fields(obj)]
+                for mname, m in vars(obj).items():
+                    if inspect.isfunction(m) and (not mname.startswith('_') or mname == '__init__'):
+                        entry[mname] = _params(m)
+                out[name] = entry
+            elif inspect.isfunction(obj):
+                out[name] = _params(obj)
+    out['__all__'] = list(sg.__all__)
+    with open(os.path.join(OUT, "api.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def main():
     sg = _import_reference()
+    api_case(sg)
     print("reference", sg.__version__)
     print("knn small", knn_case(sg, "small", 1, 64, 768, 10, 0.5, 10.0, True, 0.0, 8, 0.6))
     print("knn gaps", knn_case(sg, "gaps", 2, 300, 768, 10, 0.5, 10.0, True, 0.1, 40, 0.8))
     print("knn nogate", knn_case(sg, "nogate", 3, 300, 768, 7, 0.6, 5.0, False, 0.0, 40, 0.8))
     print("knn k20", knn_case(sg, "k20", 4, 500, 768, 20, 0.45, 10.0, True, 0.0, 30, 0.9))
     print("knn d4096", knn_case(sg, "d4096", 5, 200, 4096, 10, 0.5, 10.0, True, 0.05, 25, 0.9))
-    print("knn wide", knn_case(sg, "wide", 6, 2000, 768, 10, 0.5, 10.0, True, 0.0, 150, 0.9))
+    print("knn wide", knn_case(sg, "wide", 6, 2000, 768, 6, 0.55, 10.0, True, 0.0, 400, 1.0))
     print("knn selfgap0", knn_case(sg, "selfgap0", 8, 120, 768, 5, 0.5, 0.0, True, 0.0, 20, 0.8))
     print("knn tiny", knn_case(sg, "tiny", 9, 3, 768, 10, -1.0, 0.5, True, 0.0, 1, 0.5))
     pairwise_case(sg)

@@ -1,0 +1,187 @@
+"""Host-side API surface of the drop-in (CPU only): signatures against the reference's
+recorded API, the gate / IMU-floor / verifier-skip logic against golden vectors, and
+the C ABI library exports.  Mirrors how the reference's own demos exercise these
+classes (loop_closure_gate.py:261-304, floor_detector.py:202-237)."""
+import ctypes
+import dataclasses
+import inspect
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import mlgate
+from mlgate import _native
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _params(fn):
+    return [[p.name, None if p.default is inspect.Parameter.empty else repr(p.default)]
+            for p in inspect.signature(fn).parameters.values()]
+
+
+@pytest.fixture(scope="module")
+def api():
+    with open(os.path.join(GOLD, "api.json")) as f:
+        return json.load(f)
+
+
+IN_SCOPE = set(mlgate.__all__)
+OUT_OF_SCOPE = {'LiDARFloorTracker', 'MultiModalFloorDetector', 'FloorEstimate', 'SemanticGatingPipeline',
+                'ORBSlam3SemanticIntegration', 'DroidSlamSemanticIntegration', 'LegoLoamSemanticIntegration'}
+
+
+def test_export_list_covers_reference(api):
+    assert set(api['__all__']) - OUT_OF_SCOPE <= IN_SCOPE
+
+
+@pytest.mark.parametrize("name", ['SemanticPlaceRecognition', 'PlaceMatch', 'PlaceDescriptor', 'CricaVPR', 'AnyLoc',
+                                  'MixVPR', 'SALAD', 'SemanticLoopClosureGate', 'LoopClosureCandidate',
+                                  'ContextualPriorFactor', 'IMUFloorDetector', 'ElevatorEvent', 'GeometricVerifier',
+                                  'SemanticGeometricVerifier', 'MatchResult', 'LightGlue', 'SuperGlue', 'LoFTR'])
+def test_class_signatures_match_reference(api, name):
+    ref = api[name]
+    cls = getattr(mlgate, name)
+    if '__fields__' in ref:
+        ours = [(f.name, repr(f.default) if f.default is not dataclasses.MISSING else None)
+                for f in dataclasses.fields(cls)]
+        assert ours == [tuple(x) for x in ref['__fields__']]
+    for meth, params in ref.items():
+        if meth == '__fields__' or (meth == '__init__' and '__fields__' in ref):
+            continue
+        assert hasattr(cls, meth), f"{name}.{meth} missing"
+        assert _params(getattr(cls, meth)) == params, f"{name}.{meth}"
+
+
+@pytest.mark.parametrize("name", ['process_image_sequence', 'integrate_with_orbslam3', 'load_imu_from_bag'])
+def test_function_signatures(api, name):
+    assert _params(getattr(mlgate, name)) == api[name]
+
+
+def test_gate_matches_reference():
+    with open(os.path.join(GOLD, "gate.json")) as f:
+        G = json.load(f)
+    labels = np.zeros(10000, dtype=int)
+    for a, b, fl in G["labels_blocks"]:
+        labels[a:b] = fl
+    for key, case in G.items():
+        if not isinstance(case, dict) or "candidates" not in case:
+            continue
+        gate = mlgate.SemanticLoopClosureGate(labels, strict_mode=key.endswith("strict"))
+        cands = [tuple(c) for c in case["candidates"]]
+        valid, rejected = gate.gate_candidates(cands)
+        assert [[c.query_idx, c.match_idx, float(c.similarity_score), int(c.query_floor), int(c.match_floor)]
+                for c in valid] == case["valid"]
+        assert [[c.query_idx, c.match_idx, c.rejection_reason] for c in rejected] == case["rejected"]
+        assert all(c.is_valid for c in valid) and not any(c.is_valid for c in rejected)
+        assert gate.get_stats() == pytest.approx(case["stats"])
+    assert mlgate.SemanticLoopClosureGate(labels).get_stats() == G["empty_stats"]
+
+
+def test_gate_single_candidate_path_agrees_with_batch():
+    labels = np.repeat([5, 1, 4, 2], [50, 20, 20, 30])
+    rng = np.random.default_rng(0)
+    cands = [(int(a), int(b), float(s)) for a, b, s in zip(rng.integers(0, 120, 300), rng.integers(0, 120, 300),
+                                                            rng.random(300))]
+    for strict in (True, False):
+        g1, g2 = mlgate.SemanticLoopClosureGate(labels, strict), mlgate.SemanticLoopClosureGate(labels, strict)
+        one = [g1.gate_candidate(*c) for c in cands]
+        v, r = g2.gate_candidates(cands)
+        assert [c for c in one if c.is_valid] == v and [c for c in one if not c.is_valid] == r
+        assert g1.get_stats() == g2.get_stats()
+
+
+def test_gate_out_of_range_raises_index_error():
+    gate = mlgate.SemanticLoopClosureGate(np.array([1, 2, 3]))
+    with pytest.raises(IndexError):
+        gate.gate_candidate(0, 7)
+    with pytest.raises(IndexError):
+        gate.gate_candidates([(0, 1, 0.5), (0, 9, 0.5)])
+
+
+def test_contextual_prior_factor():
+    f = mlgate.ContextualPriorFactor(np.array([5, 5, 1]))
+    assert f.create_floor_constraint(2) == {'type': 'floor_prior', 'pose_idx': 2, 'floor': 1, 'expected_z': 3.0,
+                                            'noise_model': 'diagonal', 'sigma_z': 0.5}
+    assert f.create_elevator_transition_factor(0, 1, 'down')['expected_dz'] == -3.0
+    assert "CheckFloorConsistency" in mlgate.integrate_with_orbslam3(np.zeros(3), None)
+
+
+def test_imu_floor_detector_matches_reference():
+    g = dict(np.load(os.path.join(GOLD, "imu.npz")))
+    det = mlgate.IMUFloorDetector()
+    ev = det.detect_elevator_events(g["t"], g["ax"], g["ay"], g["az"])
+    arr = np.array([[e.start_time, e.end_time, e.duration, e.start_idx, e.end_idx, e.floor_change] for e in ev],
+                   np.float64).reshape(-1, 6)
+    assert np.array_equal(arr, g["events"])
+    assert [e.direction for e in ev] == list(g["directions"])
+    assert np.array_equal(det.assign_floor_labels(g["traj"], start_floor=5), g["labels"])
+    with pytest.raises(NotImplementedError):
+        det.get_floor_at_time(1.0)
+    with pytest.raises(ValueError):
+        mlgate.IMUFloorDetector().get_floor_at_time(1.0)
+
+
+def test_verifier_skip_branch_matches_reference():
+    with open(os.path.join(GOLD, "verifier.json")) as f:
+        G = json.load(f)
+    v = mlgate.SemanticGeometricVerifier(device="cpu")
+    res = [v.verify_with_semantics(None, None, f1, f2, None, q, m)
+           for (f1, f2, q, m) in ((1, 2, 3, 4), (5, 1, 7, 9), (2, 4, 0, 0))]
+    assert [r.__dict__ for r in res] == G["results"]
+    assert v.get_statistics() == G["stats"]
+    assert mlgate.SemanticGeometricVerifier(device="cpu").get_statistics() == G["fresh_stats"]
+    assert list(mlgate.MatchResult.__dataclass_fields__) == G["fields"]
+
+
+def test_verifier_decision_rule():
+    gv = mlgate.GeometricVerifier(device="cpu")
+    k = np.zeros((40, 2), np.float32)
+    r = gv.decide(k, k, np.array([True] * 20 + [False] * 20), None, 0.5)
+    assert r.is_valid and r.num_inliers == 20 and r.confidence == 0.5 and r.num_matches == 40
+    r = gv.decide(k, k, np.array([True] * 19 + [False] * 21), None, 19 / 40)
+    assert not r.is_valid
+    with pytest.raises(ValueError):
+        mlgate.GeometricVerifier(matcher_type="sift")
+
+
+def test_unknown_vpr_method_raises():
+    with pytest.raises(ValueError):
+        mlgate.SemanticPlaceRecognition(vpr_method="netvlad", device="cpu")
+
+
+def test_empty_database_semantics_need_no_device():
+    spr = mlgate.SemanticPlaceRecognition("cricavpr", device="cpu")
+    assert spr.find_loop_closures() == []
+    assert spr.vpr.query(None) == []
+    assert spr.vpr.compute_all_pairwise_similarities().size == 0
+    assert spr.get_statistics([]) == {'total_matches': 0, 'valid_matches': 0, 'rejected_matches': 0,
+                                      'rejection_rate': 0.0}
+
+
+def test_cpu_device_is_refused_loudly():
+    spr = mlgate.SemanticPlaceRecognition("mixvpr", device="cpu")
+    for i in range(3):
+        spr.vpr.descriptors.append(mlgate.PlaceDescriptor(timestamp=100.0 * i, descriptor=np.ones(8, np.float32)))
+    with pytest.raises(_native.MlgateError):
+        spr.find_loop_closures()
+
+
+def test_library_exports_every_header_symbol():
+    """libmlgate.so loads without a GPU and exports every function include/mlgate.h declares."""
+    header = open(os.path.join(ROOT, "include", "mlgate.h")).read()
+    declared = set(re.findall(r"^\s*(?:const\s+)?\w[\w\s\*]*?\b(mlg_\w+)\s*\(", header, flags=re.M))
+    assert len(declared) >= 20
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(_native.EXPORTS) <= declared
+    L = _native.lib()
+    assert L.mlg_abi_version() == 1
+    assert L.mlg_vit_workspace_bytes(64, 322) > 0
+    assert L.mlg_vit_workspace_bytes(64, 300) == 0
+    assert L.mlg_strerror(-1).decode().startswith("invalid")

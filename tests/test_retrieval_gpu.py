@@ -1,6 +1,6 @@
 """Retrieval + gate parity on the GPU against golden vectors captured from the reference
 (tests/golden/make_goldens.py).  Indices, emission order and gate decisions must be
-bit-exact; similarities agree to 1e-6 (the reference's OpenBLAS SGEMM and the f32
+bit-exact; similarities agree to SIM_TOL (the reference's OpenBLAS SGEMM and the f32
 MFMA differ only in summation order)."""
 import glob
 import json
@@ -14,7 +14,9 @@ from mlgate import retrieval
 
 pytestmark = pytest.mark.gpu
 
-SIM_TOL = 1e-6
+# float32 dot products of unit vectors over D = 768..4096 terms: two summation orders
+# (OpenBLAS SGEMM vs the f32 MFMA chain) differ by up to ~sqrt(D) * 2^-24 * few.
+SIM_TOL = 4e-6
 
 
 def load(path):
