@@ -1,0 +1,65 @@
+"""World-size-2 gloo test of the frame-parallel path (CPU): sharding, the descriptor
+all-gather and the row-sharded retrieval must reproduce the single-process result.
+The per-rank retrieval compute here is the oracle (no GPU in this test); on the GPU
+box the same plumbing drives the HIP kernels (bench.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mlgate import distributed as mdist
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n, d, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import _lib, retrieval as oret
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((40, d)).astype(np.float32)[rng.integers(0, 40, n)]
+    X = X + 0.7 * rng.standard_normal((n, d)).astype(np.float32)
+    t = np.arange(n) * 0.765
+    fl = np.repeat(np.array([5, 1, 4, 2], np.int64), [n // 4, n // 4, n // 4, n - 3 * (n // 4)])
+    hf = np.ones(n, np.uint8)
+    lo, hi = mdist.shard(n, world, rank)
+    local = torch.from_numpy(X[lo:hi])  # this rank's "extracted" descriptors
+    gather = mdist.RowGather(n, d, world, "cpu")
+    full = gather(local).numpy()
+    assert np.array_equal(full, X)
+    S = oret.pairwise_similarities(full)[lo:hi]
+    idx, sim, valid, count = _lib.knn_rows(S, lo, t, fl, hf, 10.0, 0.5, 10, True)
+    sel = np.arange(10)[None, :] < count[:, None]
+    part = (np.repeat(np.arange(lo, hi), count), idx[sel].astype(np.int64), sim[sel], valid[sel])
+    parts = mdist.gather_objects_to_rank0(part, world, rank)
+    if rank == 0:
+        merged = mdist.merge_matches(parts)
+        ref = oret.find_loop_closures(X, t, fl, hf, 10.0, 0.5, 10, True)
+        ok = all(np.array_equal(a, b) for a, b in zip(merged, ref)) and len(merged[0]) > 0
+        with open(out_path, "w") as f:
+            f.write("ok" if ok else "mismatch")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [301, 1000])
+def test_row_sharded_gate_equals_single_process(tmp_path, n):
+    out = str(tmp_path / "result.txt")
+    mp.spawn(_worker, args=(2, _free_port(), n, 64, out), nprocs=2, join=True)
+    assert open(out).read() == "ok"
+
+
+def test_shards_cover_exactly():
+    for n in (1, 7, 5000, 19163):
+        for w in (1, 2, 4, 8):
+            rs = [mdist.shard(n, w, r) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert sum(mdist.shard_sizes(n, w)) == n
