@@ -32,7 +32,7 @@ extern "C" {
 
 #define MLG_VIT_DEPTH 12
 #define MLG_VIT_EMBED 768
-#define MLG_VIT_PATCH_K 640 /* 3*14*14 = 588 patch inputs, zero-padded to a multiple of 64 */
+#define MLG_VIT_PATCH_K 768 /* 3*14*14 = 588 patch inputs, zero-padded to 12 K-tiles of 64 */
 
 int mlg_abi_version(void);
 const char* mlg_strerror(int status);
@@ -127,6 +127,11 @@ int mlg_xcorr_score(const float* q, int n1, const float* m, int n2, int D, void*
 /* ----------------------------------------------------------- op-level access --
  * Individual kernels of the ViT path (parity tests against a float32 reference). */
 int mlg_op_gemm_f32out(const uint16_t* A, const uint16_t* W, float* C, int M, int N, int K, void* stream);
+/* GEMM kernel generation: 1 = 128x128 register-staged, 2 = 128x256 3-stage LDS-DMA
+ * (default; used when N % 256 == 0 and K / 64 % 3 == 0, else 1). */
+int mlg_set_gemm_variant(int variant);
+int mlg_op_gemm_f32out_variant(int variant, const uint16_t* A, const uint16_t* W, float* C, int M, int N, int K,
+                               void* stream);
 int mlg_op_gemm_bias_gelu(const uint16_t* A, const uint16_t* W, const float* bias, uint16_t* C, int M, int N,
                           int K, void* stream);
 int mlg_op_gemm_residual(const uint16_t* A, const uint16_t* W, const float* bias, const float* gamma, float* X,

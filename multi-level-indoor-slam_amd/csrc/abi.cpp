@@ -245,6 +245,11 @@ int mlg_xcorr_score(const float* q, int n1, const float* m, int n2, int D, void*
 int mlg_op_gemm_f32out(const uint16_t* A, const uint16_t* W, float* C, int M, int N, int K, void* stream) {
     return mlg_gemm_f32out(A, W, C, M, N, K, (hipStream_t)stream);
 }
+int mlg_op_gemm_f32out_variant(int variant, const uint16_t* A, const uint16_t* W, float* C, int M, int N, int K,
+                               void* stream) {
+    return mlg_gemm_f32out_variant(variant, A, W, C, M, N, K, (hipStream_t)stream);
+}
+int mlg_set_gemm_variant(int variant) { return mlg_gemm_set_variant(variant); }
 int mlg_op_gemm_bias_gelu(const uint16_t* A, const uint16_t* W, const float* bias, uint16_t* C, int M, int N,
                           int K, void* stream) {
     return mlg_gemm_bias_gelu_bf16(A, W, bias, C, M, N, K, (hipStream_t)stream);

@@ -11,6 +11,9 @@ typedef uint16_t bf16_t;
 
 // gemm_bf16.hip -- C = epi(A[M,K] . W[N,K]^T), N % 128 == 0, K % 64 == 0
 int mlg_gemm_f32out(const bf16_t* A, const bf16_t* W, float* C, int M, int N, int K, hipStream_t s);
+int mlg_gemm_f32out_variant(int variant, const bf16_t* A, const bf16_t* W, float* C, int M, int N, int K,
+                            hipStream_t s);
+int mlg_gemm_set_variant(int variant);
 int mlg_gemm_bias_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,
                        hipStream_t s);
 int mlg_gemm_bias_gelu_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,

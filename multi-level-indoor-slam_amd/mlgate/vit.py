@@ -17,7 +17,7 @@ import torch.nn.functional as F
 from . import _native
 from .weights import DEPTH, EMBED, PATCH
 
-PATCH_K = 640  # 3*14*14 = 588 patch inputs zero-padded to a multiple of 64 (include/mlgate.h)
+PATCH_K = 768  # 3*14*14 = 588 patch inputs zero-padded to 12 K-tiles of 64 (include/mlgate.h)
 P = ctypes.c_void_p
 
 

@@ -29,14 +29,16 @@ def rel_err(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (1060, 256, 768), (530, 3072, 768), (777, 768, 3072)])
-def test_gemm_f32out(dev, M, N, K):
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (1060, 256, 768), (530, 3072, 768), (777, 768, 3072),
+                                   (33920 - 17, 2304, 768), (129, 256, 192)])
+def test_gemm_f32out(dev, M, N, K, variant):
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g).to(dev)
     W = torch.randn(N, K, generator=g).to(dev)
     Ab, Wb = bf16_bits(A), bf16_bits(W)
     C = torch.full((M, N), float("nan"), device=dev)
-    _native.check(_native.lib().mlg_op_gemm_f32out(P(Ab), P(Wb), P(C), M, N, K, S(dev)), "gemm")
+    _native.check(_native.lib().mlg_op_gemm_f32out_variant(variant, P(Ab), P(Wb), P(C), M, N, K, S(dev)), "gemm")
     ref = Ab.float().cpu() @ Wb.float().cpu().T
     torch.cuda.synchronize()
     assert torch.isfinite(C).all()
@@ -133,7 +135,8 @@ def test_preprocess_bit_exact(dev, shape):
     fr = torch.from_numpy(imgs).to(dev)
     H, W = shape[:2]
     C = 1 if len(shape) == 2 else shape[2]
-    out = torch.empty(2 * 529, 640, dtype=torch.bfloat16, device=dev)
+    from mlgate.vit import PATCH_K
+    out = torch.empty(2 * 529, PATCH_K, dtype=torch.bfloat16, device=dev)
     _native.check(_native.lib().mlg_op_preprocess_patches(P(fr), 2, H, W, C, H * W * C, 322, P(out), S(dev)),
                   "prep")
     torch.cuda.synchronize()
