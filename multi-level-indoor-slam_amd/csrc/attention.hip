@@ -26,8 +26,11 @@ constexpr int VTILE_BYTES = 64 * KB * 2;
 __device__ __forceinline__ int k_off(int key, int chunk) {  // K image [key][d], 16-B chunks
     return key * 128 + ((chunk ^ ((key >> 1) & 7)) << 4);
 }
-__device__ __forceinline__ int v_off(int d, int gran) {  // V^T image [d][key], 8-B granules
-    return d * 128 + ((gran ^ ((d >> 1) & 15)) << 3);
+// V^T image [d][key], 8-B granules.  The (d >> 5) term makes the d and d + 32 rows of
+// one lane non-constant apart, so hipcc cannot fuse the two ds_read_b64 into a
+// ds_read2st64_b64 (which banks mod 32 dwords and would 2-way conflict).
+__device__ __forceinline__ int v_off(int d, int gran) {
+    return d * 128 + ((gran ^ (((d >> 1) ^ (d >> 5)) & 15)) << 3);
 }
 
 __global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,

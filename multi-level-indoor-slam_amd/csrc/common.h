@@ -23,16 +23,16 @@ __device__ __forceinline__ float bf16_to_f32(bf16_t v) {
     return __uint_as_float(((uint32_t)v) << 16);
 }
 
-// Round-to-nearest-even f32 -> bf16 (NaN kept a NaN by the quiet-bit OR).
-__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (bf16_t)(u >> 16);
-}
+// Round-to-nearest-even f32 -> bf16 (v_cvt_pk_bf16_f32; NaN stays NaN).
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-    return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
+    bf16x2_t v = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(uint32_t, v);
+}
+
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
+    return (bf16_t)(pack_bf16x2(f, 0.0f) & 0xffffu);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -224,23 +224,25 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(const bf16_t* __restrict__ A
 #undef GEMM_LSTORE
 }
 
-// ------------------------------------------------------------- kernel v2
-// 128 x 256 x 64 tile, 512 threads = 8 waves (2 along M x 4 along N, 64 x 64 each),
-// three LDS stages filled by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+// ------------------------------------------------------- LDS-DMA kernels
+// 128 x 256 x BK tile, 512 threads = 8 waves (2 along M x 4 along N, 64 x 64 each),
+// STAGES LDS stages filled by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
 // wave-instruction), K-tile t+2 prefetched while t is computed.  The XOR swizzle
-// moves to the per-lane SOURCE address (the DMA writes lane-linear); fragment reads
-// apply the same involution.  Waits are counted (s_waitcnt vmcnt(6) = the six DMAs of
-// the newest tile stay in flight across the raw s_barrier); each stage is its own
-// __shared__ object and the loop is unrolled by 3 so stage addresses are constants.
-namespace v2 {
-constexpr int BM = 128, BN = 256, BK = 64;
-constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;  // 48 KiB
+// (chunk ^ (row >> 1) & (chunks/row - 1), conflict-free for every ds_read_b128
+// fragment read at BK = 32 and 64 -- checked by script) moves to the per-lane SOURCE
+// address since the DMA writes lane-linear; fragment reads apply the same involution.
+// Waits are counted (s_waitcnt vmcnt(#DMA per tile): the newest tile's DMAs stay in
+// flight across the raw s_barrier); each stage is its own __shared__ object and the
+// loop is unrolled by 3 so stage addresses are constants.
+//   BK = 64: 3 x 48 KiB stages, one workgroup per CU.
+//   BK = 32: 3 x 24 KiB stages, two workgroups per CU (16 waves): one workgroup's
+//            epilogue / prologue overlaps the other's MFMA main loop.
+namespace dma {
+constexpr int BM = 128, BN = 256;
 typedef __attribute__((address_space(3))) char lds_char;
 
 // LDS byte address of a __shared__ object (the value M0 carries for LDS-DMA).
-__device__ __forceinline__ unsigned lds_addr(char* p) {
-    return (unsigned)(uintptr_t)(lds_char*)p;
-}
+__device__ __forceinline__ unsigned lds_addr(char* p) { return (unsigned)(uintptr_t)(lds_char*)p; }
 
 // One global_load_lds_dwordx4: 16 B per lane from `g` into LDS [m0 + 16 * lane].
 // Issued through inline asm so hipcc's waitcnt pass does not conservatively drain
@@ -249,10 +251,25 @@ __device__ __forceinline__ unsigned lds_addr(char* p) {
 __device__ __forceinline__ void dma16(const void* g, unsigned m0) {
     asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
 }
+// Same with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset.
+__device__ __forceinline__ void dma16s(unsigned voff, const void* sbase, unsigned m0) {
+    asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
+}
 
-template <class Epi>
-__global__ __launch_bounds__(512, 1) void k_gemm(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, int M,
-                                                 int N, int K, int lda, int ldw, Epi epi) {
+template <int BK>
+__device__ __forceinline__ int soff(int row, int chunk) {
+    return row * (BK * 2) + ((chunk ^ ((row >> 1) & (BK / 8 - 1))) << 4);
+}
+
+template <class Epi, int BK>
+__global__ __launch_bounds__(512, BK == 32 ? 4 : 2) void k_gemm(const bf16_t* __restrict__ A,
+                                                                 const bf16_t* __restrict__ W, int M, int N, int K,
+                                                                 int lda, int ldw, Epi epi) {
+    constexpr int CH = BK / 8;                         // 16-B chunks per row
+    constexpr int RPI = 64 / CH;                       // rows per DMA wave-instruction
+    constexpr int NA = BM / RPI / 8, NB = BN / RPI / 8;  // DMAs per wave per K-tile
+    constexpr int A_BYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
+    constexpr int WAIT_NEWEST = 0xF70 | (NA + NB);     // s_waitcnt vmcnt(NA + NB)
     __shared__ __attribute__((aligned(16))) char st0[STAGE];
     __shared__ __attribute__((aligned(16))) char st1[STAGE];
     __shared__ __attribute__((aligned(16))) char st2[STAGE];
@@ -263,31 +280,27 @@ __global__ __launch_bounds__(512, 1) void k_gemm(const bf16_t* __restrict__ A, c
     const int mt = wgid / nN, nt = wgid - mt * nN;
     const int m0 = mt * BM, n0 = nt * BN;
 
-    // DMA sources: wave w fills A row-groups 2w, 2w+1 and B row-groups 4w .. 4w+3 (8 rows each)
-    const int lr = lane >> 3, lp = lane & 7;
-    int ra = (2 * wave) * 8 + lr;
-    const bf16_t* pa0 = A + (size_t)min(m0 + ra, M - 1) * lda + ((lp ^ ((ra >> 1) & 7)) * 8);
-    ra += 8;
-    const bf16_t* pa1 = A + (size_t)min(m0 + ra, M - 1) * lda + ((lp ^ ((ra >> 1) & 7)) * 8);
-    int rb = (4 * wave) * 8 + lr;
-    const bf16_t* pb0 = W + (size_t)(n0 + rb) * ldw + ((lp ^ ((rb >> 1) & 7)) * 8);
-    rb += 8;
-    const bf16_t* pb1 = W + (size_t)(n0 + rb) * ldw + ((lp ^ ((rb >> 1) & 7)) * 8);
-    rb += 8;
-    const bf16_t* pb2 = W + (size_t)(n0 + rb) * ldw + ((lp ^ ((rb >> 1) & 7)) * 8);
-    rb += 8;
-    const bf16_t* pb3 = W + (size_t)(n0 + rb) * ldw + ((lp ^ ((rb >> 1) & 7)) * 8);
-    const int da = (2 * wave) * 1024, db = A_BYTES + (4 * wave) * 1024;
+    // DMA sources: wave w fills A row-groups NA*w .. and B row-groups NB*w .. (RPI rows each)
+    const int lr = lane / CH, lp = lane % CH;
+    const bf16_t* pa[NA];
+    const bf16_t* pb[NB];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+        const int row = (NA * wave + i) * RPI + lr;
+        pa[i] = A + (size_t)min(m0 + row, M - 1) * lda + ((lp ^ ((row >> 1) & (CH - 1))) * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int row = (NB * wave + i) * RPI + lr;
+        pb[i] = W + (size_t)(n0 + row) * ldw + ((lp ^ ((row >> 1) & (CH - 1))) * 8);
+    }
+    const int da = NA * wave * 1024, db = A_BYTES + NB * wave * 1024;
 
-#define V2_ISSUE(ST, k0)                                                                                   \
+#define DMA_ISSUE(ST, k0)                                                                                  \
     {                                                                                                      \
         const unsigned b_ = lds_addr(ST);                                                                  \
-        dma16(pa0 + (k0), b_ + da);                                                                        \
-        dma16(pa1 + (k0), b_ + da + 1024);                                                                 \
-        dma16(pb0 + (k0), b_ + db);                                                                        \
-        dma16(pb1 + (k0), b_ + db + 1024);                                                                 \
-        dma16(pb2 + (k0), b_ + db + 2048);                                                                 \
-        dma16(pb3 + (k0), b_ + db + 3072);                                                                 \
+        _Pragma("unroll") for (int i = 0; i < NA; ++i) dma16(pa[i] + (k0), b_ + da + i * 1024);            \
+        _Pragma("unroll") for (int i = 0; i < NB; ++i) dma16(pb[i] + (k0), b_ + db + i * 1024);            \
     }
 
     const int wm = wave & 1, wn = wave >> 1;
@@ -297,48 +310,46 @@ __global__ __launch_bounds__(512, 1) void k_gemm(const bf16_t* __restrict__ A, c
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#define V2_COMPUTE(ST)                                                                                     \
-    _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                                        \
+#define DMA_COMPUTE(ST)                                                                                    \
+    _Pragma("unroll") for (int s = 0; s < BK / 32; ++s) {                                                  \
         bf16x8 af[4], wf[4];                                                                               \
         const int ch = s * 4 + (lane >> 4);                                                                \
         _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                                    \
             const int row = wm * 64 + j * 16 + (lane & 15);                                                \
-            af[j] = *reinterpret_cast<const bf16x8*>((ST) + swz_off(row, ch));                             \
+            af[j] = *reinterpret_cast<const bf16x8*>((ST) + soff<BK>(row, ch));                            \
         }                                                                                                  \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                    \
             const int row = wn * 64 + i * 16 + (lane & 15);                                                \
-            wf[i] = *reinterpret_cast<const bf16x8*>((ST) + A_BYTES + swz_off(row, ch));                   \
+            wf[i] = *reinterpret_cast<const bf16x8*>((ST) + A_BYTES + soff<BK>(row, ch));                  \
         }                                                                                                  \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < 4; ++j)        \
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], af[j], acc[i][j], 0, 0, 0);         \
     }
 
-    // s_waitcnt encodings (gfx9): vmcnt(6) = 0xF76, vmcnt(0) = 0xF70 (lgkm/exp untouched).
     // Every step issues its DMA unconditionally (past the last K-tile it re-reads the
-    // last tile into a stage that is never read again) so the waitcnt pass sees the
-    // same pending-DMA state on every path and never falls back to vmcnt(0).
-#define V2_STEP(TT, CUR, NXT)                                                                              \
+    // last tile into a stage that is never read again): one code path, one wait count.
+#define DMA_STEP(TT, CUR, NXT)                                                                             \
     {                                                                                                      \
-        V2_ISSUE(NXT, min((TT) + 2, nk - 1) * BK);                                                         \
-        V2_COMPUTE(CUR);                                                                                   \
-        __builtin_amdgcn_s_waitcnt(0xF76);                                                                 \
+        DMA_ISSUE(NXT, min((TT) + 2, nk - 1) * BK);                                                        \
+        DMA_COMPUTE(CUR);                                                                                  \
+        __builtin_amdgcn_s_waitcnt(WAIT_NEWEST);                                                           \
         __builtin_amdgcn_s_barrier();                                                                      \
     }
 
     const int nk = K / BK;  // multiple of 3 (checked by the launcher)
-    V2_ISSUE(st0, 0);
-    V2_ISSUE(st1, BK);
-    __builtin_amdgcn_s_waitcnt(0xF76);
+    DMA_ISSUE(st0, 0);
+    DMA_ISSUE(st1, BK);
+    __builtin_amdgcn_s_waitcnt(WAIT_NEWEST);
     __builtin_amdgcn_s_barrier();
     for (int t = 0; t < nk; t += 3) {
-        V2_STEP(t, st0, st2)
-        V2_STEP(t + 1, st1, st0)
-        V2_STEP(t + 2, st2, st1)
+        DMA_STEP(t, st0, st2)
+        DMA_STEP(t + 1, st1, st0)
+        DMA_STEP(t + 2, st2, st1)
     }
     __builtin_amdgcn_s_waitcnt(0xF70);  // no DMA may still be writing LDS when the block retires
-#undef V2_STEP
-#undef V2_COMPUTE
-#undef V2_ISSUE
+#undef DMA_STEP
+#undef DMA_COMPUTE
+#undef DMA_ISSUE
 
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -349,20 +360,166 @@ __global__ __launch_bounds__(512, 1) void k_gemm(const bf16_t* __restrict__ A, c
             if (m < M) epi(m, n, acc[i][j]);
         }
 }
-}  // namespace v2
+// 256 x 256 x 64 tile, 8 waves (2 along M x 4 along N, 128 x 64 each: 32 accumulators),
+// two 64 KiB LDS stages (K-tile t+1 lands while t is computed), one workgroup per CU,
+// PERSISTENT: the grid is one workgroup per CU and each walks a contiguous range of
+// output tiles of its XCD (N fastest, so the 32 workgroups of an XCD share A panels
+// in that XCD's L2).  The last K-step of a tile already DMAs K-tile 0 of the next tile,
+// so the next tile's first wait overlaps this tile's epilogue, and the epilogue's
+// stores drain while the next tile's MFMAs run.  Twice the MFMAs per barrier and
+// 0.375 fragment reads per MFMA (vs 0.5 at 64 x 64 per wave).
+template <class Epi>
+__global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                   int M, int N, int K, int lda, int ldw, Epi epi) {
+    constexpr int BK = 64, TM = 256, TN = 256;
+    constexpr int A_BYTES = TM * BK * 2, STAGE = (TM + TN) * BK * 2;  // 64 KiB
+    constexpr int NA = 4, NB = 4;                                      // DMAs per wave per K-tile
+    __shared__ __attribute__((aligned(16))) char st0[STAGE];
+    __shared__ __attribute__((aligned(16))) char st1[STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nN = N / TN, nM = (M + TM - 1) / TM, ntiles = nN * nM;
+    const int xcd = blockIdx.x & 7, per_xcd = gridDim.x >> 3;  // grid is a multiple of 8
+    const int tx = (ntiles + 7) >> 3;
+    const int tile_end = min((xcd + 1) * tx, ntiles);
+    int tile = xcd * tx + (blockIdx.x >> 3);
+    if (tile >= tile_end) return;
 
-int g_variant = 2;  // 1: 128x128 register-staged, 2: 128x256 3-stage LDS-DMA
+    const int lr = lane >> 3, lp = lane & 7;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int da = NA * wave * 1024, db = A_BYTES + NB * wave * 1024;
+    const int nk = K / BK;  // even (checked by the launcher)
+
+    // DMA addressing: wave-uniform tile bases (SGPRs) + 32-bit per-lane byte offsets.
+    // B offsets are the same for every tile (N % 256 == 0); A offsets change only for
+    // the ragged last M-tile, whose rows are clamped to M - 1.
+    unsigned ob[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int row = (NB * wave + i) * 8 + lr;
+        ob[i] = (unsigned)(row * ldw + ((lp ^ ((row >> 1) & 7)) * 8)) * 2u;
+    }
+    auto a_offsets = [&](int t, unsigned* oa) {
+        const int m0 = (t / nN) * TM;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int row = (NA * wave + i) * 8 + lr;
+            oa[i] = (unsigned)((min(m0 + row, M - 1) - m0) * lda + ((lp ^ ((row >> 1) & 7)) * 8)) * 2u;
+        }
+    };
+    auto a_base = [&](int t) { return A + (size_t)((t / nN) * TM) * lda; };
+    auto b_base = [&](int t) { return W + (size_t)((t % nN) * TN) * ldw; };
+    unsigned oa[NA];
+    const bf16_t* sa = a_base(tile);
+    const bf16_t* sb = b_base(tile);
+    a_offsets(tile, oa);
+#define D256_DMA(ST, OA, SA, SB, k0)                                                                       \
+    {                                                                                                      \
+        const unsigned b_ = lds_addr(ST);                                                                  \
+        const bf16_t* sa_ = (SA) + (k0);                                                                   \
+        const bf16_t* sb_ = (SB) + (k0);                                                                   \
+        _Pragma("unroll") for (int i = 0; i < NA; ++i) dma16s((OA)[i], sa_, b_ + da + i * 1024);           \
+        _Pragma("unroll") for (int i = 0; i < NB; ++i) dma16s(ob[i], sb_, b_ + db + i * 1024);             \
+    }
+#define D256_COMPUTE(ST)                                                                                   \
+    _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                                        \
+        bf16x8 af[8], wf[4];                                                                               \
+        const int ch = s * 4 + (lane >> 4);                                                                \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                    \
+            const int row = wn * 64 + i * 16 + (lane & 15);                                                \
+            wf[i] = *reinterpret_cast<const bf16x8*>((ST) + A_BYTES + soff<64>(row, ch));                  \
+        }                                                                                                  \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                    \
+            const int row = wm * 128 + j * 16 + (lane & 15);                                               \
+            af[j] = *reinterpret_cast<const bf16x8*>((ST) + soff<64>(row, ch));                            \
+        }                                                                                                  \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) _Pragma("unroll") for (int i = 0; i < 4; ++i)        \
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], af[j], acc[i][j], 0, 0, 0);         \
+    }
+
+    D256_DMA(st0, oa, sa, sb, 0);
+    __builtin_amdgcn_s_waitcnt(0xF70);
+    __builtin_amdgcn_s_barrier();
+    for (; tile < tile_end; tile += per_xcd) {
+        const int next = tile + per_xcd < tile_end ? tile + per_xcd : tile;
+        unsigned na[NA];
+        a_offsets(next, na);
+        const bf16_t* nsa = a_base(next);
+        const bf16_t* nsb = b_base(next);
+        const int kn = next != tile ? 0 : (nk - 1) * BK;  // no next tile: harmless re-read
+        f32x4 acc[4][8];  // [n-tile][m-tile]
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < nk; t += 2) {
+            D256_DMA(st1, oa, sa, sb, (t + 1) * BK);
+            D256_COMPUTE(st0);
+            __builtin_amdgcn_s_waitcnt(0xF70);
+            __builtin_amdgcn_s_barrier();
+            if (t + 2 < nk) {
+                D256_DMA(st0, oa, sa, sb, (t + 2) * BK);
+            } else {
+                D256_DMA(st0, na, nsa, nsb, kn);  // K-tile 0 of the next output tile
+            }
+            D256_COMPUTE(st1);
+            __builtin_amdgcn_s_waitcnt(0xF70);
+            __builtin_amdgcn_s_barrier();
+        }
+        const int mt = tile / nN, m0 = mt * TM, n0 = (tile - mt * nN) * TN;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4;
+                const int m = m0 + wm * 128 + j * 16 + (lane & 15);
+                if (m < M) epi(m, n, acc[i][j]);
+            }
+#pragma unroll
+        for (int i = 0; i < NA; ++i) oa[i] = na[i];
+        sa = nsa;
+        sb = nsb;
+    }
+    __builtin_amdgcn_s_waitcnt(0xF70);
+#undef D256_COMPUTE
+#undef D256_DMA
+}
+}  // namespace dma
+
+// 1: 128x128 register-staged; 2: 128x256 DMA BK=64 (3 stages); 3: 128x256 DMA BK=32 (2 WG/CU);
+// 4: 256x256 DMA where N allows (N % 256 == 0 and N >= 2048), else 2.
+int g_variant = 4;
+int g_num_cus = 256;  // multiple of 8 (refreshed from the device on first use)
+
+int num_cus() {
+    static int cached = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount,
+                                                                         dev) != hipSuccess || n < 8)
+            return 256;
+        return n / 8 * 8;
+    }();
+    return cached;
+}
 
 template <class Epi>
 int launch(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldw, Epi epi, hipStream_t s,
            int variant = -1) {
     if (variant < 0) variant = g_variant;
+    g_num_cus = num_cus();
     if (M <= 0 || N <= 0 || K <= 0 || (K % BK) || (lda % 8) || (ldw % 8) || lda < K || ldw < K)
         return MLG_EINVAL;
     if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W)) & 15) return MLG_EINVAL;
-    if (variant == 2 && N % v2::BN == 0 && (K / BK) % 3 == 0) {
-        const long nwg = (long)(N / v2::BN) * ((M + v2::BM - 1) / v2::BM);
-        hipLaunchKernelGGL(v2::k_gemm<Epi>, dim3((unsigned)nwg), dim3(512), 0, s, A, W, M, N, K, lda, ldw, epi);
+    const long nwg_dma = (long)(N / dma::BN) * ((M + dma::BM - 1) / dma::BM);
+    if (variant == 4 && N % 256 == 0 && N >= 2048 && (K / 64) % 2 == 0) {
+        const long ntiles = (long)(N / 256) * ((M + 255) / 256);
+        const long grid = std::min<long>(g_num_cus, (ntiles + 7) / 8 * 8);  // persistent: <= 1 per CU
+        hipLaunchKernelGGL(dma::k_gemm256<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K, lda, ldw, epi);
+    } else if (variant == 3 && N % dma::BN == 0 && (K / 32) % 3 == 0) {
+        hipLaunchKernelGGL((dma::k_gemm<Epi, 32>), dim3((unsigned)nwg_dma), dim3(512), 0, s, A, W, M, N, K, lda, ldw,
+                           epi);
+    } else if (variant >= 2 && N % dma::BN == 0 && (K / 64) % 3 == 0) {
+        hipLaunchKernelGGL((dma::k_gemm<Epi, 64>), dim3((unsigned)nwg_dma), dim3(512), 0, s, A, W, M, N, K, lda, ldw,
+                           epi);
     } else {
         if (N % BN) return MLG_EINVAL;
         const long nwg = (long)(N / BN) * ((M + BM - 1) / BM);
@@ -382,7 +539,7 @@ int mlg_gemm_f32out_variant(int variant, const bf16_t* A, const bf16_t* W, float
     return launch(A, W, M, N, K, K, K, EpiF32{C, N}, s, variant);
 }
 int mlg_gemm_set_variant(int variant) {
-    if (variant != 1 && variant != 2) return MLG_EINVAL;
+    if (variant < 1 || variant > 4) return MLG_EINVAL;
     g_variant = variant;
     return MLG_OK;
 }

@@ -34,7 +34,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--variants", default="2,3,4")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     L = _native.lib()
@@ -43,13 +43,34 @@ def main():
     A = torch.randn(33920 - 17, 768, device=dev, generator=g).to(torch.bfloat16)
     W = torch.randn(3072, 768, device=dev, generator=g).to(torch.bfloat16)
     outs = {}
-    for v in (1, 2):
+    for v in (1, 2, 3, 4):
         C = torch.empty(A.shape[0], 3072, device=dev)
         _native.check(L.mlg_op_gemm_f32out_variant(v, _native.ptr(A), _native.ptr(W), _native.ptr(C), A.shape[0],
                                                    3072, 768, _native.stream_of(dev)), "gemm")
         outs[v] = C
     torch.cuda.synchronize()
-    print(json.dumps({"variants_bit_identical": bool(torch.equal(outs[1], outs[2]))}), flush=True)
+    print(json.dumps({"variants_bit_identical": bool(torch.equal(outs[1], outs[2]) and torch.equal(outs[1], outs[3]) and torch.equal(outs[1], outs[4]))}),
+          flush=True)
+
+    # loop throughput vs fixed per-tile cost: time C = A W^T (f32 out) at K = 768 .. 6144
+    for v in (2, 4):
+        row = {"variant": v, "M": 33920, "N": 3072}
+        for K in (768, 1536, 3072, 6144):
+            A = torch.randn(33920, K, device=dev, generator=g).to(torch.bfloat16)
+            W = torch.randn(3072, K, device=dev, generator=g).to(torch.bfloat16)
+            C = torch.empty(33920, 3072, device=dev)
+            args_ = (v, _native.ptr(A), _native.ptr(W), _native.ptr(C), 33920, 3072, K, _native.stream_of(dev))
+            L.mlg_op_gemm_f32out_variant(*args_)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                L.mlg_op_gemm_f32out_variant(*args_)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 100.0
+            row[f"K{K}_us"] = round(us, 1)
+            row[f"K{K}_tflops"] = round(2 * 33920 * 3072 * K / us / 1e6, 1)
+        print(json.dumps(row), flush=True)
 
     eng = VitB14(synthetic_state_dict(0), device=dev, max_batch=args.batch)
     frames = torch.randint(0, 256, (args.batch, 480, 640, 3), dtype=torch.uint8, device=dev)
