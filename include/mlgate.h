@@ -127,8 +127,11 @@ int mlg_xcorr_score(const float* q, int n1, const float* m, int n2, int D, void*
 /* ----------------------------------------------------------- op-level access --
  * Individual kernels of the ViT path (parity tests against a float32 reference). */
 int mlg_op_gemm_f32out(const uint16_t* A, const uint16_t* W, float* C, int M, int N, int K, void* stream);
-/* GEMM kernel generation: 1 = 128x128 register-staged, 2 = 128x256 3-stage LDS-DMA
- * (default; used when N % 256 == 0 and K / 64 % 3 == 0, else 1). */
+/* GEMM kernel generation (all bit-identical): 1 = 128x128 register-staged;
+ * 2 = 128x256 3-stage LDS-DMA, BK 64 (N % 256 == 0 and K / 64 % 3 == 0);
+ * 3 = the same with BK 32 (K / 32 % 3 == 0); 4 = persistent 256x256 2-stage LDS-DMA,
+ * one workgroup per CU walking XCD-local tiles (default; N % 256 == 0,
+ * K / 64 even).  A shape a variant cannot take falls back 4 -> 2 -> 1. */
 int mlg_set_gemm_variant(int variant);
 int mlg_op_gemm_f32out_variant(int variant, const uint16_t* A, const uint16_t* W, float* C, int M, int N, int K,
                                void* stream);
@@ -141,6 +144,25 @@ int mlg_op_attention(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, u
                      void* stream);
 int mlg_op_preprocess_patches(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, int S,
                               uint16_t* patches, void* stream);
+
+/* ------------------------------------------------- trajectory proximity --
+ * Replaces detect_loop_closure_candidates + apply_floor_gating of the SLAM
+ * integrations (scripts/semantic_gating/orb_slam3_integration.py:167-281,
+ * lego_loam_integration.py:121-204): every pair (i, j), j - i >= min_gap,
+ * ||p_i - p_j|| <= radius (float64, inclusive), for query rows i in
+ * [row0, row0 + nrows), emitted in (i, j) order with the float64 distance and the
+ * SemanticLoopClosureGate verdict (strict: equal floors; non-strict: |diff| <= 1).
+ * pos: device float64 [N, 3]; floor: device int64 [N] or NULL (all accepted).
+ * Two calls share one workspace: mlg_proximity_count writes the device int64
+ * totals[2] = {candidates, accepted}; the caller sizes the outputs from totals[0]
+ * and calls mlg_proximity_emit with the same arguments.  N <= 65536. */
+size_t mlg_proximity_workspace_bytes(int N, int nrows);
+int mlg_proximity_count(const double* pos, const int64_t* floor, int N, int row0, int nrows, double radius,
+                        int min_gap, int strict, void* workspace, size_t workspace_bytes, long long* totals,
+                        void* stream);
+int mlg_proximity_emit(const double* pos, const int64_t* floor, int N, int row0, int nrows, double radius,
+                       int min_gap, int strict, const void* workspace, size_t workspace_bytes, int32_t* pairs,
+                       double* dist, uint8_t* valid, void* stream);
 
 /* ------------------------------------------------------------- profiling --
  * Per-launch HIP-event timing of selected kernels inside mlg_vit_forward, recorded on

@@ -222,6 +222,24 @@ int mlg_similarity(const float* A, int Q, const float* B, int N, int D, float* S
     return mlg_similarity_f32(A, Q, B, N, D, S, N, (hipStream_t)stream);
 }
 
+size_t mlg_proximity_workspace_bytes(int N, int nrows) { return mlg_proximity_ws_bytes(N, nrows); }
+
+int mlg_proximity_count(const double* pos, const int64_t* floor, int N, int row0, int nrows, double radius,
+                        int min_gap, int strict, void* workspace, size_t workspace_bytes, long long* totals,
+                        void* stream) {
+    if ((!pos && N > 0) || !workspace || !totals) return MLG_EINVAL;
+    return mlg_proximity_count_run(pos, floor, N, row0, nrows, radius, min_gap, strict, workspace, workspace_bytes,
+                                   totals, (hipStream_t)stream);
+}
+
+int mlg_proximity_emit(const double* pos, const int64_t* floor, int N, int row0, int nrows, double radius,
+                       int min_gap, int strict, const void* workspace, size_t workspace_bytes, int32_t* pairs,
+                       double* dist, uint8_t* valid, void* stream) {
+    if ((!pos && N > 0) || !workspace || !pairs || !dist || !valid) return MLG_EINVAL;
+    return mlg_proximity_emit_run(pos, floor, N, row0, nrows, radius, min_gap, strict, workspace, workspace_bytes,
+                                  pairs, dist, valid, (hipStream_t)stream);
+}
+
 size_t mlg_xcorr_workspace_bytes(int n1, int n2, int D) {
     if (n1 <= 0 || n2 <= 0 || D <= 0) return 0;
     return align_up((size_t)n1 * D * 4) + align_up((size_t)n2 * D * 4) + align_up((size_t)n1 * n2 * 4);

@@ -486,7 +486,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A
 }  // namespace dma
 
 // 1: 128x128 register-staged; 2: 128x256 DMA BK=64 (3 stages); 3: 128x256 DMA BK=32 (2 WG/CU);
-// 4: 256x256 DMA where N allows (N % 256 == 0 and N >= 2048), else 2.
+// 4: persistent 256x256 DMA where N allows (N % 256 == 0, K / 64 even), else 2.
 int g_variant = 4;
 int g_num_cus = 256;  // multiple of 8 (refreshed from the device on first use)
 
@@ -510,7 +510,7 @@ int launch(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int l
         return MLG_EINVAL;
     if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W)) & 15) return MLG_EINVAL;
     const long nwg_dma = (long)(N / dma::BN) * ((M + dma::BM - 1) / dma::BM);
-    if (variant == 4 && N % 256 == 0 && N >= 2048 && (K / 64) % 2 == 0) {
+    if (variant == 4 && N % 256 == 0 && (K / 64) % 2 == 0) {
         const long ntiles = (long)(N / 256) * ((M + 255) / 256);
         const long grid = std::min<long>(g_num_cus, (ntiles + 7) / 8 * 8);  // persistent: <= 1 per CU
         hipLaunchKernelGGL(dma::k_gemm256<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K, lda, ldw, epi);

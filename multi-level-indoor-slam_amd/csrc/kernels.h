@@ -46,3 +46,12 @@ int mlg_topk_gate(const float* S, int lds, int N, int Q, const double* tq, const
                   int gating, int32_t* idx, float* sim, uint8_t* valid, int32_t* count, unsigned long long* totals,
                   hipStream_t s);
 int mlg_xcorr_reduce(const float* C, int n1, int n2, float* out, hipStream_t s);
+
+// proximity.hip -- trajectory-proximity candidates + floor gate
+bool mlg_proximity_shape_ok(int N, int row0, int nrows);
+size_t mlg_proximity_ws_bytes(int N, int nrows);
+int mlg_proximity_count_run(const double* pos, const int64_t* floor, int N, int row0, int nrows, double radius,
+                            int min_gap, int strict, void* ws, size_t ws_bytes, long long* totals, hipStream_t s);
+int mlg_proximity_emit_run(const double* pos, const int64_t* floor, int N, int row0, int nrows, double radius,
+                           int min_gap, int strict, const void* ws, size_t ws_bytes, int32_t* pairs, double* dist,
+                           uint8_t* valid, hipStream_t s);

@@ -30,6 +30,11 @@ EXPORTS = {
     "mlg_xcorr_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mlg_xcorr_score": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p,
                                 c_void_p]),
+    "mlg_proximity_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "mlg_proximity_count": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_double, c_int, c_int, c_void_p,
+                                    c_size_t, c_void_p, c_void_p]),
+    "mlg_proximity_emit": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_double, c_int, c_int, c_void_p,
+                                   c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mlg_op_gemm_f32out": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_op_gemm_f32out_variant": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_set_gemm_variant": (c_int, [c_int]),
