@@ -164,6 +164,54 @@ int mlg_proximity_emit(const double* pos, const int64_t* floor, int N, int row0,
                        int min_gap, int strict, const void* workspace, size_t workspace_bytes, int32_t* pairs,
                        double* dist, uint8_t* valid, void* stream);
 
+/* -------------------------------------------------------- SuperPoint --
+ * Replaces the extractor half of LightGlue._detect_and_match_native
+ * (scripts/semantic_gating/geometric_verification.py:263-312): cv2 BGR2GRAY / 255 ->
+ * LightGlue's SuperPoint(max_num_keypoints, detection_threshold) forward (NMS radius,
+ * border removal, top-k, bilinear descriptor sampling) for B frames at once.
+ * frames: device uint8 [B] x (H x W x C), C in {1, 3 (BGR), 4}, H and W multiples of 8.
+ * Outputs (device): keypoints f32 [B, max_kp, 2] (x, y), scores f32 [B, max_kp],
+ * descriptors f32 [B, max_kp, 256] (unit L2; zero rows past counts[b]) and optionally
+ * the same in bf16, counts int32 [B].  Keypoint order: raster order when at most
+ * max_kp pass the threshold, else score-descending (raster index ascending on ties). */
+typedef struct mlg_sp_weights {
+    const float* conv1a_w;  /* f32 [64][3][3] */
+    const float* conv1a_b;  /* f32 [64] */
+    const uint16_t* w[11];  /* bf16: conv1b conv2a conv2b conv3a conv3b conv4a conv4b convPa
+                               ([Cout][3][3][Cin]); convPb [128][256] (rows 65..127 zero);
+                               convDa [256][3][3][128]; convDb [256][256] */
+    const float* b[11];     /* f32 [Cout] */
+} mlg_sp_weights;
+size_t mlg_superpoint_workspace_bytes(int B, int H, int W);
+int mlg_superpoint(const mlg_sp_weights* w, const uint8_t* frames, int B, int H, int W, int C, long frame_stride,
+                   float detection_threshold, int max_keypoints, int nms_radius, int remove_borders, void* workspace,
+                   size_t workspace_bytes, float* keypoints, float* scores, float* descriptors,
+                   uint16_t* descriptors_bf16, int32_t* counts, void* stream);
+
+/* ------------------------------------------------------------ RANSAC --
+ * Batched replacement for BaseFeatureMatcher.verify_geometric_consistency and
+ * estimate_relative_pose (scripts/semantic_gating/geometric_verification.py:104-188),
+ * i.e. cv2.findEssentialMat(RANSAC, prob 0.999) / cv2.findFundamentalMat(FM_RANSAC)
+ * and cv2.recoverPose, for P pairs at once.  Pair p owns matches
+ * [offsets[p], offsets[p+1]) of kp1 / kp2 (device float32 [S_total, 2], pixels).
+ * K: device float64 3x3 row-major per pair (k_stride 9) or shared (k_stride 0), or
+ * NULL for the fundamental-matrix path.  `hypotheses` minimal samples per pair
+ * (5-point for E, 7-point for F) are drawn from a counter-based RNG (`seed`),
+ * solved and scored in parallel; the best model has the most inliers (lowest
+ * hypothesis index on ties).  Outputs (device): model float64 [P, 9] (E or F),
+ * mask uint8 [S_total], inliers int32 [P], pose float64 [P, 16] ([R|t; 0 0 0 1],
+ * may be NULL; E path only), status int32 [P]: 0 ok, 1 no model (E: < 5 matches;
+ * F: < 7), 2 model but fewer than 5 inliers (no pose). */
+size_t mlg_ransac_workspace_bytes(int P, long S_total, int hypotheses);
+int mlg_ransac_epipolar(const float* kp1, const float* kp2, const int32_t* offsets, int P, long S_total,
+                        const double* K, int k_stride, double threshold, int hypotheses, uint64_t seed,
+                        void* workspace, size_t workspace_bytes, double* model, uint8_t* mask, int32_t* inliers,
+                        double* pose, int32_t* status, void* stream);
+/* cv2.recoverPose(E, k1[mask], k2[mask], K) for P pairs given E [P, 9] and mask
+ * (geometric_verification.py:155-188): pose [P, 16]; zeros when < 5 inliers. */
+int mlg_recover_pose(const float* kp1, const float* kp2, const int32_t* offsets, int P, const double* K,
+                     int k_stride, const double* E, const uint8_t* mask, double* pose, void* stream);
+
 /* ------------------------------------------------------------- profiling --
  * Per-launch HIP-event timing of selected kernels inside mlg_vit_forward, recorded on
  * the stream the kernel is launched on.  slot: 0 fc1 GEMM, 1 fc2 GEMM, 2 qkv GEMM,

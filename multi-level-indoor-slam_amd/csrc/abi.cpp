@@ -240,6 +240,52 @@ int mlg_proximity_emit(const double* pos, const int64_t* floor, int N, int row0,
                                   pairs, dist, valid, (hipStream_t)stream);
 }
 
+size_t mlg_superpoint_workspace_bytes(int B, int H, int W) { return mlg_superpoint_ws_bytes(B, H, W); }
+
+int mlg_superpoint(const mlg_sp_weights* w, const uint8_t* frames, int B, int H, int W, int C, long frame_stride,
+                   float detection_threshold, int max_keypoints, int nms_radius, int remove_borders, void* workspace,
+                   size_t workspace_bytes, float* keypoints, float* scores, float* descriptors,
+                   uint16_t* descriptors_bf16, int32_t* counts, void* stream) {
+    if (!w || !frames || !workspace || !keypoints || !scores || !descriptors || !counts) return MLG_EINVAL;
+    if (!w->conv1a_w || !w->conv1a_b) return MLG_EINVAL;
+    mlg_sp_weights_i wi;
+    wi.conv1a_w = w->conv1a_w;
+    wi.conv1a_b = w->conv1a_b;
+    for (int i = 0; i < 11; ++i) {
+        if (!w->w[i] || !w->b[i]) return MLG_EINVAL;
+        if ((reinterpret_cast<uintptr_t>(w->w[i]) & 15) || (reinterpret_cast<uintptr_t>(w->b[i]) & 15))
+            return MLG_EINVAL;
+        wi.w[i] = (const bf16_t*)w->w[i];
+        wi.b[i] = w->b[i];
+    }
+    if (frame_stride < (long)H * W * C) return MLG_EINVAL;
+    return mlg_superpoint_run(wi, frames, B, H, W, C, frame_stride, detection_threshold, max_keypoints, nms_radius,
+                              remove_borders, workspace, workspace_bytes, keypoints, scores, descriptors,
+                              descriptors_bf16, counts, (hipStream_t)stream);
+}
+
+size_t mlg_ransac_workspace_bytes(int P, long S_total, int hypotheses) {
+    return mlg_ransac_ws_bytes(P, S_total, hypotheses);
+}
+
+int mlg_ransac_epipolar(const float* kp1, const float* kp2, const int32_t* offsets, int P, long S_total,
+                        const double* K, int k_stride, double threshold, int hypotheses, uint64_t seed,
+                        void* workspace, size_t workspace_bytes, double* model, uint8_t* mask, int32_t* inliers,
+                        double* pose, int32_t* status, void* stream) {
+    if (!offsets || !workspace || !model || !inliers || !status || (S_total > 0 && (!kp1 || !kp2 || !mask)))
+        return MLG_EINVAL;
+    if (K && k_stride != 0 && k_stride != 9) return MLG_EINVAL;
+    return mlg_ransac_run(kp1, kp2, offsets, P, S_total, K, k_stride, threshold, hypotheses, seed, workspace,
+                          workspace_bytes, model, mask, inliers, pose, status, (hipStream_t)stream);
+}
+
+int mlg_recover_pose(const float* kp1, const float* kp2, const int32_t* offsets, int P, const double* K,
+                     int k_stride, const double* E, const uint8_t* mask, double* pose, void* stream) {
+    if (!kp1 || !kp2 || !offsets || !K || !E || !mask || !pose) return MLG_EINVAL;
+    if (k_stride != 0 && k_stride != 9) return MLG_EINVAL;
+    return mlg_recover_pose_run(kp1, kp2, offsets, P, K, k_stride, E, mask, pose, (hipStream_t)stream);
+}
+
 size_t mlg_xcorr_workspace_bytes(int n1, int n2, int D) {
     if (n1 <= 0 || n2 <= 0 || D <= 0) return 0;
     return align_up((size_t)n1 * D * 4) + align_up((size_t)n2 * D * 4) + align_up((size_t)n1 * n2 * 4);

@@ -55,3 +55,23 @@ int mlg_proximity_count_run(const double* pos, const int64_t* floor, int N, int 
 int mlg_proximity_emit_run(const double* pos, const int64_t* floor, int N, int row0, int nrows, double radius,
                            int min_gap, int strict, const void* ws, size_t ws_bytes, int32_t* pairs, double* dist,
                            uint8_t* valid, hipStream_t s);
+
+// ransac.hip -- batched epipolar RANSAC + recoverPose
+size_t mlg_ransac_ws_bytes(int P, long S_total, int H);
+int mlg_ransac_run(const float* kp1, const float* kp2, const int32_t* offs, int P, long S_total, const double* K,
+                   int k_stride, double thr, int H, uint64_t seed, void* ws, size_t ws_bytes, double* model_out,
+                   uint8_t* mask, int32_t* inliers, double* pose, int32_t* status, hipStream_t s);
+int mlg_recover_pose_run(const float* kp1, const float* kp2, const int32_t* offs, int P, const double* K,
+                         int k_stride, const double* E, const uint8_t* mask, double* pose, hipStream_t s);
+
+// superpoint.hip -- SuperPoint detector / descriptor
+struct mlg_sp_weights_i {
+    const float* conv1a_w;  // f32 [64][9]
+    const float* conv1a_b;  // f32 [64]
+    const bf16_t* w[11];    // conv1b conv2a conv2b conv3a conv3b conv4a conv4b convPa convPb convDa convDb
+    const float* b[11];
+};
+size_t mlg_superpoint_ws_bytes(int B, int H, int W);
+int mlg_superpoint_run(const mlg_sp_weights_i& w, const uint8_t* frames, int B, int H, int W, int C, long frame_stride,
+                       float det_thr, int max_kp, int nms_radius, int border, void* ws, size_t ws_bytes, float* kpts,
+                       float* kscores, float* desc, uint16_t* desc_bf16, int32_t* count, hipStream_t s);

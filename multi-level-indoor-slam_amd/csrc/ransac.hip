@@ -1,0 +1,1054 @@
+// Batched epipolar RANSAC + relative pose for geometric verification.
+//
+// Replaces, for a batch of candidate pairs at once, the OpenCV calls of
+// BaseFeatureMatcher.verify_geometric_consistency / estimate_relative_pose
+// (geometric_verification.py:104-188):
+//   K given : cv2.findEssentialMat(k1, k2, K, RANSAC, prob 0.999, threshold) -- points
+//             normalised by K, threshold / ((fx + fy) / 2), 5-point minimal solver,
+//             Sampson error, inlier iff (float)err <= (float)thr^2; then
+//             cv2.recoverPose(E, k1[in], k2[in], K) (4-fold decomposition, cheirality
+//             with depth < 50, ties in the order (R1,t), (R2,t), (R1,-t), (R2,-t)).
+//   K absent: cv2.findFundamentalMat(k1, k2, FM_RANSAC, threshold, 0.999) -- 7-point
+//             solver, error max(d1^2, d2^2) of the two point-to-epiline distances in
+//             pixels; 7 points: the 7-point model directly; 8..14 points: LMedS (as
+//             OpenCV does below 15 points); fewer than 7: no model.
+// OpenCV draws hypotheses adaptively from its own RNG; here a fixed budget of H
+// hypotheses per pair (counter-based RNG, seeded) is solved and scored in parallel
+// and the best model is the one with the most inliers (lowest hypothesis index on
+// ties), so results are deterministic.  Parity is on decisions.
+//
+// Pipeline (one pair = one segment of the flat match arrays):
+//   k_ransac_prep   : normalised double coordinates (+ Hartley transforms for F)
+//   k_ransac_hyp    : one thread per hypothesis: sample, solve (<= 10 models)
+//   k_ransac_score  : one thread per hypothesis: inlier count (or LMedS median) of
+//                     each model over the pair's points, staged in LDS
+//   k_ransac_select : one workgroup per pair: best model, inlier mask
+//   k_recover_pose  : one workgroup per pair: E -> [R|t] by cheirality on the inliers
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+#define RS_HD __host__ __device__  // solvers also build for host-side unit checks
+
+constexpr int MAXSOL = 10;
+constexpr int RS_CHUNK = 1024;  // points per LDS stage in scoring (4 doubles each = 32 KB)
+
+// ------------------------------------------------------------------ small linear algebra
+
+// Null space of an m x 9 matrix (m = 5 or 7) by Gauss-Jordan elimination with partial
+// pivoting; writes 9 - m basis vectors (rank-deficient samples return false).
+template <int MR>
+RS_HD bool null_space9(double (&A)[MR][9], double (&N)[9 - MR][9]) {
+    int piv_col[MR];
+    int r = 0;
+    for (int c = 0; c < 9 && r < MR; ++c) {
+        int best = r;
+        double bv = fabs(A[r][c]);
+        for (int i = r + 1; i < MR; ++i)
+            if (fabs(A[i][c]) > bv) { bv = fabs(A[i][c]); best = i; }
+        if (bv < 1e-12) continue;
+        if (best != r)
+            for (int j = 0; j < 9; ++j) { double t = A[r][j]; A[r][j] = A[best][j]; A[best][j] = t; }
+        const double inv = 1.0 / A[r][c];
+        for (int j = 0; j < 9; ++j) A[r][j] *= inv;
+        for (int i = 0; i < MR; ++i)
+            if (i != r) {
+                const double f = A[i][c];
+                if (f != 0.0)
+                    for (int j = 0; j < 9; ++j) A[i][j] -= f * A[r][j];
+            }
+        piv_col[r++] = c;
+    }
+    if (r < MR) return false;
+    bool is_piv[9] = {false, false, false, false, false, false, false, false, false};
+    for (int i = 0; i < MR; ++i) is_piv[piv_col[i]] = true;
+    int k = 0;
+    for (int f = 0; f < 9; ++f) {
+        if (is_piv[f]) continue;
+        for (int j = 0; j < 9; ++j) N[k][j] = 0.0;
+        N[k][f] = 1.0;
+        for (int i = 0; i < MR; ++i) N[k][piv_col[i]] = -A[i][f];
+        ++k;
+    }
+    // orthonormalise (modified Gram-Schmidt, two passes): keeps the hidden-variable
+    // polynomial well conditioned (coefficients O(1), roots of moderate size)
+    for (int pass = 0; pass < 2; ++pass)
+        for (int a = 0; a < 9 - MR; ++a) {
+            for (int q = 0; q < a; ++q) {
+                double d = 0.0;
+                for (int j = 0; j < 9; ++j) d += N[a][j] * N[q][j];
+                for (int j = 0; j < 9; ++j) N[a][j] -= d * N[q][j];
+            }
+            double n2 = 0.0;
+            for (int j = 0; j < 9; ++j) n2 += N[a][j] * N[a][j];
+            n2 = 1.0 / sqrt(n2);
+            for (int j = 0; j < 9; ++j) N[a][j] *= n2;
+        }
+    return true;
+}
+
+RS_HD double det3(const double* F) {
+    return F[0] * (F[4] * F[8] - F[5] * F[7]) - F[1] * (F[3] * F[8] - F[5] * F[6]) +
+           F[2] * (F[3] * F[7] - F[4] * F[6]);
+}
+
+// Real roots of sum_i c[i] x^i (degree <= 10) by recursive isolation between the
+// roots of the derivative, refined by safeguarded bisection / regula falsi.
+RS_HD double peval(const double* c, int n, double x) {
+    double v = c[n];
+    for (int i = n - 1; i >= 0; --i) v = v * x + c[i];
+    return v;
+}
+
+RS_HD double refine_root(const double* c, int n, double lo, double hi, double flo) {
+    double fl = flo, fh = peval(c, n, hi);
+    int side = 0;
+    for (int it = 0; it < 100; ++it) {
+        double x = (lo * fh - hi * fl) / (fh - fl);
+        if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
+        const double fx = peval(c, n, x);
+        if (fx == 0.0) return x;
+        if ((fx < 0) == (fl < 0)) {
+            lo = x; fl = fx;
+            if (side == -1) fh *= 0.5;
+            side = -1;
+        } else {
+            hi = x; fh = fx;
+            if (side == 1) fl *= 0.5;
+            side = 1;
+        }
+        if (hi - lo <= 1e-14 * fmax(1.0, fabs(lo))) break;
+    }
+    return 0.5 * (lo + hi);
+}
+
+RS_HD int real_roots(const double* cin, int deg, double* roots) {
+    double c[11];
+    int n = deg;
+    double mx = 0.0;
+    for (int i = 0; i <= deg; ++i) { c[i] = cin[i]; mx = fmax(mx, fabs(c[i])); }
+    if (mx == 0.0) return 0;
+    while (n > 0 && fabs(c[n]) <= 1e-13 * mx) --n;
+    if (n == 0) return 0;
+    for (int i = 0; i <= n; ++i) c[i] /= c[n];
+    double B = 0.0;
+    for (int i = 0; i < n; ++i) B = fmax(B, fabs(c[i]));
+    B += 1.0;
+    // derivative chain d[k] = c^(k) / k!-scaled (monic not needed)
+    double d[11][11];
+    for (int i = 0; i <= n; ++i) d[0][i] = c[i];
+    for (int k = 1; k < n; ++k)
+        for (int i = 0; i <= n - k; ++i) d[k][i] = d[k - 1][i + 1] * (double)(i + 1);
+    double crit[11];
+    int ncrit = 0;
+    // linear d[n-1]: root
+    crit[0] = -d[n - 1][0] / d[n - 1][1];
+    ncrit = 1;
+    for (int k = n - 2; k >= 0; --k) {
+        const int dg = n - k;
+        double pts[12];
+        int np = 0;
+        pts[np++] = -B;
+        for (int i = 0; i < ncrit; ++i)
+            if (crit[i] > -B && crit[i] < B) pts[np++] = crit[i];
+        pts[np++] = B;
+        double nr[11];
+        int nn = 0;
+        double fprev = peval(d[k], dg, pts[0]);
+        for (int i = 1; i < np; ++i) {
+            const double f = peval(d[k], dg, pts[i]);
+            if (fprev == 0.0) {
+                if (nn == 0 || nr[nn - 1] != pts[i - 1]) nr[nn++] = pts[i - 1];
+            } else if ((fprev < 0) != (f < 0) && f != 0.0) {
+                nr[nn++] = refine_root(d[k], dg, pts[i - 1], pts[i], fprev);
+            }
+            fprev = f;
+        }
+        if (fprev == 0.0 && (nn == 0 || nr[nn - 1] != pts[np - 1])) nr[nn++] = pts[np - 1];
+        ncrit = nn;
+        for (int i = 0; i < nn; ++i) crit[i] = nr[i];
+    }
+    for (int i = 0; i < ncrit; ++i) roots[i] = crit[i];
+    return ncrit;
+}
+
+// ------------------------------------------------------------------ 5-point solver
+// E = x X + y Y + z Z + W over the 4-dim null space; the 10 cubic constraints
+// det(E) = 0 and 2 E E^T E - tr(E E^T) E = 0 in monomials x^a y^b z^c (a+b+c <= 3).
+// Hidden variable z (Li & Hartley): C(z) m = 0 with m = [x^3 x^2y xy^2 y^3 x^2 xy y^2 x y 1];
+// det C(z) is a degree-10 polynomial, recovered exactly from its values at the 11th
+// roots of unity; each real root gives m from the null vector of C(z).
+
+// monomial index for exponents (a, b, c), a+b+c <= 3: 20 slots
+RS_HD __forceinline__ int midx(int a, int b, int c) { return (a * 4 + b) * 4 + c; }  // sparse 64-slot map
+
+struct P1 { double v[4]; };    // coefficients of x, y, z, 1
+struct P3 { double v[64]; };   // sparse map over (a, b, c) with a, b, c < 4
+
+RS_HD void p1_mul_p1(const P1& a, const P1& b, double (&out)[64]) {
+    const int ex[4][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}};
+    for (int i = 0; i < 64; ++i) out[i] = 0.0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            out[midx(ex[i][0] + ex[j][0], ex[i][1] + ex[j][1], ex[i][2] + ex[j][2])] += a.v[i] * b.v[j];
+}
+
+RS_HD void p2_mul_p1(const double (&a)[64], const P1& b, double (&out)[64]) {
+    const int ex[4][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}};
+    for (int i = 0; i < 64; ++i) out[i] = 0.0;
+    for (int aa = 0; aa < 3; ++aa)
+        for (int bb = 0; bb + aa < 3; ++bb)
+            for (int cc = 0; cc + aa + bb < 3; ++cc) {
+                const double s = a[midx(aa, bb, cc)];
+                if (s == 0.0) continue;
+                for (int j = 0; j < 4; ++j)
+                    out[midx(aa + ex[j][0], bb + ex[j][1], cc + ex[j][2])] += s * b.v[j];
+            }
+}
+
+struct Cplx { double re, im; };
+RS_HD __forceinline__ Cplx cmul(Cplx a, Cplx b) { return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+RS_HD __forceinline__ Cplx csub(Cplx a, Cplx b) { return {a.re - b.re, a.im - b.im}; }
+RS_HD __forceinline__ double cabs2(Cplx a) { return a.re * a.re + a.im * a.im; }
+RS_HD __forceinline__ Cplx cdiv(Cplx a, Cplx b) {
+    const double d = cabs2(b);
+    return {(a.re * b.re + a.im * b.im) / d, (a.im * b.re - a.re * b.im) / d};
+}
+
+
+RS_HD int solve_5pt(const double (&q1)[5][2], const double (&q2)[5][2], double* Eout) {
+    // x,y monomial columns of C(z): (a, b) exponents
+    const int kXY[10][2] = {{3, 0}, {2, 1}, {1, 2}, {0, 3}, {2, 0}, {1, 1}, {0, 2}, {1, 0}, {0, 1}, {0, 0}};
+    double A[5][9];
+    for (int i = 0; i < 5; ++i) {
+        const double x1 = q1[i][0], y1 = q1[i][1], x2 = q2[i][0], y2 = q2[i][1];
+        // q2^T E q1 = 0, E row-major
+        A[i][0] = x2 * x1; A[i][1] = x2 * y1; A[i][2] = x2;
+        A[i][3] = y2 * x1; A[i][4] = y2 * y1; A[i][5] = y2;
+        A[i][6] = x1;      A[i][7] = y1;      A[i][8] = 1.0;
+    }
+    double Nb[4][9];
+    if (!null_space9<5>(A, Nb)) return 0;
+    P1 E[9];
+    for (int k = 0; k < 9; ++k) E[k] = P1{{Nb[0][k], Nb[1][k], Nb[2][k], Nb[3][k]}};
+    // equations as sparse 64-slot polynomials
+    double eq[10][64];
+    {
+        // det(E) = E0 (E4 E8 - E5 E7) - E1 (E3 E8 - E5 E6) + E2 (E3 E7 - E4 E6)
+        double t1[64], t2[64], m[64];
+        for (int i = 0; i < 64; ++i) eq[0][i] = 0.0;
+        const int cof[3][5] = {{0, 4, 8, 5, 7}, {1, 3, 8, 5, 6}, {2, 3, 7, 4, 6}};
+        const double sg[3] = {1.0, -1.0, 1.0};
+        for (int r = 0; r < 3; ++r) {
+            p1_mul_p1(E[cof[r][1]], E[cof[r][2]], t1);
+            p1_mul_p1(E[cof[r][3]], E[cof[r][4]], t2);
+            for (int i = 0; i < 64; ++i) t1[i] -= t2[i];
+            p2_mul_p1(t1, E[cof[r][0]], m);
+            for (int i = 0; i < 64; ++i) eq[0][i] += sg[r] * m[i];
+        }
+    }
+    {
+        // EEt[i][j] = sum_k E[i][k] E[j][k]  (quadratics)
+        double EEt[3][3][64];
+        double t[64];
+        for (int i = 0; i < 3; ++i)
+            for (int j = i; j < 3; ++j) {
+                for (int s = 0; s < 64; ++s) EEt[i][j][s] = 0.0;
+                for (int k = 0; k < 3; ++k) {
+                    p1_mul_p1(E[i * 3 + k], E[j * 3 + k], t);
+                    for (int s = 0; s < 64; ++s) EEt[i][j][s] += t[s];
+                }
+                if (j != i)
+                    for (int s = 0; s < 64; ++s) EEt[j][i][s] = EEt[i][j][s];
+            }
+        double tr[64];
+        for (int s = 0; s < 64; ++s) tr[s] = 0.5 * (EEt[0][0][s] + EEt[1][1][s] + EEt[2][2][s]);
+        // (E E^T - 1/2 tr) E  -> 9 cubics
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                double* o = eq[1 + i * 3 + j];
+                for (int s = 0; s < 64; ++s) o[s] = 0.0;
+                double m[64];
+                for (int k = 0; k < 3; ++k) {
+                    double a[64];
+                    for (int s = 0; s < 64; ++s) a[s] = EEt[i][k][s] - (i == k ? tr[s] : 0.0);
+                    p2_mul_p1(a, E[k * 3 + j], m);
+                    for (int s = 0; s < 64; ++s) o[s] += m[s];
+                }
+            }
+    }
+    // coefficient of z^c in column (a, b) of row r
+    // det C(z) at the 11th roots of unity
+    Cplx dv[11];
+    for (int k = 0; k < 11; ++k) {
+        const double ang = 2.0 * M_PI * k / 11.0;
+        const Cplx w{cos(ang), sin(ang)};
+        Cplx zp[4] = {{1.0, 0.0}, w, cmul(w, w), cmul(cmul(w, w), w)};
+        Cplx C[10][10];
+        for (int r = 0; r < 10; ++r)
+            for (int col = 0; col < 10; ++col) {
+                const int a = kXY[col][0], b = kXY[col][1];
+                Cplx s{0.0, 0.0};
+                for (int c = 0; a + b + c <= 3; ++c) {
+                    const double co = eq[r][midx(a, b, c)];
+                    s.re += co * zp[c].re;
+                    s.im += co * zp[c].im;
+                }
+                C[r][col] = s;
+            }
+        Cplx det{1.0, 0.0};
+        for (int c = 0; c < 10; ++c) {
+            int p = c;
+            double bv = cabs2(C[c][c]);
+            for (int r = c + 1; r < 10; ++r)
+                if (cabs2(C[r][c]) > bv) { bv = cabs2(C[r][c]); p = r; }
+            if (bv == 0.0) { det = {0.0, 0.0}; break; }
+            if (p != c) {
+                for (int j = 0; j < 10; ++j) { Cplx t = C[c][j]; C[c][j] = C[p][j]; C[p][j] = t; }
+                det = {-det.re, -det.im};
+            }
+            det = cmul(det, C[c][c]);
+            for (int r = c + 1; r < 10; ++r) {
+                const Cplx f = cdiv(C[r][c], C[c][c]);
+                for (int j = c; j < 10; ++j) C[r][j] = csub(C[r][j], cmul(f, C[c][j]));
+            }
+        }
+        dv[k] = det;
+    }
+    double poly[11];
+    for (int j = 0; j <= 10; ++j) {
+        double s = 0.0;
+        for (int k = 0; k < 11; ++k) {
+            const double ang = -2.0 * M_PI * ((j * k) % 11) / 11.0;
+            s += dv[k].re * cos(ang) - dv[k].im * sin(ang);
+        }
+        poly[j] = s / 11.0;
+    }
+    double zr[10];
+    const int nz = real_roots(poly, 10, zr);
+    int nsol = 0;
+    for (int t = 0; t < nz && nsol < MAXSOL; ++t) {
+        const double z = zr[t];
+        double C[10][10];
+        for (int r = 0; r < 10; ++r)
+            for (int col = 0; col < 10; ++col) {
+                const int a = kXY[col][0], b = kXY[col][1];
+                double s = 0.0, zp = 1.0;
+                for (int c = 0; a + b + c <= 3; ++c) { s += eq[r][midx(a, b, c)] * zp; zp *= z; }
+                C[r][col] = s;
+            }
+        // null vector of C: Gaussian elimination with full pivoting, smallest pivot last
+        int colp[10];
+        for (int i = 0; i < 10; ++i) colp[i] = i;
+        for (int c = 0; c < 9; ++c) {
+            int pr = c, pc = c;
+            double bv = 0.0;
+            for (int r = c; r < 10; ++r)
+                for (int q = c; q < 10; ++q)
+                    if (fabs(C[r][q]) > bv) { bv = fabs(C[r][q]); pr = r; pc = q; }
+            if (bv == 0.0) break;
+            if (pr != c)
+                for (int j = 0; j < 10; ++j) { double tt = C[c][j]; C[c][j] = C[pr][j]; C[pr][j] = tt; }
+            if (pc != c) {
+                for (int r = 0; r < 10; ++r) { double tt = C[r][c]; C[r][c] = C[r][pc]; C[r][pc] = tt; }
+                int ti = colp[c]; colp[c] = colp[pc]; colp[pc] = ti;
+            }
+            for (int r = c + 1; r < 10; ++r) {
+                const double f = C[r][c] / C[c][c];
+                for (int j = c; j < 10; ++j) C[r][j] -= f * C[c][j];
+            }
+        }
+        double v[10];
+        v[9] = 1.0;
+        for (int r = 8; r >= 0; --r) {
+            double s = C[r][9] * v[9];
+            for (int j = r + 1; j < 9; ++j) s += C[r][j] * v[j];
+            v[r] = -s / C[r][r];
+        }
+        double m[10];
+        for (int i = 0; i < 10; ++i) m[colp[i]] = v[i];
+        if (fabs(m[9]) < 1e-300) continue;
+        const double x = m[7] / m[9], y = m[8] / m[9];
+        if (!(fabs(x) < 1e300) || !(fabs(y) < 1e300)) continue;  // also rejects NaN
+        double* Eo = Eout + nsol * 9;
+        double nrm = 0.0;
+        for (int k = 0; k < 9; ++k) {
+            Eo[k] = x * Nb[0][k] + y * Nb[1][k] + z * Nb[2][k] + Nb[3][k];
+            nrm += Eo[k] * Eo[k];
+        }
+        nrm = 1.0 / sqrt(nrm);
+        for (int k = 0; k < 9; ++k) Eo[k] *= nrm;
+        ++nsol;
+    }
+    return nsol;
+}
+
+// ------------------------------------------------------------------ 7-point solver
+RS_HD int solve_7pt(const double (&q1)[7][2], const double (&q2)[7][2], double* Fout) {
+    double A[7][9];
+    for (int i = 0; i < 7; ++i) {
+        const double x1 = q1[i][0], y1 = q1[i][1], x2 = q2[i][0], y2 = q2[i][1];
+        A[i][0] = x2 * x1; A[i][1] = x2 * y1; A[i][2] = x2;
+        A[i][3] = y2 * x1; A[i][4] = y2 * y1; A[i][5] = y2;
+        A[i][6] = x1;      A[i][7] = y1;      A[i][8] = 1.0;
+    }
+    double Nb[2][9];
+    if (!null_space9<7>(A, Nb)) return 0;
+    // det(a F1 + (1 - a) F2) = cubic in a, interpolated at a = -1, 0, 1, 2
+    double f[4];
+    const double as[4] = {-1.0, 0.0, 1.0, 2.0};
+    for (int i = 0; i < 4; ++i) {
+        double F[9];
+        for (int k = 0; k < 9; ++k) F[k] = as[i] * Nb[0][k] + (1.0 - as[i]) * Nb[1][k];
+        f[i] = det3(F);
+    }
+    // Newton divided differences -> monomial coefficients
+    const double d1 = f[1] - f[0], d2 = f[2] - f[1], d3 = f[3] - f[2];
+    const double e1 = (d2 - d1) / 2.0, e2 = (d3 - d2) / 2.0;
+    const double g = (e2 - e1) / 3.0;
+    // p(a) = f0 + d1 (a+1) + e1 (a+1) a + g (a+1) a (a-1)
+    double c[4];
+    c[3] = g;
+    c[2] = e1;
+    c[1] = d1 + e1 - g;
+    c[0] = f[0] + d1;
+    double roots[3];
+    const int nr = real_roots(c, 3, roots);
+    int ns = 0;
+    for (int t = 0; t < nr; ++t) {
+        double* F = Fout + ns * 9;
+        double nrm = 0.0;
+        for (int k = 0; k < 9; ++k) {
+            F[k] = roots[t] * Nb[0][k] + (1.0 - roots[t]) * Nb[1][k];
+            nrm += F[k] * F[k];
+        }
+        if (!(nrm > 0.0)) continue;
+        nrm = 1.0 / sqrt(nrm);
+        for (int k = 0; k < 9; ++k) F[k] *= nrm;
+        ++ns;
+    }
+    return ns;
+}
+
+// ------------------------------------------------------------------ errors
+// Sampson error of E on normalised points (OpenCV EMEstimatorCallback::computeError).
+RS_HD __forceinline__ float err_sampson(const double* E, double x1, double y1, double x2, double y2) {
+    const double ex0 = E[0] * x1 + E[1] * y1 + E[2];
+    const double ex1 = E[3] * x1 + E[4] * y1 + E[5];
+    const double ex2 = E[6] * x1 + E[7] * y1 + E[8];
+    const double et0 = E[0] * x2 + E[3] * y2 + E[6];
+    const double et1 = E[1] * x2 + E[4] * y2 + E[7];
+    const double r = x2 * ex0 + y2 * ex1 + ex2;
+    return (float)(r * r / (ex0 * ex0 + ex1 * ex1 + et0 * et0 + et1 * et1));
+}
+
+// max of the squared point-to-epiline distances in pixels (FMEstimatorCallback).
+RS_HD __forceinline__ float err_epiline(const double* F, double x1, double y1, double x2, double y2) {
+    double a = F[0] * x1 + F[1] * y1 + F[2];
+    double b = F[3] * x1 + F[4] * y1 + F[5];
+    double c = F[6] * x1 + F[7] * y1 + F[8];
+    const double s2 = 1.0 / (a * a + b * b);
+    const double d2 = x2 * a + y2 * b + c;
+    a = F[0] * x2 + F[3] * y2 + F[6];
+    b = F[1] * x2 + F[4] * y2 + F[7];
+    c = F[2] * x2 + F[5] * y2 + F[8];
+    const double s1 = 1.0 / (a * a + b * b);
+    const double d1 = x1 * a + y1 * b + c;
+    return (float)fmax(d1 * d1 * s1, d2 * d2 * s2);
+}
+
+RS_HD __forceinline__ uint64_t splitmix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// per-pair parameters in workspace
+struct PairInfo {
+    int start, count, mode;  // mode: 0 none, 1 E RANSAC, 2 F RANSAC, 3 F LMedS, 4 F direct (7 pts), 5 E direct (5 pts)
+    int pad;
+    double thr2;          // squared threshold in the error's units
+    double T1[3], T2[3];  // F: Hartley transforms (s, tx, ty): x' = s x + tx
+    double Kn[4];         // E: fx, fy, cx, cy
+};
+
+// pts layout per match: [x1n, y1n, x2n, y2n] (E: K-normalised, F: Hartley-normalised);
+// raw pixel copy for F scoring: [x1, y1, x2, y2]
+__global__ void k_ransac_prep(const float* __restrict__ kp1, const float* __restrict__ kp2,
+                              const int32_t* __restrict__ offs, const double* __restrict__ K, int k_stride, double thr,
+                              PairInfo* __restrict__ info, double4* __restrict__ ptsn, double4* __restrict__ ptsr) {
+    const int p = blockIdx.x;
+    const int s0 = offs[p], S = offs[p + 1] - offs[p];
+    __shared__ double red[4][256];
+    PairInfo pi;
+    pi.start = s0;
+    pi.count = S;
+    pi.pad = 0;
+    const bool ess = K != nullptr;
+    if (ess) {
+        const double* Kp = K + (size_t)p * k_stride;
+        const double fx = Kp[0], fy = Kp[4], cx = Kp[2], cy = Kp[5];
+        pi.Kn[0] = fx; pi.Kn[1] = fy; pi.Kn[2] = cx; pi.Kn[3] = cy;
+        const double t = thr / ((fx + fy) * 0.5);
+        pi.thr2 = t * t;
+        pi.mode = S < 5 ? 0 : (S == 5 ? 5 : 1);
+        for (int i = threadIdx.x; i < S; i += blockDim.x) {
+            const double x1 = kp1[2 * (s0 + i)], y1 = kp1[2 * (s0 + i) + 1];
+            const double x2 = kp2[2 * (s0 + i)], y2 = kp2[2 * (s0 + i) + 1];
+            ptsn[s0 + i] = make_double4((x1 - cx) / fx, (y1 - cy) / fy, (x2 - cx) / fx, (y2 - cy) / fy);
+        }
+        for (int j = 0; j < 3; ++j) { pi.T1[j] = 0.0; pi.T2[j] = 0.0; }
+    } else {
+        pi.thr2 = thr * thr;
+        pi.mode = S < 7 ? 0 : (S == 7 ? 4 : (S < 15 ? 3 : 2));
+        for (int j = 0; j < 4; ++j) pi.Kn[j] = 0.0;
+        // Hartley normalisation: centroid + mean distance sqrt(2)
+        double s[4] = {0, 0, 0, 0};
+        for (int i = threadIdx.x; i < S; i += blockDim.x) {
+            s[0] += kp1[2 * (s0 + i)]; s[1] += kp1[2 * (s0 + i) + 1];
+            s[2] += kp2[2 * (s0 + i)]; s[3] += kp2[2 * (s0 + i) + 1];
+        }
+        for (int j = 0; j < 4; ++j) red[j][threadIdx.x] = s[j];
+        __syncthreads();
+        for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o)
+                for (int j = 0; j < 4; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + o];
+            __syncthreads();
+        }
+        const double inv = S > 0 ? 1.0 / S : 0.0;
+        const double m1x = red[0][0] * inv, m1y = red[1][0] * inv, m2x = red[2][0] * inv, m2y = red[3][0] * inv;
+        __syncthreads();
+        double d[2] = {0, 0};
+        for (int i = threadIdx.x; i < S; i += blockDim.x) {
+            d[0] += hypot(kp1[2 * (s0 + i)] - m1x, kp1[2 * (s0 + i) + 1] - m1y);
+            d[1] += hypot(kp2[2 * (s0 + i)] - m2x, kp2[2 * (s0 + i) + 1] - m2y);
+        }
+        red[0][threadIdx.x] = d[0];
+        red[1][threadIdx.x] = d[1];
+        __syncthreads();
+        for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) {
+                red[0][threadIdx.x] += red[0][threadIdx.x + o];
+                red[1][threadIdx.x] += red[1][threadIdx.x + o];
+            }
+            __syncthreads();
+        }
+        const double md1 = red[0][0] * inv, md2 = red[1][0] * inv;
+        const double sc1 = md1 > 0 ? M_SQRT2 / md1 : 1.0, sc2 = md2 > 0 ? M_SQRT2 / md2 : 1.0;
+        pi.T1[0] = sc1; pi.T1[1] = -sc1 * m1x; pi.T1[2] = -sc1 * m1y;
+        pi.T2[0] = sc2; pi.T2[1] = -sc2 * m2x; pi.T2[2] = -sc2 * m2y;
+        for (int i = threadIdx.x; i < S; i += blockDim.x) {
+            const double x1 = kp1[2 * (s0 + i)], y1 = kp1[2 * (s0 + i) + 1];
+            const double x2 = kp2[2 * (s0 + i)], y2 = kp2[2 * (s0 + i) + 1];
+            ptsn[s0 + i] = make_double4(sc1 * x1 + pi.T1[1], sc1 * y1 + pi.T1[2], sc2 * x2 + pi.T2[1],
+                                        sc2 * y2 + pi.T2[2]);
+            ptsr[s0 + i] = make_double4(x1, y1, x2, y2);
+        }
+    }
+    if (threadIdx.x == 0) info[p] = pi;
+}
+
+// F in pixel space from the normalised-space solution: F = T2^T Fn T1
+RS_HD void denorm_F(const double* Fn, const double* T1, const double* T2, double* F) {
+    const double A[9] = {T1[0], 0, T1[1], 0, T1[0], T1[2], 0, 0, 1};
+    const double B[9] = {T2[0], 0, T2[1], 0, T2[0], T2[2], 0, 0, 1};
+    double t[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) t[i * 3 + j] = Fn[i * 3 + 0] * A[0 * 3 + j] + Fn[i * 3 + 1] * A[1 * 3 + j] + Fn[i * 3 + 2] * A[2 * 3 + j];
+    double nrm = 0.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            F[i * 3 + j] = B[0 * 3 + i] * t[0 * 3 + j] + B[1 * 3 + i] * t[1 * 3 + j] + B[2 * 3 + i] * t[2 * 3 + j];
+            nrm += F[i * 3 + j] * F[i * 3 + j];
+        }
+    nrm = 1.0 / sqrt(nrm);
+    for (int k = 0; k < 9; ++k) F[k] *= nrm;
+}
+
+__global__ __launch_bounds__(64) void k_ransac_hyp(const PairInfo* __restrict__ info, const double4* __restrict__ ptsn,
+                                                   int H, uint64_t seed, double* __restrict__ models,
+                                                   int8_t* __restrict__ nsol) {
+    const int p = blockIdx.y;
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= H) return;
+    const PairInfo pi = info[p];
+    double* out = models + ((size_t)p * H + h) * MAXSOL * 9;
+    int ns = 0;
+    const bool direct = pi.mode == 4 || pi.mode == 5;
+    if (pi.mode == 0 || (direct && h > 0)) {
+        nsol[(size_t)p * H + h] = 0;
+        return;
+    }
+    const int m = (pi.mode == 1 || pi.mode == 5) ? 5 : 7;
+    int idx[7];
+    // the stream depends on (seed, h) only, so a pair's result does not depend on the batch
+    uint64_t st = splitmix(seed ^ (uint64_t)h * 0x632BE59BD9B4E019ull);
+    if (direct) {
+        for (int i = 0; i < m; ++i) idx[i] = i;
+    } else {
+        for (int i = 0; i < m; ++i) {
+            int v;
+            bool dup;
+            do {
+                st = splitmix(st);
+                v = (int)((st >> 11) % (uint64_t)pi.count);
+                dup = false;
+                for (int j = 0; j < i; ++j) dup |= idx[j] == v;
+            } while (dup);
+            idx[i] = v;
+        }
+    }
+    if (m == 5) {
+        double q1[5][2], q2[5][2];
+        for (int i = 0; i < 5; ++i) {
+            const double4 q = ptsn[pi.start + idx[i]];
+            q1[i][0] = q.x; q1[i][1] = q.y; q2[i][0] = q.z; q2[i][1] = q.w;
+        }
+        ns = solve_5pt(q1, q2, out);
+    } else {
+        double q1[7][2], q2[7][2];
+        for (int i = 0; i < 7; ++i) {
+            const double4 q = ptsn[pi.start + idx[i]];
+            q1[i][0] = q.x; q1[i][1] = q.y; q2[i][0] = q.z; q2[i][1] = q.w;
+        }
+        double Fn[3 * 9];
+        ns = solve_7pt(q1, q2, Fn);
+        for (int s = 0; s < ns; ++s) denorm_F(Fn + s * 9, pi.T1, pi.T2, out + s * 9);
+    }
+    nsol[(size_t)p * H + h] = (int8_t)ns;
+}
+
+// score[p][h][s]: inlier count (RANSAC / direct) or -median error (LMedS); -inf if absent
+__global__ __launch_bounds__(256) void k_ransac_score(const PairInfo* __restrict__ info, const double4* __restrict__ ptsn,
+                                                      const double4* __restrict__ ptsr, int H,
+                                                      const double* __restrict__ models,
+                                                      const int8_t* __restrict__ nsol, float* __restrict__ score) {
+    __shared__ double4 sp[RS_CHUNK];
+    const int p = blockIdx.y;
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    const PairInfo pi = info[p];
+    if (pi.mode == 0) {
+        if (h < H)
+            for (int s = 0; s < MAXSOL; ++s) score[((size_t)p * H + h) * MAXSOL + s] = -INFINITY;
+        return;
+    }
+    const bool ess = pi.mode == 1 || pi.mode == 5;
+    const double4* src = (ess ? ptsn : ptsr) + pi.start;
+    const int ns = h < H ? nsol[(size_t)p * H + h] : 0;
+    // waves skip the loads of absent hypotheses but keep the barrier count uniform
+    int cnt[MAXSOL];
+    for (int s = 0; s < MAXSOL; ++s) cnt[s] = 0;
+    const float t2 = (float)pi.thr2;
+    const double* mh = models + ((size_t)p * H + (h < H ? h : 0)) * MAXSOL * 9;
+    if (pi.mode == 3) {
+        // LMedS: fewer than 15 points; median of the errors per model
+        for (int s = 0; s < MAXSOL; ++s) {
+            float med = INFINITY;
+            if (s < ns) {
+                float e[16];
+                for (int i = 0; i < pi.count; ++i) {
+                    const double4 q = src[i];
+                    e[i] = err_epiline(mh + s * 9, q.x, q.y, q.z, q.w);
+                }
+                for (int i = 1; i < pi.count; ++i) {  // insertion sort
+                    const float v = e[i];
+                    int j = i - 1;
+                    while (j >= 0 && e[j] > v) { e[j + 1] = e[j]; --j; }
+                    e[j + 1] = v;
+                }
+                med = e[pi.count / 2];
+            }
+            if (h < H) score[((size_t)p * H + h) * MAXSOL + s] = s < ns ? -med : -INFINITY;
+        }
+        return;
+    }
+    for (int c0 = 0; c0 < pi.count; c0 += RS_CHUNK) {
+        const int cn = min(RS_CHUNK, pi.count - c0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < cn; i += blockDim.x) sp[i] = src[c0 + i];
+        __syncthreads();
+        for (int s = 0; s < ns; ++s) {
+            double M[9];
+            for (int k = 0; k < 9; ++k) M[k] = mh[s * 9 + k];
+            int c = 0;
+            if (ess) {
+                for (int i = 0; i < cn; ++i) {
+                    const double4 q = sp[i];
+                    c += err_sampson(M, q.x, q.y, q.z, q.w) <= t2;
+                }
+            } else {
+                for (int i = 0; i < cn; ++i) {
+                    const double4 q = sp[i];
+                    c += err_epiline(M, q.x, q.y, q.z, q.w) <= t2;
+                }
+            }
+            cnt[s] += c;
+        }
+    }
+    if (h < H)
+        for (int s = 0; s < MAXSOL; ++s)
+            score[((size_t)p * H + h) * MAXSOL + s] = s < ns ? (float)cnt[s] : -INFINITY;
+}
+
+// ------------------------------------------------------------------ pose (recoverPose)
+// Symmetric 3x3 eigen-decomposition (cyclic Jacobi): A = V diag(w) V^T.
+RS_HD void jacobi3(double (&A)[3][3], double (&V)[3][3], double (&w)[3]) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) V[i][j] = i == j ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 50; ++sweep) {
+        const double off = fabs(A[0][1]) + fabs(A[0][2]) + fabs(A[1][2]);
+        if (off < 1e-300) break;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                if (fabs(A[p][q]) < 1e-300) continue;
+                const double th = (A[q][q] - A[p][p]) / (2.0 * A[p][q]);
+                const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < 3; ++k) {
+                    const double akp = A[k][p], akq = A[k][q];
+                    A[k][p] = c * akp - s * akq;
+                    A[k][q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    const double apk = A[p][k], aqk = A[q][k];
+                    A[p][k] = c * apk - s * aqk;
+                    A[q][k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < 3; ++k) {
+                    const double vkp = V[k][p], vkq = V[k][q];
+                    V[k][p] = c * vkp - s * vkq;
+                    V[k][q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    for (int i = 0; i < 3; ++i) w[i] = A[i][i];
+}
+
+// E = U diag(s) V^T with s descending; det(U), det(V) made positive (as OpenCV's
+// decomposeEssentialMat after its SVD).  Returns R1 = U W V^T, R2 = U W^T V^T, t = U[:,2].
+RS_HD void decompose_E(const double* E, double (&R1)[3][3], double (&R2)[3][3], double (&t)[3]) {
+    double A[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) A[i][j] = E[0 * 3 + i] * E[0 * 3 + j] + E[1 * 3 + i] * E[1 * 3 + j] + E[2 * 3 + i] * E[2 * 3 + j];
+    double V[3][3], w[3];
+    jacobi3(A, V, w);
+    int o[3] = {0, 1, 2};  // sort descending
+    for (int i = 0; i < 3; ++i)
+        for (int j = i + 1; j < 3; ++j)
+            if (w[o[j]] > w[o[i]]) { int tt = o[i]; o[i] = o[j]; o[j] = tt; }
+    double Vs[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Vs[i][j] = V[i][o[j]];
+    double U[3][3];
+    for (int c = 0; c < 2; ++c) {
+        double n = 0.0;
+        for (int i = 0; i < 3; ++i) {
+            U[i][c] = E[i * 3 + 0] * Vs[0][c] + E[i * 3 + 1] * Vs[1][c] + E[i * 3 + 2] * Vs[2][c];
+            n += U[i][c] * U[i][c];
+        }
+        n = n > 0 ? 1.0 / sqrt(n) : 0.0;
+        for (int i = 0; i < 3; ++i) U[i][c] *= n;
+    }
+    // u2 orthogonal to u1 (numerical hygiene), u3 = u1 x u2
+    double d = U[0][0] * U[0][1] + U[1][0] * U[1][1] + U[2][0] * U[2][1];
+    double n2 = 0.0;
+    for (int i = 0; i < 3; ++i) { U[i][1] -= d * U[i][0]; n2 += U[i][1] * U[i][1]; }
+    n2 = 1.0 / sqrt(n2);
+    for (int i = 0; i < 3; ++i) U[i][1] *= n2;
+    U[0][2] = U[1][0] * U[2][1] - U[2][0] * U[1][1];
+    U[1][2] = U[2][0] * U[0][1] - U[0][0] * U[2][1];
+    U[2][2] = U[0][0] * U[1][1] - U[1][0] * U[0][1];
+    double Uc[9], Vc[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) { Uc[i * 3 + j] = U[i][j]; Vc[i * 3 + j] = Vs[i][j]; }
+    if (det3(Uc) < 0)
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) U[i][j] = -U[i][j];
+    if (det3(Vc) < 0)
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) Vs[i][j] = -Vs[i][j];
+    const double W[3][3] = {{0, 1, 0}, {-1, 0, 0}, {0, 0, 1}};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double a = 0.0, b = 0.0;
+            for (int k = 0; k < 3; ++k)
+                for (int l = 0; l < 3; ++l) {
+                    a += U[i][k] * W[k][l] * Vs[j][l];
+                    b += U[i][k] * W[l][k] * Vs[j][l];
+                }
+            R1[i][j] = a;
+            R2[i][j] = b;
+        }
+    for (int i = 0; i < 3; ++i) t[i] = U[i][2];
+}
+
+// Linear triangulation (DLT null vector via the 4x4 normal matrix) with P0 = [I|0],
+// P1 = [R|t]; OpenCV's recoverPose test: z*w > 0, depth < dist in both cameras.
+RS_HD bool cheiral(const double (&R)[3][3], const double (&t)[3], double x1, double y1, double x2, double y2,
+                        double dist) {
+    double P1[3][4];
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) P1[i][j] = R[i][j];
+        P1[i][3] = t[i];
+    }
+    const double P0[3][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}};
+    double A[4][4];
+    for (int j = 0; j < 4; ++j) {
+        A[0][j] = x1 * P0[2][j] - P0[0][j];
+        A[1][j] = y1 * P0[2][j] - P0[1][j];
+        A[2][j] = x2 * P1[2][j] - P1[0][j];
+        A[3][j] = y2 * P1[2][j] - P1[1][j];
+    }
+    // null vector of A: smallest eigenvector of A^T A by inverse iteration on a
+    // Gaussian-eliminated A (4 x 4, rank 3 for exact data)
+    double M[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double s = 0.0;
+            for (int k = 0; k < 4; ++k) s += A[k][i] * A[k][j];
+            M[i][j] = s;
+        }
+    // shift-free inverse iteration with a tiny regulariser
+    double tr = M[0][0] + M[1][1] + M[2][2] + M[3][3];
+    for (int i = 0; i < 4; ++i) M[i][i] += 1e-15 * tr;
+    // LU of M (symmetric positive definite): Cholesky
+    double L[4][4] = {{0}};
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double s = M[i][j];
+            for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
+            if (i == j) {
+                L[i][i] = sqrt(fmax(s, 1e-300));
+            } else {
+                L[i][j] = s / L[j][j];
+            }
+        }
+    double X[4] = {0.5, 0.5, 0.5, 0.5};
+    for (int it = 0; it < 6; ++it) {
+        double y[4];
+        for (int i = 0; i < 4; ++i) {
+            double s = X[i];
+            for (int k = 0; k < i; ++k) s -= L[i][k] * y[k];
+            y[i] = s / L[i][i];
+        }
+        for (int i = 3; i >= 0; --i) {
+            double s = y[i];
+            for (int k = i + 1; k < 4; ++k) s -= L[k][i] * X[k];
+            X[i] = s / L[i][i];
+        }
+        double n = sqrt(X[0] * X[0] + X[1] * X[1] + X[2] * X[2] + X[3] * X[3]);
+        for (int i = 0; i < 4; ++i) X[i] /= n;
+    }
+    if (!(X[2] * X[3] > 0)) return false;
+    const double X0 = X[0] / X[3], X1 = X[1] / X[3], X2 = X[2] / X[3];
+    if (!(X2 < dist)) return false;
+    const double z2 = R[2][0] * X0 + R[2][1] * X1 + R[2][2] * X2 + t[2];
+    return z2 > 0 && z2 < dist;
+}
+
+__global__ __launch_bounds__(256) void k_ransac_select(const PairInfo* __restrict__ info,
+                                                       const double4* __restrict__ ptsn,
+                                                       const double4* __restrict__ ptsr, int H,
+                                                       const double* __restrict__ models,
+                                                       const float* __restrict__ score, double* __restrict__ model_out,
+                                                       uint8_t* __restrict__ mask, int32_t* __restrict__ inliers,
+                                                       int32_t* __restrict__ status) {
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const PairInfo pi = info[p];
+    __shared__ float bs[256];
+    __shared__ int bi[256];
+    __shared__ double Mb[9];
+    __shared__ int cnt_sh;
+    const int total = H * MAXSOL;
+    float best = -INFINITY;
+    int bidx = 0x7fffffff;
+    for (int i = tid; i < total; i += 256) {
+        const float v = score[(size_t)p * total + i];
+        if (v > best || (v == best && i < bidx)) { best = v; bidx = i; }
+    }
+    bs[tid] = best;
+    bi[tid] = bidx;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) {
+            const float v = bs[tid + o];
+            const int ii = bi[tid + o];
+            if (v > bs[tid] || (v == bs[tid] && ii < bi[tid])) { bs[tid] = v; bi[tid] = ii; }
+        }
+        __syncthreads();
+    }
+    const bool have = pi.mode != 0 && bs[0] > -INFINITY;
+    if (!have) {
+        for (int i = tid; i < pi.count; i += 256) mask[pi.start + i] = 0;
+        if (tid == 0) {
+            status[p] = 1;
+            inliers[p] = 0;
+            for (int k = 0; k < 9; ++k) model_out[p * 9 + k] = 0.0;
+        }
+        return;
+    }
+    if (tid < 9) Mb[tid] = models[(size_t)p * total * 9 + (size_t)bi[0] * 9 + tid];
+    if (tid == 0) cnt_sh = 0;
+    __syncthreads();
+    const bool ess = pi.mode == 1 || pi.mode == 5;
+    const bool all_in = pi.mode == 4 || pi.mode == 5;
+    float t2 = (float)pi.thr2;
+    if (pi.mode == 3) {  // LMedS inlier threshold from the best median
+        const double med = -(double)bs[0];
+        double sigma = 2.5 * 1.4826 * (1.0 + 5.0 / (pi.count - 7)) * sqrt(med);
+        sigma = fmax(sigma, 0.001);
+        t2 = (float)(sigma * sigma);
+    }
+    int c = 0;
+    for (int i = tid; i < pi.count; i += 256) {
+        bool in;
+        if (all_in) {
+            in = true;
+        } else {
+            const double4 q = ess ? ptsn[pi.start + i] : ptsr[pi.start + i];
+            const float e = ess ? err_sampson(Mb, q.x, q.y, q.z, q.w) : err_epiline(Mb, q.x, q.y, q.z, q.w);
+            in = e <= t2;
+        }
+        mask[pi.start + i] = in;
+        c += in;
+    }
+    atomicAdd(&cnt_sh, c);
+    __syncthreads();
+    const int n_in = cnt_sh;
+    if (tid == 0) {
+        status[p] = 0;
+        inliers[p] = n_in;
+        for (int k = 0; k < 9; ++k) model_out[p * 9 + k] = Mb[k];
+    }
+}
+
+// recoverPose (distanceThresh 50) of one pair per workgroup from E and the inlier
+// mask; points normalised by K.  pose [P, 16]; status set to 2 when < 5 inliers.
+__global__ __launch_bounds__(256) void k_recover_pose(const float* __restrict__ kp1, const float* __restrict__ kp2,
+                                                      const int32_t* __restrict__ offs, const double* __restrict__ K,
+                                                      int k_stride, const double* __restrict__ Es,
+                                                      const uint8_t* __restrict__ mask, double* __restrict__ pose,
+                                                      int32_t* __restrict__ status) {
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int s0 = offs[p], S = offs[p + 1] - offs[p];
+    __shared__ int good[4];
+    __shared__ int nin;
+    if (tid < 4) good[tid] = 0;
+    if (tid == 0) nin = 0;
+    __syncthreads();
+    int c = 0;
+    for (int i = tid; i < S; i += 256) c += mask[s0 + i] != 0;
+    atomicAdd(&nin, c);
+    __syncthreads();
+    if (status && status[p] == 1) {
+        if (tid < 16) pose[p * 16 + tid] = 0.0;
+        return;
+    }
+    if (nin < 5) {
+        if (tid < 16) pose[p * 16 + tid] = 0.0;
+        if (tid == 0 && status) status[p] = 2;
+        return;
+    }
+    const double* Kp = K + (size_t)p * k_stride;
+    const double fx = Kp[0], fy = Kp[4], cx = Kp[2], cy = Kp[5];
+    double E[9];
+    for (int k = 0; k < 9; ++k) E[k] = Es[p * 9 + k];
+    double R1[3][3], R2[3][3], tv[3];
+    decompose_E(E, R1, R2, tv);
+    double nt[3] = {-tv[0], -tv[1], -tv[2]};
+    int g[4] = {0, 0, 0, 0};
+    for (int i = tid; i < S; i += 256) {
+        if (!mask[s0 + i]) continue;
+        const double x1 = (kp1[2 * (s0 + i)] - cx) / fx, y1 = (kp1[2 * (s0 + i) + 1] - cy) / fy;
+        const double x2 = (kp2[2 * (s0 + i)] - cx) / fx, y2 = (kp2[2 * (s0 + i) + 1] - cy) / fy;
+        g[0] += cheiral(R1, tv, x1, y1, x2, y2, 50.0);
+        g[1] += cheiral(R2, tv, x1, y1, x2, y2, 50.0);
+        g[2] += cheiral(R1, nt, x1, y1, x2, y2, 50.0);
+        g[3] += cheiral(R2, nt, x1, y1, x2, y2, 50.0);
+    }
+    for (int k = 0; k < 4; ++k) atomicAdd(&good[k], g[k]);
+    __syncthreads();
+    if (tid == 0) {
+        const int a = good[0], b = good[1], cc = good[2], d = good[3];
+        int pick;
+        if (a >= b && a >= cc && a >= d) pick = 0;
+        else if (b >= a && b >= cc && b >= d) pick = 1;
+        else if (cc >= a && cc >= b && cc >= d) pick = 2;
+        else pick = 3;
+        const double (*R)[3] = (pick & 1) ? R2 : R1;
+        const double* tt = (pick & 2) ? nt : tv;
+        double* T = pose + p * 16;
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) T[i * 4 + j] = R[i][j];
+            T[i * 4 + 3] = tt[i];
+        }
+        T[12] = 0.0; T[13] = 0.0; T[14] = 0.0; T[15] = 1.0;
+    }
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct RsLayout {
+    size_t info, ptsn, ptsr, models, nsol, score, total;
+};
+
+RsLayout rs_layout(int P, long S_total, int H) {
+    RsLayout L;
+    L.info = 0;
+    L.ptsn = align256(sizeof(PairInfo) * (size_t)P);
+    L.ptsr = L.ptsn + align256(sizeof(double4) * (size_t)S_total);
+    L.models = L.ptsr + align256(sizeof(double4) * (size_t)S_total);
+    L.nsol = L.models + align256(sizeof(double) * 9 * MAXSOL * (size_t)P * H);
+    L.score = L.nsol + align256((size_t)P * H);
+    L.total = L.score + align256(sizeof(float) * MAXSOL * (size_t)P * H);
+    return L;
+}
+
+}  // namespace
+
+size_t mlg_ransac_ws_bytes(int P, long S_total, int H) {
+    if (P <= 0 || S_total < 0 || H <= 0) return 0;
+    return rs_layout(P, S_total, H).total;
+}
+
+int mlg_ransac_run(const float* kp1, const float* kp2, const int32_t* offs, int P, long S_total, const double* K,
+                   int k_stride, double thr, int H, uint64_t seed, void* ws, size_t ws_bytes, double* model_out,
+                   uint8_t* mask, int32_t* inliers, double* pose, int32_t* status, hipStream_t s) {
+    if (P <= 0 || H <= 0 || H > (1 << 20) || !(thr > 0.0) || S_total < 0) return MLG_EINVAL;
+    const RsLayout L = rs_layout(P, S_total, H);
+    if (ws_bytes < L.total) return MLG_EINVAL;
+    char* w = (char*)ws;
+    PairInfo* info = (PairInfo*)(w + L.info);
+    double4* ptsn = (double4*)(w + L.ptsn);
+    double4* ptsr = (double4*)(w + L.ptsr);
+    double* models = (double*)(w + L.models);
+    int8_t* nsol = (int8_t*)(w + L.nsol);
+    float* score = (float*)(w + L.score);
+    hipLaunchKernelGGL(k_ransac_prep, dim3(P), dim3(256), 0, s, kp1, kp2, offs, K, k_stride, thr, info, ptsn, ptsr);
+    MLG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ransac_hyp, dim3((H + 63) / 64, P), dim3(64), 0, s, info, ptsn, H, seed, models, nsol);
+    MLG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ransac_score, dim3((H + 255) / 256, P), dim3(256), 0, s, info, ptsn, ptsr, H, models, nsol,
+                       score);
+    MLG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ransac_select, dim3(P), dim3(256), 0, s, info, ptsn, ptsr, H, models, score, model_out, mask,
+                       inliers, status);
+    MLG_LAUNCH_CHECK();
+    if (pose && K) {
+        hipLaunchKernelGGL(k_recover_pose, dim3(P), dim3(256), 0, s, kp1, kp2, offs, K, k_stride, model_out, mask, pose,
+                           status);
+        MLG_LAUNCH_CHECK();
+    }
+    return MLG_OK;
+}
+
+int mlg_recover_pose_run(const float* kp1, const float* kp2, const int32_t* offs, int P, const double* K,
+                         int k_stride, const double* E, const uint8_t* mask, double* pose, hipStream_t s) {
+    if (P <= 0) return MLG_EINVAL;
+    hipLaunchKernelGGL(k_recover_pose, dim3(P), dim3(256), 0, s, kp1, kp2, offs, K, k_stride, E, mask, pose,
+                       (int32_t*)nullptr);
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}

@@ -35,6 +35,15 @@ EXPORTS = {
                                     c_size_t, c_void_p, c_void_p]),
     "mlg_proximity_emit": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_double, c_int, c_int, c_void_p,
                                    c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mlg_ransac_workspace_bytes": (c_size_t, [c_int, c_long, c_int]),
+    "mlg_ransac_epipolar": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_long, c_void_p, c_int, c_double, c_int,
+                                    ctypes.c_uint64, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p]),
+    "mlg_recover_pose": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                 c_void_p]),
+    "mlg_superpoint_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mlg_superpoint": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_long, c_float, c_int, c_int, c_int,
+                               c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mlg_op_gemm_f32out": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_op_gemm_f32out_variant": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_set_gemm_variant": (c_int, [c_int]),

@@ -1,18 +1,17 @@
 """Geometric verification: drop-in mirror of scripts/semantic_gating/geometric_verification.py.
 
-Status (round 1): the dataclasses, the verifier decision rule
-(geometric_verification.py:586-634), the semantic cross-floor skip and its statistics
-(:688-744) are complete.  The matcher back-ends -- SuperPoint + LightGlue attention
-matching, SuperGlue Sinkhorn, LoFTR, and GPU RANSAC (essential / fundamental) with
-recoverPose -- are the next HIP kernels on the roadmap; until they exist,
-``detect_and_match`` / ``verify_geometric_consistency`` raise MlgateError instead of
-silently running on the CPU.
+The dataclasses, the verifier decision rule (geometric_verification.py:586-634),
+the semantic cross-floor skip and its statistics (:688-744) and the RANSAC stage --
+essential / fundamental matrix + recoverPose (:104-188), batched on the GPU by
+mlgate.geometry -- are complete.  Matcher back-ends without HIP kernels yet raise
+MlgateError from ``detect_and_match`` instead of silently running on the CPU.
 """
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
+from . import geometry
 from ._native import MlgateError
 
 
@@ -50,21 +49,29 @@ class BaseFeatureMatcher:
     def __init__(self, device: str = 'cuda'):
         self.device = device
         self.model = None
+        self.ransac_hypotheses = geometry.DEFAULT_HYPOTHESES
+        self.ransac_seed = 0
 
     def detect_and_match(self, image1: np.ndarray, image2: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         raise NotImplementedError
 
     def verify_geometric_consistency(self, kpts1: np.ndarray, kpts2: np.ndarray, K: Optional[np.ndarray] = None,
                                      ransac_threshold: float = 3.0) -> Tuple[np.ndarray, np.ndarray, float]:
+        """cv2.findEssentialMat (K given) / cv2.findFundamentalMat (FM_RANSAC) on the GPU."""
         if len(kpts1) < 5:
             return np.array([]), None, 0.0
-        raise MlgateError("GPU RANSAC (essential / fundamental matrix) is not implemented on MI355X yet")
+        r = geometry.epipolar_ransac([kpts1], [kpts2], K, ransac_threshold, self.ransac_hypotheses,
+                                     self.ransac_seed, self.device, with_pose=False)[0]
+        if r.model is None:
+            return np.array([]), None, 0.0
+        return r.mask, r.model, float(np.sum(r.mask) / len(kpts1))
 
     def estimate_relative_pose(self, kpts1: np.ndarray, kpts2: np.ndarray, K: np.ndarray, inlier_mask: np.ndarray,
                                E: np.ndarray) -> Optional[np.ndarray]:
+        """cv2.recoverPose(E, kpts1[mask], kpts2[mask], K) on the GPU -> 4x4 [R|t]."""
         if E is None or np.sum(inlier_mask) < 5:
             return None
-        raise MlgateError("recoverPose is not implemented on MI355X yet")
+        return geometry.recover_pose(kpts1, kpts2, K, inlier_mask, E, self.device)
 
 
 class _PendingMatcher(BaseFeatureMatcher):
@@ -138,6 +145,34 @@ class GeometricVerifier:
             return _rejected(query_idx, match_idx)
         mask, E, ratio = self.matcher.verify_geometric_consistency(k1, k2, K, self.ransac_threshold)
         return self.decide(k1, k2, mask, E, ratio, K, query_idx, match_idx)
+
+    def verify_matches_batch(self, matches: List[Tuple[np.ndarray, np.ndarray]], K: Optional[np.ndarray] = None,
+                             indices: Optional[List[Tuple[int, int]]] = None) -> List[MatchResult]:
+        """verify() for already-matched keypoints of many pairs: ONE batched GPU RANSAC +
+        recoverPose over all pairs, then the reference's decision rule per pair."""
+        run = [i for i, (k1, _) in enumerate(matches) if len(k1) >= 5]
+        res = geometry.epipolar_ransac([matches[i][0] for i in run], [matches[i][1] for i in run], K,
+                                       self.ransac_threshold, self.matcher.ransac_hypotheses,
+                                       self.matcher.ransac_seed, self.matcher.device, with_pose=K is not None)
+        by_pair = dict(zip(run, res))
+        out = []
+        for i, (k1, k2) in enumerate(matches):
+            q, m = indices[i] if indices is not None else (i, i)
+            r = by_pair.get(i)
+            if r is None:
+                out.append(_rejected(q, m))
+                continue
+            if r.model is None:
+                mask, E, ratio = np.array([]), None, 0.0
+            else:
+                mask, E, ratio = r.mask, r.model, float(np.sum(r.mask) / len(k1))
+            n_in = int(np.sum(mask)) if len(mask) > 0 else 0
+            pose = r.pose if (K is not None and E is not None and n_in >= 5) else None
+            out.append(MatchResult(query_idx=q, match_idx=m, num_keypoints_query=len(k1), num_keypoints_match=len(k2),
+                                   num_matches=len(k1), num_inliers=n_in, inlier_ratio=ratio, relative_pose=pose,
+                                   essential_matrix=E, confidence=min(1.0, ratio * (n_in / self.min_inliers)),
+                                   is_valid=n_in >= self.min_inliers and ratio >= self.min_inlier_ratio))
+        return out
 
     def verify_batch(self, image_pairs: List[Tuple[np.ndarray, np.ndarray]], K: Optional[np.ndarray] = None,
                      indices: Optional[List[Tuple[int, int]]] = None) -> List[MatchResult]:

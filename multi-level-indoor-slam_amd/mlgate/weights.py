@@ -82,3 +82,40 @@ def resolve_state_dict(pretrained_path=None, seed=0):
     if path:
         return load_hub_state_dict(path), path
     return synthetic_state_dict(seed), f"synthetic(seed={seed})"
+
+
+# ----------------------------------------------------------------- SuperPoint
+# LightGlue's SuperPoint (geometric_verification.py:224-233): layer name, Cin, Cout, kernel
+SUPERPOINT_LAYERS = [("conv1a", 1, 64, 3), ("conv1b", 64, 64, 3), ("conv2a", 64, 64, 3), ("conv2b", 64, 64, 3),
+                     ("conv3a", 64, 128, 3), ("conv3b", 128, 128, 3), ("conv4a", 128, 128, 3),
+                     ("conv4b", 128, 128, 3), ("convPa", 128, 256, 3), ("convPb", 256, 65, 1),
+                     ("convDa", 128, 256, 3), ("convDb", 256, 256, 1)]
+
+
+def superpoint_state_dict(seed=0):
+    """Seeded float32 SuperPoint weights (He-normal convs, small biases), LightGlue key names."""
+    rng = np.random.default_rng(seed)
+    sd = {}
+    for name, cin, cout, k in SUPERPOINT_LAYERS:
+        std = np.float32((2.0 / (cin * k * k)) ** 0.5)
+        sd[f"{name}.weight"] = rng.standard_normal((cout, cin, k, k), dtype=np.float32) * std
+        sd[f"{name}.bias"] = rng.standard_normal((cout,), dtype=np.float32) * np.float32(0.01)
+    return sd
+
+
+def load_superpoint_state_dict(path):
+    """LightGlue superpoint_v1.pth-style checkpoint from a local file (weights only)."""
+    import torch
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    keys = [f"{n}.{p}" for n, *_ in SUPERPOINT_LAYERS for p in ("weight", "bias")]
+    missing = [k for k in keys if k not in sd]
+    if missing:
+        raise KeyError(f"checkpoint {path} lacks SuperPoint keys, e.g. {missing[:3]}")
+    return {k: sd[k].float().cpu().numpy() for k in keys}
+
+
+def resolve_superpoint_state_dict(path=None, seed=0):
+    path = path or os.environ.get("MLGATE_SUPERPOINT_WEIGHTS")
+    if path:
+        return load_superpoint_state_dict(path), path
+    return superpoint_state_dict(seed), f"synthetic(seed={seed})"

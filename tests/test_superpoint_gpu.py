@@ -1,0 +1,99 @@
+"""SuperPoint on the GPU (superpoint.hip via mlg_superpoint) against the torch-fp32
+restatement (oracle/superpoint.py) with the same seeded weights.
+
+The oracle stores bf16 activations like the kernels (emulate_bf16), so differences
+come from summation order only; keypoint selection (NMS, threshold, top-k) can then
+flip only at near-ties.  One-ulp bf16 rounding flips of intermediate activations
+accumulate over the 10 conv layers to ~1 % in the logits, hence the tolerances:
+>= 98 % of keypoints identical (same (x, y)), scores of common keypoints within
+3e-2 relative, descriptors cosine >= 0.99.
+Parity vs the trained LightGlue model is unpinned (no weights / package offline).
+"""
+import numpy as np
+import pytest
+import torch
+
+from mlgate.superpoint import SuperPointGPU
+from mlgate.weights import superpoint_state_dict
+from oracle import superpoint as osp
+
+pytestmark = pytest.mark.gpu
+
+
+def scene(rng, h=480, w=640):
+    img = np.zeros((h, w, 3), np.int32) + rng.integers(0, 60, 3)
+    for _ in range(rng.integers(20, 41)):
+        y0, x0 = rng.integers(0, h - 8), rng.integers(0, w - 8)
+        y1, x1 = y0 + rng.integers(8, h // 3), x0 + rng.integers(8, w // 3)
+        img[y0:y1, x0:x1] = rng.integers(0, 256, 3)
+    img += rng.integers(0, 30, img.shape)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+@pytest.fixture(scope="module")
+def sd():
+    return superpoint_state_dict(0)
+
+
+def _compare(g, o, min_overlap=0.98):
+    gk = {tuple(k): i for i, k in enumerate(np.round(g["keypoints"]).astype(int).tolist())}
+    ok = {tuple(k): i for i, k in enumerate(np.round(o["keypoints"].numpy()).astype(int).tolist())}
+    common = set(gk) & set(ok)
+    assert len(common) >= min_overlap * max(len(gk), len(ok)), (len(common), len(gk), len(ok))
+    gi = np.array([gk[c] for c in common])
+    oi = np.array([ok[c] for c in common])
+    np.testing.assert_allclose(g["keypoint_scores"][gi], o["keypoint_scores"].numpy()[oi], rtol=3e-2, atol=1e-6)
+    cos = np.sum(g["descriptors"][gi] * o["descriptors"].numpy()[oi], 1)
+    assert cos.min() >= 0.99, cos.min()
+    return gk, ok
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_superpoint_topk_matches_oracle(dev, sd, seed):
+    rng = np.random.default_rng(seed)
+    imgs = [scene(rng), scene(rng)]
+    sp = SuperPointGPU(sd, device=str(dev))
+    got = sp.extract(imgs)
+    ref = osp.superpoint(sd, imgs, max_kp=2048, det_thr=0.001)
+    for g, o in zip(got, ref):
+        assert len(g["keypoints"]) == len(o["keypoints"]) == 2048
+        _compare(g, o)
+        # score-descending order
+        assert np.all(np.diff(g["keypoint_scores"]) <= 0)
+        assert np.allclose(np.linalg.norm(g["descriptors"], axis=1), 1.0, atol=1e-5)
+
+
+def test_superpoint_raster_order_below_k(dev, sd):
+    """Fewer than max_kp above threshold: all of them, in raster (y, x) order."""
+    rng = np.random.default_rng(5)
+    imgs = [scene(rng, 96, 128)]
+    sp = SuperPointGPU(sd, device=str(dev), max_num_keypoints=4096, detection_threshold=0.001)
+    g = sp.extract(imgs)[0]
+    o = osp.superpoint(sd, imgs, max_kp=4096, det_thr=0.001)[0]
+    assert len(g["keypoints"]) < 4096
+    gk, ok = _compare(g, o, 0.99)
+    ras = g["keypoints"][:, 1] * 128 + g["keypoints"][:, 0]
+    assert np.all(np.diff(ras) > 0)
+
+
+def test_superpoint_batch_equals_single(dev, sd):
+    rng = np.random.default_rng(9)
+    imgs = [scene(rng, 240, 320) for _ in range(3)]
+    sp = SuperPointGPU(sd, device=str(dev), max_num_keypoints=512)
+    batch = sp.extract(imgs)
+    for im, b in zip(imgs, batch):
+        s = sp.extract([im])[0]
+        assert np.array_equal(s["keypoints"], b["keypoints"])
+        assert np.array_equal(s["descriptors"], b["descriptors"])
+
+
+def test_superpoint_gray_input_and_errors(dev, sd):
+    rng = np.random.default_rng(3)
+    img = scene(rng, 64, 64)
+    gray = osp.bgr_to_gray_u8(img)
+    sp = SuperPointGPU(sd, device=str(dev), max_num_keypoints=256)
+    a = sp.extract([img])[0]
+    b = sp.extract([gray])[0]
+    assert np.array_equal(a["keypoints"], b["keypoints"])
+    with pytest.raises(ValueError):
+        sp.extract([np.zeros((60, 60, 3), np.uint8)])
