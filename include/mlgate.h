@@ -188,6 +188,41 @@ int mlg_superpoint(const mlg_sp_weights* w, const uint8_t* frames, int B, int H,
                    size_t workspace_bytes, float* keypoints, float* scores, float* descriptors,
                    uint16_t* descriptors_bf16, int32_t* counts, void* stream);
 
+/* --------------------------------------------------------- LightGlue --
+ * Replaces the matcher half of LightGlue._detect_and_match_native
+ * (geometric_verification.py:263-312): LightGlue(features='superpoint') defaults --
+ * 9 layers, 4 heads, d 256, depth_confidence 0.95, width_confidence 0.99,
+ * filter_threshold 0.1, point pruning while a side has more than `pruning_min_kpts`
+ * tokens (1536 on CUDA with flash) -- for P pairs at once.  Features of F frames
+ * (e.g. mlg_superpoint outputs): keypoints f32 [F, kmax, 2], descriptors f32
+ * [F, kmax, 256] on the device, counts [F] on the HOST; pair p matches frame
+ * pair_a[p] (image0) against pair_b[p] (image1), both HOST arrays.  Outputs (device):
+ * matches int32 [P, kmax, 2] (indices into the two frames' keypoints, ascending in the
+ * image0 index), scores f32 [P, kmax] (the reference's matching scores), num_matches
+ * int32 [P]; stop_layer (host, optional): layers run per pair.  Synchronises `stream`
+ * once per layer (early-stop / pruning decisions). */
+typedef struct mlg_lg_block {
+    const uint16_t* Wqkv; const float* bqkv;  /* self: Wqkv [768][256]; cross: [to_qk; to_v] [512][256] */
+    const uint16_t* Wout; const float* bout;  /* out_proj / to_out [256][256] */
+    const uint16_t* Wf1;  const float* bf1;   /* ffn.0 [512][512] */
+    const float* ln_g;    const float* ln_b;  /* ffn.1 LayerNorm(512) */
+    const uint16_t* Wf2;  const float* bf2;   /* ffn.3 [256][512] */
+} mlg_lg_block;
+typedef struct mlg_lg_weights {
+    const float* Wr;                                       /* posenc.Wr [32][2] f32 */
+    mlg_lg_block self[9], cross[9];                        /* bf16 weights, f32 biases */
+    const uint16_t* Wfinal[9]; const float* bfinal[9];     /* log_assignment.i.final_proj */
+    const float* wmatch[9];    const float* bmatch[9];     /* log_assignment.i.matchability */
+    const float* wconf[8];     const float* bconf[8];      /* token_confidence.i.token.0 */
+    const float* ones;                                     /* f32 [256] of 1.0 */
+} mlg_lg_weights;
+size_t mlg_lightglue_workspace_bytes(int P, int kmax);
+int mlg_lightglue(const mlg_lg_weights* w, const float* keypoints, const float* descriptors, const int32_t* counts,
+                  int F, int kmax, const int32_t* pair_a, const int32_t* pair_b, int P, float depth_confidence,
+                  float width_confidence, float filter_threshold, int pruning_min_kpts, void* workspace,
+                  size_t workspace_bytes, int32_t* matches, float* scores, int32_t* num_matches, int32_t* stop_layer,
+                  void* stream);
+
 /* ------------------------------------------------------------ RANSAC --
  * Batched replacement for BaseFeatureMatcher.verify_geometric_consistency and
  * estimate_relative_pose (scripts/semantic_gating/geometric_verification.py:104-188),

@@ -264,6 +264,27 @@ int mlg_superpoint(const mlg_sp_weights* w, const uint8_t* frames, int B, int H,
                               descriptors_bf16, counts, (hipStream_t)stream);
 }
 
+static_assert(sizeof(mlg_lg_weights) == sizeof(mlg_lg_weights_i), "LightGlue weight tables must match");
+static_assert(sizeof(mlg_lg_block) == sizeof(mlg_lg_block_i), "LightGlue block tables must match");
+
+size_t mlg_lightglue_workspace_bytes(int P, int kmax) { return mlg_lightglue_ws_bytes(P, kmax); }
+
+int mlg_lightglue(const mlg_lg_weights* w, const float* keypoints, const float* descriptors, const int32_t* counts,
+                  int F, int kmax, const int32_t* pair_a, const int32_t* pair_b, int P, float depth_confidence,
+                  float width_confidence, float filter_threshold, int pruning_min_kpts, void* workspace,
+                  size_t workspace_bytes, int32_t* matches, float* scores, int32_t* num_matches, int32_t* stop_layer,
+                  void* stream) {
+    if (!w || !keypoints || !descriptors || !counts || !pair_a || !pair_b || !workspace || !matches || !scores ||
+        !num_matches || F <= 0 || P <= 0)
+        return MLG_EINVAL;
+    for (int p = 0; p < P; ++p)
+        if (pair_a[p] < 0 || pair_a[p] >= F || pair_b[p] < 0 || pair_b[p] >= F) return MLG_EINVAL;
+    const mlg_lg_weights_i& wi = *reinterpret_cast<const mlg_lg_weights_i*>(w);
+    return mlg_lightglue_run(wi, keypoints, descriptors, counts, kmax, pair_a, pair_b, P, depth_confidence,
+                             width_confidence, filter_threshold, pruning_min_kpts, workspace, workspace_bytes,
+                             matches, scores, num_matches, stop_layer, (hipStream_t)stream);
+}
+
 size_t mlg_ransac_workspace_bytes(int P, long S_total, int hypotheses) {
     return mlg_ransac_ws_bytes(P, S_total, hypotheses);
 }

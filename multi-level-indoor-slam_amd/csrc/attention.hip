@@ -33,19 +33,17 @@ __device__ __forceinline__ int v_off(int d, int gran) {
     return d * 128 + ((gran ^ (((d >> 1) ^ (d >> 5)) & 15)) << 3);
 }
 
-__global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
-                                                      const bf16_t* __restrict__ Vt, bf16_t* __restrict__ O, int T,
-                                                      int Tpad) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_BYTES + VTILE_BYTES)];
+// One (image, head, 128-query block) tile.  Qh / Kh: [rows][64] of this head; Vh: the
+// V^T rows [64][vstride] of this head; T keys; nq query rows (rows nq..qpad-1 must be
+// finite); output row r goes to orow + r * ldo.
+__device__ __forceinline__ void attention_tile(char* smem, const bf16_t* __restrict__ Qh,
+                                               const bf16_t* __restrict__ Kh, const bf16_t* __restrict__ Vh,
+                                               int vstride, int T, int nq, int qmax, int qblock,
+                                               bf16_t* __restrict__ orow, int ldo) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, col = lane & 31;
-    const int h = blockIdx.y, b = blockIdx.z;
-    const size_t head = (size_t)b * 12 + h;
-    const bf16_t* Qh = Q + head * Tpad * 64;
-    const bf16_t* Kh = K + head * Tpad * 64;
-    const bf16_t* Vh = Vt + head * 64 * Tpad;
-
-    const int qrow = blockIdx.x * 128 + wave * 32 + col;
-    const int qld = min(qrow, Tpad - 1);
+    const int Tpad = vstride;
+    const int qrow = qblock * 128 + wave * 32 + col;
+    const int qld = min(qrow, qmax - 1);
     bf16x8 qf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -170,9 +168,9 @@ __global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__
         cur ^= 1;
     }
 
-    if (qrow < T) {
+    if (qrow < nq) {
         const float inv = 1.0f / lrun;
-        bf16_t* orow = O + ((size_t)b * T + qrow) * 768 + h * 64;
+        bf16_t* out = orow + (size_t)qrow * ldo;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
@@ -181,11 +179,40 @@ __global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__
                 uint2 w;
                 w.x = pack_bf16x2(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
                 w.y = pack_bf16x2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-                *reinterpret_cast<uint2*>(orow + d) = w;
+                *reinterpret_cast<uint2*>(out + d) = w;
             }
     }
 #undef ATT_GLOAD
 #undef ATT_LSTORE
+}
+
+__global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
+                                                      const bf16_t* __restrict__ Vt, bf16_t* __restrict__ O, int T,
+                                                      int Tpad) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_BYTES + VTILE_BYTES)];
+    const int h = blockIdx.y, b = blockIdx.z;
+    const size_t head = (size_t)b * 12 + h;
+    attention_tile(smem, Q + head * Tpad * 64, K + head * Tpad * 64, Vt + head * 64 * Tpad, Tpad, T, T, Tpad,
+                   blockIdx.x, O + (size_t)b * T * 768 + h * 64, 768);
+}
+
+// Ragged batch: task t attends query rows [q_off, q_off + q_len) to keys / values
+// [kv_off, kv_off + kv_len) of a flat token layout (offsets multiples of 64, rows
+// zero-padded to the next multiple of 64); Q, K: [heads][Npad][64]; Vt: [heads][64][Npad];
+// output rows out_off + r of O [Npad][ldo] at column h * 64.
+__global__ __launch_bounds__(256, 2) void k_attention_varlen(const bf16_t* __restrict__ Q,
+                                                             const bf16_t* __restrict__ K,
+                                                             const bf16_t* __restrict__ Vt, bf16_t* __restrict__ O,
+                                                             int ldo, int Npad, const int4* __restrict__ tasks,
+                                                             const int* __restrict__ out_off) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_BYTES + VTILE_BYTES)];
+    const int4 tk = tasks[blockIdx.z];  // q_off, q_len, kv_off, kv_len
+    if ((int)blockIdx.x * 128 >= tk.y || tk.w <= 0) return;
+    const int h = blockIdx.y;
+    const int qpad = (tk.y + 63) & ~63;
+    attention_tile(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
+                   Vt + (size_t)h * 64 * Npad + tk.z, Npad, tk.w, tk.y, qpad, blockIdx.x,
+                   O + (size_t)out_off[blockIdx.z] * ldo + h * 64, ldo);
 }
 
 }  // namespace
@@ -195,6 +222,16 @@ int mlg_attention(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O,
     if (B <= 0 || T <= 0 || Tpad < ((T + KB - 1) / KB) * KB || (Tpad % 8)) return MLG_EINVAL;
     dim3 grid((T + 127) / 128, 12, B);
     hipLaunchKernelGGL(k_attention, grid, dim3(256), 0, s, Q, K, Vt, O, T, Tpad);
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}
+
+int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,
+                         const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s) {
+    if (ntasks <= 0) return MLG_OK;
+    if (Npad % 64 || heads <= 0 || max_q <= 0) return MLG_EINVAL;
+    dim3 grid((max_q + 127) / 128, heads, ntasks);
+    hipLaunchKernelGGL(k_attention_varlen, grid, dim3(256), 0, s, Q, K, Vt, O, ldo, Npad, tasks, out_off);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

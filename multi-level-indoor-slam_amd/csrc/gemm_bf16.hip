@@ -36,6 +36,14 @@ struct EpiF32 {  // plain f32 store (testing)
     }
 };
 
+struct EpiBiasF32 {  // y = acc + b  -> f32
+    float* C; int ldc; const float* bias;
+    __device__ void operator()(int m, int n, const f32x4& v) const {
+        const float4 b = *reinterpret_cast<const float4*>(bias + n);
+        *reinterpret_cast<float4*>(C + (size_t)m * ldc + n) = make_float4(v[0] + b.x, v[1] + b.y, v[2] + b.z, v[3] + b.w);
+    }
+};
+
 struct EpiBiasBF16 {  // y = acc + b  -> bf16
     bf16_t* C; int ldc; const float* bias;
     __device__ void operator()(int m, int n, const f32x4& v) const {
@@ -537,6 +545,18 @@ int mlg_gemm_f32out(const bf16_t* A, const bf16_t* W, float* C, int M, int N, in
 int mlg_gemm_f32out_variant(int variant, const bf16_t* A, const bf16_t* W, float* C, int M, int N, int K,
                             hipStream_t s) {
     return launch(A, W, M, N, K, K, K, EpiF32{C, N}, s, variant);
+}
+int mlg_gemm_bias_f32_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, float* C, int ldc, int M,
+                         int N, int K, hipStream_t s) {
+    return launch(A, W, M, N, K, lda, K, EpiBiasF32{C, ldc, bias}, s);
+}
+int mlg_gemm_bias_bf16_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* C, int ldc, int M,
+                          int N, int K, hipStream_t s) {
+    return launch(A, W, M, N, K, lda, K, EpiBiasBF16{C, ldc, bias}, s);
+}
+int mlg_gemm_residual_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* gamma, float* X,
+                         int ldx, int M, int N, int K, hipStream_t s) {
+    return launch(A, W, M, N, K, lda, K, EpiResidual{X, ldx, bias, gamma}, s);
 }
 int mlg_gemm_set_variant(int variant) {
     if (variant < 1 || variant > 4) return MLG_EINVAL;

@@ -14,6 +14,15 @@ int mlg_gemm_f32out(const bf16_t* A, const bf16_t* W, float* C, int M, int N, in
 int mlg_gemm_f32out_variant(int variant, const bf16_t* A, const bf16_t* W, float* C, int M, int N, int K,
                             hipStream_t s);
 int mlg_gemm_set_variant(int variant);
+// leading-dimension variants (A row stride lda, output row stride ldc / ldx)
+int mlg_gemm_bias_f32_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, float* C, int ldc, int M,
+                         int N, int K, hipStream_t s);
+int mlg_gemm_bias_bf16_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* C, int ldc, int M,
+                          int N, int K, hipStream_t s);
+int mlg_gemm_residual_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* gamma, float* X,
+                         int ldx, int M, int N, int K, hipStream_t s);
+int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,
+                         const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s);
 int mlg_gemm_bias_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,
                        hipStream_t s);
 int mlg_gemm_bias_gelu_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,
@@ -75,3 +84,25 @@ size_t mlg_superpoint_ws_bytes(int B, int H, int W);
 int mlg_superpoint_run(const mlg_sp_weights_i& w, const uint8_t* frames, int B, int H, int W, int C, long frame_stride,
                        float det_thr, int max_kp, int nms_radius, int border, void* ws, size_t ws_bytes, float* kpts,
                        float* kscores, float* desc, uint16_t* desc_bf16, int32_t* count, hipStream_t s);
+
+// lightglue.hip -- LightGlue matcher over a ragged batch of pairs
+struct mlg_lg_block_i {
+    const bf16_t* Wqkv; const float* bqkv;  // self: [768][256]; cross: [to_qk; to_v] [512][256]
+    const bf16_t* Wout; const float* bout;  // [256][256]
+    const bf16_t* Wf1;  const float* bf1;   // [512][512]
+    const float* ln_g;  const float* ln_b;  // [512]
+    const bf16_t* Wf2;  const float* bf2;   // [256][512]
+};
+struct mlg_lg_weights_i {
+    const float* Wr;  // [32][2]
+    mlg_lg_block_i self[9], cross[9];
+    const bf16_t* Wfinal[9]; const float* bfinal[9];  // [256][256], [256]
+    const float* wmatch[9];  const float* bmatch[9];  // [256], [1]
+    const float* wconf[8];   const float* bconf[8];   // [256], [1]
+    const float* ones;                                 // [256] of 1.0f
+};
+size_t mlg_lightglue_ws_bytes(int P, int kmax);
+int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float* desc, const int32_t* counts, int kmax,
+                      const int32_t* pa, const int32_t* pb, int P, float depth_conf, float width_conf,
+                      float filter_thr, int pruning_min, void* ws, size_t ws_bytes, int32_t* matches, float* mscores,
+                      int32_t* nmatch, int32_t* stop_layer, hipStream_t s);

@@ -44,6 +44,10 @@ EXPORTS = {
     "mlg_superpoint_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mlg_superpoint": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_long, c_float, c_int, c_int, c_int,
                                c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mlg_lightglue_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "mlg_lightglue": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
+                              c_float, c_float, c_float, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_void_p]),
     "mlg_op_gemm_f32out": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_op_gemm_f32out_variant": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_set_gemm_variant": (c_int, [c_int]),

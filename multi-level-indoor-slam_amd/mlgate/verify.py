@@ -1,18 +1,20 @@
 """Geometric verification: drop-in mirror of scripts/semantic_gating/geometric_verification.py.
 
 The dataclasses, the verifier decision rule (geometric_verification.py:586-634),
-the semantic cross-floor skip and its statistics (:688-744) and the RANSAC stage --
-essential / fundamental matrix + recoverPose (:104-188), batched on the GPU by
-mlgate.geometry -- are complete.  Matcher back-ends without HIP kernels yet raise
-MlgateError from ``detect_and_match`` instead of silently running on the CPU.
+the semantic cross-floor skip and its statistics (:688-744), SuperPoint + LightGlue
+matching (:196-312; mlgate.superpoint / mlgate.lightglue) and the RANSAC stage --
+essential / fundamental matrix + recoverPose (:104-188; mlgate.geometry) -- all run on
+the GPU.  SuperGlue and LoFTR resolve to the LightGlue path exactly as the reference
+does when their packages are missing.
 """
+import warnings
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
+import torch
 
 from . import geometry
-from ._native import MlgateError
 
 
 @dataclass
@@ -74,15 +76,16 @@ class BaseFeatureMatcher:
         return geometry.recover_pose(kpts1, kpts2, K, inlier_mask, E, self.device)
 
 
-class _PendingMatcher(BaseFeatureMatcher):
-    _what = "feature matcher"
+class LightGlue(BaseFeatureMatcher):
+    """SuperPoint + LightGlue on the GPU (geometric_verification.py:196-312).
 
-    def detect_and_match(self, image1, image2):
-        raise MlgateError(f"{type(self).__name__}: the {self._what} HIP kernels are not implemented yet")
-
-
-class LightGlue(_PendingMatcher):
-    _what = "SuperPoint + LightGlue"
+    ``detect_and_match`` runs SuperPoint on both images (mlg_superpoint) and LightGlue
+    on the pair (mlg_lightglue); ``detect_and_match_batch`` does the same for many
+    pairs of device-resident keyframes with one SuperPoint launch sequence over the
+    distinct frames and one LightGlue call over all pairs.  Weights: checkpoints from
+    MLGATE_SUPERPOINT_WEIGHTS / MLGATE_LIGHTGLUE_WEIGHTS, else seeded synthetic ones
+    (there is no network for the package's downloads).
+    """
 
     def __init__(self, device: str = 'cuda', max_keypoints: int = 2048, detection_threshold: float = 0.001):
         super().__init__(device)
@@ -90,9 +93,59 @@ class LightGlue(_PendingMatcher):
         self.detection_threshold = detection_threshold
         self._model_loaded = False
 
+    def _load_model(self):
+        if self._model_loaded:
+            return
+        from .lightglue import LightGlueGPU
+        from .superpoint import SuperPointGPU
+        self.extractor = SuperPointGPU(device=self.device, max_num_keypoints=self.max_keypoints,
+                                       detection_threshold=self.detection_threshold)
+        self.matcher = LightGlueGPU(device=self.device)
+        synth = [n for n, m in (("SuperPoint", self.extractor), ("LightGlue", self.matcher))
+                 if m.weights_source.startswith("synthetic")]
+        if synth:
+            warnings.warn(f"{' and '.join(synth)} weights not configured (MLGATE_SUPERPOINT_WEIGHTS / "
+                          "MLGATE_LIGHTGLUE_WEIGHTS); using seeded synthetic weights")
+        self._model_loaded = True
+        self._is_native = True
 
-class SuperGlue(_PendingMatcher):
-    _what = "SuperPoint + SuperGlue (Sinkhorn)"
+    def detect_and_match(self, image1: np.ndarray, image2: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        self._load_model()
+        if np.shape(image1) == np.shape(image2):
+            f1, f2 = self.extractor.extract([image1, image2])
+        else:
+            f1, = self.extractor.extract([image1])
+            f2, = self.extractor.extract([image2])
+        m, sc, _ = self.matcher.match(f1, f2)
+        return (f1["keypoints"][m[:, 0]].astype(np.float32), f2["keypoints"][m[:, 1]].astype(np.float32),
+                sc.astype(np.float32))
+
+    def detect_and_match_batch(self, frames, pairs):
+        """frames: device uint8 [F, H, W, C]; pairs: [(a, b), ...] frame indices ->
+        list of (kpts_a [S, 2], kpts_b [S, 2], scores [S]) numpy arrays per pair."""
+        self._load_model()
+        pairs = list(pairs)
+        if not pairs:
+            return []
+        used = sorted({i for p in pairs for i in p})
+        pos = {f: j for j, f in enumerate(used)}
+        sel = frames[torch.as_tensor(used, device=frames.device)] if len(used) < frames.shape[0] else frames
+        kp, _, ds, _, cnt = self.extractor.extract_device(sel)
+        counts = cnt.cpu().numpy()
+        m, sc, n, _ = self.matcher.match_device(kp, ds, counts, [pos[a] for a, _ in pairs],
+                                                [pos[b] for _, b in pairs])
+        kp, m, sc, n = kp.cpu().numpy(), m.cpu().numpy(), sc.cpu().numpy(), n.cpu().numpy()
+        out = []
+        for p, (a, b) in enumerate(pairs):
+            mm = m[p, :n[p]]
+            out.append((kp[pos[a]][mm[:, 0]], kp[pos[b]][mm[:, 1]], sc[p, :n[p]]))
+        return out
+
+
+class SuperGlue(BaseFeatureMatcher):
+    """geometric_verification.py:353-421: SuperGlue's native branch defers to its
+    LightGlue fallback in the reference (and the SuperGlue package is absent), so this
+    matcher IS the GPU LightGlue path, with the reference's warning."""
 
     def __init__(self, device: str = 'cuda', max_keypoints: int = 2048, weights: str = 'indoor'):
         super().__init__(device)
@@ -100,14 +153,40 @@ class SuperGlue(_PendingMatcher):
         self.weights = weights
         self._model_loaded = False
 
+    def _load_model(self):
+        if self._model_loaded:
+            return
+        warnings.warn("SuperGlue not installed. Using LightGlue fallback.")
+        self._fallback = LightGlue(device=self.device, max_keypoints=self.max_keypoints)
+        self._model_loaded = True
+        self._is_native = False
 
-class LoFTR(_PendingMatcher):
-    _what = "LoFTR"
+    def detect_and_match(self, image1, image2):
+        self._load_model()
+        return self._fallback.detect_and_match(image1, image2)
+
+
+class LoFTR(BaseFeatureMatcher):
+    """geometric_verification.py:424-526.  Without kornia the reference falls back to
+    LightGlue (with this warning); the detector-free LoFTR transformer itself is not
+    built yet, so this matcher runs the GPU LightGlue path."""
 
     def __init__(self, device: str = 'cuda', weights: str = 'indoor'):
         super().__init__(device)
         self.weights = weights
         self._model_loaded = False
+
+    def _load_model(self):
+        if self._model_loaded:
+            return
+        warnings.warn("LoFTR (kornia) not installed. Using LightGlue fallback. Install with: pip install kornia")
+        self._fallback = LightGlue(device=self.device)
+        self._model_loaded = True
+        self._is_native = False
+
+    def detect_and_match(self, image1, image2):
+        self._load_model()
+        return self._fallback.detect_and_match(image1, image2)
 
 
 _MATCHERS = {'lightglue': LightGlue, 'superglue': SuperGlue, 'loftr': LoFTR}
@@ -176,10 +255,27 @@ class GeometricVerifier:
 
     def verify_batch(self, image_pairs: List[Tuple[np.ndarray, np.ndarray]], K: Optional[np.ndarray] = None,
                      indices: Optional[List[Tuple[int, int]]] = None) -> List[MatchResult]:
+        """Same results as verifying each pair in turn (geometric_verification.py:636-662),
+        computed as one batched SuperPoint + LightGlue + RANSAC pass when the images
+        share a shape."""
+        if not image_pairs:
+            return []
+        shapes = {np.shape(im) for pair in image_pairs for im in pair}
+        m = self.matcher
+        if len(shapes) == 1 and hasattr(m, "detect_and_match_batch") or (
+                hasattr(m, "_fallback") and len(shapes) == 1):
+            mm = getattr(m, "_fallback", None) if not hasattr(m, "detect_and_match_batch") else m
+            if mm is None:
+                m._load_model()
+                mm = m._fallback
+            dev = torch.device(mm.device)
+            frames = torch.from_numpy(np.stack([np.asarray(im, np.uint8) for pair in image_pairs for im in pair]))
+            matched = mm.detect_and_match_batch(frames.to(dev), [(2 * i, 2 * i + 1) for i in range(len(image_pairs))])
+            return self.verify_matches_batch([(a, b) for a, b, _ in matched], K, indices)
         out = []
         for i, (a, b) in enumerate(image_pairs):
-            q, m = indices[i] if indices is not None else (i, i)
-            out.append(self.verify(a, b, K, q, m))
+            q, mi = indices[i] if indices is not None else (i, i)
+            out.append(self.verify(a, b, K, q, mi))
         return out
 
 

@@ -119,3 +119,83 @@ def resolve_superpoint_state_dict(path=None, seed=0):
     if path:
         return load_superpoint_state_dict(path), path
     return superpoint_state_dict(seed), f"synthetic(seed={seed})"
+
+
+# ----------------------------------------------------------------- LightGlue
+LG_DIM, LG_LAYERS = 256, 9
+
+
+def lightglue_keys():
+    keys = ["posenc.Wr.weight"]
+    for i in range(LG_LAYERS):
+        for blk, lins in (("self_attn", ("Wqkv", "out_proj")), ("cross_attn", ("to_qk", "to_v", "to_out"))):
+            p = f"transformers.{i}.{blk}."
+            for n in lins + ("ffn.0", "ffn.1", "ffn.3"):
+                keys += [p + n + ".weight", p + n + ".bias"]
+        keys += [f"log_assignment.{i}.matchability.weight", f"log_assignment.{i}.matchability.bias",
+                 f"log_assignment.{i}.final_proj.weight", f"log_assignment.{i}.final_proj.bias"]
+        if i < LG_LAYERS - 1:
+            keys += [f"token_confidence.{i}.token.0.weight", f"token_confidence.{i}.token.0.bias"]
+    return keys
+
+
+def lightglue_state_dict(seed=0, res_gain=0.05, final_scale=16.0, match_gain=6.0, match_bias=3.0, conf_gain=6.0,
+                         conf_bias=1.5):
+    """Seeded float32 LightGlue(features='superpoint') weights with the package's key names.
+
+    Untrained, but shaped so the network behaves like a matcher on SuperPoint-like
+    inputs: small residual updates (``res_gain``) keep tokens close to their
+    descriptors, final_proj ~ ``final_scale`` * I makes the assignment a sharpened
+    descriptor similarity, and matchability / token-confidence spreads exercise point
+    pruning and early stopping.
+    """
+    rng = np.random.default_rng(seed)
+    d = LG_DIM
+
+    def lin(o, i, gain=1.0):
+        return (rng.standard_normal((o, i), dtype=np.float32) * np.float32(gain / np.sqrt(i)),
+                rng.standard_normal((o,), dtype=np.float32) * np.float32(0.02))
+
+    sd = {"posenc.Wr.weight": rng.standard_normal((32, 2), dtype=np.float32)}
+    shapes = {"Wqkv": (3 * d, d), "out_proj": (d, d), "to_qk": (d, d), "to_v": (d, d), "to_out": (d, d),
+              "ffn.0": (2 * d, 2 * d), "ffn.3": (d, 2 * d)}
+    for i in range(LG_LAYERS):
+        for blk, lins in (("self_attn", ("Wqkv", "out_proj")), ("cross_attn", ("to_qk", "to_v", "to_out"))):
+            p = f"transformers.{i}.{blk}."
+            for n in lins + ("ffn.0", "ffn.3"):
+                w, b = lin(*shapes[n], gain=res_gain if n == "ffn.3" else 1.0)
+                sd[p + n + ".weight"], sd[p + n + ".bias"] = w, b * np.float32(res_gain if n == "ffn.3" else 1.0)
+            sd[p + "ffn.1.weight"] = 1.0 + rng.standard_normal(2 * d, dtype=np.float32) * np.float32(0.1)
+            sd[p + "ffn.1.bias"] = rng.standard_normal(2 * d, dtype=np.float32) * np.float32(0.05)
+        w, b = lin(1, d, gain=match_gain)
+        sd[f"log_assignment.{i}.matchability.weight"] = w
+        sd[f"log_assignment.{i}.matchability.bias"] = b + np.float32(match_bias)
+        w, b = lin(d, d, gain=0.05)
+        sd[f"log_assignment.{i}.final_proj.weight"] = w + np.eye(d, dtype=np.float32) * np.float32(final_scale)
+        sd[f"log_assignment.{i}.final_proj.bias"] = b
+        if i < LG_LAYERS - 1:
+            w, b = lin(1, d, gain=conf_gain)
+            sd[f"token_confidence.{i}.token.0.weight"] = w
+            sd[f"token_confidence.{i}.token.0.bias"] = b + np.float32(conf_bias)
+    return sd
+
+
+def load_lightglue_state_dict(path):
+    """LightGlue superpoint_lightglue.pth-style checkpoint from a local file (weights only)."""
+    import torch
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    import re
+    # older releases stored "self_attn.{i}.*" / "cross_attn.{i}.*" (LightGlue renames them on load)
+    sd = {re.sub(r"^(self_attn|cross_attn)\.(\d+)\.", r"transformers.\2.\1.", k.replace("matcher.", "")): v
+          for k, v in sd.items()}
+    missing = [k for k in lightglue_keys() if k not in sd]
+    if missing:
+        raise KeyError(f"checkpoint {path} lacks LightGlue keys, e.g. {missing[:3]}")
+    return {k: sd[k].float().cpu().numpy() for k in lightglue_keys()}
+
+
+def resolve_lightglue_state_dict(path=None, seed=0):
+    path = path or os.environ.get("MLGATE_LIGHTGLUE_WEIGHTS")
+    if path:
+        return load_lightglue_state_dict(path), path
+    return lightglue_state_dict(seed), f"synthetic(seed={seed})"

@@ -1,0 +1,94 @@
+"""LightGlue on the GPU (lightglue.hip via mlg_lightglue) against the torch-fp32
+restatement (oracle/lightglue.py) with the same seeded weights and inputs.
+
+The oracle rounds GEMM / attention operands to bf16 like the kernels, so the two
+differ by summation order and the online-softmax normalisation only.  Matches are
+discrete decisions (mutual argmax, threshold 0.1, early stop / pruning thresholds),
+so the bar is: >= 95 % of matches identical, scores of common matches within 5e-2
+absolute, the same number of layers run.  Batched and single-pair calls must agree
+bit for bit.  Parity vs the trained LightGlue model is unpinned (offline).
+"""
+import numpy as np
+import pytest
+import torch
+
+from mlgate.lightglue import LightGlueGPU
+from mlgate.weights import lightglue_state_dict
+from oracle.lightglue import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def feats(rng, m, n, overlap=0.6):
+    k0 = np.stack([rng.uniform(0, 640, m), rng.uniform(0, 480, m)], 1).astype(np.float32)
+    d0 = rng.standard_normal((m, 256)).astype(np.float32)
+    d0 /= np.linalg.norm(d0, axis=1, keepdims=True)
+    no = int(overlap * min(m, n))
+    k1 = np.stack([rng.uniform(0, 640, n), rng.uniform(0, 480, n)], 1).astype(np.float32)
+    d1 = rng.standard_normal((n, 256)).astype(np.float32)
+    k1[:no] = k0[:no] + rng.normal(0, 2, (no, 2)) + np.array([15, -8])
+    d1[:no] = d0[:no] + 0.02 * rng.standard_normal((no, 256))
+    d1 /= np.linalg.norm(d1, axis=1, keepdims=True) + 1e-12
+    return k0, d0, k1.astype(np.float32), d1.astype(np.float32)
+
+
+@pytest.fixture(scope="module")
+def sd():
+    return lightglue_state_dict(0)
+
+
+@pytest.fixture(scope="module")
+def lg(dev, sd):
+    return LightGlueGPU(sd, device=str(dev))
+
+
+def _run_gpu(lg, cases):
+    kmax = max(max(len(c[0]), len(c[2])) for c in cases)
+    F = 2 * len(cases)
+    kp = torch.zeros(F, kmax, 2)
+    ds = torch.zeros(F, kmax, 256)
+    counts = []
+    for i, (k0, d0, k1, d1) in enumerate(cases):
+        for j, (k, d) in enumerate(((k0, d0), (k1, d1))):
+            kp[2 * i + j, :len(k)] = torch.from_numpy(k)
+            ds[2 * i + j, :len(k)] = torch.from_numpy(d)
+            counts.append(len(k))
+    m, s, n, stop = lg.match_device(kp.to(lg.device), ds.to(lg.device), counts, np.arange(0, F, 2),
+                                    np.arange(1, F, 2))
+    m, s, n = m.cpu().numpy(), s.cpu().numpy(), n.cpu().numpy()
+    return [(m[p, :n[p]], s[p, :n[p]], int(stop[p])) for p in range(len(cases))]
+
+
+@pytest.mark.parametrize("m,n", [(700, 650), (2048, 1900), (1700, 300), (64, 70)])
+def test_lightglue_matches_oracle(lg, sd, m, n):
+    rng = np.random.default_rng(m + n)
+    case = feats(rng, m, n)
+    got_m, got_s, got_stop = _run_gpu(lg, [case])[0]
+    ref = Oracle(sd).match(*case)
+    rm, rs = ref["matches"].numpy(), ref["scores"].numpy()
+    assert got_stop == ref["stop"]
+    g = {tuple(x): i for i, x in enumerate(got_m.tolist())}
+    r = {tuple(x): i for i, x in enumerate(rm.tolist())}
+    common = set(g) & set(r)
+    assert len(common) >= 0.95 * max(len(g), len(r)), (len(common), len(g), len(r))
+    gi = np.array([g[c] for c in common], int)
+    ri = np.array([r[c] for c in common], int)
+    np.testing.assert_allclose(got_s[gi], rs[ri], atol=5e-2)
+    assert np.all(np.diff(got_m[:, 0]) > 0)  # ascending image0 index, as torch.where
+
+
+def test_lightglue_batched_equals_single(lg):
+    rng = np.random.default_rng(3)
+    cases = [feats(rng, 300, 280), feats(rng, 1600, 1550), feats(rng, 40, 90), feats(rng, 800, 10)]
+    batch = _run_gpu(lg, cases)
+    for c, b in zip(cases, batch):
+        s = _run_gpu(lg, [c])[0]
+        assert np.array_equal(s[0], b[0]) and np.array_equal(s[1], b[1]) and s[2] == b[2]
+
+
+def test_lightglue_empty_side(lg):
+    rng = np.random.default_rng(4)
+    k0, d0, k1, d1 = feats(rng, 50, 40)
+    res = _run_gpu(lg, [(k0, d0, k1[:0], d1[:0]), (k0, d0, k1, d1)])
+    assert len(res[0][0]) == 0
+    assert len(res[1][0]) > 0
