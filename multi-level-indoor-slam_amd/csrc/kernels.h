@@ -21,6 +21,13 @@ int mlg_gemm_bias_bf16_ld(const bf16_t* A, int lda, const bf16_t* W, const float
                           int N, int K, hipStream_t s);
 int mlg_gemm_residual_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* gamma, float* X,
                          int ldx, int M, int N, int K, hipStream_t s);
+int mlg_gemm_lg_self(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* ecos,
+                     const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, int K_,
+                     hipStream_t s);
+int mlg_gemm_lg_cross(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const uint8_t* live, bf16_t* Q,
+                      bf16_t* Vt, int Npad, int K_, hipStream_t s);
+int mlg_gemm_residual_copy(const bf16_t* A, int lda, const bf16_t* W, const float* bias, float* X, int ldx, bf16_t* C,
+                           int ldc, int M, int N, int K_, hipStream_t s);
 int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,
                          const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s);
 int mlg_gemm_bias_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,

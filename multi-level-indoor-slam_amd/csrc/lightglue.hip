@@ -89,48 +89,6 @@ __global__ __launch_bounds__(256) void k_lg_init(const Seg* __restrict__ segs, c
     }
 }
 
-// ------------------------------------------------------------------ head rearrangement
-// self: qkv f32 [Npad, 768] laid out (head, 64, 3) -> rotary q, k -> Q, K [4][Npad][64],
-// V^T [4][64][Npad] (bf16); rows outside any segment's live range are zeroed.
-__global__ __launch_bounds__(256) void k_lg_heads_self(const float* __restrict__ qkv, const float* __restrict__ ecos,
-                                                       const float* __restrict__ esin, const uint8_t* __restrict__ live,
-                                                       int Npad, bf16_t* __restrict__ Q, bf16_t* __restrict__ K,
-                                                       bf16_t* __restrict__ Vt) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (row, head, pair of dims)
-    if (e >= (long)Npad * LG_H * 32) return;
-    const int r = (int)(e / (LG_H * 32)), h = (int)((e / 32) % LG_H), j = (int)(e % 32);
-    const bool on = live[r];
-    const float* b = qkv + (size_t)r * 768 + h * 192;
-    const int d0 = 2 * j, d1 = 2 * j + 1;
-    float q0 = b[d0 * 3 + 0], q1 = b[d1 * 3 + 0];
-    float k0 = b[d0 * 3 + 1], k1 = b[d1 * 3 + 1];
-    const float v0 = b[d0 * 3 + 2], v1 = b[d1 * 3 + 2];
-    const float c = ecos[(size_t)r * 32 + j], s = esin[(size_t)r * 32 + j];
-    // t * cos + rotate_half(t) * sin; rotate_half(t)[2j] = -t[2j+1], [2j+1] = t[2j]
-    const float rq0 = q0 * c + (-q1) * s, rq1 = q1 * c + q0 * s;
-    const float rk0 = k0 * c + (-k1) * s, rk1 = k1 * c + k0 * s;
-    const size_t qi = ((size_t)h * Npad + r) * 64 + d0;
-    *reinterpret_cast<uint32_t*>(Q + qi) = on ? pack_bf16x2(rq0, rq1) : 0u;
-    *reinterpret_cast<uint32_t*>(K + qi) = on ? pack_bf16x2(rk0, rk1) : 0u;
-    Vt[((size_t)h * 64 + d0) * Npad + r] = on ? f32_to_bf16(v0) : (bf16_t)0;
-    Vt[((size_t)h * 64 + d1) * Npad + r] = on ? f32_to_bf16(v1) : (bf16_t)0;
-}
-
-// cross: qkv f32 [Npad, 512] = [to_qk | to_v] -> Q = K = qk heads, V^T = v heads
-__global__ __launch_bounds__(256) void k_lg_heads_cross(const float* __restrict__ qkv, const uint8_t* __restrict__ live,
-                                                        int Npad, bf16_t* __restrict__ Q, bf16_t* __restrict__ Vt) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (row, head, pair of dims)
-    if (e >= (long)Npad * LG_H * 32) return;
-    const int r = (int)(e / (LG_H * 32)), h = (int)((e / 32) % LG_H), j = (int)(e % 32);
-    const bool on = live[r];
-    const float* b = qkv + (size_t)r * 512;
-    const int d0 = 2 * j;
-    const size_t qi = ((size_t)h * Npad + r) * 64 + d0;
-    *reinterpret_cast<uint32_t*>(Q + qi) = on ? pack_bf16x2(b[h * 64 + d0], b[h * 64 + d0 + 1]) : 0u;
-    Vt[((size_t)h * 64 + d0) * Npad + r] = on ? f32_to_bf16(b[256 + h * 64 + d0]) : (bf16_t)0;
-    Vt[((size_t)h * 64 + d0 + 1) * Npad + r] = on ? f32_to_bf16(b[256 + h * 64 + d0 + 1]) : (bf16_t)0;
-}
-
 // ------------------------------------------------------------------ FFN middle
 // h = GELU(LayerNorm_512(h_f32)) -> bf16; one wave per row (8 values per lane).
 __global__ __launch_bounds__(256) void k_lg_ln_gelu(const float* __restrict__ hf, const float* __restrict__ g,
@@ -162,73 +120,39 @@ __global__ __launch_bounds__(256) void k_lg_ln_gelu(const float* __restrict__ hf
     }
 }
 
-// cat[:, :256] = bf16(x)
-__global__ void k_lg_sync(const float* __restrict__ x, bf16_t* __restrict__ cat, long n) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n) return;
-    const long r = e / LG_D, c = e % LG_D;
-    cat[r * 512 + c] = f32_to_bf16(x[e]);
-}
-
 // ------------------------------------------------------------------ confidences
-// One workgroup per segment, one wave per token: conf = sigmoid(x . wc + bc),
-// z = x . wm + bm.  stats[seg] = {#(conf < thr), #keep} with keep = sigmoid(z) > 1 - wc
-// or conf <= thr (only meaningful when the segment is pruned).
-__global__ __launch_bounds__(256) void k_lg_conf(const Seg* __restrict__ segs, const float* __restrict__ x,
+// One wave per live token: conf = sigmoid(x . wc + bc), z = x . wm + bm; lz = logsigmoid(z)
+// (the assignment's certainty term); keep = sigmoid(z) > 1 - width or conf <= thr.
+// stats[seg] += {#(conf < thr), #keep}  (zeroed by the caller).  wc == nullptr: only lz.
+__global__ __launch_bounds__(256) void k_lg_conf(const int* __restrict__ rowseg, int Npad, const float* __restrict__ x,
                                                  const float* __restrict__ wc, const float* __restrict__ bc,
                                                  const float* __restrict__ wm, const float* __restrict__ bm,
-                                                 float thr, float width_conf, float* __restrict__ z,
+                                                 float thr, float width_conf, float* __restrict__ lz,
                                                  uint8_t* __restrict__ keep, int* __restrict__ stats) {
-    const Seg sg = segs[blockIdx.x];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    __shared__ int cnt[2];
-    if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    int low = 0, kp = 0;
-    for (int i = wave; i < sg.len; i += 4) {
-        const float* xr = x + (size_t)(sg.off + i) * LG_D;
-        float a = 0.f, m = 0.f;
+    const int lane = threadIdx.x & 63;
+    const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= Npad) return;
+    const int sg = rowseg[r];
+    if (sg < 0) return;
+    const float* xr = x + r * LG_D;
+    float a = 0.f, m = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float v = xr[lane + 64 * j];
-            a += v * wc[lane + 64 * j];
-            m += v * wm[lane + 64 * j];
-        }
-        a = wave_sum(a) + bc[0];
-        m = wave_sum(m) + bm[0];
-        if (lane == 0) {
+    for (int j = 0; j < 4; ++j) {
+        const float v = xr[lane + 64 * j];
+        if (wc) a += v * wc[lane + 64 * j];
+        m += v * wm[lane + 64 * j];
+    }
+    m = wave_sum(m) + bm[0];
+    if (wc) a = wave_sum(a) + bc[0];
+    if (lane == 0) {
+        lz[r] = logsigmoidf(m);
+        if (wc) {
             const float conf = sigmoidf(a);
             const bool k = sigmoidf(m) > 1.f - width_conf || conf <= thr;
-            z[sg.off + i] = m;
-            keep[sg.off + i] = k;
-            low += conf < thr;
-            kp += k;
+            keep[r] = k;
+            if (conf < thr) atomicAdd(&stats[2 * sg], 1);
+            if (k) atomicAdd(&stats[2 * sg + 1], 1);
         }
-    }
-    if (lane == 0) {
-        atomicAdd(&cnt[0], low);
-        atomicAdd(&cnt[1], kp);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        stats[2 * blockIdx.x] = cnt[0];
-        stats[2 * blockIdx.x + 1] = cnt[1];
-    }
-}
-
-// z = x . wm + bm for every live token of the given segments (last-layer assignment)
-__global__ __launch_bounds__(256) void k_lg_matchability(const Seg* __restrict__ segs, const float* __restrict__ x,
-                                                         const float* __restrict__ wm, const float* __restrict__ bm,
-                                                         float* __restrict__ z) {
-    const Seg sg = segs[blockIdx.x];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int i = wave; i < sg.len; i += 4) {
-        const float* xr = x + (size_t)(sg.off + i) * LG_D;
-        float m = 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) m += xr[lane + 64 * j] * wm[lane + 64 * j];
-        m = wave_sum(m) + bm[0];
-        if (lane == 0) z[sg.off + i] = m;
     }
 }
 
@@ -297,128 +221,217 @@ __global__ __launch_bounds__(256) void k_lg_compact(const int4* __restrict__ mov
     for (int i = newlen + tid; i < padded; i += 256) ind2[mv.z + i] = -1;
 }
 
-__global__ void k_lg_live(const Seg* __restrict__ segs, int nseg, uint8_t* __restrict__ live, int Npad) {
+__global__ void k_lg_live(const Seg* __restrict__ segs, int nseg, uint8_t* __restrict__ live,
+                          int* __restrict__ rowseg, int Npad) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= Npad) return;
-    uint8_t on = 0;
+    int sgi = -1;
     for (int s = 0; s < nseg; ++s) {
         const Seg sg = segs[s];
-        if (r >= sg.off && r < sg.off + sg.len) on = 1;
+        if (r >= sg.off && r < sg.off + sg.len) sgi = s;
     }
-    live[r] = on;
+    live[r] = sgi >= 0;
+    rowseg[r] = sgi;
 }
 
 // ------------------------------------------------------------------ assignment
-// S [m, n] (already / 16): row log-sum-exp, column log-sum-exp, then the row / column
-// argmax of  (S - lse_row) + (S - lse_col) + (logsig(z0) + logsig(z1))  and the mutual
-// filter (filter_matches).  One wave per row / column.
-__global__ __launch_bounds__(256) void k_lg_row_lse(const float* __restrict__ S, int m, int n, float* __restrict__ lse) {
+// For every finishing pair a (table entry Asg): S = final_proj(x0) . final_proj(x1)^T
+// (f32; the two 1/4 scales applied here as one exact 1/16), the row / column
+// log_softmax terms (torch form (x - max) - log(sum exp(x - max))), and the row /
+// column argmax of  (s0 + s1) + (lz0 + lz1)  (first index on ties, as torch.max), then
+// the mutual filter.  Row / column statistics are indexed by layout row, so all
+// pairs share the buffers.  Grids carry the pair in blockIdx.y / z.
+struct Asg {
+    int m, n, ra, rb;  // rows of image a / b, their first layout rows
+    long soff;         // S offset (floats)
+    int pair, pad;
+};
+
+constexpr int CH = 256;  // rows per column-statistics chunk
+
+__global__ __launch_bounds__(256) void k_asg_rowlse(const Asg* __restrict__ tab, const float* __restrict__ Sall,
+                                                    float* __restrict__ rmax, float* __restrict__ rlog) {
+    const Asg a = tab[blockIdx.y];
     const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= m) return;
-    const float* row = S + (size_t)i * n;
+    if (i >= a.m) return;
+    const float* row = Sall + a.soff + (size_t)i * a.n;
     float mx = -INFINITY;
-    for (int j = lane; j < n; j += 64) mx = fmaxf(mx, row[j]);
+    for (int j = lane; j < a.n; j += 64) mx = fmaxf(mx, row[j] * 0.0625f);
     mx = wave_max(mx);
     float s = 0.f;
-    for (int j = lane; j < n; j += 64) s += expf(row[j] - mx);
+    for (int j = lane; j < a.n; j += 64) s += expf(row[j] * 0.0625f - mx);
     s = wave_sum(s);
-    if (lane == 0) lse[i] = mx + logf(s);
+    if (lane == 0) {
+        rmax[a.ra + i] = mx;
+        rlog[a.ra + i] = logf(s);
+    }
 }
 
-__global__ __launch_bounds__(256) void k_lg_col_lse(const float* __restrict__ S, int m, int n, float* __restrict__ lse) {
-    // 64 columns per workgroup; 4 waves split the rows, lanes own columns
+// per (64-column block, 256-row chunk): online (max, sum) of the column slice
+__global__ __launch_bounds__(256) void k_asg_colpart(const Asg* __restrict__ tab, const float* __restrict__ Sall,
+                                                     float2* __restrict__ part, int kmax) {
+    const Asg a = tab[blockIdx.z];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int j = blockIdx.x * 64 + lane;
-    __shared__ float sm[4][64], ss[4][64];
-    float mx = -INFINITY;
-    if (j < n)
-        for (int i = wave; i < m; i += 4) mx = fmaxf(mx, S[(size_t)i * n + j]);
-    sm[wave][lane] = mx;
+    const int j = blockIdx.x * 64 + lane, i0 = blockIdx.y * CH;
+    if ((int)blockIdx.x * 64 >= a.n || i0 >= a.m) return;
+    __shared__ float2 sp[4][64];
+    float mx = -INFINITY, sm = 0.f;
+    if (j < a.n)
+        for (int i = i0 + wave; i < min(a.m, i0 + CH); i += 4) {
+            const float v = Sall[a.soff + (size_t)i * a.n + j] * 0.0625f;
+            if (v > mx) {
+                sm = sm * expf(mx - v) + 1.f;
+                mx = v;
+            } else {
+                sm += expf(v - mx);
+            }
+        }
+    sp[wave][lane] = make_float2(mx, sm);
     __syncthreads();
-    mx = fmaxf(fmaxf(sm[0][lane], sm[1][lane]), fmaxf(sm[2][lane], sm[3][lane]));
-    float s = 0.f;
-    if (j < n)
-        for (int i = wave; i < m; i += 4) s += expf(S[(size_t)i * n + j] - mx);
-    ss[wave][lane] = s;
-    __syncthreads();
-    if (wave == 0 && j < n) lse[j] = mx + logf(ss[0][lane] + ss[1][lane] + ss[2][lane] + ss[3][lane]);
+    if (wave == 0 && j < a.n) {
+        float M = sp[0][lane].x;
+        for (int w = 1; w < 4; ++w) M = fmaxf(M, sp[w][lane].x);
+        float S = 0.f;
+        for (int w = 0; w < 4; ++w)
+            if (sp[w][lane].y > 0.f) S += sp[w][lane].y * expf(sp[w][lane].x - M);
+        part[((size_t)blockIdx.z * (kmax / CH + 1) + blockIdx.y) * kmax + j] = make_float2(M, S);
+    }
 }
 
-__device__ __forceinline__ float lg_score(float sij, float lr, float lc, float cert) {
-    return ((sij - lr) + (sij - lc)) + cert;
+__global__ void k_asg_colfinal(const Asg* __restrict__ tab, const float2* __restrict__ part, int kmax,
+                               float* __restrict__ cmax, float* __restrict__ clog) {
+    const Asg a = tab[blockIdx.y];
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= a.n) return;
+    const int nch = (a.m + CH - 1) / CH;
+    const float2* p = part + (size_t)blockIdx.y * (kmax / CH + 1) * kmax + j;
+    float M = -INFINITY;
+    for (int c = 0; c < nch; ++c) M = fmaxf(M, p[(size_t)c * kmax].x);
+    float S = 0.f;
+    for (int c = 0; c < nch; ++c) S += p[(size_t)c * kmax].y * expf(p[(size_t)c * kmax].x - M);
+    cmax[a.rb + j] = M;
+    clog[a.rb + j] = logf(S);
 }
 
-// rows: best column + value; columns: best row (first index on ties, as torch.max)
-__global__ __launch_bounds__(256) void k_lg_row_arg(const float* __restrict__ S, int m, int n,
-                                                    const float* __restrict__ lr, const float* __restrict__ lc,
-                                                    const float* __restrict__ z0, const float* __restrict__ z1,
-                                                    int* __restrict__ arg, float* __restrict__ val) {
+__device__ __forceinline__ float lg_score(float v, float rm, float rl, float cm, float cl, float cert) {
+    return (((v - rm) - rl) + ((v - cm) - cl)) + cert;
+}
+
+__global__ __launch_bounds__(256) void k_asg_rowarg(const Asg* __restrict__ tab, const float* __restrict__ Sall,
+                                                    const float* __restrict__ rmax, const float* __restrict__ rlog,
+                                                    const float* __restrict__ cmax, const float* __restrict__ clog,
+                                                    const float* __restrict__ lz, int* __restrict__ arg,
+                                                    float* __restrict__ val) {
+    const Asg a = tab[blockIdx.y];
     const int lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= m) return;
-    const float l0 = logsigmoidf(z0[i]);
+    if (i >= a.m) return;
+    const float* row = Sall + a.soff + (size_t)i * a.n;
+    const float rm = rmax[a.ra + i], rl = rlog[a.ra + i], l0 = lz[a.ra + i];
     float best = -INFINITY;
     int bj = 0x7fffffff;
-    for (int j = lane; j < n; j += 64) {
-        const float v = lg_score(S[(size_t)i * n + j], lr[i], lc[j], l0 + logsigmoidf(z1[j]));
-        if (v > best || (v == best && j < bj)) { best = v; bj = j; }
+    for (int j = lane; j < a.n; j += 64) {
+        const float v = lg_score(row[j] * 0.0625f, rm, rl, cmax[a.rb + j], clog[a.rb + j], l0 + lz[a.rb + j]);
+        if (v > best || (v == best && j < bj)) {
+            best = v;
+            bj = j;
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {
         const float ov = __shfl_xor(best, o, 64);
         const int oj = __shfl_xor(bj, o, 64);
-        if (ov > best || (ov == best && oj < bj)) { best = ov; bj = oj; }
+        if (ov > best || (ov == best && oj < bj)) {
+            best = ov;
+            bj = oj;
+        }
     }
-    if (lane == 0) { arg[i] = bj; val[i] = best; }
+    if (lane == 0) {
+        arg[a.ra + i] = bj;
+        val[a.ra + i] = best;
+    }
 }
 
-__global__ __launch_bounds__(256) void k_lg_col_arg(const float* __restrict__ S, int m, int n,
-                                                    const float* __restrict__ lr, const float* __restrict__ lc,
-                                                    const float* __restrict__ z0, const float* __restrict__ z1,
-                                                    int* __restrict__ arg) {
+__global__ __launch_bounds__(256) void k_asg_colargpart(const Asg* __restrict__ tab, const float* __restrict__ Sall,
+                                                        const float* __restrict__ rmax, const float* __restrict__ rlog,
+                                                        const float* __restrict__ cmax, const float* __restrict__ clog,
+                                                        const float* __restrict__ lz, float2* __restrict__ part,
+                                                        int kmax) {
+    const Asg a = tab[blockIdx.z];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int j = blockIdx.x * 64 + lane;
+    const int j = blockIdx.x * 64 + lane, i0 = blockIdx.y * CH;
+    if ((int)blockIdx.x * 64 >= a.n || i0 >= a.m) return;
     __shared__ float sb[4][64];
     __shared__ int si[4][64];
     float best = -INFINITY;
     int bi = 0x7fffffff;
-    if (j < n) {
-        const float l1 = logsigmoidf(z1[j]);
-        for (int i = wave; i < m; i += 4) {
-            const float v = lg_score(S[(size_t)i * n + j], lr[i], lc[j], logsigmoidf(z0[i]) + l1);
-            if (v > best || (v == best && i < bi)) { best = v; bi = i; }
+    if (j < a.n) {
+        const float cm = cmax[a.rb + j], cl = clog[a.rb + j], l1 = lz[a.rb + j];
+        for (int i = i0 + wave; i < min(a.m, i0 + CH); i += 4) {
+            const float v = lg_score(Sall[a.soff + (size_t)i * a.n + j] * 0.0625f, rmax[a.ra + i], rlog[a.ra + i], cm,
+                                     cl, lz[a.ra + i] + l1);
+            if (v > best || (v == best && i < bi)) {
+                best = v;
+                bi = i;
+            }
         }
     }
     sb[wave][lane] = best;
     si[wave][lane] = bi;
     __syncthreads();
-    if (wave == 0 && j < n) {
+    if (wave == 0 && j < a.n) {
         for (int w = 1; w < 4; ++w)
-            if (sb[w][lane] > best || (sb[w][lane] == best && si[w][lane] < bi)) { best = sb[w][lane]; bi = si[w][lane]; }
-        arg[j] = bi;
+            if (sb[w][lane] > best || (sb[w][lane] == best && si[w][lane] < bi)) {
+                best = sb[w][lane];
+                bi = si[w][lane];
+            }
+        part[((size_t)blockIdx.z * (kmax / CH + 1) + blockIdx.y) * kmax + j] = make_float2(best, __int_as_float(bi));
     }
 }
 
+__global__ void k_asg_colargfinal(const Asg* __restrict__ tab, const float2* __restrict__ part, int kmax,
+                                  int* __restrict__ arg) {
+    const Asg a = tab[blockIdx.y];
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= a.n) return;
+    const int nch = (a.m + CH - 1) / CH;
+    const float2* p = part + (size_t)blockIdx.y * (kmax / CH + 1) * kmax + j;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = 0; c < nch; ++c) {
+        const float2 q = p[(size_t)c * kmax];
+        const int qi = __float_as_int(q.y);
+        if (q.x > best || (q.x == best && qi < bi)) {
+            best = q.x;
+            bi = qi;
+        }
+    }
+    arg[a.rb + j] = bi;
+}
+
 // mutual nearest + exp(score) > th -> matches (ind0[i], ind1[m0[i]]) in row order.
-// One workgroup per pair.
-__global__ __launch_bounds__(256) void k_lg_filter(const int* __restrict__ a0, const float* __restrict__ v0,
-                                                   const int* __restrict__ a1, int m, const int32_t* __restrict__ ind0,
-                                                   const int32_t* __restrict__ ind1, float th,
-                                                   int32_t* __restrict__ matches, float* __restrict__ scores,
-                                                   int32_t* __restrict__ count) {
+// One workgroup per finishing pair.
+__global__ __launch_bounds__(256) void k_lg_filter(const Asg* __restrict__ tab, const int* __restrict__ arg,
+                                                   const float* __restrict__ val, const int32_t* __restrict__ ind,
+                                                   float th, int kmax, int32_t* __restrict__ matches,
+                                                   float* __restrict__ scores, int32_t* __restrict__ count) {
+    const Asg a = tab[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ int wsum[4];
     __shared__ int base_sh;
     if (tid == 0) base_sh = 0;
     __syncthreads();
-    for (int c0 = 0; c0 < m; c0 += 256) {
+    int32_t* mo = matches + (size_t)a.pair * kmax * 2;
+    float* so = scores + (size_t)a.pair * kmax;
+    for (int c0 = 0; c0 < a.m; c0 += 256) {
         const int i = c0 + tid;
         bool ok = false;
         float sc = 0.f;
-        if (i < m) {
-            const int j = a0[i];
-            const bool mutual = a1[j] == i;
-            sc = mutual ? expf(v0[i]) : 0.f;
+        int j = 0;
+        if (i < a.m) {
+            j = arg[a.ra + i];
+            const bool mutual = arg[a.rb + j] == i;
+            sc = mutual ? expf(val[a.ra + i]) : 0.f;
             ok = mutual && sc > th;
         }
         int v = ok;
@@ -432,35 +445,35 @@ __global__ __launch_bounds__(256) void k_lg_filter(const int* __restrict__ a0, c
         for (int w = 0; w < wave; ++w) off += wsum[w];
         if (ok) {
             const int slot = off + v - 1;
-            matches[2 * slot] = ind0[i];
-            matches[2 * slot + 1] = ind1[a0[i]];
-            scores[slot] = sc;
+            mo[2 * slot] = ind[a.ra + i];
+            mo[2 * slot + 1] = ind[a.rb + j];
+            so[slot] = sc;
         }
         __syncthreads();
         if (tid == 0) base_sh += wsum[0] + wsum[1] + wsum[2] + wsum[3];
         __syncthreads();
     }
-    if (tid == 0) *count = base_sh;
-}
-
-__global__ void k_scale(float* p, long n, float s) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) p[e] *= s;
+    if (tid == 0) count[a.pair] = base_sh;
 }
 
 size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct LgLayout {
-    size_t x, cat, ecos, esin, ind, x2, cat2, ecos2, esin2, ind2, qkv, Q, K, Vt, ctx, hf, hb, live, z, keep, stats,
-        segs, tasks, outoff, moves, mdesc, S, lr, lc, arg0, val0, arg1, total;
+    size_t x, cat, ecos, esin, ind, x2, cat2, ecos2, esin2, ind2, Q, K, Vt, ctx, hf, hb, live, rowseg, lz, keep,
+        stats, segs, tasks, outoff, moves, mdesc, rmax, rlog, cmax, clog, arg, val, part, asg, S, total;
+    int asg_cap;
 };
 
 LgLayout lg_layout(int P, int kmax) {
     const size_t N = (size_t)2 * P * (((size_t)kmax + 63) & ~(size_t)63);
-    const size_t K2 = (size_t)kmax * kmax;
     LgLayout L;
+    L.asg_cap = std::min(P, 64);
     size_t o = 0;
-    auto take = [&](size_t bytes) { size_t r = o; o += a256(bytes); return r; };
+    auto take = [&](size_t bytes) {
+        size_t r = o;
+        o += a256(bytes);
+        return r;
+    };
     L.x = take(N * LG_D * 4);
     L.cat = take(N * 512 * 2);
     L.ecos = take(N * 32 * 4);
@@ -471,7 +484,6 @@ LgLayout lg_layout(int P, int kmax) {
     L.ecos2 = take(N * 32 * 4);
     L.esin2 = take(N * 32 * 4);
     L.ind2 = take(N * 4);
-    L.qkv = take(N * 768 * 4);
     L.Q = take(N * LG_D * 2);
     L.K = take(N * LG_D * 2);
     L.Vt = take(N * LG_D * 2);
@@ -479,7 +491,8 @@ LgLayout lg_layout(int P, int kmax) {
     L.hf = take(N * 512 * 4);
     L.hb = take(N * 512 * 2);
     L.live = take(N);
-    L.z = take(N * 4);
+    L.rowseg = take(N * 4);
+    L.lz = take(N * 4);
     L.keep = take(N);
     L.stats = take((size_t)2 * P * 2 * 4);
     L.segs = take((size_t)2 * P * sizeof(Seg));
@@ -487,12 +500,15 @@ LgLayout lg_layout(int P, int kmax) {
     L.outoff = take((size_t)4 * P * 4);
     L.moves = take((size_t)2 * P * sizeof(int4));
     L.mdesc = take(N * LG_D * 4);
-    L.S = take(K2 * 4);
-    L.lr = take((size_t)kmax * 4);
-    L.lc = take((size_t)kmax * 4);
-    L.arg0 = take((size_t)kmax * 4);
-    L.val0 = take((size_t)kmax * 4);
-    L.arg1 = take((size_t)kmax * 4);
+    L.rmax = take(N * 4);
+    L.rlog = take(N * 4);
+    L.cmax = take(N * 4);
+    L.clog = take(N * 4);
+    L.arg = take(N * 4);
+    L.val = take(N * 4);
+    L.part = take((size_t)L.asg_cap * (kmax / CH + 1) * kmax * sizeof(float2));
+    L.asg = take((size_t)P * sizeof(Asg));
+    L.S = take((size_t)L.asg_cap * kmax * kmax * 4);
     L.total = o;
     return L;
 }
@@ -533,7 +549,6 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     float* EC2 = (float*)(base + L.ecos2);
     float* ES2 = (float*)(base + L.esin2);
     int32_t* IND2 = (int32_t*)(base + L.ind2);
-    float* QKV = (float*)(base + L.qkv);
     bf16_t* Q = (bf16_t*)(base + L.Q);
     bf16_t* K = (bf16_t*)(base + L.K);
     bf16_t* VT = (bf16_t*)(base + L.Vt);
@@ -541,7 +556,8 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     float* HF = (float*)(base + L.hf);
     bf16_t* HB = (bf16_t*)(base + L.hb);
     uint8_t* LIVE = (uint8_t*)(base + L.live);
-    float* Z = (float*)(base + L.z);
+    int* ROWSEG = (int*)(base + L.rowseg);
+    float* LZ = (float*)(base + L.lz);
     uint8_t* KEEP = (uint8_t*)(base + L.keep);
     int* STATS = (int*)(base + L.stats);
     Seg* SEGS = (Seg*)(base + L.segs);
@@ -549,12 +565,15 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     int* OUTOFF = (int*)(base + L.outoff);
     int4* MOVES = (int4*)(base + L.moves);
     float* MD = (float*)(base + L.mdesc);
+    float* RMAX = (float*)(base + L.rmax);
+    float* RLOG = (float*)(base + L.rlog);
+    float* CMAX = (float*)(base + L.cmax);
+    float* CLOG = (float*)(base + L.clog);
+    int* ARG = (int*)(base + L.arg);
+    float* VAL = (float*)(base + L.val);
+    float2* PART = (float2*)(base + L.part);
+    Asg* ASG = (Asg*)(base + L.asg);
     float* SS = (float*)(base + L.S);
-    float* LR = (float*)(base + L.lr);
-    float* LC = (float*)(base + L.lc);
-    int* A0 = (int*)(base + L.arg0);
-    float* V0 = (float*)(base + L.val0);
-    int* A1 = (int*)(base + L.arg1);
 
     // Host tables below are uploaded with hipMemcpyAsync on `s` and only rewritten after
     // the stream has been synchronised (the per-layer statistics read-back), so the
@@ -565,6 +584,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     std::vector<int4> h_tasks;
     std::vector<int> h_out;
     std::vector<int4> h_moves;
+    std::vector<Asg> h_asg;
     int off = 0;
     if (hipMemsetAsync(nmatch, 0, sizeof(int32_t) * P, s) != hipSuccess) return MLG_EHIP;
     for (int p = 0; p < P; ++p) {
@@ -583,7 +603,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     int Npad = off;
     int maxq = 0;
     auto upload_layout = [&]() -> int {
-        // segments, live-row mask, self / cross attention task lists
+        // segments, live-row mask / row -> segment map, self and cross attention tasks
         h_tasks.clear();
         h_out.clear();
         maxq = 0;
@@ -605,7 +625,8 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
                 hipSuccess ||
             hipMemcpyAsync(OUTOFF, h_out.data(), h_out.size() * sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess)
             return MLG_EHIP;
-        hipLaunchKernelGGL(k_lg_live, dim3((Npad + 255) / 256), dim3(256), 0, s, SEGS, (int)segs.size(), LIVE, Npad);
+        hipLaunchKernelGGL(k_lg_live, dim3((Npad + 255) / 256), dim3(256), 0, s, SEGS, (int)segs.size(), LIVE, ROWSEG,
+                           Npad);
         MLG_LAUNCH_CHECK();
         return MLG_OK;
     };
@@ -623,72 +644,90 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         LG_TRY(mlg_gemm_bias_bf16_ld(CTX, LG_D, bw.Wout, bw.bout, CAT + LG_D, 512, Npad, LG_D, LG_D, s));
         LG_TRY(mlg_gemm_bias_f32_ld(CAT, 512, bw.Wf1, bw.bf1, HF, 512, Npad, 512, 512, s));
         hipLaunchKernelGGL(k_lg_ln_gelu, dim3((Npad + 3) / 4), dim3(256), 0, s, HF, bw.ln_g, bw.ln_b, HB, Npad);
-        LG_TRY(mlg_gemm_residual_ld(HB, 512, bw.Wf2, bw.bf2, w.ones, X, LG_D, Npad, LG_D, 512, s));
-        const long n = (long)Npad * LG_D;
-        hipLaunchKernelGGL(k_lg_sync, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, X, CAT, n);
         MLG_LAUNCH_CHECK();
-        return MLG_OK;
+        return mlg_gemm_residual_copy(HB, 512, bw.Wf2, bw.bf2, X, LG_D, CAT, 512, Npad, LG_D, 512, s);
     };
-    // assignment + filter for the segment pair (sa, sb) of pair p at layer i
-    auto assign = [&](int i, const Seg& sa, const Seg& sb, int p) -> int {
-        const int m = sa.len, n = sb.len;
-        float* m0 = MD + (size_t)sa.off * LG_D;
-        float* m1 = MD + (size_t)sb.off * LG_D;
-        LG_TRY(mlg_similarity_f32(m0, m, m1, n, LG_D, SS, n, s));
-        const long nn = (long)m * n;
-        hipLaunchKernelGGL(k_scale, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, s, SS, nn, 1.0f / 16.0f);
-        hipLaunchKernelGGL(k_lg_row_lse, dim3((m + 3) / 4), dim3(256), 0, s, SS, m, n, LR);
-        hipLaunchKernelGGL(k_lg_col_lse, dim3((n + 63) / 64), dim3(256), 0, s, SS, m, n, LC);
-        hipLaunchKernelGGL(k_lg_row_arg, dim3((m + 3) / 4), dim3(256), 0, s, SS, m, n, LR, LC, Z + sa.off,
-                           Z + sb.off, A0, V0);
-        hipLaunchKernelGGL(k_lg_col_arg, dim3((n + 63) / 64), dim3(256), 0, s, SS, m, n, LR, LC, Z + sa.off,
-                           Z + sb.off, A1);
-        hipLaunchKernelGGL(k_lg_filter, dim3(1), dim3(256), 0, s, A0, V0, A1, m, IND + sa.off, IND + sb.off,
-                           filter_thr, matches + (size_t)p * kmax * 2, mscores + (size_t)p * kmax, nmatch + p);
-        MLG_LAUNCH_CHECK();
-        if (stop_layer) stop_layer[p] = i + 1;
-        (void)i;
-        return MLG_OK;
+    // matchability log-sigmoid of every live token (layer i's head)
+    auto certainty = [&](int i) {
+        hipLaunchKernelGGL(k_lg_conf, dim3((Npad + 3) / 4), dim3(256), 0, s, ROWSEG, Npad, X, (const float*)nullptr,
+                           (const float*)nullptr, w.wmatch[i], w.bmatch[i], 0.f, 0.f, LZ, KEEP, STATS);
     };
-    auto final_proj = [&](int i) -> int {
-        // mdesc = final_proj(x) for every token (the scale 1/4 per side folds into S / 16)
-        return mlg_gemm_bias_f32_ld(CAT, 512, w.Wfinal[i], w.bfinal[i], MD, LG_D, Npad, LG_D, LG_D, s);
+    // assignment + filter of the listed segment pairs (k = index of image a's segment)
+    auto assign = [&](int i, const std::vector<size_t>& ks) -> int {
+        // mdesc = final_proj(x) for every token; the 1/4 per side folds into S / 16
+        LG_TRY(mlg_gemm_bias_f32_ld(CAT, 512, w.Wfinal[i], w.bfinal[i], MD, LG_D, Npad, LG_D, LG_D, s));
+        for (size_t c0 = 0; c0 < ks.size(); c0 += L.asg_cap) {
+            const size_t c1 = std::min(ks.size(), c0 + L.asg_cap);
+            if (c0 > 0 && hipStreamSynchronize(s) != hipSuccess) return MLG_EHIP;  // h_asg reuse
+            h_asg.clear();
+            int maxm = 0, maxn = 0;
+            for (size_t c = c0; c < c1; ++c) {
+                const Seg sa = segs[ks[c]], sb = segs[ks[c] + 1];
+                Asg a;
+                a.m = sa.len;
+                a.n = sb.len;
+                a.ra = sa.off;
+                a.rb = sb.off;
+                a.soff = (long)(c - c0) * kmax * kmax;
+                a.pair = pair_of[ks[c] / 2];
+                a.pad = 0;
+                h_asg.push_back(a);
+                maxm = std::max(maxm, a.m);
+                maxn = std::max(maxn, a.n);
+                LG_TRY(mlg_similarity_f32(MD + (size_t)sa.off * LG_D, sa.len, MD + (size_t)sb.off * LG_D, sb.len, LG_D,
+                                          SS + a.soff, sb.len, s));
+                if (stop_layer) stop_layer[a.pair] = i + 1;
+            }
+            const unsigned na = (unsigned)h_asg.size();
+            if (hipMemcpyAsync(ASG, h_asg.data(), na * sizeof(Asg), hipMemcpyHostToDevice, s) != hipSuccess)
+                return MLG_EHIP;
+            const dim3 rows((maxm + 3) / 4, na), cols((maxn + 63) / 64, (maxm + CH - 1) / CH, na),
+                cfin((maxn + 255) / 256, na);
+            hipLaunchKernelGGL(k_asg_rowlse, rows, dim3(256), 0, s, ASG, SS, RMAX, RLOG);
+            hipLaunchKernelGGL(k_asg_colpart, cols, dim3(256), 0, s, ASG, SS, PART, kmax);
+            hipLaunchKernelGGL(k_asg_colfinal, cfin, dim3(256), 0, s, ASG, PART, kmax, CMAX, CLOG);
+            hipLaunchKernelGGL(k_asg_rowarg, rows, dim3(256), 0, s, ASG, SS, RMAX, RLOG, CMAX, CLOG, LZ, ARG, VAL);
+            hipLaunchKernelGGL(k_asg_colargpart, cols, dim3(256), 0, s, ASG, SS, RMAX, RLOG, CMAX, CLOG, LZ, PART,
+                               kmax);
+            hipLaunchKernelGGL(k_asg_colargfinal, cfin, dim3(256), 0, s, ASG, PART, kmax, ARG);
+            hipLaunchKernelGGL(k_lg_filter, dim3(na), dim3(256), 0, s, ASG, ARG, VAL, IND, filter_thr, kmax, matches,
+                               mscores, nmatch);
+            MLG_LAUNCH_CHECK();
+        }
+        return MLG_OK;
     };
 
     std::vector<int> stats(segs.size() * 2);
     for (int i = 0; i < LG_L && !segs.empty(); ++i) {
-        // self block
-        LG_TRY(mlg_gemm_bias_f32_ld(CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, QKV, 768, Npad, 768, LG_D, s));
-        const long nh = (long)Npad * LG_H * 32;
-        hipLaunchKernelGGL(k_lg_heads_self, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, s, QKV, EC, ES, LIVE,
-                           Npad, Q, K, VT);
+        // self block: projection + rotary + head split fused in the GEMM epilogue
+        LG_TRY(mlg_gemm_lg_self(CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, LG_D, s));
         LG_TRY(attention(false));
         LG_TRY(ffn(w.self[i]));
         // cross block
-        LG_TRY(mlg_gemm_bias_f32_ld(CAT, 512, w.cross[i].Wqkv, w.cross[i].bqkv, QKV, 512, Npad, 512, LG_D, s));
-        hipLaunchKernelGGL(k_lg_heads_cross, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, s, QKV, LIVE, Npad, Q,
-                           VT);
+        LG_TRY(mlg_gemm_lg_cross(CAT, 512, w.cross[i].Wqkv, w.cross[i].bqkv, LIVE, Q, VT, Npad, LG_D, s));
         LG_TRY(attention(true));
         LG_TRY(ffn(w.cross[i]));
 
         if (i == LG_L - 1) {
-            LG_TRY(final_proj(i));
-            hipLaunchKernelGGL(k_lg_matchability, dim3((unsigned)segs.size()), dim3(256), 0, s, SEGS, X, w.wmatch[i],
-                               w.bmatch[i], Z);
-            for (size_t k = 0; k < segs.size(); k += 2) LG_TRY(assign(i, segs[k], segs[k + 1], pair_of[k / 2]));
+            certainty(i);
+            std::vector<size_t> ks;
+            for (size_t k = 0; k < segs.size(); k += 2) ks.push_back(k);
+            LG_TRY(assign(i, ks));
             break;
         }
         const float thr = conf_threshold(i);
-        hipLaunchKernelGGL(k_lg_conf, dim3((unsigned)segs.size()), dim3(256), 0, s, SEGS, X, w.wconf[i], w.bconf[i],
-                           w.wmatch[i], w.bmatch[i], thr, width_conf, Z, KEEP, STATS);
+        if (hipMemsetAsync(STATS, 0, segs.size() * 2 * sizeof(int), s) != hipSuccess) return MLG_EHIP;
+        hipLaunchKernelGGL(k_lg_conf, dim3((Npad + 3) / 4), dim3(256), 0, s, ROWSEG, Npad, X, w.wconf[i], w.bconf[i],
+                           w.wmatch[i], w.bmatch[i], thr, width_conf, LZ, KEEP, STATS);
         MLG_LAUNCH_CHECK();
         if (hipMemcpyAsync(stats.data(), STATS, segs.size() * 2 * sizeof(int), hipMemcpyDeviceToHost, s) !=
                 hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return MLG_EHIP;
-        // early stop per pair
+        // early stop per pair; point pruning per segment
         std::vector<char> stop(segs.size() / 2, 0);
-        bool any_stop = false, any_prune = false;
+        std::vector<size_t> stopped;
+        bool any_prune = false;
         for (size_t k = 0; k < segs.size(); k += 2) {
             const int p = pair_of[k / 2];
             if (depth_conf > 0.f) {
@@ -696,22 +735,17 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
                 const float ratio = 1.0f - low / (float)orig_total[p];
                 if (ratio > depth_conf) {
                     stop[k / 2] = 1;
-                    any_stop = true;
+                    stopped.push_back(k);
                 }
             }
             if (!stop[k / 2] && width_conf > 0.f)
                 for (int q = 0; q < 2; ++q)
                     if (segs[k + q].len > pruning_min && stats[2 * (k + q) + 1] != segs[k + q].len) any_prune = true;
         }
-        if (any_stop) {
-            LG_TRY(final_proj(i));
-            for (size_t k = 0; k < segs.size(); k += 2)
-                if (stop[k / 2]) LG_TRY(assign(i, segs[k], segs[k + 1], pair_of[k / 2]));
-        }
-        if (!any_stop && !any_prune) continue;
+        if (!stopped.empty()) LG_TRY(assign(i, stopped));  // the matchability lz came with the confidences
+        if (stopped.empty() && !any_prune) continue;
         // compact: drop stopped pairs, prune segments above the threshold
-        std::vector<int4>& moves = h_moves;
-        moves.clear();
+        h_moves.clear();
         std::vector<Seg> nsegs;
         std::vector<int> npair;
         int noff = 0;
@@ -721,17 +755,18 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
                 const Seg sg = segs[k + q];
                 const bool prune = width_conf > 0.f && sg.len > pruning_min;
                 const int nl = prune ? stats[2 * (k + q) + 1] : sg.len;
-                moves.push_back(make_int4(sg.off, sg.len, noff, prune ? 0 : 1));
+                h_moves.push_back(make_int4(sg.off, sg.len, noff, prune ? 0 : 1));
                 nsegs.push_back(Seg{noff, nl, sg.frame, 0});
                 noff += (nl + 63) & ~63;
             }
             npair.push_back(pair_of[k / 2]);
         }
-        if (!moves.empty()) {
-            if (hipMemcpyAsync(MOVES, moves.data(), moves.size() * sizeof(int4), hipMemcpyHostToDevice, s) !=
+        if (!h_moves.empty()) {
+            if (!stopped.empty() && hipStreamSynchronize(s) != hipSuccess) return MLG_EHIP;  // h_asg in flight
+            if (hipMemcpyAsync(MOVES, h_moves.data(), h_moves.size() * sizeof(int4), hipMemcpyHostToDevice, s) !=
                 hipSuccess)
                 return MLG_EHIP;
-            hipLaunchKernelGGL(k_lg_compact, dim3((unsigned)moves.size()), dim3(256), 0, s, MOVES, KEEP, X, EC, ES,
+            hipLaunchKernelGGL(k_lg_compact, dim3((unsigned)h_moves.size()), dim3(256), 0, s, MOVES, KEEP, X, EC, ES,
                                IND, X2, CAT2, EC2, ES2, IND2);
             MLG_LAUNCH_CHECK();
             std::swap(X, X2);
@@ -740,7 +775,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
             std::swap(ES, ES2);
             std::swap(IND, IND2);
         }
-        // empty side after pruning -> no matches for that pair (reference loop break)
+        // an empty side after pruning ends that pair with no matches (reference loop break)
         segs.clear();
         pair_of.clear();
         for (size_t k = 0; k < nsegs.size(); k += 2) {

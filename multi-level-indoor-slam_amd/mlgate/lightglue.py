@@ -26,6 +26,14 @@ class _Weights(ctypes.Structure):
                 ("wconf", ctypes.c_void_p * 8), ("bconf", ctypes.c_void_p * 8), ("ones", ctypes.c_void_p)]
 
 
+def qkv_row_order():
+    """Row permutation of SelfBlock.Wqkv from the reference's (head, 64, 3) interleave
+    (``qkv.unflatten(-1, (heads, -1, 3))``) to [q | k | v] x (head, dim), the layout the
+    fused GEMM epilogue expects (csrc/gemm_bf16.hip EpiLgSelf)."""
+    s, h, d = np.meshgrid(np.arange(3), np.arange(4), np.arange(64), indexing="ij")
+    return (h * 192 + d * 3 + s).reshape(-1)
+
+
 class LightGlueGPU:
     """Batched LightGlue(features='superpoint') on the HIP device."""
 
@@ -56,7 +64,9 @@ class LightGlueGPU:
         for i in range(LG_LAYERS):
             p = f"transformers.{i}.self_attn."
             b = w.self_[i]
-            b.Wqkv, b.bqkv = self._t(sd[p + "Wqkv.weight"], bf), self._t(sd[p + "Wqkv.bias"], f32)
+            perm = qkv_row_order()
+            b.Wqkv = self._t(np.asarray(sd[p + "Wqkv.weight"])[perm], bf)
+            b.bqkv = self._t(np.asarray(sd[p + "Wqkv.bias"])[perm], f32)
             b.Wout, b.bout = self._t(sd[p + "out_proj.weight"], bf), self._t(sd[p + "out_proj.bias"], f32)
             self._ffn(b, sd, p)
             p = f"transformers.{i}.cross_attn."
