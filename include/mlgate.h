@@ -248,14 +248,17 @@ int mlg_recover_pose(const float* kp1, const float* kp2, const int32_t* offsets,
                      int k_stride, const double* E, const uint8_t* mask, double* pose, void* stream);
 
 /* ------------------------------------------------------------- profiling --
- * Per-launch HIP-event timing of selected kernels inside mlg_vit_forward, recorded on
- * the stream the kernel is launched on.  slot: 0 fc1 GEMM, 1 fc2 GEMM, 2 qkv GEMM,
- * 3 proj GEMM, 4 attention.  slot_mask selects the slots recorded (0 = off); a pool
- * of 16384 event pairs is recycled by mlg_prof_read / mlg_prof_reset, which
- * synchronise the recorded events.  Not for use inside graph capture. */
+ * Per-launch HIP-event timing of selected kernels, recorded on the stream the kernel
+ * is launched on, with the algorithmic FLOPs of each launch.  slot: 0 ViT fc1 GEMM,
+ * 1 fc2, 2 qkv, 3 proj, 4 ViT attention, 5 LightGlue attention (ragged, all tasks of
+ * a launch), 6 LightGlue projection / FFN GEMMs, 7 SuperPoint 3x3 convs.  slot_mask
+ * selects the slots recorded (0 = off); a pool of 16384 event pairs is recycled by
+ * mlg_prof_read / mlg_prof_read_work / mlg_prof_reset, which synchronise the recorded
+ * events.  Not for use inside graph capture. */
 int mlg_prof_enable(int slot_mask);
 int mlg_prof_reset(void);
 int mlg_prof_read(int slot, double* total_ms, long* launches);
+int mlg_prof_read_work(int slot, double* flops);
 
 #ifdef __cplusplus
 }

@@ -58,34 +58,15 @@ struct Prof {
     std::mutex mu;
     unsigned mask = 0;  // slots being recorded
     std::vector<hipEvent_t> pool;
-    struct Rec { int slot; hipEvent_t a, b; };
+    struct Rec { int slot; hipEvent_t a, b; double work; };
     std::vector<Rec> recs;
     size_t next = 0;
-    double total[8] = {0};
-    long count[8] = {0};
+    double total[MLG_PROF_SLOTS] = {0};
+    double work[MLG_PROF_SLOTS] = {0};
+    long count[MLG_PROF_SLOTS] = {0};
 } g_prof;
 
 constexpr size_t PROF_POOL = 32768;
-
-struct ProfScope {
-    int slot;
-    hipStream_t s;
-    hipEvent_t a = nullptr, b = nullptr;
-    ProfScope(int slot_, hipStream_t s_) : slot(slot_), s(s_) {
-        if (!(g_prof.mask & (1u << slot))) return;
-        std::lock_guard<std::mutex> lk(g_prof.mu);
-        if (g_prof.next + 2 > g_prof.pool.size()) return;  // pool exhausted: stop recording
-        a = g_prof.pool[g_prof.next++];
-        b = g_prof.pool[g_prof.next++];
-        (void)hipEventRecord(a, s);
-    }
-    ~ProfScope() {
-        if (!a) return;
-        (void)hipEventRecord(b, s);
-        std::lock_guard<std::mutex> lk(g_prof.mu);
-        g_prof.recs.push_back({slot, a, b});
-    }
-};
 
 void prof_collect() {
     for (auto& r : g_prof.recs) {
@@ -93,6 +74,7 @@ void prof_collect() {
         (void)hipEventSynchronize(r.b);
         if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
             g_prof.total[r.slot] += ms;
+            g_prof.work[r.slot] += r.work;
             g_prof.count[r.slot] += 1;
         }
     }
@@ -107,6 +89,22 @@ void prof_collect() {
     } while (0)
 
 }  // namespace
+
+MlgProfScope::MlgProfScope(int slot_, hipStream_t s_, double work_) : slot(slot_), s(s_), work(work_) {
+    if (slot < 0 || slot >= MLG_PROF_SLOTS || !(g_prof.mask & (1u << slot))) return;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    if (g_prof.next + 2 > g_prof.pool.size()) return;  // pool exhausted: stop recording
+    a = g_prof.pool[g_prof.next++];
+    b = g_prof.pool[g_prof.next++];
+    (void)hipEventRecord(a, s);
+}
+
+MlgProfScope::~MlgProfScope() {
+    if (!a) return;
+    (void)hipEventRecord(b, s);
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    g_prof.recs.push_back({slot, a, b, work});
+}
 
 extern "C" {
 
@@ -149,24 +147,24 @@ int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, 
         const mlg_vit_block& bl = w->blocks[l];
         TRY(mlg_layernorm_bf16(ws.x, bl.norm1_w, bl.norm1_b, ws.xn, M, s));
         {
-            ProfScope p(2, s);
+            MlgProfScope p(2, s, 2.0 * M * 2304 * 768);
             TRY(mlg_gemm_qkv(ws.xn, bl.qkv_w, bl.qkv_b, ws.q, ws.k, ws.vt, M, g.T, g.Tpad, s));
         }
         {
-            ProfScope p(4, s);
+            MlgProfScope p(4, s, 4.0 * g.B * 12 * (double)g.T * g.T * 64);
             TRY(mlg_attention(ws.q, ws.k, ws.vt, ws.o, g.B, g.T, g.Tpad, s));
         }
         {
-            ProfScope p(3, s);
+            MlgProfScope p(3, s, 2.0 * M * 768 * 768);
             TRY(mlg_gemm_residual(ws.o, bl.proj_w, bl.proj_b, bl.ls1, ws.x, M, 768, 768, s));
         }
         TRY(mlg_layernorm_bf16(ws.x, bl.norm2_w, bl.norm2_b, ws.xn, M, s));
         {
-            ProfScope p(0, s);
+            MlgProfScope p(0, s, 2.0 * M * 3072 * 768);
             TRY(mlg_gemm_bias_gelu_bf16(ws.xn, bl.fc1_w, bl.fc1_b, ws.h, M, 3072, 768, s));
         }
         {
-            ProfScope p(1, s);
+            MlgProfScope p(1, s, 2.0 * M * 768 * 3072);
             TRY(mlg_gemm_residual(ws.h, bl.fc2_w, bl.fc2_b, bl.ls2, ws.x, M, 768, 3072, s));
         }
     }
@@ -363,23 +361,35 @@ int mlg_prof_enable(int slot_mask) {
         for (auto& e : g_prof.pool)
             if (hipEventCreate(&e) != hipSuccess) return MLG_EHIP;
     }
-    g_prof.mask = (unsigned)slot_mask & 0xffu;
+    g_prof.mask = (unsigned)slot_mask & ((1u << MLG_PROF_SLOTS) - 1);
     return MLG_OK;
 }
 
 int mlg_prof_reset(void) {
     std::lock_guard<std::mutex> lk(g_prof.mu);
     prof_collect();
-    for (int i = 0; i < 8; ++i) { g_prof.total[i] = 0; g_prof.count[i] = 0; }
+    for (int i = 0; i < MLG_PROF_SLOTS; ++i) {
+        g_prof.total[i] = 0;
+        g_prof.work[i] = 0;
+        g_prof.count[i] = 0;
+    }
     return MLG_OK;
 }
 
 int mlg_prof_read(int slot, double* total_ms, long* launches) {
-    if (slot < 0 || slot >= 8 || !total_ms || !launches) return MLG_EINVAL;
+    if (slot < 0 || slot >= MLG_PROF_SLOTS || !total_ms || !launches) return MLG_EINVAL;
     std::lock_guard<std::mutex> lk(g_prof.mu);
     prof_collect();
     *total_ms = g_prof.total[slot];
     *launches = g_prof.count[slot];
+    return MLG_OK;
+}
+
+int mlg_prof_read_work(int slot, double* flops) {
+    if (slot < 0 || slot >= MLG_PROF_SLOTS || !flops) return MLG_EINVAL;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    prof_collect();
+    *flops = g_prof.work[slot];
     return MLG_OK;
 }
 

@@ -9,6 +9,20 @@
 
 typedef uint16_t bf16_t;
 
+// HIP-event profiling scope (abi.cpp): records the launches between construction and
+// destruction on stream s into `slot` with `work` algorithmic FLOPs (or bytes).
+// Slots: 0 fc1, 1 fc2, 2 qkv, 3 proj, 4 ViT attention, 5 LightGlue attention,
+// 6 LightGlue projections / FFN GEMMs, 7 SuperPoint 3x3 convs.
+#define MLG_PROF_SLOTS 8
+struct MlgProfScope {
+    int slot;
+    hipStream_t s;
+    double work;
+    hipEvent_t a = nullptr, b = nullptr;
+    MlgProfScope(int slot, hipStream_t s, double work);
+    ~MlgProfScope();
+};
+
 // gemm_bf16.hip -- C = epi(A[M,K] . W[N,K]^T), N % 128 == 0, K % 64 == 0
 int mlg_gemm_f32out(const bf16_t* A, const bf16_t* W, float* C, int M, int N, int K, hipStream_t s);
 int mlg_gemm_f32out_variant(int variant, const bf16_t* A, const bf16_t* W, float* C, int M, int N, int K,

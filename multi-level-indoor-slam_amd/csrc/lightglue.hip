@@ -33,25 +33,26 @@ struct Seg {
 };
 
 // ------------------------------------------------------------------ init
-// One workgroup per segment: normalize_keypoints (size = 1 + max - min), Fourier
-// positional encoding (cos / sin of Wr . k, 32 frequencies), x = desc, cat[:, :256] =
-// bf16(desc), ind = source index; rows past len zeroed.
-__global__ __launch_bounds__(256) void k_lg_init(const Seg* __restrict__ segs, const float* __restrict__ kpts,
-                                                 const float* __restrict__ desc, int kmax,
-                                                 const float* __restrict__ Wr, float* __restrict__ x,
-                                                 bf16_t* __restrict__ cat, float* __restrict__ ecos,
-                                                 float* __restrict__ esin, int32_t* __restrict__ ind) {
+// normalize_keypoints without image_size: size = 1 + max - min per image,
+// k' = (k - size / 2) / (max(size) / 2).  One workgroup per segment -> norm[seg] =
+// (shift_x, shift_y, scale).
+__global__ __launch_bounds__(256) void k_lg_kpnorm(const Seg* __restrict__ segs, const float* __restrict__ kpts,
+                                                   int kmax, float4* __restrict__ norm) {
     const Seg sg = segs[blockIdx.x];
     const int tid = threadIdx.x;
     const float* kp = kpts + (size_t)sg.frame * kmax * 2;
-    const float* ds = desc + (size_t)sg.frame * kmax * LG_D;
     __shared__ float red[4][256];
     float mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY;
     for (int i = tid; i < sg.len; i += 256) {
-        mnx = fminf(mnx, kp[2 * i]); mxx = fmaxf(mxx, kp[2 * i]);
-        mny = fminf(mny, kp[2 * i + 1]); mxy = fmaxf(mxy, kp[2 * i + 1]);
+        mnx = fminf(mnx, kp[2 * i]);
+        mxx = fmaxf(mxx, kp[2 * i]);
+        mny = fminf(mny, kp[2 * i + 1]);
+        mxy = fmaxf(mxy, kp[2 * i + 1]);
     }
-    red[0][tid] = mnx; red[1][tid] = mny; red[2][tid] = mxx; red[3][tid] = mxy;
+    red[0][tid] = mnx;
+    red[1][tid] = mny;
+    red[2][tid] = mxx;
+    red[3][tid] = mxy;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
         if (tid < o) {
@@ -62,30 +63,51 @@ __global__ __launch_bounds__(256) void k_lg_init(const Seg* __restrict__ segs, c
         }
         __syncthreads();
     }
-    const float sx = 1.f + red[2][0] - red[0][0], sy = 1.f + red[3][0] - red[1][0];
-    const float shx = sx / 2.f, shy = sy / 2.f, scale = fmaxf(sx, sy) / 2.f;
-    const int padded = (sg.len + 63) & ~63;
-    for (int i = tid; i < padded; i += 256) {
+    if (tid == 0) {
+        const float sx = 1.f + red[2][0] - red[0][0], sy = 1.f + red[3][0] - red[1][0];
+        norm[blockIdx.x] = make_float4(sx / 2.f, sy / 2.f, fmaxf(sx, sy) / 2.f, 0.f);
+    }
+}
+
+// 64 rows of one segment per workgroup: Fourier positional encoding (cos / sin of
+// Wr . k', 32 frequencies), x = desc, cat[:, :256] = bf16(desc), ind = source index;
+// rows past len zeroed.
+__global__ __launch_bounds__(256) void k_lg_init(const Seg* __restrict__ segs, const float4* __restrict__ norm,
+                                                 const float* __restrict__ kpts, const float* __restrict__ desc,
+                                                 int kmax, const float* __restrict__ Wr, float* __restrict__ x,
+                                                 bf16_t* __restrict__ cat, float* __restrict__ ecos,
+                                                 float* __restrict__ esin, int32_t* __restrict__ ind) {
+    const Seg sg = segs[blockIdx.y];
+    const int r0 = blockIdx.x * 64;
+    if (r0 >= ((sg.len + 63) & ~63)) return;
+    const float4 nm = norm[blockIdx.y];
+    const float* kp = kpts + (size_t)sg.frame * kmax * 2;
+    const float* ds = desc + (size_t)sg.frame * kmax * LG_D;
+    for (int e = threadIdx.x; e < 64 * 32; e += 256) {
+        const int i = r0 + e / 32, f = e % 32;
         const size_t r = (size_t)sg.off + i;
         const bool live = i < sg.len;
-        float kx = 0.f, ky = 0.f;
+        float c = 0.f, sn = 0.f;
         if (live) {
-            kx = (kp[2 * i] - shx) / scale;
-            ky = (kp[2 * i + 1] - shy) / scale;
+            const float kx = (kp[2 * i] - nm.x) / nm.z, ky = (kp[2 * i + 1] - nm.y) / nm.z;
+            const float pr = kx * Wr[2 * f] + ky * Wr[2 * f + 1];
+            c = cosf(pr);
+            sn = sinf(pr);
         }
-        for (int f = 0; f < 32; ++f) {
-            const float pr = live ? kx * Wr[2 * f] + ky * Wr[2 * f + 1] : 0.f;
-            ecos[r * 32 + f] = live ? cosf(pr) : 0.f;
-            esin[r * 32 + f] = live ? sinf(pr) : 0.f;
-        }
-        ind[r] = live ? i : -1;
+        ecos[r * 32 + f] = c;
+        esin[r * 32 + f] = sn;
+        if (f == 0) ind[r] = live ? i : -1;
     }
-    for (int e = tid; e < padded * LG_D; e += 256) {
-        const int i = e / LG_D, c = e % LG_D;
+    for (int e = threadIdx.x; e < 64 * LG_D / 4; e += 256) {
+        const int i = r0 + e / (LG_D / 4), c4 = (e % (LG_D / 4)) * 4;
         const size_t r = (size_t)sg.off + i;
-        const float v = i < sg.len ? ds[(size_t)i * LG_D + c] : 0.f;
-        x[r * LG_D + c] = v;
-        cat[r * 512 + c] = f32_to_bf16(v);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < sg.len) v = *reinterpret_cast<const float4*>(ds + (size_t)i * LG_D + c4);
+        *reinterpret_cast<float4*>(x + r * LG_D + c4) = v;
+        uint2 o;
+        o.x = pack_bf16x2(v.x, v.y);
+        o.y = pack_bf16x2(v.z, v.w);
+        *reinterpret_cast<uint2*>(cat + r * 512 + c4) = o;
     }
 }
 
@@ -122,18 +144,20 @@ __global__ __launch_bounds__(256) void k_lg_ln_gelu(const float* __restrict__ hf
 
 // ------------------------------------------------------------------ confidences
 // One wave per live token: conf = sigmoid(x . wc + bc), z = x . wm + bm; lz = logsigmoid(z)
-// (the assignment's certainty term); keep = sigmoid(z) > 1 - width or conf <= thr.
-// stats[seg] += {#(conf < thr), #keep}  (zeroed by the caller).  wc == nullptr: only lz.
+// (the assignment's certainty term); flags[r] = (conf < thr) | keep << 1 with
+// keep = sigmoid(z) > 1 - width or conf <= thr.  wc == nullptr: only lz.
 __global__ __launch_bounds__(256) void k_lg_conf(const int* __restrict__ rowseg, int Npad, const float* __restrict__ x,
                                                  const float* __restrict__ wc, const float* __restrict__ bc,
                                                  const float* __restrict__ wm, const float* __restrict__ bm,
                                                  float thr, float width_conf, float* __restrict__ lz,
-                                                 uint8_t* __restrict__ keep, int* __restrict__ stats) {
+                                                 uint8_t* __restrict__ flags) {
     const int lane = threadIdx.x & 63;
     const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= Npad) return;
-    const int sg = rowseg[r];
-    if (sg < 0) return;
+    if (rowseg[r] < 0) {
+        if (lane == 0 && wc) flags[r] = 0;
+        return;
+    }
     const float* xr = x + r * LG_D;
     float a = 0.f, m = 0.f;
 #pragma unroll
@@ -149,10 +173,30 @@ __global__ __launch_bounds__(256) void k_lg_conf(const int* __restrict__ rowseg,
         if (wc) {
             const float conf = sigmoidf(a);
             const bool k = sigmoidf(m) > 1.f - width_conf || conf <= thr;
-            keep[r] = k;
-            if (conf < thr) atomicAdd(&stats[2 * sg], 1);
-            if (k) atomicAdd(&stats[2 * sg + 1], 1);
+            flags[r] = (uint8_t)((conf < thr) | (k << 1));
         }
+    }
+}
+
+// stats[seg] = {#(conf < thr), #keep}: one workgroup per segment
+__global__ __launch_bounds__(256) void k_lg_segstats(const Seg* __restrict__ segs, const uint8_t* __restrict__ flags,
+                                                     int* __restrict__ stats) {
+    const Seg sg = segs[blockIdx.x];
+    int low = 0, kp = 0;
+    for (int i = threadIdx.x; i < sg.len; i += 256) {
+        const uint8_t f = flags[sg.off + i];
+        low += f & 1;
+        kp += f >> 1;
+    }
+    low = wave_sum((float)low) + 0.5f;  // exact for counts < 2^24
+    kp = wave_sum((float)kp) + 0.5f;
+    __shared__ int sh[2][4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) { sh[0][wave] = low; sh[1][wave] = kp; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        stats[2 * blockIdx.x] = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
+        stats[2 * blockIdx.x + 1] = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
     }
 }
 
@@ -173,7 +217,7 @@ __global__ __launch_bounds__(256) void k_lg_compact(const int4* __restrict__ mov
     const int per = (mv.y + 255) / 256;
     const int a0 = tid * per, a1 = min(mv.y, a0 + per);
     int c = 0;
-    for (int i = a0; i < a1; ++i) c += mv.w ? 1 : keep[mv.x + i];
+    for (int i = a0; i < a1; ++i) c += mv.w ? 1 : (keep[mv.x + i] >> 1);
     // block exclusive scan of c
     int v = c;
     const int lane = tid & 63, wave = tid >> 6;
@@ -186,7 +230,7 @@ __global__ __launch_bounds__(256) void k_lg_compact(const int4* __restrict__ mov
     int base = 0;
     for (int w = 0; w < wave; ++w) base += wsum[w];
     int r = base + v - c;
-    for (int i = a0; i < a1; ++i) rank[i] = (mv.w || keep[mv.x + i]) ? r++ : -1;
+    for (int i = a0; i < a1; ++i) rank[i] = (mv.w || (keep[mv.x + i] >> 1)) ? r++ : -1;
     const int newlen = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     __syncthreads();
     const int padded = (newlen + 63) & ~63;
@@ -460,7 +504,7 @@ size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct LgLayout {
     size_t x, cat, ecos, esin, ind, x2, cat2, ecos2, esin2, ind2, Q, K, Vt, ctx, hf, hb, live, rowseg, lz, keep,
-        stats, segs, tasks, outoff, moves, mdesc, rmax, rlog, cmax, clog, arg, val, part, asg, S, total;
+        stats, segs, tasks, outoff, moves, mdesc, rmax, rlog, cmax, clog, arg, val, part, asg, norm, S, total;
     int asg_cap;
 };
 
@@ -508,6 +552,7 @@ LgLayout lg_layout(int P, int kmax) {
     L.val = take(N * 4);
     L.part = take((size_t)L.asg_cap * (kmax / CH + 1) * kmax * sizeof(float2));
     L.asg = take((size_t)P * sizeof(Asg));
+    L.norm = take((size_t)2 * P * sizeof(float4));
     L.S = take((size_t)L.asg_cap * kmax * kmax * 4);
     L.total = o;
     return L;
@@ -631,26 +676,43 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         return MLG_OK;
     };
     LG_TRY(upload_layout());
-    hipLaunchKernelGGL(k_lg_init, dim3((unsigned)segs.size()), dim3(256), 0, s, SEGS, kpts, desc, kmax, w.Wr, X, CAT,
-                       EC, ES, IND);
+    hipLaunchKernelGGL(k_lg_kpnorm, dim3((unsigned)segs.size()), dim3(256), 0, s, SEGS, kpts, kmax, (float4*)(base + L.norm));
+    hipLaunchKernelGGL(k_lg_init, dim3((unsigned)((kmax + 63) / 64), (unsigned)segs.size()), dim3(256), 0, s, SEGS,
+                       (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X, CAT, EC, ES, IND);
     MLG_LAUNCH_CHECK();
 
+    auto live_tokens = [&]() {
+        double t = 0;
+        for (const Seg& sg : segs) t += sg.len;
+        return t;
+    };
     auto attention = [&](bool cross) -> int {
         const int nt = (int)segs.size();
         const int o = cross ? nt : 0;
+        double work = 0;  // 4 * heads * q * kv * 64 per task (QK^T and PV)
+        for (size_t k = 0; k < segs.size(); k += 2) {
+            const double a = segs[k].len, b = segs[k + 1].len;
+            work += 4.0 * LG_H * 64 * (cross ? 2 * a * b : a * a + b * b);
+        }
+        MlgProfScope prof(5, s, work);
         return mlg_attention_varlen(Q, cross ? Q : K, VT, CTX, LG_D, Npad, LG_H, TASKS + o, OUTOFF + o, nt, maxq, s);
     };
     auto ffn = [&](const mlg_lg_block_i& bw) -> int {
-        LG_TRY(mlg_gemm_bias_bf16_ld(CTX, LG_D, bw.Wout, bw.bout, CAT + LG_D, 512, Npad, LG_D, LG_D, s));
-        LG_TRY(mlg_gemm_bias_f32_ld(CAT, 512, bw.Wf1, bw.bf1, HF, 512, Npad, 512, 512, s));
+        const double t = live_tokens();
+        {
+            MlgProfScope prof(6, s, 2.0 * t * (256.0 * 256 + 512.0 * 512));
+            LG_TRY(mlg_gemm_bias_bf16_ld(CTX, LG_D, bw.Wout, bw.bout, CAT + LG_D, 512, Npad, LG_D, LG_D, s));
+            LG_TRY(mlg_gemm_bias_f32_ld(CAT, 512, bw.Wf1, bw.bf1, HF, 512, Npad, 512, 512, s));
+        }
         hipLaunchKernelGGL(k_lg_ln_gelu, dim3((Npad + 3) / 4), dim3(256), 0, s, HF, bw.ln_g, bw.ln_b, HB, Npad);
         MLG_LAUNCH_CHECK();
+        MlgProfScope prof(6, s, 2.0 * t * 512.0 * 256);
         return mlg_gemm_residual_copy(HB, 512, bw.Wf2, bw.bf2, X, LG_D, CAT, 512, Npad, LG_D, 512, s);
     };
     // matchability log-sigmoid of every live token (layer i's head)
     auto certainty = [&](int i) {
         hipLaunchKernelGGL(k_lg_conf, dim3((Npad + 3) / 4), dim3(256), 0, s, ROWSEG, Npad, X, (const float*)nullptr,
-                           (const float*)nullptr, w.wmatch[i], w.bmatch[i], 0.f, 0.f, LZ, KEEP, STATS);
+                           (const float*)nullptr, w.wmatch[i], w.bmatch[i], 0.f, 0.f, LZ, KEEP);
     };
     // assignment + filter of the listed segment pairs (k = index of image a's segment)
     auto assign = [&](int i, const std::vector<size_t>& ks) -> int {
@@ -700,11 +762,17 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     std::vector<int> stats(segs.size() * 2);
     for (int i = 0; i < LG_L && !segs.empty(); ++i) {
         // self block: projection + rotary + head split fused in the GEMM epilogue
-        LG_TRY(mlg_gemm_lg_self(CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, LG_D, s));
+        {
+            MlgProfScope prof(6, s, 2.0 * live_tokens() * 768 * 256);
+            LG_TRY(mlg_gemm_lg_self(CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, LG_D, s));
+        }
         LG_TRY(attention(false));
         LG_TRY(ffn(w.self[i]));
         // cross block
-        LG_TRY(mlg_gemm_lg_cross(CAT, 512, w.cross[i].Wqkv, w.cross[i].bqkv, LIVE, Q, VT, Npad, LG_D, s));
+        {
+            MlgProfScope prof(6, s, 2.0 * live_tokens() * 512 * 256);
+            LG_TRY(mlg_gemm_lg_cross(CAT, 512, w.cross[i].Wqkv, w.cross[i].bqkv, LIVE, Q, VT, Npad, LG_D, s));
+        }
         LG_TRY(attention(true));
         LG_TRY(ffn(w.cross[i]));
 
@@ -716,9 +784,9 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
             break;
         }
         const float thr = conf_threshold(i);
-        if (hipMemsetAsync(STATS, 0, segs.size() * 2 * sizeof(int), s) != hipSuccess) return MLG_EHIP;
         hipLaunchKernelGGL(k_lg_conf, dim3((Npad + 3) / 4), dim3(256), 0, s, ROWSEG, Npad, X, w.wconf[i], w.bconf[i],
-                           w.wmatch[i], w.bmatch[i], thr, width_conf, LZ, KEEP, STATS);
+                           w.wmatch[i], w.bmatch[i], thr, width_conf, LZ, KEEP);
+        hipLaunchKernelGGL(k_lg_segstats, dim3((unsigned)segs.size()), dim3(256), 0, s, SEGS, KEEP, STATS);
         MLG_LAUNCH_CHECK();
         if (hipMemcpyAsync(stats.data(), STATS, segs.size() * 2 * sizeof(int), hipMemcpyDeviceToHost, s) !=
                 hipSuccess ||

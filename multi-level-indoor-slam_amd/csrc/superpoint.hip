@@ -516,6 +516,7 @@ int conv(const bf16_t* in, const bf16_t* w, const float* b, bf16_t* out, int B, 
          hipStream_t s) {
     if (Cout % COUT_T) return MLG_EINVAL;
     const int tx = (W + TS - 1) / TS, ty = (H + TS - 1) / TS;
+    MlgProfScope prof(7, s, 2.0 * B * H * W * Cout * 9.0 * CIN);
     hipLaunchKernelGGL((k_conv3x3<CIN, COUT_T, POOL>), dim3(tx * ty, Cout / COUT_T, B), dim3(512), 0, s, in, w, b,
                        out, H, W, Cout, tx);
     MLG_LAUNCH_CHECK();

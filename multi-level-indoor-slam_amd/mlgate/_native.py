@@ -61,6 +61,7 @@ EXPORTS = {
     "mlg_prof_enable": (c_int, [c_int]),
     "mlg_prof_reset": (c_int, []),
     "mlg_prof_read": (c_int, [c_int, ctypes.POINTER(c_double), ctypes.POINTER(c_long)]),
+    "mlg_prof_read_work": (c_int, [c_int, ctypes.POINTER(c_double)]),
 }
 
 _lib = None
