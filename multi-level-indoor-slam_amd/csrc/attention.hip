@@ -36,6 +36,7 @@ __device__ __forceinline__ int v_off(int d, int gran) {
 // One (image, head, 128-query block) tile.  Qh / Kh: [rows][64] of this head; Vh: the
 // V^T rows [64][vstride] of this head; T keys; nq query rows (rows nq..qpad-1 must be
 // finite); output row r goes to orow + r * ldo.
+template <bool VTILED>
 __device__ __forceinline__ void attention_tile(char* smem, const bf16_t* __restrict__ Qh,
                                                const bf16_t* __restrict__ Kh, const bf16_t* __restrict__ Vh,
                                                int vstride, int T, int nq, int qmax, int qblock,
@@ -66,8 +67,14 @@ __device__ __forceinline__ void attention_tile(char* smem, const bf16_t* __restr
     {                                                                                        \
         rk0 = *reinterpret_cast<const uint4*>(Kh + (size_t)((kb) + srow) * 64 + sch * 8);      \
         rk1 = *reinterpret_cast<const uint4*>(Kh + (size_t)((kb) + srow + 32) * 64 + sch * 8); \
-        rv0 = *reinterpret_cast<const uint4*>(Vh + (size_t)srow * Tpad + (kb) + sch * 8);      \
-        rv1 = *reinterpret_cast<const uint4*>(Vh + (size_t)(srow + 32) * Tpad + (kb) + sch * 8); \
+        if (VTILED) {  /* [key block][64 d][64 keys]: one contiguous 8 KB tile per block */     \
+            const bf16_t* vb_ = Vh + (size_t)((kb) >> 6) * 4096 + sch * 8;                    \
+            rv0 = *reinterpret_cast<const uint4*>(vb_ + srow * 64);                            \
+            rv1 = *reinterpret_cast<const uint4*>(vb_ + (srow + 32) * 64);                     \
+        } else {                                                                               \
+            rv0 = *reinterpret_cast<const uint4*>(Vh + (size_t)srow * Tpad + (kb) + sch * 8);  \
+            rv1 = *reinterpret_cast<const uint4*>(Vh + (size_t)(srow + 32) * Tpad + (kb) + sch * 8); \
+        }                                                                                      \
     }
 #define ATT_LSTORE(buf)                                                                      \
     {                                                                                        \
@@ -192,14 +199,16 @@ __global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__
     __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_BYTES + VTILE_BYTES)];
     const int h = blockIdx.y, b = blockIdx.z;
     const size_t head = (size_t)b * 12 + h;
-    attention_tile(smem, Q + head * Tpad * 64, K + head * Tpad * 64, Vt + head * 64 * Tpad, Tpad, T, T, Tpad,
+    attention_tile<false>(smem, Q + head * Tpad * 64, K + head * Tpad * 64, Vt + head * 64 * Tpad, Tpad, T, T, Tpad,
                    blockIdx.x, O + (size_t)b * T * 768 + h * 64, 768);
 }
 
 // Ragged batch: task t attends query rows [q_off, q_off + q_len) to keys / values
 // [kv_off, kv_off + kv_len) of a flat token layout (offsets multiples of 64, rows
-// zero-padded to the next multiple of 64); Q, K: [heads][Npad][64]; Vt: [heads][64][Npad];
-// output rows out_off + r of O [Npad][ldo] at column h * 64.
+// zero-padded to the next multiple of 64); Q, K: [heads][Npad][64]; V^T tiled per 64-key
+// block, [heads][Npad / 64][64 d][64 keys] (a plain [64][Npad] V^T would put each d-row
+// of a block in a different 2 MB page at large Npad); output rows out_off + r of
+// O [Npad][ldo] at column h * 64.
 __global__ __launch_bounds__(256, 2) void k_attention_varlen(const bf16_t* __restrict__ Q,
                                                              const bf16_t* __restrict__ K,
                                                              const bf16_t* __restrict__ Vt, bf16_t* __restrict__ O,
@@ -210,8 +219,8 @@ __global__ __launch_bounds__(256, 2) void k_attention_varlen(const bf16_t* __res
     if ((int)blockIdx.x * 128 >= tk.y || tk.w <= 0) return;
     const int h = blockIdx.y;
     const int qpad = (tk.y + 63) & ~63;
-    attention_tile(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
-                   Vt + (size_t)h * 64 * Npad + tk.z, Npad, tk.w, tk.y, qpad, blockIdx.x,
+    attention_tile<true>(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
+                         Vt + ((size_t)h * Npad + tk.z) * 64, Npad, tk.w, tk.y, qpad, blockIdx.x,
                    O + (size_t)out_off[blockIdx.z] * ldo + h * 64, ldo);
 }
 

@@ -146,11 +146,12 @@ struct EpiLgSelf {
             }
             *reinterpret_cast<uint2*>((which == 0 ? Q : K) + ((size_t)h * Npad + m) * 64 + d) = o;
         } else {
-            bf16_t* p = Vt + ((size_t)h * 64 + d) * Npad + m;
+            // V^T tiled per 64-key block: [h][m / 64][64 d][64 keys] (attention.hip)
+            bf16_t* p = Vt + (((size_t)h * Npad + (m & ~63)) * 64) + (size_t)d * 64 + (m & 63);
             p[0] = on ? f32_to_bf16(x0) : (bf16_t)0;
-            p[(size_t)Npad] = on ? f32_to_bf16(x1) : (bf16_t)0;
-            p[(size_t)2 * Npad] = on ? f32_to_bf16(x2) : (bf16_t)0;
-            p[(size_t)3 * Npad] = on ? f32_to_bf16(x3) : (bf16_t)0;
+            p[64] = on ? f32_to_bf16(x1) : (bf16_t)0;
+            p[128] = on ? f32_to_bf16(x2) : (bf16_t)0;
+            p[192] = on ? f32_to_bf16(x3) : (bf16_t)0;
         }
     }
 };
@@ -171,11 +172,12 @@ struct EpiLgCross {
             }
             *reinterpret_cast<uint2*>(Q + ((size_t)h * Npad + m) * 64 + d) = o;
         } else {
-            bf16_t* p = Vt + ((size_t)h * 64 + d) * Npad + m;
+            // V^T tiled per 64-key block: [h][m / 64][64 d][64 keys] (attention.hip)
+            bf16_t* p = Vt + (((size_t)h * Npad + (m & ~63)) * 64) + (size_t)d * 64 + (m & 63);
             p[0] = on ? f32_to_bf16(x0) : (bf16_t)0;
-            p[(size_t)Npad] = on ? f32_to_bf16(x1) : (bf16_t)0;
-            p[(size_t)2 * Npad] = on ? f32_to_bf16(x2) : (bf16_t)0;
-            p[(size_t)3 * Npad] = on ? f32_to_bf16(x3) : (bf16_t)0;
+            p[64] = on ? f32_to_bf16(x1) : (bf16_t)0;
+            p[128] = on ? f32_to_bf16(x2) : (bf16_t)0;
+            p[192] = on ? f32_to_bf16(x3) : (bf16_t)0;
         }
     }
 };
