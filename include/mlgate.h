@@ -164,6 +164,34 @@ int mlg_proximity_emit(const double* pos, const int64_t* floor, int N, int row0,
                        int min_gap, int strict, const void* workspace, size_t workspace_bytes, int32_t* pairs,
                        double* dist, uint8_t* valid, void* stream);
 
+/* ----------------------------------------------------------- ResNet-50 --
+ * Replaces MixVPR / SALAD's executed path, the torchvision ResNet-50 fallback
+ * (scripts/semantic_gating/place_recognition.py:248-306): BGR taken as RGB ->
+ * Pillow bilinear (antialiased) resize to 224x224 -> /255 -> ImageNet normalise ->
+ * resnet50 minus fc -> 2048-d global average pool, zero-padded / truncated to
+ * descriptor_dim.  BatchNorm (eval) folded into the conv weights / biases by the
+ * caller.  frames: device uint8 [B] x (H x W x C), C in {1, 3, 4}; desc: device f32
+ * [B, descriptor_dim]. */
+typedef struct mlg_rn_block {
+    const uint16_t* w1; const float* b1;  /* conv1 1x1: bf16 [max(width,128)][Cin] (rows >= width zero) */
+    const uint16_t* w2; const float* b2;  /* conv2 3x3: bf16 [max(width,128)][9 * width], k = tap * width + c */
+    const uint16_t* w3; const float* b3;  /* conv3 1x1: bf16 [4 width][width] */
+    const uint16_t* wd; const float* bd;  /* downsample 1x1: bf16 [4 width][Cin], or NULL */
+} mlg_rn_block;
+typedef struct mlg_rn_weights {
+    const float* stem_w;  /* f32 [64][7][7][3] */
+    const float* stem_b;  /* f32 [64] */
+    mlg_rn_block blocks[16];
+} mlg_rn_weights;
+size_t mlg_resnet50_workspace_bytes(int B, int H, int W);
+int mlg_resnet50_forward(const mlg_rn_weights* w, const uint8_t* frames, int B, int H, int W, int C,
+                         long frame_stride, int descriptor_dim, void* workspace, size_t workspace_bytes,
+                         float* desc, void* stream);
+/* Parity entry: only the Pillow bilinear resize of the above -> uint8 [B, 224, 224, 3]
+ * (workspace sized by mlg_resnet50_workspace_bytes). */
+int mlg_op_pillow_resize_224(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, void* workspace,
+                             size_t workspace_bytes, uint8_t* out, void* stream);
+
 /* -------------------------------------------------------- SuperPoint --
  * Replaces the extractor half of LightGlue._detect_and_match_native
  * (scripts/semantic_gating/geometric_verification.py:263-312): cv2 BGR2GRAY / 255 ->

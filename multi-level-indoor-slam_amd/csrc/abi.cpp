@@ -238,6 +238,33 @@ int mlg_proximity_emit(const double* pos, const int64_t* floor, int N, int row0,
                                   pairs, dist, valid, (hipStream_t)stream);
 }
 
+static_assert(sizeof(mlg_rn_weights) == sizeof(mlg_rn_weights_i), "ResNet weight tables must match");
+
+size_t mlg_resnet50_workspace_bytes(int B, int H, int W) { return mlg_resnet50_ws_bytes(B, H, W); }
+
+int mlg_resnet50_forward(const mlg_rn_weights* w, const uint8_t* frames, int B, int H, int W, int C,
+                         long frame_stride, int descriptor_dim, void* workspace, size_t workspace_bytes,
+                         float* desc, void* stream) {
+    if (!w || !frames || !workspace || !desc || !w->stem_w || !w->stem_b) return MLG_EINVAL;
+    for (int i = 0; i < 16; ++i) {
+        const mlg_rn_block& b = w->blocks[i];
+        if (!b.w1 || !b.b1 || !b.w2 || !b.b2 || !b.w3 || !b.b3) return MLG_EINVAL;
+        const bool first = i == 0 || i == 3 || i == 7 || i == 13;
+        if (first != (b.wd != nullptr) || (b.wd && !b.bd)) return MLG_EINVAL;
+    }
+    if (frame_stride < (long)H * W * C) return MLG_EINVAL;
+    return mlg_resnet50_run(*reinterpret_cast<const mlg_rn_weights_i*>(w), frames, B, H, W, C, frame_stride,
+                            descriptor_dim, workspace, workspace_bytes, desc, nullptr, (hipStream_t)stream);
+}
+
+int mlg_op_pillow_resize_224(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, void* workspace,
+                             size_t workspace_bytes, uint8_t* out, void* stream) {
+    if (!frames || !workspace || !out || frame_stride < (long)H * W * C) return MLG_EINVAL;
+    mlg_rn_weights_i none{};
+    return mlg_resnet50_run(none, frames, B, H, W, C, frame_stride, 1, workspace, workspace_bytes, nullptr, out,
+                            (hipStream_t)stream);
+}
+
 size_t mlg_superpoint_workspace_bytes(int B, int H, int W) { return mlg_superpoint_ws_bytes(B, H, W); }
 
 int mlg_superpoint(const mlg_sp_weights* w, const uint8_t* frames, int B, int H, int W, int C, long frame_stride,

@@ -201,6 +201,38 @@ struct EpiResidualCopy {
     }
 };
 
+// relu(acc + b) -> bf16, columns >= nvalid dropped (N padded to the tile width)
+struct EpiBiasReluBF16 {
+    bf16_t* C; int ldc; const float* bias; int nvalid;
+    __device__ void operator()(int m, int n, const f32x4& v) const {
+        if (n >= nvalid) return;
+        const float4 b = *reinterpret_cast<const float4*>(bias + n);
+        uint2 o;
+        o.x = pack_bf16x2(fmaxf(v[0] + b.x, 0.f), fmaxf(v[1] + b.y, 0.f));
+        o.y = pack_bf16x2(fmaxf(v[2] + b.z, 0.f), fmaxf(v[3] + b.w, 0.f));
+        *reinterpret_cast<uint2*>(C + (size_t)m * ldc + n) = o;
+    }
+};
+
+// X = relu((acc + b) + R) in f32 (R may alias X) and its bf16 copy (ResNet conv3 + shortcut)
+struct EpiBiasAddRelu {
+    const float* R; float* X; int ldx; bf16_t* C; const float* bias;
+    __device__ void operator()(int m, int n, const f32x4& v) const {
+        const float4 b = *reinterpret_cast<const float4*>(bias + n);
+        const float4 r = *reinterpret_cast<const float4*>(R + (size_t)m * ldx + n);
+        float4 x;
+        x.x = fmaxf((v[0] + b.x) + r.x, 0.f);
+        x.y = fmaxf((v[1] + b.y) + r.y, 0.f);
+        x.z = fmaxf((v[2] + b.z) + r.z, 0.f);
+        x.w = fmaxf((v[3] + b.w) + r.w, 0.f);
+        *reinterpret_cast<float4*>(X + (size_t)m * ldx + n) = x;
+        uint2 o;
+        o.x = pack_bf16x2(x.x, x.y);
+        o.y = pack_bf16x2(x.z, x.w);
+        *reinterpret_cast<uint2*>(C + (size_t)m * ldx + n) = o;
+    }
+};
+
 struct EpiPatch {  // patch tokens: X[b, 1 + p, :] = acc + b + pos[1 + p]
     float* X; const float* bias; const float* pos; int P;  // P = patches per image
     __device__ void operator()(int m, int n, const f32x4& v) const {
@@ -653,6 +685,14 @@ int mlg_gemm_lg_cross(const bf16_t* A, int lda, const bf16_t* W, const float* bi
 int mlg_gemm_residual_copy(const bf16_t* A, int lda, const bf16_t* W, const float* bias, float* X, int ldx, bf16_t* C,
                            int ldc, int M, int N, int K_, hipStream_t s) {
     return launch(A, W, M, N, K_, lda, K_, EpiResidualCopy{X, ldx, bias, C, ldc}, s);
+}
+int mlg_gemm_bias_relu_bf16(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* C, int ldc,
+                            int nvalid, int M, int N, int K_, hipStream_t s) {
+    return launch(A, W, M, N, K_, lda, K_, EpiBiasReluBF16{C, ldc, bias, nvalid}, s);
+}
+int mlg_gemm_bias_add_relu(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, float* X,
+                           int ldx, bf16_t* C, int M, int N, int K_, hipStream_t s) {
+    return launch(A, W, M, N, K_, lda, K_, EpiBiasAddRelu{R, X, ldx, C, bias}, s);
 }
 int mlg_gemm_set_variant(int variant) {
     if (variant < 1 || variant > 4) return MLG_EINVAL;

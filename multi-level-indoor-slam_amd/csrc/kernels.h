@@ -42,6 +42,10 @@ int mlg_gemm_lg_cross(const bf16_t* A, int lda, const bf16_t* W, const float* bi
                       bf16_t* Vt, int Npad, int K_, hipStream_t s);
 int mlg_gemm_residual_copy(const bf16_t* A, int lda, const bf16_t* W, const float* bias, float* X, int ldx, bf16_t* C,
                            int ldc, int M, int N, int K_, hipStream_t s);
+int mlg_gemm_bias_relu_bf16(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* C, int ldc,
+                            int nvalid, int M, int N, int K_, hipStream_t s);
+int mlg_gemm_bias_add_relu(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, float* X,
+                           int ldx, bf16_t* C, int M, int N, int K_, hipStream_t s);
 int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,
                          const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s);
 int mlg_gemm_bias_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,
@@ -127,3 +131,20 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
                       const int32_t* pa, const int32_t* pb, int P, float depth_conf, float width_conf,
                       float filter_thr, int pruning_min, void* ws, size_t ws_bytes, int32_t* matches, float* mscores,
                       int32_t* nmatch, int32_t* stop_layer, hipStream_t s);
+
+// resnet.hip -- ResNet-50 GAP descriptor (MixVPR / SALAD fallback)
+struct mlg_rn_block_i {
+    const bf16_t* w1; const float* b1;  // conv1 1x1 [max(width,128)][Cin] (BN folded; pad rows zero)
+    const bf16_t* w2; const float* b2;  // conv2 3x3 [max(width,128)][9 * width] (k = tap * width + c)
+    const bf16_t* w3; const float* b3;  // conv3 1x1 [4 width][width]
+    const bf16_t* wd; const float* bd;  // downsample 1x1 [4 width][Cin] or NULL
+};
+struct mlg_rn_weights_i {
+    const float* stem_w;  // f32 [64][7][7][3] (BN folded)
+    const float* stem_b;  // f32 [64]
+    mlg_rn_block_i blocks[16];
+};
+size_t mlg_resnet50_ws_bytes(int B, int H, int W);
+// resized_u8 != NULL: only the Pillow resize runs, into [B, 224, 224, 3] (parity entry)
+int mlg_resnet50_run(const mlg_rn_weights_i& w, const uint8_t* frames, int B, int H, int W, int C, long frame_stride,
+                     int D, void* ws, size_t ws_bytes, float* desc, uint8_t* resized_u8, hipStream_t s);

@@ -41,6 +41,11 @@ EXPORTS = {
                                     c_void_p, c_void_p]),
     "mlg_recover_pose": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                  c_void_p]),
+    "mlg_resnet50_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mlg_resnet50_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_long, c_int, c_void_p,
+                                     c_size_t, c_void_p, c_void_p]),
+    "mlg_op_pillow_resize_224": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_long, c_void_p, c_size_t,
+                                         c_void_p, c_void_p]),
     "mlg_superpoint_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mlg_superpoint": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_long, c_float, c_int, c_int, c_int,
                                c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

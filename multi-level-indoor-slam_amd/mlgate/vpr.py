@@ -154,18 +154,34 @@ class BasePlaceRecognition:
 
 class _ResNetFallback(BasePlaceRecognition):
     """MixVPR / SALAD: what the reference executes is a torchvision ResNet-50 GAP
-    (place_recognition.py:248-306).  Not built on HIP yet."""
+    (place_recognition.py:248-306) -- the MixVPR / SALAD packages are never importable
+    under the names it tries, so every call lands in ``_load_fallback_model``.  Here
+    that network runs on the GPU (mlgate.resnet, HIP kernels + bf16 MFMA GEMMs)."""
 
     def __init__(self, descriptor_dim, device, pretrained_path=None):
         super().__init__(descriptor_dim, device)
         self.pretrained_path = pretrained_path
         self._model_loaded = False
 
+    def _load_model(self):
+        if self._model_loaded:
+            return
+        from .resnet import ResNet50GPU
+        self._net = ResNet50GPU(device=self.device)
+        if self._net.weights_source.startswith("synthetic"):
+            warnings.warn("ImageNet ResNet-50 weights are not available offline; using seeded synthetic resnet50 "
+                          "weights (set MLGATE_RESNET50_WEIGHTS to a local torchvision checkpoint).")
+        self._model_loaded = True
+        self._is_fallback = True
+
+    def extract_descriptors(self, images) -> np.ndarray:
+        self._load_model()
+        torch = _torch()
+        frames = torch.from_numpy(_as_frames(images)).to(self._net.device)
+        return self._net.forward_device(frames, self.descriptor_dim).cpu().numpy()
+
     def extract_descriptor(self, image: np.ndarray) -> np.ndarray:
-        raise _native.MlgateError(
-            f"{type(self).__name__}: the ResNet-50 descriptor path (the reference's MixVPR/SALAD fallback) is "
-            "not implemented on MI355X yet; use vpr_method='cricavpr' or 'anyloc', or inject descriptors into "
-            ".descriptors")
+        return self.extract_descriptors([image])[0]
 
 
 class MixVPR(_ResNetFallback):

@@ -199,3 +199,73 @@ def resolve_lightglue_state_dict(path=None, seed=0):
     if path:
         return load_lightglue_state_dict(path), path
     return lightglue_state_dict(seed), f"synthetic(seed={seed})"
+
+
+# ----------------------------------------------------------------- ResNet-50 (MixVPR / SALAD fallback)
+RESNET_STAGES = ((64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2))  # width, blocks, first stride
+
+
+def resnet50_keys():
+    keys = ["conv1.weight"] + [f"bn1.{s}" for s in ("weight", "bias", "running_mean", "running_var")]
+    for li, (width, blocks, _) in enumerate(RESNET_STAGES, 1):
+        for b in range(blocks):
+            p = f"layer{li}.{b}."
+            for c in (1, 2, 3):
+                keys.append(p + f"conv{c}.weight")
+                keys += [p + f"bn{c}.{s}" for s in ("weight", "bias", "running_mean", "running_var")]
+            if b == 0:
+                keys.append(p + "downsample.0.weight")
+                keys += [p + f"downsample.1.{s}" for s in ("weight", "bias", "running_mean", "running_var")]
+    return keys
+
+
+def resnet50_state_dict(seed=0):
+    """Seeded float32 torchvision resnet50 weights (He-normal convs, BatchNorm statistics
+    around identity), torchvision key names, fc omitted (the fallback drops it)."""
+    rng = np.random.default_rng(seed)
+    sd = {}
+
+    def conv(name, cout, cin, k, gain=1.0):
+        std = np.float32(gain * np.sqrt(2.0 / (cin * k * k)))
+        sd[name] = rng.standard_normal((cout, cin, k, k), dtype=np.float32) * std
+
+    def bn(name, c, scale=1.0):
+        sd[name + ".weight"] = (np.float32(scale) * (1.0 + 0.1 * rng.standard_normal(c))).astype(np.float32)
+        sd[name + ".bias"] = (0.05 * rng.standard_normal(c)).astype(np.float32)
+        sd[name + ".running_mean"] = (0.05 * rng.standard_normal(c)).astype(np.float32)
+        sd[name + ".running_var"] = (1.0 + 0.2 * rng.random(c)).astype(np.float32)
+
+    conv("conv1.weight", 64, 3, 7)
+    bn("bn1", 64)
+    cin = 64
+    for li, (width, blocks, _) in enumerate(RESNET_STAGES, 1):
+        for b in range(blocks):
+            p = f"layer{li}.{b}."
+            conv(p + "conv1.weight", width, cin, 1)
+            bn(p + "bn1", width)
+            conv(p + "conv2.weight", width, width, 3)
+            bn(p + "bn2", width)
+            conv(p + "conv3.weight", width * 4, width, 1)
+            bn(p + "bn3", width * 4, scale=0.3)  # residual branch damped as in trained nets
+            if b == 0:
+                conv(p + "downsample.0.weight", width * 4, cin, 1)
+                bn(p + "downsample.1", width * 4)
+            cin = width * 4
+    return sd
+
+
+def load_resnet50_state_dict(path):
+    """torchvision resnet50 checkpoint (e.g. resnet50-0676ba61.pth) from a local file."""
+    import torch
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    missing = [k for k in resnet50_keys() if k not in sd]
+    if missing:
+        raise KeyError(f"checkpoint {path} lacks resnet50 keys, e.g. {missing[:3]}")
+    return {k: sd[k].float().cpu().numpy() for k in resnet50_keys()}
+
+
+def resolve_resnet50_state_dict(path=None, seed=0):
+    path = path or os.environ.get("MLGATE_RESNET50_WEIGHTS")
+    if path:
+        return load_resnet50_state_dict(path), path
+    return resnet50_state_dict(seed), f"synthetic(seed={seed})"

@@ -72,6 +72,28 @@ def main():
             row[f"K{K}_tflops"] = round(2 * 33920 * 3072 * K / us / 1e6, 1)
         print(json.dumps(row), flush=True)
 
+    # LightGlue shapes: ~1M token rows, K = 256 / 512 (per-variant f32-out timing)
+    for (N, K) in ((768, 256), (512, 512), (256, 512), (256, 256)):
+        M = 1 << 20
+        A = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+        W = torch.randn(N, K, device=dev, generator=g).to(torch.bfloat16)
+        C = torch.empty(M, N, device=dev)
+        row = {"lightglue_shape": [M, N, K]}
+        for v in (1, 2, 4):
+            args_ = (v, _native.ptr(A), _native.ptr(W), _native.ptr(C), M, N, K, _native.stream_of(dev))
+            L.mlg_op_gemm_f32out_variant(*args_)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                L.mlg_op_gemm_f32out_variant(*args_)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 200.0
+            row[f"v{v}_us"] = round(us, 1)
+            row[f"v{v}_tflops"] = round(2.0 * M * N * K / us / 1e6, 1)
+        print(json.dumps(row), flush=True)
+        del A, W, C
+
     eng = VitB14(synthetic_state_dict(0), device=dev, max_batch=args.batch)
     frames = torch.randint(0, 256, (args.batch, 480, 640, 3), dtype=torch.uint8, device=dev)
     desc = {}
