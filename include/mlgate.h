@@ -145,6 +145,18 @@ int mlg_op_attention(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, u
 int mlg_op_preprocess_patches(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, int S,
                               uint16_t* patches, void* stream);
 
+/* ----------------------------------------------- LiDAR ground plane --
+ * Replaces LiDARFloorTracker.fit_ground_plane_ransac (lidar_floor_tracker.py:92-141)
+ * for S scans at once: scan s owns ground points [offsets[s], offsets[s+1]) of pts
+ * (device f32 [N, 3]).  `iterations` 3-point hypotheses per scan (counter-based RNG of
+ * (seed, hypothesis)); inlier iff |n . p + d| < threshold (float64); best = most
+ * inliers, first on ties.  Outputs (device): plane f64 [S, 4] (NaN if none), inlier
+ * ratio f64 [S], inlier count int32 [S]. */
+size_t mlg_plane_ransac_workspace_bytes(int S, int iterations);
+int mlg_plane_ransac(const float* pts, const int32_t* offsets, int S, int iterations, uint64_t seed, double threshold,
+                     void* workspace, size_t workspace_bytes, double* plane, double* ratio, int32_t* inliers,
+                     void* stream);
+
 /* ------------------------------------------------- trajectory proximity --
  * Replaces detect_loop_closure_candidates + apply_floor_gating of the SLAM
  * integrations (scripts/semantic_gating/orb_slam3_integration.py:167-281,

@@ -220,6 +220,16 @@ int mlg_similarity(const float* A, int Q, const float* B, int N, int D, float* S
     return mlg_similarity_f32(A, Q, B, N, D, S, N, (hipStream_t)stream);
 }
 
+size_t mlg_plane_ransac_workspace_bytes(int S, int iterations) { return mlg_plane_ws_bytes(S, iterations); }
+
+int mlg_plane_ransac(const float* pts, const int32_t* offsets, int S, int iterations, uint64_t seed, double threshold,
+                     void* workspace, size_t workspace_bytes, double* plane, double* ratio, int32_t* inliers,
+                     void* stream) {
+    if (!pts || !offsets || !workspace || !plane || !ratio || !inliers) return MLG_EINVAL;
+    return mlg_plane_ransac_run(pts, offsets, S, iterations, seed, threshold, workspace, workspace_bytes, plane,
+                                ratio, inliers, (hipStream_t)stream);
+}
+
 size_t mlg_proximity_workspace_bytes(int N, int nrows) { return mlg_proximity_ws_bytes(N, nrows); }
 
 int mlg_proximity_count(const double* pos, const int64_t* floor, int N, int row0, int nrows, double radius,

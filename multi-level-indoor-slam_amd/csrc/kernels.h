@@ -148,3 +148,8 @@ size_t mlg_resnet50_ws_bytes(int B, int H, int W);
 // resized_u8 != NULL: only the Pillow resize runs, into [B, 224, 224, 3] (parity entry)
 int mlg_resnet50_run(const mlg_rn_weights_i& w, const uint8_t* frames, int B, int H, int W, int C, long frame_stride,
                      int D, void* ws, size_t ws_bytes, float* desc, uint8_t* resized_u8, hipStream_t s);
+
+// plane.hip -- batched LiDAR ground-plane RANSAC
+size_t mlg_plane_ws_bytes(int S, int H);
+int mlg_plane_ransac_run(const float* pts, const int32_t* offs, int S, int H, uint64_t seed, double thr, void* ws,
+                         size_t ws_bytes, double* plane, double* ratio, int32_t* inliers, hipStream_t s);

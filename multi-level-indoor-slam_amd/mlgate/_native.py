@@ -30,6 +30,9 @@ EXPORTS = {
     "mlg_xcorr_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mlg_xcorr_score": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_size_t, c_void_p,
                                 c_void_p]),
+    "mlg_plane_ransac_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "mlg_plane_ransac": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_uint64, c_double, c_void_p, c_size_t,
+                                 c_void_p, c_void_p, c_void_p, c_void_p]),
     "mlg_proximity_workspace_bytes": (c_size_t, [c_int, c_int]),
     "mlg_proximity_count": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_double, c_int, c_int, c_void_p,
                                     c_size_t, c_void_p, c_void_p]),

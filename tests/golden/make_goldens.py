@@ -281,10 +281,10 @@ def api_case(sg):
     """Public signatures / dataclass fields of the reference API (the drop-in contract)."""
     import dataclasses
     import inspect
-    from scripts.semantic_gating import floor_detector, geometric_verification, loop_closure_gate
+    from scripts.semantic_gating import floor_detector, geometric_verification, lidar_floor_tracker, loop_closure_gate
     from scripts.semantic_gating import place_recognition
     out = {}
-    for mod in (floor_detector, loop_closure_gate, place_recognition, geometric_verification):
+    for mod in (floor_detector, loop_closure_gate, place_recognition, geometric_verification, lidar_floor_tracker):
         for name, obj in vars(mod).items():
             if name.startswith('_') or getattr(obj, '__module__', None) != mod.__name__:
                 continue
@@ -307,6 +307,8 @@ def api_case(sg):
 def main():
     sg = _import_reference()
     api_case(sg)
+    if "--api-only" in sys.argv:
+        return
     print("reference", sg.__version__)
     print("knn small", knn_case(sg, "small", 1, 64, 768, 10, 0.5, 10.0, True, 0.0, 8, 0.6))
     print("knn gaps", knn_case(sg, "gaps", 2, 300, 768, 10, 0.5, 10.0, True, 0.1, 40, 0.8))
