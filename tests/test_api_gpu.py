@@ -147,6 +147,9 @@ def test_anyloc_end_to_end(dev):
     assert got.shape == (768,) and 1 - cos < 1e-4
 
 
-def test_resnet_methods_fail_loudly(dev):
-    with pytest.raises(mlgate._native.MlgateError if hasattr(mlgate, "_native") else RuntimeError):
-        mlgate.MixVPR(device="cuda").extract_descriptor(np.zeros((480, 640, 3), np.uint8))
+def test_resnet_methods_refuse_cpu_device(dev):
+    """The ResNet-50 fallback runs on the GPU only: device='cpu' raises, never a CPU path."""
+    with pytest.raises(mlgate._native.MlgateError):
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            mlgate.MixVPR(device="cpu").extract_descriptor(np.zeros((480, 640, 3), np.uint8))
