@@ -251,11 +251,13 @@ def main():
             _native.check(L.mlg_prof_enable(all_slots), "prof")
         gate.step()
     torch.cuda.synchronize()
-    tot = {}
+    tot, tflops = {}, {}
     for s in SLOTS:
-        ms, cnt = ctypes.c_double(), ctypes.c_long()
+        ms, cnt, work = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
         L.mlg_prof_read(s, ctypes.byref(ms), ctypes.byref(cnt))
+        L.mlg_prof_read_work(s, ctypes.byref(work))
         tot[s] = ms.value
+        tflops[s] = work.value / (ms.value * 1e9) if ms.value > 0 else 0.0
     dom = max(tot, key=tot.get) if args.warmup > 0 else 0
     L.mlg_prof_reset()
     _native.check(L.mlg_prof_enable(1 << dom), "prof")
@@ -315,7 +317,8 @@ def main():
                          "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4) if achieved else None,
                          "traffic": None, "avg_launch_us": round(avg_s * 1e6, 2), "launches": cnt.value,
                          "flops_per_launch": round(flops, 1),
-                         "stage_ms_per_step": {SLOTS[s]: round(tot[s], 2) for s in SLOTS}},
+                         "stage_ms_per_step": {SLOTS[s]: round(tot[s], 2) for s in SLOTS},
+                         "stage_tflops": {SLOTS[s]: round(tflops[s], 1) for s in SLOTS}},
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(pairs_per_kf=(n_pairs / steps / N) if gate.verify else 0.0)

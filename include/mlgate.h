@@ -142,6 +142,22 @@ int mlg_op_gemm_residual(const uint16_t* A, const uint16_t* W, const float* bias
 int mlg_op_layernorm_bf16(const float* X, const float* g, const float* b, uint16_t* Y, int M, void* stream);
 int mlg_op_attention(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, uint16_t* O, int B, int T, int Tpad,
                      void* stream);
+/* Ragged multi-head attention (LightGlue self / cross, geometric_verification.py:263-312
+ * via upstream SelfBlock / CrossBlock).  Task t = int32 x4 (q_off, q_len, kv_off, kv_len)
+ * over a flat token layout; Q, K bf16 [heads][Npad][64] (Q pre-scaled by 1/8 is NOT
+ * assumed: the kernel scales), Vt bf16 tiled [heads][Npad/64][64 d][64 keys]; output row
+ * out_off[t] + r of O [Npad][ldo] at column h*64.  Device pointers. */
+int mlg_op_attention_varlen(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, uint16_t* O, int ldo, int Npad,
+                            int heads, const int32_t* tasks, const int32_t* out_off, int ntasks, int max_q,
+                            void* stream);
+/* Fused LightGlue block tail (SelfBlock / CrossBlock after the attention):
+ * msg = ctx Wout^T + bout; X += Wf2 GELU(LN(Wf1 [bf16(X) | bf16(msg)] + bf1)) + bf2 for M token
+ * rows; X f32 [M][256] in place, bf16(X) into xcopy [M][ldc] cols 0..255.  bf16 weights
+ * packed k-step-major: W[n][k] of an nn.Linear ([out][in]) stored at [k/16][n][k%16].
+ * Device pointers. */
+int mlg_op_lg_ffn(const uint16_t* ctx, float* X, uint16_t* xcopy, int ldc, int M, const uint16_t* Wout,
+                  const float* bout, const uint16_t* Wf1, const float* bf1, const float* ln_g, const float* ln_b,
+                  const uint16_t* Wf2, const float* bf2, void* stream);
 int mlg_op_preprocess_patches(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, int S,
                               uint16_t* patches, void* stream);
 
@@ -243,10 +259,10 @@ int mlg_superpoint(const mlg_sp_weights* w, const uint8_t* frames, int B, int H,
  * once per layer (early-stop / pruning decisions). */
 typedef struct mlg_lg_block {
     const uint16_t* Wqkv; const float* bqkv;  /* self: Wqkv [768][256]; cross: [to_qk; to_v] [512][256] */
-    const uint16_t* Wout; const float* bout;  /* out_proj / to_out [256][256] */
-    const uint16_t* Wf1;  const float* bf1;   /* ffn.0 [512][512] */
-    const float* ln_g;    const float* ln_b;  /* ffn.1 LayerNorm(512) */
-    const uint16_t* Wf2;  const float* bf2;   /* ffn.3 [256][512] */
+    const uint16_t* Wout; const float* bout;  /* out_proj / to_out [256][256]  } k-step-major: */
+    const uint16_t* Wf1;  const float* bf1;   /* ffn.0 [512][512]             } W[n][k] at   */
+    const float* ln_g;    const float* ln_b;  /* ffn.1 LayerNorm(512)                          */
+    const uint16_t* Wf2;  const float* bf2;   /* ffn.3 [256][512]             } [k/16][n][k%16] */
 } mlg_lg_block;
 typedef struct mlg_lg_weights {
     const float* Wr;                                       /* posenc.Wr [32][2] f32 */

@@ -385,6 +385,19 @@ int mlg_op_attention(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, u
                      void* stream) {
     return mlg_attention(Q, K, Vt, O, B, T, Tpad, (hipStream_t)stream);
 }
+int mlg_op_attention_varlen(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, uint16_t* O, int ldo, int Npad,
+                            int heads, const int32_t* tasks, const int32_t* out_off, int ntasks, int max_q,
+                            void* stream) {
+    return mlg_attention_varlen(Q, K, Vt, O, ldo, Npad, heads, reinterpret_cast<const int4*>(tasks), out_off, ntasks,
+                                max_q, (hipStream_t)stream);
+}
+int mlg_op_lg_ffn(const uint16_t* ctx, float* X, uint16_t* xcopy, int ldc, int M, const uint16_t* Wout,
+                  const float* bout, const uint16_t* Wf1, const float* bf1, const float* ln_g, const float* ln_b,
+                  const uint16_t* Wf2, const float* bf2, void* stream) {
+    mlg_lg_block_i w{};
+    w.Wout = Wout; w.bout = bout; w.Wf1 = Wf1; w.bf1 = bf1; w.ln_g = ln_g; w.ln_b = ln_b; w.Wf2 = Wf2; w.bf2 = bf2;
+    return mlg_lg_ffn(ctx, X, xcopy, ldc, M, w, (hipStream_t)stream);
+}
 int mlg_op_preprocess_patches(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, int S,
                               uint16_t* patches, void* stream) {
     return mlg_preprocess_patches(frames, B, H, W, C, frame_stride, S, MLG_VIT_PATCH_K, 1, patches,

@@ -203,25 +203,227 @@ __global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__
                    blockIdx.x, O + (size_t)b * T * 768 + h * 64, 768);
 }
 
+// v_max3_f32 without the NaN-canonicalising v_max_f32 hipcc puts in front of every
+// MFMA-produced operand of fmaxf (scores are finite or -inf here).
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// Wide tile for the ragged (LightGlue) path: one workgroup = 4 waves = 256 query rows of
+// one (task, head); each wave owns 64 queries as two 32-column MFMA tiles, so every K and
+// V^T fragment read from LDS feeds two MFMAs (half the LDS bytes per FLOP of the 32-query
+// tile, whose LDS read rate equalled its MFMA rate).  VALU per score, the other bound of
+// a d = 64 attention: no key mask except on the last block; exponent as one fma + one
+// v_exp (log2 domain, 1/8 folded into the constant); row sums kept per lane half and
+// combined once at the end; the running max moves lazily -- P and the O / l
+// accumulators are rescaled only when some lane's block max exceeds its running max by
+// more than 2^8, so P <= 256 (exact softmax either way: numerator and denominator share
+// the same stale max).
+template <bool VTILED>
+__device__ __forceinline__ void attention_tile_q64(char* smem, const bf16_t* __restrict__ Qh,
+                                                   const bf16_t* __restrict__ Kh, const bf16_t* __restrict__ Vh,
+                                                   int vstride, int T, int nq, int qmax, int qblock,
+                                                   bf16_t* __restrict__ orow, int ldo) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, col = lane & 31;
+    const int Tpad = vstride;
+    const int qbase = qblock * 256 + wave * 64;
+    constexpr float C = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+    bf16x8 qf[2][4];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+        const int qld = min(qbase + qt * 32 + col, qmax - 1);
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+            qf[qt][st] = *reinterpret_cast<const bf16x8*>(Qh + (size_t)qld * 64 + st * 16 + hh * 8);
+    }
+
+    const int srow = tid >> 3, sch = tid & 7;
+    const int sk0 = k_off(srow, sch), sk1 = k_off(srow + 32, sch);
+    const int sv0a = v_off(srow, 2 * sch), sv0b = v_off(srow, 2 * sch + 1);
+    const int sv1a = v_off(srow + 32, 2 * sch), sv1b = v_off(srow + 32, 2 * sch + 1);
+    uint4 rk0, rk1, rv0, rv1;
+#define ATT_GLOAD(kb)                                                                        \
+    {                                                                                        \
+        rk0 = *reinterpret_cast<const uint4*>(Kh + (size_t)((kb) + srow) * 64 + sch * 8);      \
+        rk1 = *reinterpret_cast<const uint4*>(Kh + (size_t)((kb) + srow + 32) * 64 + sch * 8); \
+        if (VTILED) {                                                                          \
+            const bf16_t* vb_ = Vh + (size_t)((kb) >> 6) * 4096 + sch * 8;                    \
+            rv0 = *reinterpret_cast<const uint4*>(vb_ + srow * 64);                            \
+            rv1 = *reinterpret_cast<const uint4*>(vb_ + (srow + 32) * 64);                     \
+        } else {                                                                               \
+            rv0 = *reinterpret_cast<const uint4*>(Vh + (size_t)srow * Tpad + (kb) + sch * 8);  \
+            rv1 = *reinterpret_cast<const uint4*>(Vh + (size_t)(srow + 32) * Tpad + (kb) + sch * 8); \
+        }                                                                                      \
+    }
+#define ATT_LSTORE(buf)                                                                      \
+    {                                                                                        \
+        char* kb_ = smem + (buf) * (KTILE_BYTES + VTILE_BYTES);                              \
+        char* vb_ = kb_ + KTILE_BYTES;                                                       \
+        *reinterpret_cast<uint4*>(kb_ + sk0) = rk0;                                          \
+        *reinterpret_cast<uint4*>(kb_ + sk1) = rk1;                                          \
+        *reinterpret_cast<uint2*>(vb_ + sv0a) = make_uint2(rv0.x, rv0.y);                    \
+        *reinterpret_cast<uint2*>(vb_ + sv0b) = make_uint2(rv0.z, rv0.w);                    \
+        *reinterpret_cast<uint2*>(vb_ + sv1a) = make_uint2(rv1.x, rv1.y);                    \
+        *reinterpret_cast<uint2*>(vb_ + sv1b) = make_uint2(rv1.z, rv1.w);                    \
+    }
+
+    f32x16 o[2][2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { o[0][0][i] = 0.f; o[0][1][i] = 0.f; o[1][0][i] = 0.f; o[1][1][i] = 0.f; }
+    float mrun[2] = {-INFINITY, -INFINITY}, lrun[2] = {0.f, 0.f};
+
+    const int nkb = (T + KB - 1) / KB;
+    ATT_GLOAD(0);
+    ATT_LSTORE(0);
+    __syncthreads();
+    int cur = 0;
+    for (int kb = 0; kb < nkb; ++kb) {
+        if (kb + 1 < nkb) { ATT_GLOAD((kb + 1) * KB); }
+        const char* kbase = smem + cur * (KTILE_BYTES + VTILE_BYTES);
+        const char* vbase = kbase + KTILE_BYTES;
+
+        f32x16 s[2][2];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { s[0][0][i] = 0.f; s[0][1][i] = 0.f; s[1][0][i] = 0.f; s[1][1][i] = 0.f; }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbase + k_off(kt * 32 + col, 2 * st + hh));
+                s[0][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[0][st], s[0][kt], 0, 0, 0);
+                s[1][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[1][st], s[1][kt], 0, 0, 0);
+            }
+        const int key0 = kb * KB;
+        if (key0 + KB > T) {  // last, partial block: mask keys >= T
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = key0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                    if (key >= T) { s[0][kt][r] = -INFINITY; s[1][kt][r] = -INFINITY; }
+                }
+        }
+        float mnew[2];
+        bool grow = false;
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+            float bm = -INFINITY;
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int r = 0; r < 16; r += 2) bm = max3_raw(bm, s[qt][kt][r], s[qt][kt][r + 1]);
+            bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+            mnew[qt] = fmaxf(mrun[qt], bm);
+            grow |= (mnew[qt] - mrun[qt]) * C > 8.0f;
+        }
+        if (__any(grow)) {
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt) {
+                const float alpha = __builtin_amdgcn_exp2f((mrun[qt] - mnew[qt]) * C);
+                lrun[qt] *= alpha;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) { o[qt][0][i] *= alpha; o[qt][1][i] *= alpha; }
+                mrun[qt] = mnew[qt];
+            }
+        }
+        // O^T += V^T . P^T; P of one 16-key step made right before its MFMAs (short live
+        // ranges); each V^T fragment feeds both query tiles
+        const float mc0 = mrun[0] * C, mc1 = mrun[1] * C;
+        float ps[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                bf16x8 pf[2];
+#pragma unroll
+                for (int qt = 0; qt < 2; ++qt) {
+                    const float mc = qt ? mc1 : mc0;
+#pragma unroll
+                    for (int j = 0; j < 8; j += 2) {
+                        const float p0 = __builtin_amdgcn_exp2f(fmaf(s[qt][kt][8 * st + j], C, -mc));
+                        const float p1 = __builtin_amdgcn_exp2f(fmaf(s[qt][kt][8 * st + j + 1], C, -mc));
+                        ps[qt][0] += p0;
+                        ps[qt][1] += p1;
+                        const uint32_t w = pack_bf16x2(p0, p1);
+                        pf[qt][j] = (short)(w & 0xffff);
+                        pf[qt][j + 1] = (short)(w >> 16);
+                    }
+                }
+                const int g0 = kt * 8 + st * 4 + hh;
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt) {
+                    const int d = dt * 32 + col;
+                    const uint2 lo = *reinterpret_cast<const uint2*>(vbase + v_off(d, g0));
+                    const uint2 hi = *reinterpret_cast<const uint2*>(vbase + v_off(d, g0 + 2));
+                    bf16x8 vf;
+                    vf[0] = (short)(lo.x & 0xffff); vf[1] = (short)(lo.x >> 16);
+                    vf[2] = (short)(lo.y & 0xffff); vf[3] = (short)(lo.y >> 16);
+                    vf[4] = (short)(hi.x & 0xffff); vf[5] = (short)(hi.x >> 16);
+                    vf[6] = (short)(hi.y & 0xffff); vf[7] = (short)(hi.y >> 16);
+                    o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0], o[0][dt], 0, 0, 0);
+                    o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[1], o[1][dt], 0, 0, 0);
+                }
+            }
+        lrun[0] += ps[0][0] + ps[0][1];
+        lrun[1] += ps[1][0] + ps[1][1];
+        if (kb + 1 < nkb) { ATT_LSTORE(cur ^ 1); }
+        __syncthreads();
+        cur ^= 1;
+    }
+
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+        const float l = lrun[qt] + __shfl_xor(lrun[qt], 32, 64);
+        const int qrow = qbase + qt * 32 + col;
+        if (qrow < nq) {
+            const float inv = 1.0f / l;
+            bf16_t* out = orow + (size_t)qrow * ldo;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int d = dt * 32 + 8 * g + 4 * hh;
+                    uint2 w;
+                    w.x = pack_bf16x2(o[qt][dt][4 * g] * inv, o[qt][dt][4 * g + 1] * inv);
+                    w.y = pack_bf16x2(o[qt][dt][4 * g + 2] * inv, o[qt][dt][4 * g + 3] * inv);
+                    *reinterpret_cast<uint2*>(out + d) = w;
+                }
+        }
+    }
+#undef ATT_GLOAD
+#undef ATT_LSTORE
+}
+
 // Ragged batch: task t attends query rows [q_off, q_off + q_len) to keys / values
 // [kv_off, kv_off + kv_len) of a flat token layout (offsets multiples of 64, rows
 // zero-padded to the next multiple of 64); Q, K: [heads][Npad][64]; V^T tiled per 64-key
 // block, [heads][Npad / 64][64 d][64 keys] (a plain [64][Npad] V^T would put each d-row
 // of a block in a different 2 MB page at large Npad); output rows out_off + r of
 // O [Npad][ldo] at column h * 64.
+// 1-D grid of qblocks x heads x tasks (rounded up to a multiple of 8), dealt so that the
+// query blocks of one (task, head) -- which all stream the same K / V^T -- land on one
+// XCD (hardware deals linear block b to XCD b % 8) and share its L2.
 __global__ __launch_bounds__(256, 2) void k_attention_varlen(const bf16_t* __restrict__ Q,
                                                              const bf16_t* __restrict__ K,
                                                              const bf16_t* __restrict__ Vt, bf16_t* __restrict__ O,
                                                              int ldo, int Npad, const int4* __restrict__ tasks,
-                                                             const int* __restrict__ out_off) {
+                                                             const int* __restrict__ out_off, int nqb, int heads,
+                                                             int total) {
     __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_BYTES + VTILE_BYTES)];
-    const int4 tk = tasks[blockIdx.z];  // q_off, q_len, kv_off, kv_len
-    if ((int)blockIdx.x * 128 >= tk.y || tk.w <= 0) return;
-    const int h = blockIdx.y;
+    const int per_xcd = (int)gridDim.x >> 3;
+    const int logical = ((int)blockIdx.x & 7) * per_xcd + ((int)blockIdx.x >> 3);
+    if (logical >= total) return;
+    const int qb = logical % nqb;
+    const int h = (logical / nqb) % heads;
+    const int t = logical / (nqb * heads);
+    const int4 tk = tasks[t];  // q_off, q_len, kv_off, kv_len
+    if (qb * 256 >= tk.y || tk.w <= 0) return;
     const int qpad = (tk.y + 63) & ~63;
-    attention_tile<true>(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
-                         Vt + ((size_t)h * Npad + tk.z) * 64, Npad, tk.w, tk.y, qpad, blockIdx.x,
-                   O + (size_t)out_off[blockIdx.z] * ldo + h * 64, ldo);
+    attention_tile_q64<true>(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
+                             Vt + ((size_t)h * Npad + tk.z) * 64, Npad, tk.w, tk.y, qpad, qb,
+                             O + (size_t)out_off[t] * ldo + h * 64, ldo);
 }
 
 }  // namespace
@@ -239,8 +441,12 @@ int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf1
                          const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s) {
     if (ntasks <= 0) return MLG_OK;
     if (Npad % 64 || heads <= 0 || max_q <= 0) return MLG_EINVAL;
-    dim3 grid((max_q + 127) / 128, heads, ntasks);
-    hipLaunchKernelGGL(k_attention_varlen, grid, dim3(256), 0, s, Q, K, Vt, O, ldo, Npad, tasks, out_off);
+    const int nqb = (max_q + 255) / 256;
+    const long total = (long)nqb * heads * ntasks;
+    if (total > (1L << 30)) return MLG_EINVAL;
+    const int grid = (int)((total + 7) & ~7L);
+    hipLaunchKernelGGL(k_attention_varlen, dim3(grid), dim3(256), 0, s, Q, K, Vt, O, ldo, Npad, tasks, out_off, nqb,
+                       heads, (int)total);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

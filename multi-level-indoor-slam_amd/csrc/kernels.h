@@ -113,10 +113,10 @@ int mlg_superpoint_run(const mlg_sp_weights_i& w, const uint8_t* frames, int B, 
 // lightglue.hip -- LightGlue matcher over a ragged batch of pairs
 struct mlg_lg_block_i {
     const bf16_t* Wqkv; const float* bqkv;  // self: [768][256]; cross: [to_qk; to_v] [512][256]
-    const bf16_t* Wout; const float* bout;  // [256][256]
-    const bf16_t* Wf1;  const float* bf1;   // [512][512]
+    const bf16_t* Wout; const float* bout;  // [256][256]   } packed k-step-major,
+    const bf16_t* Wf1;  const float* bf1;   // [512][512]   } [K/16][N][16] (lg_ffn.hip)
     const float* ln_g;  const float* ln_b;  // [512]
-    const bf16_t* Wf2;  const float* bf2;   // [256][512]
+    const bf16_t* Wf2;  const float* bf2;   // [256][512]   }
 };
 struct mlg_lg_weights_i {
     const float* Wr;  // [32][2]
@@ -126,6 +126,10 @@ struct mlg_lg_weights_i {
     const float* wconf[8];   const float* bconf[8];   // [256], [1]
     const float* ones;                                 // [256] of 1.0f
 };
+// lg_ffn.hip -- fused out_proj + FFN (Linear, LayerNorm, GELU, Linear) + residual of one
+// LightGlue block over M token rows: X f32 [M][256] updated in place, its bf16 copy into
+// xcopy [M][ldc] (cols 0..255); ctx bf16 [M][256] is the attention output.
+int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s);
 size_t mlg_lightglue_ws_bytes(int P, int kmax);
 int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float* desc, const int32_t* counts, int kmax,
                       const int32_t* pa, const int32_t* pb, int P, float depth_conf, float width_conf,

@@ -111,37 +111,6 @@ __global__ __launch_bounds__(256) void k_lg_init(const Seg* __restrict__ segs, c
     }
 }
 
-// ------------------------------------------------------------------ FFN middle
-// h = GELU(LayerNorm_512(h_f32)) -> bf16; one wave per row (8 values per lane).
-__global__ __launch_bounds__(256) void k_lg_ln_gelu(const float* __restrict__ hf, const float* __restrict__ g,
-                                                    const float* __restrict__ b, bf16_t* __restrict__ hb, int M) {
-    const int lane = threadIdx.x & 63;
-    const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= M) return;
-    const float* x = hf + r * 512;
-    float v[8];
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        v[i] = x[lane + 64 * i];
-        s += v[i];
-    }
-    const float mean = wave_sum(s) / 512.f;
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const float d = v[i] - mean;
-        q += d * d;
-    }
-    const float rstd = rsqrtf(wave_sum(q) / 512.f + 1e-5f);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int c = lane + 64 * i;
-        const float y = (v[i] - mean) * rstd * g[c] + b[c];
-        hb[r * 512 + c] = f32_to_bf16(0.5f * y * (1.f + erff(y * 0.70710678118654752f)));
-    }
-}
-
 // ------------------------------------------------------------------ confidences
 // One wave per live token: conf = sigmoid(x . wc + bc), z = x . wm + bm; lz = logsigmoid(z)
 // (the assignment's certainty term); flags[r] = (conf < thr) | keep << 1 with
@@ -532,8 +501,6 @@ LgLayout lg_layout(int P, int kmax) {
     L.K = take(N * LG_D * 2);
     L.Vt = take(N * LG_D * 2);
     L.ctx = take(N * LG_D * 2);
-    L.hf = take(N * 512 * 4);
-    L.hb = take(N * 512 * 2);
     L.live = take(N);
     L.rowseg = take(N * 4);
     L.lz = take(N * 4);
@@ -598,8 +565,6 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     bf16_t* K = (bf16_t*)(base + L.K);
     bf16_t* VT = (bf16_t*)(base + L.Vt);
     bf16_t* CTX = (bf16_t*)(base + L.ctx);
-    float* HF = (float*)(base + L.hf);
-    bf16_t* HB = (bf16_t*)(base + L.hb);
     uint8_t* LIVE = (uint8_t*)(base + L.live);
     int* ROWSEG = (int*)(base + L.rowseg);
     float* LZ = (float*)(base + L.lz);
@@ -697,17 +662,10 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         MlgProfScope prof(5, s, work);
         return mlg_attention_varlen(Q, cross ? Q : K, VT, CTX, LG_D, Npad, LG_H, TASKS + o, OUTOFF + o, nt, maxq, s);
     };
+    // out_proj / to_out + FFN + residual, fused (lg_ffn.hip)
     auto ffn = [&](const mlg_lg_block_i& bw) -> int {
-        const double t = live_tokens();
-        {
-            MlgProfScope prof(6, s, 2.0 * t * (256.0 * 256 + 512.0 * 512));
-            LG_TRY(mlg_gemm_bias_bf16_ld(CTX, LG_D, bw.Wout, bw.bout, CAT + LG_D, 512, Npad, LG_D, LG_D, s));
-            LG_TRY(mlg_gemm_bias_f32_ld(CAT, 512, bw.Wf1, bw.bf1, HF, 512, Npad, 512, 512, s));
-        }
-        hipLaunchKernelGGL(k_lg_ln_gelu, dim3((Npad + 3) / 4), dim3(256), 0, s, HF, bw.ln_g, bw.ln_b, HB, Npad);
-        MLG_LAUNCH_CHECK();
-        MlgProfScope prof(6, s, 2.0 * t * 512.0 * 256);
-        return mlg_gemm_residual_copy(HB, 512, bw.Wf2, bw.bf2, X, LG_D, CAT, 512, Npad, LG_D, 512, s);
+        MlgProfScope prof(6, s, 2.0 * live_tokens() * (256.0 * 256 + 512.0 * 512 + 512.0 * 256));
+        return mlg_lg_ffn(CTX, X, CAT, 512, Npad, bw, s);
     };
     // matchability log-sigmoid of every live token (layer i's head)
     auto certainty = [&](int i) {

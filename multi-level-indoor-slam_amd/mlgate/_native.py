@@ -9,6 +9,10 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmlgate.so")
+# A/B tooling only (tools/*_bench.py): load another build of the same library
+_LIB_OVERRIDE = os.environ.get("MLGATE_LIB_AB")
+if _LIB_OVERRIDE:
+    LIB_PATH = _LIB_OVERRIDE
 
 c_int, c_long, c_size_t, c_float, c_double, c_void_p = (
     ctypes.c_int, ctypes.c_long, ctypes.c_size_t, ctypes.c_float, ctypes.c_double, ctypes.c_void_p)
@@ -64,6 +68,9 @@ EXPORTS = {
                                      c_void_p]),
     "mlg_op_layernorm_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "mlg_op_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mlg_op_attention_varlen": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                        c_void_p, c_int, c_int, c_void_p]),
+    "mlg_op_lg_ffn": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 8 + [c_void_p]),
     "mlg_op_preprocess_patches": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_long, c_int, c_void_p,
                                           c_void_p]),
     "mlg_prof_enable": (c_int, [c_int]),
@@ -88,6 +95,8 @@ def lib():
                               "g.build()'` (hipcc --offload-arch=gfx950)")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in EXPORTS.items():
+            if _LIB_OVERRIDE and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -34,6 +34,15 @@ def qkv_row_order():
     return (h * 192 + d * 3 + s).reshape(-1)
 
 
+def pack_kstep(w):
+    """nn.Linear weight [N, K] -> k-step-major [K/16, N, 16] (the layout of the fused
+    block-tail kernel, csrc/lg_ffn.hip: a wave's 32 rows x 16 k of one MFMA step are one
+    contiguous 1 KiB)."""
+    w = np.asarray(w, np.float32)
+    n, k = w.shape
+    return np.ascontiguousarray(w.reshape(n, k // 16, 16).transpose(1, 0, 2))
+
+
 class LightGlueGPU:
     """Batched LightGlue(features='superpoint') on the HIP device."""
 
@@ -67,13 +76,15 @@ class LightGlueGPU:
             perm = qkv_row_order()
             b.Wqkv = self._t(np.asarray(sd[p + "Wqkv.weight"])[perm], bf)
             b.bqkv = self._t(np.asarray(sd[p + "Wqkv.bias"])[perm], f32)
-            b.Wout, b.bout = self._t(sd[p + "out_proj.weight"], bf), self._t(sd[p + "out_proj.bias"], f32)
+            b.Wout = self._t(pack_kstep(sd[p + "out_proj.weight"]), bf)
+            b.bout = self._t(sd[p + "out_proj.bias"], f32)
             self._ffn(b, sd, p)
             p = f"transformers.{i}.cross_attn."
             c = w.cross[i]
             c.Wqkv = self._t(np.concatenate([sd[p + "to_qk.weight"], sd[p + "to_v.weight"]]), bf)
             c.bqkv = self._t(np.concatenate([sd[p + "to_qk.bias"], sd[p + "to_v.bias"]]), f32)
-            c.Wout, c.bout = self._t(sd[p + "to_out.weight"], bf), self._t(sd[p + "to_out.bias"], f32)
+            c.Wout = self._t(pack_kstep(sd[p + "to_out.weight"]), bf)
+            c.bout = self._t(sd[p + "to_out.bias"], f32)
             self._ffn(c, sd, p)
             p = f"log_assignment.{i}."
             w.Wfinal[i] = self._t(sd[p + "final_proj.weight"], bf)
@@ -89,9 +100,9 @@ class LightGlueGPU:
 
     def _ffn(self, b, sd, p):
         bf, f32 = torch.bfloat16, torch.float32
-        b.Wf1, b.bf1 = self._t(sd[p + "ffn.0.weight"], bf), self._t(sd[p + "ffn.0.bias"], f32)
+        b.Wf1, b.bf1 = self._t(pack_kstep(sd[p + "ffn.0.weight"]), bf), self._t(sd[p + "ffn.0.bias"], f32)
         b.ln_g, b.ln_b = self._t(sd[p + "ffn.1.weight"], f32), self._t(sd[p + "ffn.1.bias"], f32)
-        b.Wf2, b.bf2 = self._t(sd[p + "ffn.3.weight"], bf), self._t(sd[p + "ffn.3.bias"], f32)
+        b.Wf2, b.bf2 = self._t(pack_kstep(sd[p + "ffn.3.weight"]), bf), self._t(sd[p + "ffn.3.bias"], f32)
 
     def match_device(self, kpts, desc, counts, pair_a, pair_b):
         """kpts f32 [F, kmax, 2], desc f32 [F, kmax, 256] on the device; counts, pair_a, pair_b

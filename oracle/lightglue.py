@@ -137,8 +137,13 @@ class Oracle:
         return torch.where(valid0, m0, -1), torch.where(valid1, m1, -1), ms0, ms1
 
     def match(self, kpts0, desc0, kpts1, desc1, depth_confidence=0.95, width_confidence=0.99,
-              filter_threshold=0.1, pruning_min_kpts=1536):
-        """One pair -> dict(matches [S, 2] (indices into the inputs), scores [S], stop, prune0, prune1)."""
+              filter_threshold=0.1, pruning_min_kpts=1536, force_stop=None, band=5e-3):
+        """One pair -> dict(matches [S, 2] (indices into the inputs), scores [S], stop, prune0, prune1,
+        depth_band).  depth_band[i] = (lo, hi): the early-stop ratio of layer i if every token
+        confidence within `band` of the threshold fell on the low / the high side -- the
+        decision is numerically ambiguous when lo <= depth_confidence < hi.  force_stop = s
+        replaces the early-stop test by "stop after layer s" (to compare matches when a
+        bf16 kernel took the other side of an ambiguous decision)."""
         k0 = normalize_keypoints(torch.as_tensor(kpts0, dtype=torch.float32))
         k1 = normalize_keypoints(torch.as_tensor(kpts1, dtype=torch.float32))
         x0 = torch.as_tensor(desc0, dtype=torch.float32).clone()
@@ -148,6 +153,7 @@ class Oracle:
         ind0, ind1 = torch.arange(m), torch.arange(n)
         prune0, prune1 = torch.ones(m, dtype=torch.long), torch.ones(n, dtype=torch.long)
         i = 0
+        depth_band = []
         for i in range(L):
             if len(x0) == 0 or len(x1) == 0:
                 break
@@ -159,8 +165,11 @@ class Oracle:
             t0, t1 = self.confidence(x0, i), self.confidence(x1, i)
             if depth_confidence > 0:
                 c = torch.cat([t0, t1])
-                ratio = 1.0 - (c < conf_threshold(i)).float().sum() / (m + n)
-                if ratio > depth_confidence:
+                thr = conf_threshold(i)
+                ratio = 1.0 - (c < thr).float().sum() / (m + n)
+                depth_band.append((float(1.0 - (c < thr + band).float().sum() / (m + n)),
+                                   float(1.0 - (c < thr - band).float().sum() / (m + n))))
+                if (ratio > depth_confidence) if force_stop is None else (i + 1 == force_stop):
                     break
             if width_confidence > 0 and len(x0) > pruning_min_kpts:
                 keep = (torch.sigmoid(self.matchability(x0, i)).squeeze(-1) > 1 - width_confidence) | \
@@ -176,11 +185,11 @@ class Oracle:
                 prune1[ind1] += 1
         if len(x0) == 0 or len(x1) == 0:
             return {"matches": torch.zeros(0, 2, dtype=torch.long), "scores": torch.zeros(0), "stop": i + 1,
-                    "prune0": prune0, "prune1": prune1}
+                    "prune0": prune0, "prune1": prune1, "depth_band": depth_band}
         scores = self.assignment(x0, x1, i)
         mm0, mm1, ms0, ms1 = self.filter_matches(scores, filter_threshold)
         valid = mm0 > -1
         a = torch.where(valid)[0]
         b = mm0[valid]
         return {"matches": torch.stack([ind0[a], ind1[b]], -1), "scores": ms0[valid], "stop": i + 1,
-                "prune0": prune0, "prune1": prune1}
+                "prune0": prune0, "prune1": prune1, "depth_band": depth_band}

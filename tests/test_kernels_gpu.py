@@ -146,3 +146,69 @@ def test_preprocess_bit_exact(dev, shape):
         got = out[b * 529:(b + 1) * 529]
         assert torch.equal(got[:, :588].view(torch.int16), ref.view(torch.int16))
         assert torch.count_nonzero(got[:, 588:].float()) == 0
+
+
+@pytest.mark.parametrize("lens", [(64, 70), (1, 200, 3, 129), (700, 650, 2048, 1900), (300, 17)])
+def test_attention_varlen(dev, lens):
+    """LightGlue's ragged self / cross attention (k_attention_varlen) vs float32 softmax."""
+    H = 4
+    lens = np.array(lens)
+    offs = np.concatenate([[0], np.cumsum((lens + 63) // 64 * 64)])
+    Npad = int(offs[-1])
+    g = torch.Generator().manual_seed(int(lens.sum()))
+    Q = bf16_bits(torch.randn(H, Npad, 64, generator=g) * 1.5)
+    K = bf16_bits(torch.randn(H, Npad, 64, generator=g) * 1.5)
+    V = bf16_bits(torch.randn(H, Npad, 64, generator=g))
+    Vt = V.view(H, Npad // 64, 64, 64).transpose(2, 3).contiguous()
+    tasks, outs = [], []
+    for i in range(len(lens)):  # self, then cross with the next segment
+        j = (i + 1) % len(lens)
+        tasks += [(offs[i], lens[i], offs[i], lens[i])]
+        tasks += [(offs[i], lens[i], offs[j], lens[j])]
+    O = torch.zeros(2, Npad, H * 64, dtype=torch.bfloat16, device=dev)
+    L = _native.lib()
+    Qd, Kd, Vd = Q.to(dev), K.to(dev), Vt.to(dev)  # kept alive until the launches have run
+    for kind in range(2):
+        T = torch.tensor(np.array(tasks[kind::2], np.int32), device=dev)
+        OO = torch.tensor(np.array([t[0] for t in tasks[kind::2]], np.int32), device=dev)
+        _native.check(L.mlg_op_attention_varlen(P(Qd), P(Kd), P(Vd), P(O[kind]), H * 64, Npad, H, P(T), P(OO),
+                                                len(T), int(lens.max()), S(dev)), "attn varlen")
+        torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    O = O.float().cpu()
+    for n, (qo, ql, ko, kl) in enumerate(tasks):
+        q, k, v = Q[:, qo:qo + ql].float(), K[:, ko:ko + kl].float(), V[:, ko:ko + kl].float()
+        ref = (torch.softmax(q @ k.transpose(1, 2) / 8.0, -1) @ v).transpose(0, 1).reshape(ql, H * 64)
+        got = O[n % 2, qo:qo + ql]
+        assert rel_err(got, ref) < 1e-2, (n, rel_err(got, ref))
+
+
+@pytest.mark.parametrize("M", [192, 1000, 128])
+def test_lg_ffn_fused(dev, M):
+    """Fused LightGlue block tail (lg_ffn.hip) vs float32 torch on the same bf16 operands."""
+    g = torch.Generator().manual_seed(M)
+    w = {"Wout": (256, 256), "Wf1": (512, 512), "Wf2": (256, 512)}
+    W = {k: bf16_bits(torch.randn(*s, generator=g) / s[1] ** 0.5) for k, s in w.items()}
+    b = {k: torch.randn(n, generator=g) * 0.1 for k, n in (("bout", 256), ("bf1", 512), ("bf2", 256))}
+    ln_g, ln_b = 1 + 0.1 * torch.randn(512, generator=g), 0.1 * torch.randn(512, generator=g)
+    X = torch.randn(M, 256, generator=g)
+    ctx = bf16_bits(torch.randn(M, 256, generator=g))
+    Xd = X.to(dev)
+    xc = torch.zeros(M, 512, dtype=torch.bfloat16, device=dev)
+    from mlgate.lightglue import pack_kstep
+    dW = {k: torch.from_numpy(pack_kstep(v.float().numpy())).to(torch.bfloat16).to(dev) for k, v in W.items()}
+    db = {k: v.to(dev) for k, v in b.items()}
+    gd, bd = ln_g.to(dev), ln_b.to(dev)
+    ctxd = ctx.to(dev)
+    _native.check(_native.lib().mlg_op_lg_ffn(P(ctxd), P(Xd), P(xc), 512, M, P(dW["Wout"]), P(db["bout"]),
+                                              P(dW["Wf1"]), P(db["bf1"]), P(gd), P(bd), P(dW["Wf2"]), P(db["bf2"]),
+                                              S(dev)), "lg_ffn")
+    torch.cuda.synchronize()
+    msg = bf16_bits(ctx.float() @ W["Wout"].float().T + b["bout"]).float()
+    cat = torch.cat([bf16_bits(X).float(), msg], -1)
+    h = cat @ W["Wf1"].float().T + b["bf1"]
+    h = bf16_bits(F.gelu(F.layer_norm(h, (512,), ln_g, ln_b))).float()
+    ref = X + h @ W["Wf2"].float().T + b["bf2"]
+    got = Xd.cpu()
+    assert rel_err(got - X, ref - X) < 1e-2
+    assert torch.equal(xc[:, :256].cpu(), bf16_bits(got))
