@@ -152,7 +152,8 @@ int mlg_op_attention_varlen(const uint16_t* Q, const uint16_t* K, const uint16_t
                             void* stream);
 /* Fused LightGlue block tail (SelfBlock / CrossBlock after the attention):
  * msg = ctx Wout^T + bout; X += Wf2 GELU(LN(Wf1 [bf16(X) | bf16(msg)] + bf1)) + bf2 for M token
- * rows; X f32 [M][256] in place, bf16(X) into xcopy [M][ldc] cols 0..255.  bf16 weights
+ * rows; X f32 [M][256] in place; xcopy [M][ldc] cols 0..255 holds bf16(X) on entry (the
+ * GEMM operand, as the previous block left it) and on exit.  bf16 weights
  * packed k-step-major: W[n][k] of an nn.Linear ([out][in]) stored at [k/16][n][k%16].
  * Device pointers. */
 int mlg_op_lg_ffn(const uint16_t* ctx, float* X, uint16_t* xcopy, int ldc, int M, const uint16_t* Wout,

@@ -127,8 +127,9 @@ struct mlg_lg_weights_i {
     const float* ones;                                 // [256] of 1.0f
 };
 // lg_ffn.hip -- fused out_proj + FFN (Linear, LayerNorm, GELU, Linear) + residual of one
-// LightGlue block over M token rows: X f32 [M][256] updated in place, its bf16 copy into
-// xcopy [M][ldc] (cols 0..255); ctx bf16 [M][256] is the attention output.
+// LightGlue block over M token rows: X f32 [M][256] updated in place, its bf16 copy
+// xcopy [M][ldc] (cols 0..255; read as the GEMM operand, then rewritten); ctx bf16
+// [M][256] is the attention output.
 int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s);
 size_t mlg_lightglue_ws_bytes(int P, int kmax);
 int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float* desc, const int32_t* counts, int kmax,

@@ -5,23 +5,26 @@
 //   msg = out_proj(ctx)                               (to_out for the cross block)
 //   x  += Linear2( GELU( LayerNorm( Linear1( [x | msg] ) ) ) )
 //
-// in ONE kernel per 128-token tile.  Unfused, this tail moved ~10.5 KB of HBM per token
+// in ONE kernel per 64-token tile.  Unfused, this tail moved ~10.5 KB of HBM per token
 // (ctx, msg, the f32 FFN hidden, its bf16 GELU output, x twice); fused, the
-// concatenation, the hidden and the GELU output never leave LDS: ~3 KB per token (ctx
-// in, x f32 in and out, the bf16 copy of x the next block's projections read).
+// concatenation, the hidden and the GELU output never leave LDS: 3.5 KB per token (ctx
+// and the bf16 copy of x in; the f32 residual read, updated and written; the new bf16
+// copy of x, which the next block's projections read, written).
 //
-// One workgroup = 8 waves = 128 token rows.  LDS holds the tile's [x | ctx] as bf16
-// [128][512] (XOR-swizzled 16-B chunks); the three GEMMs run as C^T = W . T^T with
-// v_mfma_f32_32x32x16_bf16 (W fragments from global/L2, k-step-major packed, in a
-// register ring one 64-K block ahead; token fragments from LDS), each wave owning a slice of the output
-// columns for all 128 rows:
-//   1. msg  : wave w -> cols [32w, 32w+32) of 256   (K = 256 over the ctx half);
+// One workgroup = 4 waves = 64 token rows, two workgroups per CU, so one workgroup's
+// HBM phases (tile in, residual out) overlap the other's MFMAs.  LDS holds the tile's
+// [x | ctx] as bf16 [64][512] (XOR-swizzled 16-B chunks); the three GEMMs run as
+// C^T = W . T^T with v_mfma_f32_32x32x16_bf16 (W fragments from global/L2, k-step-major
+// packed, in a register ring four k-steps ahead; token fragments from LDS,
+// double-buffered one k-step ahead), each wave owning a slice of the output columns for
+// all 64 rows:
+//   1. msg  : wave w -> cols [64w, 64w+64) of 256   (K = 256 over the ctx half);
 //             msg + bias, bf16, overwrites the ctx half in LDS
-//   2. ffn1 : wave w -> cols [64w, 64w+64) of 512   (K = 512 over [x | msg]);
+//   2. ffn1 : wave w -> cols [128w, 128w+128) of 512 (K = 512 over [x | msg]);
 //             + bias, LayerNorm(512, eps 1e-5) statistics reduced lane -> half-wave ->
-//             8 waves through LDS (two passes: mean, then centred variance), GELU (erf),
+//             4 waves through LDS (two passes: mean, then centred variance), GELU (erf),
 //             bf16, overwrites [x | msg] in LDS
-//   3. ffn2 : wave w -> cols [32w, 32w+32) of 256   (K = 512);
+//   3. ffn2 : wave w -> cols [64w, 64w+64) of 256   (K = 512);
 //             x += acc + bias (f32), bf16 copy of x written for the next projections.
 // The accumulator of the transposed product gives each lane 4 consecutive output
 // columns of one token: LayerNorm sums are lane-local up to one cross-half exchange,
@@ -31,11 +34,15 @@
 
 namespace {
 
-constexpr int R = 128;      // token rows per workgroup
+constexpr int R = 64;       // token rows per workgroup
+constexpr int NW = 4;       // waves per workgroup
+constexpr int MT = R / 32;  // 32-row m-tiles
 constexpr int ROWB = 1024;  // LDS bytes per token row: 512 bf16
 constexpr int LDS_CAT = R * ROWB;
 
-__device__ __forceinline__ int cat_off(int row, int chunk) { return row * ROWB + ((chunk ^ (row & 7)) << 4); }
+// 16-B chunk c of row r at slot c ^ (r & 15): the 16 lanes of each ds_read_b128 lane
+// group (rows {0-3,12-15,20-27} + 32 k, one chunk) then hit 16 distinct bank quads.
+__device__ __forceinline__ int cat_off(int row, int chunk) { return row * ROWB + ((chunk ^ (row & 15)) << 4); }
 
 __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
@@ -54,141 +61,174 @@ __device__ __forceinline__ float gelu_erf_fast(float x) {
 }
 
 // acc[t][mt] += W[n0 + 32 t + i][k] * T[32 mt + j][k] over K = 64 * nkb, with T the LDS
-// tile starting at 16-B chunk `chunk0`.  W is packed k-step-major, [K/16][N][16] bf16
-// (mlgate.lightglue.pack_kstep), so the 32 rows x 32 B a wave reads per k-step are one
-// contiguous 1 KiB: every fetched line is consumed by the instruction that fetched it.
-// W fragments live in a 4-step ring: step s's registers are refilled with step s of
-// the next 64-K block as soon as its MFMAs have issued (three steps of MFMAs cover the
-// L2 latency).
+// tile starting at 16-B chunk `chunk0` (k-step ks at chunk chunk0 + 2 ks + hh).  W is
+// packed k-step-major, [K/16][N][16] bf16 (mlgate.lightglue.pack_kstep), so the 32 rows
+// x 32 B a wave reads per k-step are one contiguous 1 KiB: every fetched line is
+// consumed by the instruction that fetched it.  W fragments live in a 4-step register
+// ring (slot s refilled with step ks + 4 as soon as step ks's MFMAs have issued); token
+// fragments are read one k-step ahead into the other half of a double buffer.  Loads
+// past the last step re-read the last step (no branches, so the waitcnt pass counts
+// the in-flight loads exactly); addresses are recomputed per call, not hoisted.
 template <int NT>
 __device__ __forceinline__ void gemm_phase(const bf16_t* __restrict__ W, int N, int n0, int nkb, int chunk0,
-                                           const char* lds, f32x16 (&acc)[NT][4]) {
+                                           const char* lds, f32x16 (&acc)[NT][MT]) {
     const int lane = threadIdx.x & 63, col = lane & 31, hh = lane >> 5;
     const size_t step = (size_t)N * 16;
+    const int last = 4 * nkb - 1;
     const bf16_t* wrow[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) wrow[t] = W + (size_t)(n0 + 32 * t + col) * 16 + 8 * hh;
-    bf16x8 wf[NT][4];
+    const char* xrow = lds + col * ROWB;  // + 32 mt rows per m-tile
+    const int sw = col & 15;             // = row & 15 for every m-tile
+    bf16x8 wf[NT][4], xa[MT], xb[MT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int s = 0; s < 4; ++s) wf[t][s] = ld16(wrow[t] + s * step);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+        xa[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + (((chunk0 + hh) ^ sw) << 4));
 #pragma unroll 1
     for (int kb = 0; kb < nkb; ++kb) {
-        const bool more = kb + 1 < nkb;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            const int ch = chunk0 + kb * 8 + 2 * s + hh;
+            const int ks = 4 * kb + s;
+            const int cn = ((chunk0 + 2 * min(ks + 1, last) + hh) ^ sw) << 4;
+            bf16x8(&cur)[MT] = (s & 1) ? xb : xa;
+            bf16x8(&nxt)[MT] = (s & 1) ? xa : xb;
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-                const bf16x8 xf = *reinterpret_cast<const bf16x8*>(lds + cat_off(32 * mt + col, ch));
+            for (int mt = 0; mt < MT; ++mt) nxt[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + cn);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                 for (int t = 0; t < NT; ++t)
-                    acc[t][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[t][s], xf, acc[t][mt], 0, 0, 0);
-            }
-            if (more) {
+                    acc[t][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[t][s], cur[mt], acc[t][mt], 0, 0, 0);
 #pragma unroll
-                for (int t = 0; t < NT; ++t) wf[t][s] = ld16(wrow[t] + (4 * kb + 4 + s) * step);
-            }
+            for (int t = 0; t < NT; ++t) wf[t][s] = ld16(wrow[t] + min(ks + 4, last) * step);
+            // pin the refill here: left alone, the scheduler sinks it next to its use
+            // (minimising live ranges) and every step waits on a fresh L2 round trip
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
 
 template <int NT>
-__device__ __forceinline__ void zero(f32x16 (&acc)[NT][4]) {
+__device__ __forceinline__ void zero(f32x16 (&acc)[NT][MT]) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[t][mt][i] = 0.f;
 }
 
-__global__ __launch_bounds__(512) void k_lg_ffn(const bf16_t* __restrict__ ctx, float* __restrict__ X,
-                                               bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w) {
+__global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ctx, float* __restrict__ X,
+                                                  bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_CAT];
-    __shared__ float red[2][8][R];
+    __shared__ float red[2][NW][R];
+    // biases and LayerNorm affine, staged in LDS: epilogue reads never wait on VMEM
+    // behind the in-flight weight loads
+    __shared__ __attribute__((aligned(16))) float prm[256 + 512 + 512 + 512 + 256];
+    float* s_bout = prm;
+    float* s_bf1 = prm + 256;
+    float* s_lng = prm + 768;
+    float* s_lnb = prm + 1280;
+    float* s_bf2 = prm + 1792;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
     const int m0 = blockIdx.x * R;
-
-    // 0. tile -> LDS: x (f32 -> bf16) into chunks 0..31, ctx (bf16) into chunks 32..63
-#pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-        const int f = i * 512 + tid, row = f >> 6, c4 = f & 63;
-        const int gr = min(m0 + row, M - 1);
-        const float4 v = *reinterpret_cast<const float4*>(X + (size_t)gr * 256 + c4 * 4);
-        *reinterpret_cast<uint2*>(lds + cat_off(row, c4 >> 1) + (c4 & 1) * 8) =
-            make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+    for (int i = tid; i < 512; i += 256) {
+        s_bf1[i] = w.bf1[i];
+        s_lng[i] = w.ln_g[i];
+        s_lnb[i] = w.ln_b[i];
+        if (i < 256) {
+            s_bout[i] = w.bout[i];
+            s_bf2[i] = w.bf2[i];
+        }
     }
+    // 0. tile -> LDS: the bf16 copy of x (written by the previous block) into chunks
+    //    0..31, ctx into chunks 32..63; 32 lanes x 16 B = one 512-B row per half-wave,
+    //    rows clamped to M - 1 (never stored)
+    {
+        uint4 rx[8], rc[8];
+        const int c = lane & 31;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int f = i * 512 + tid, row = f >> 5, c = f & 31;
-        const int gr = min(m0 + row, M - 1);
-        *reinterpret_cast<uint4*>(lds + cat_off(row, 32 + c)) =
-            *reinterpret_cast<const uint4*>(ctx + (size_t)gr * 256 + c * 8);
+        for (int i = 0; i < 8; ++i) {
+            const int row = 8 * i + 2 * wave + hh;
+            const size_t gr = (size_t)min(m0 + row, M - 1);
+            rx[i] = *reinterpret_cast<const uint4*>(xcopy + gr * ldc + c * 8);
+            rc[i] = *reinterpret_cast<const uint4*>(ctx + gr * 256 + c * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int row = 8 * i + 2 * wave + hh;
+            *reinterpret_cast<uint4*>(lds + cat_off(row, c)) = rx[i];
+            *reinterpret_cast<uint4*>(lds + cat_off(row, 32 + c)) = rc[i];
+        }
     }
     __syncthreads();
 
     // 1. msg = ctx . Wout^T + bout  -> bf16 over the ctx half
     {
-        f32x16 acc[1][4];
+        f32x16 acc[2][MT];
         zero(acc);
-        gemm_phase<1>(w.Wout, 256, 32 * wave, 4, 32, lds, acc);
+        gemm_phase<2>(w.Wout, 256, 64 * wave, 4, 32, lds, acc);
         __syncthreads();  // every wave has read the ctx half
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int n = 32 * wave + 8 * g + 4 * hh;
-            const float4 b = *reinterpret_cast<const float4*>(w.bout + n);
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-                const f32x16& a = acc[0][mt];
-                *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, 32 + 4 * wave + g) + 8 * hh) =
-                    make_uint2(pack_bf16x2(a[4 * g] + b.x, a[4 * g + 1] + b.y),
-                               pack_bf16x2(a[4 * g + 2] + b.z, a[4 * g + 3] + b.w));
+            for (int g = 0; g < 4; ++g) {
+                const int n = 64 * wave + 32 * t + 8 * g + 4 * hh;
+                const float4 b = *reinterpret_cast<const float4*>(s_bout + n);
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    const f32x16& a = acc[t][mt];
+                    *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, 32 + n / 8) + 8 * hh) =
+                        make_uint2(pack_bf16x2(a[4 * g] + b.x, a[4 * g + 1] + b.y),
+                                   pack_bf16x2(a[4 * g + 2] + b.z, a[4 * g + 3] + b.w));
+                }
             }
-        }
     }
     __syncthreads();
 
     // 2. h = [x | msg] . W1^T + b1; LayerNorm; GELU -> bf16 over [x | msg]
     {
-        f32x16 acc[2][4];
+        f32x16 acc[4][MT];
         zero(acc);
-        gemm_phase<2>(w.Wf1, 512, 64 * wave, 8, 0, lds, acc);
+        gemm_phase<4>(w.Wf1, 512, 128 * wave, 8, 0, lds, acc);
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const float4 b = *reinterpret_cast<const float4*>(w.bf1 + 64 * wave + 32 * t + 8 * g + 4 * hh);
+                const float4 b = *reinterpret_cast<const float4*>(s_bf1 + 128 * wave + 32 * t + 8 * g + 4 * hh);
 #pragma unroll
-                for (int mt = 0; mt < 4; ++mt) {
+                for (int mt = 0; mt < MT; ++mt) {
                     acc[t][mt][4 * g] += b.x;
                     acc[t][mt][4 * g + 1] += b.y;
                     acc[t][mt][4 * g + 2] += b.z;
                     acc[t][mt][4 * g + 3] += b.w;
                 }
             }
-        float mean[4], rstd[4];
+        float mean[MT], rstd[MT];
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            float s = 0.f;
+        for (int mt = 0; mt < MT; ++mt) {
+            float sum = 0.f;
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
+            for (int t = 0; t < 4; ++t)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) s += acc[t][mt][i];
-            s += __shfl_xor(s, 32, 64);
-            if (hh == 0) red[0][wave][32 * mt + col] = s;
+                for (int i = 0; i < 16; ++i) sum += acc[t][mt][i];
+            sum += __shfl_xor(sum, 32, 64);
+            if (hh == 0) red[0][wave][32 * mt + col] = sum;
         }
         __syncthreads();  // also: every wave has finished reading [x | msg]
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-            float s = 0.f;
+        for (int mt = 0; mt < MT; ++mt) {
+            float sum = 0.f;
 #pragma unroll
-            for (int v = 0; v < 8; ++v) s += red[0][v][32 * mt + col];
-            mean[mt] = s * (1.0f / 512.0f);
+            for (int v = 0; v < NW; ++v) sum += red[0][v][32 * mt + col];
+            mean[mt] = sum * (1.0f / 512.0f);
             float q = 0.f;
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
+            for (int t = 0; t < 4; ++t)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const float d = acc[t][mt][i] - mean[mt];
@@ -199,27 +239,27 @@ __global__ __launch_bounds__(512) void k_lg_ffn(const bf16_t* __restrict__ ctx, 
         }
         __syncthreads();
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
+        for (int mt = 0; mt < MT; ++mt) {
             float q = 0.f;
 #pragma unroll
-            for (int v = 0; v < 8; ++v) q += red[1][v][32 * mt + col];
+            for (int v = 0; v < NW; ++v) q += red[1][v][32 * mt + col];
             rstd[mt] = rsqrtf(q * (1.0f / 512.0f) + 1e-5f);
         }
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < 4; ++t)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const int n = 64 * wave + 32 * t + 8 * g + 4 * hh;
-                const float4 lg = *reinterpret_cast<const float4*>(w.ln_g + n);
-                const float4 lb = *reinterpret_cast<const float4*>(w.ln_b + n);
+                const int n = 128 * wave + 32 * t + 8 * g + 4 * hh;
+                const float4 lg = *reinterpret_cast<const float4*>(s_lng + n);
+                const float4 lb = *reinterpret_cast<const float4*>(s_lnb + n);
 #pragma unroll
-                for (int mt = 0; mt < 4; ++mt) {
+                for (int mt = 0; mt < MT; ++mt) {
                     const f32x16& a = acc[t][mt];
                     const float y0 = gelu_erf_fast((a[4 * g] - mean[mt]) * rstd[mt] * lg.x + lb.x);
                     const float y1 = gelu_erf_fast((a[4 * g + 1] - mean[mt]) * rstd[mt] * lg.y + lb.y);
                     const float y2 = gelu_erf_fast((a[4 * g + 2] - mean[mt]) * rstd[mt] * lg.z + lb.z);
                     const float y3 = gelu_erf_fast((a[4 * g + 3] - mean[mt]) * rstd[mt] * lg.w + lb.w);
-                    *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, 8 * wave + 4 * t + g) + 8 * hh) =
+                    *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, n / 8) + 8 * hh) =
                         make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
                 }
             }
@@ -228,29 +268,31 @@ __global__ __launch_bounds__(512) void k_lg_ffn(const bf16_t* __restrict__ ctx, 
 
     // 3. x += GELU(..) . W2^T + b2 (f32); bf16 copy of x for the next projections
     {
-        f32x16 acc[1][4];
+        f32x16 acc[2][MT];
         zero(acc);
-        gemm_phase<1>(w.Wf2, 256, 32 * wave, 8, 0, lds, acc);
+        gemm_phase<2>(w.Wf2, 256, 64 * wave, 8, 0, lds, acc);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int n = 32 * wave + 8 * g + 4 * hh;
-            const float4 b = *reinterpret_cast<const float4*>(w.bf2 + n);
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) {
-                const int m = m0 + 32 * mt + col;
-                if (m >= M) continue;
-                const f32x16& a = acc[0][mt];
-                float4* px = reinterpret_cast<float4*>(X + (size_t)m * 256 + n);
-                float4 x = *px;
-                x.x += a[4 * g] + b.x;
-                x.y += a[4 * g + 1] + b.y;
-                x.z += a[4 * g + 2] + b.z;
-                x.w += a[4 * g + 3] + b.w;
-                *px = x;
-                *reinterpret_cast<uint2*>(xcopy + (size_t)m * ldc + n) =
-                    make_uint2(pack_bf16x2(x.x, x.y), pack_bf16x2(x.z, x.w));
+            for (int g = 0; g < 4; ++g) {
+                const int n = 64 * wave + 32 * t + 8 * g + 4 * hh;
+                const float4 b = *reinterpret_cast<const float4*>(s_bf2 + n);
+#pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    const int m = m0 + 32 * mt + col;
+                    if (m >= M) continue;
+                    const f32x16& a = acc[t][mt];
+                    float4* px = reinterpret_cast<float4*>(X + (size_t)m * 256 + n);
+                    float4 x = *px;
+                    x.x += a[4 * g] + b.x;
+                    x.y += a[4 * g + 1] + b.y;
+                    x.z += a[4 * g + 2] + b.z;
+                    x.w += a[4 * g + 3] + b.w;
+                    *px = x;
+                    *reinterpret_cast<uint2*>(xcopy + (size_t)m * ldc + n) =
+                        make_uint2(pack_bf16x2(x.x, x.y), pack_bf16x2(x.z, x.w));
+                }
             }
-        }
     }
 }
 
@@ -259,7 +301,7 @@ __global__ __launch_bounds__(512) void k_lg_ffn(const bf16_t* __restrict__ ctx, 
 int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s) {
     if (M <= 0) return MLG_OK;
     if (ldc < 256 || (ldc % 8)) return MLG_EINVAL;
-    hipLaunchKernelGGL(k_lg_ffn, dim3((unsigned)((M + R - 1) / R)), dim3(512), 0, s, ctx, X, xcopy, ldc, M, w);
+    hipLaunchKernelGGL(k_lg_ffn, dim3((unsigned)((M + R - 1) / R)), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

@@ -195,6 +195,7 @@ def test_lg_ffn_fused(dev, M):
     ctx = bf16_bits(torch.randn(M, 256, generator=g))
     Xd = X.to(dev)
     xc = torch.zeros(M, 512, dtype=torch.bfloat16, device=dev)
+    xc[:, :256] = bf16_bits(X).to(dev)  # the bf16 copy of x the previous block wrote
     from mlgate.lightglue import pack_kstep
     dW = {k: torch.from_numpy(pack_kstep(v.float().numpy())).to(torch.bfloat16).to(dev) for k, v in W.items()}
     db = {k: v.to(dev) for k, v in b.items()}
