@@ -12,8 +12,8 @@ candidate the floor gate accepts is verified: SuperPoint keypoints / descriptors
 keyframe (computed once, cached), LightGlue on the pair, essential-matrix RANSAC +
 recoverPose, and the verifier's decision rule (>= 20 inliers, ratio >= 0.25).
 Multi-GPU: frames are sharded across ranks (strong scaling: fixed total); descriptors
-and SuperPoint features are all-gathered over RCCL; each rank gates and verifies its
-own query rows.
+and SuperPoint features are all-gathered over RCCL; each rank gates its own query rows,
+then the gate-accepted pairs are all-gathered and re-split evenly for verification.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--verify all|none]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -41,8 +41,10 @@ from mlgate.vit import VitB14  # noqa: E402
 from mlgate.weights import synthetic_state_dict  # noqa: E402
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md, no sparsity)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 SLOTS = {0: "vit_fc1_gemm", 1: "vit_fc2_gemm", 2: "vit_qkv_gemm", 3: "vit_proj_gemm", 4: "vit_attention",
-         5: "lightglue_attention", 6: "lightglue_gemms", 7: "superpoint_conv3x3"}
+         5: "lightglue_attention", 6: "lightglue_qkv_gemms", 7: "superpoint_conv3x3", 8: "lightglue_ffn_fused"}
+HBM_SLOTS = {8}  # slots whose recorded work is algorithmic HBM bytes (bound "hbm"), not FLOPs
 EMBED, KP = 768, 2048
 ISEC_K = np.array([[893.63, 0.0, 376.95], [0.0, 893.97, 266.57], [0.0, 0.0, 1.0]])  # cam1, SURVEY §8
 
@@ -81,6 +83,19 @@ def make_frames(idx, n_places, dev, seed=0):
         fr = fr + torch.randint(0, 30, fr.shape, generator=g, device=dev, dtype=torch.int16)
         out[i] = fr.clamp_(0, 255).to(torch.uint8)
     return out
+
+
+def pmc_traffic(slot_name):
+    """HBM bytes per launch of the dominant kernel from the committed PMC pass
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from separate
+    `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` runs of this bench, with the
+    gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md), or None if absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        entry = json.load(f).get(slot_name)
+    return entry.get("bytes_per_launch") if entry else None
 
 
 def cpu_baseline(budget_s=12.0, pairs_per_kf=0.0):
@@ -195,8 +210,12 @@ class Gate:
         k = idx.shape[1]
         ok = (valid.bool() & (torch.arange(k, device=self.dev)[None, :] < count[:, None].long()))
         qs, js = torch.nonzero(ok, as_tuple=True)
-        pa = (qs + self.lo).cpu().numpy().astype(np.int32)
-        pb = idx[qs, js].cpu().numpy().astype(np.int32)
+        pa_t, pb_t = (qs + self.lo).to(torch.int32), idx[qs, js].to(torch.int32)
+        # pair-level load balance across ranks (features are all-gathered, so any rank
+        # can verify any pair; the union of the slices is the global pair list)
+        pa_t, pb_t = mdist.balanced_pairs(pa_t, pb_t, self.world, self.rank)
+        pa = pa_t.cpu().numpy()
+        pb = pb_t.cpu().numpy()
         verified = 0
         for c0 in range(0, len(pa), a.lg_chunk):
             ca, cb = pa[c0:c0 + a.lg_chunk], pb[c0:c0 + a.lg_chunk]
@@ -257,7 +276,7 @@ def main():
         L.mlg_prof_read(s, ctypes.byref(ms), ctypes.byref(cnt))
         L.mlg_prof_read_work(s, ctypes.byref(work))
         tot[s] = ms.value
-        tflops[s] = work.value / (ms.value * 1e9) if ms.value > 0 else 0.0
+        tflops[s] = work.value / (ms.value * 1e9) if ms.value > 0 else 0.0  # TFLOP/s, or TB/s for HBM_SLOTS
     dom = max(tot, key=tot.get) if args.warmup > 0 else 0
     L.mlg_prof_reset()
     _native.check(L.mlg_prof_enable(1 << dom), "prof")
@@ -291,8 +310,10 @@ def main():
 
     if rank == 0:
         avg_s = ms.value / 1e3 / max(cnt.value, 1)
-        flops = work.value / max(cnt.value, 1)  # algorithmic FLOPs per launch (averaged)
-        achieved = flops / avg_s / 1e12 if cnt.value else None
+        flops = work.value / max(cnt.value, 1)  # algorithmic FLOPs (bytes) per launch (averaged)
+        hbm = dom in HBM_SLOTS
+        achieved = (flops / avg_s / (1e9 if hbm else 1e12)) if cnt.value else None
+        peak = HBM_PEAK_GBS if hbm else MFMA_BF16_PEAK_TFLOPS
         valid, rejected = (int(x) for x in totals.cpu())
         n_pairs, n_ver = (int(x) for x in pv.cpu())
         steps = max(args.steps, 1)
@@ -311,14 +332,16 @@ def main():
                        "keyframes": N, "vit_batch": args.batch, "parallelism": f"frame-sharded x{world}",
                        "gate_valid": valid, "gate_rejected": rejected,  # per step (totals of the last step)
                        "pairs_verified": n_pairs // steps, "pairs_geometrically_valid": n_ver // steps},
-            "roofline": {"kernel": SLOTS[dom], "bound": "mfma",
+            "roofline": {"kernel": SLOTS[dom], "bound": "hbm" if hbm else "mfma",
                          "achieved": round(achieved, 2) if achieved else None,
-                         "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4) if achieved else None,
-                         "traffic": None, "avg_launch_us": round(avg_s * 1e6, 2), "launches": cnt.value,
-                         "flops_per_launch": round(flops, 1),
+                         "peak": peak, "unit": "GB/s" if hbm else "TFLOP/s",
+                         "frac": round(achieved / peak, 4) if achieved else None,
+                         "traffic": pmc_traffic(SLOTS[dom]), "avg_launch_us": round(avg_s * 1e6, 2),
+                         "launches": cnt.value,
+                         ("bytes_per_launch" if hbm else "flops_per_launch"): round(flops, 1),
                          "stage_ms_per_step": {SLOTS[s]: round(tot[s], 2) for s in SLOTS},
-                         "stage_tflops": {SLOTS[s]: round(tflops[s], 1) for s in SLOTS}},
+                         "stage_rate": {SLOTS[s]: (f"{tflops[s] * 1e3:.0f} GB/s" if s in HBM_SLOTS else
+                                                   f"{tflops[s]:.1f} TFLOP/s") for s in SLOTS}},
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(pairs_per_kf=(n_pairs / steps / N) if gate.verify else 0.0)

@@ -306,9 +306,10 @@ int mlg_recover_pose(const float* kp1, const float* kp2, const int32_t* offsets,
 
 /* ------------------------------------------------------------- profiling --
  * Per-launch HIP-event timing of selected kernels, recorded on the stream the kernel
- * is launched on, with the algorithmic FLOPs of each launch.  slot: 0 ViT fc1 GEMM,
- * 1 fc2, 2 qkv, 3 proj, 4 ViT attention, 5 LightGlue attention (ragged, all tasks of
- * a launch), 6 LightGlue projection / FFN GEMMs, 7 SuperPoint 3x3 convs.  slot_mask
+ * is launched on, with the algorithmic work of each launch (FLOPs; HBM bytes for slot
+ * 8).  slot: 0 ViT fc1 GEMM, 1 fc2, 2 qkv, 3 proj, 4 ViT attention, 5 LightGlue
+ * attention (ragged, all tasks of a launch), 6 LightGlue q/k/v projection GEMMs,
+ * 7 SuperPoint 3x3 convs, 8 LightGlue fused block tail (out_proj + FFN).  slot_mask
  * selects the slots recorded (0 = off); a pool of 16384 event pairs is recycled by
  * mlg_prof_read / mlg_prof_read_work / mlg_prof_reset, which synchronise the recorded
  * events.  Not for use inside graph capture. */

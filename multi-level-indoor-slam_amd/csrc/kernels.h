@@ -12,8 +12,9 @@ typedef uint16_t bf16_t;
 // HIP-event profiling scope (abi.cpp): records the launches between construction and
 // destruction on stream s into `slot` with `work` algorithmic FLOPs (or bytes).
 // Slots: 0 fc1, 1 fc2, 2 qkv, 3 proj, 4 ViT attention, 5 LightGlue attention,
-// 6 LightGlue projections / FFN GEMMs, 7 SuperPoint 3x3 convs.
-#define MLG_PROF_SLOTS 8
+// 6 LightGlue q/k/v projections, 7 SuperPoint 3x3 convs, 8 LightGlue fused block tail
+// (lg_ffn.hip; its `work` is algorithmic HBM bytes, the others' FLOPs).
+#define MLG_PROF_SLOTS 9
 struct MlgProfScope {
     int slot;
     hipStream_t s;

@@ -262,6 +262,72 @@ struct Asg {
 
 constexpr int CH = 256;  // rows per column-statistics chunk
 
+// S = MD[ra .. ra + m) . MD[rb .. rb + n)^T of every listed pair in ONE launch (grid.z =
+// pair; a per-pair launch left most of the chip idle on 2048 x 2048 x 256).  Exact-f32
+// v_mfma_f32_32x32x2_f32 (as upstream, which runs this einsum in float32); 128 x 128
+// tile, 2 x 2 waves of 64 x 64, K = 256 staged 16 at a time, transposed to [k][row].
+constexpr int SBM = 128, SBK = 16;
+__global__ __launch_bounds__(256, 2) void k_asg_sim(const Asg* __restrict__ tab, const float* __restrict__ MD,
+                                                    float* __restrict__ Sall) {
+    const Asg a = tab[blockIdx.z];
+    const int m0 = blockIdx.y * SBM, n0 = blockIdx.x * SBM;
+    if (m0 >= a.m || n0 >= a.n) return;
+    __shared__ float As[SBK][SBM + 4];
+    __shared__ float Bs[SBK][SBM + 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const float* A = MD + (size_t)a.ra * LG_D;
+    const float* B = MD + (size_t)a.rb * LG_D;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[x][y][r] = 0.f;
+    for (int k0 = 0; k0 < LG_D; k0 += SBK) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = tid + i * 256, row = c >> 2, kq = (c & 3) * 4;
+            const float4 va = *reinterpret_cast<const float4*>(A + (size_t)min(m0 + row, a.m - 1) * LG_D + k0 + kq);
+            const float4 vb = *reinterpret_cast<const float4*>(B + (size_t)min(n0 + row, a.n - 1) * LG_D + k0 + kq);
+            As[kq][row] = va.x; As[kq + 1][row] = va.y; As[kq + 2][row] = va.z; As[kq + 3][row] = va.w;
+            Bs[kq][row] = vb.x; Bs[kq + 1][row] = vb.y; Bs[kq + 2][row] = vb.z; Bs[kq + 3][row] = vb.w;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < SBK; kk += 2) {
+            const int k = kk + (lane >> 5);
+            float fa[2], fb[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                fa[t] = As[k][wm * 64 + t * 32 + (lane & 31)];
+                fb[t] = Bs[k][wn * 64 + t * 32 + (lane & 31)];
+            }
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+                for (int y = 0; y < 2; ++y)
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[x], fb[y], acc[x][y], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // D[i][j]: col j = lane & 31, row i = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    float* S = Sall + a.soff;
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+            const int j = n0 + wn * 64 + y * 32 + (lane & 31);
+            if (j >= a.n) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i = m0 + wm * 64 + x * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (i < a.m) S[(size_t)i * a.n + j] = acc[x][y][r];
+            }
+        }
+}
+
 __global__ __launch_bounds__(256) void k_asg_rowlse(const Asg* __restrict__ tab, const float* __restrict__ Sall,
                                                     float* __restrict__ rmax, float* __restrict__ rlog) {
     const Asg a = tab[blockIdx.y];
@@ -664,7 +730,9 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     };
     // out_proj / to_out + FFN + residual, fused (lg_ffn.hip)
     auto ffn = [&](const mlg_lg_block_i& bw) -> int {
-        MlgProfScope prof(6, s, 2.0 * live_tokens() * (256.0 * 256 + 512.0 * 512 + 512.0 * 256));
+        // algorithmic HBM bytes per live token: ctx + bf16 x in (512 + 512), f32 x read +
+        // written (1024 + 1024), bf16 x copy written (512)
+        MlgProfScope prof(8, s, 3584.0 * live_tokens());
         return mlg_lg_ffn(CTX, X, CAT, 512, Npad, bw, s);
     };
     // matchability log-sigmoid of every live token (layer i's head)
@@ -694,13 +762,13 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
                 h_asg.push_back(a);
                 maxm = std::max(maxm, a.m);
                 maxn = std::max(maxn, a.n);
-                LG_TRY(mlg_similarity_f32(MD + (size_t)sa.off * LG_D, sa.len, MD + (size_t)sb.off * LG_D, sb.len, LG_D,
-                                          SS + a.soff, sb.len, s));
                 if (stop_layer) stop_layer[a.pair] = i + 1;
             }
             const unsigned na = (unsigned)h_asg.size();
             if (hipMemcpyAsync(ASG, h_asg.data(), na * sizeof(Asg), hipMemcpyHostToDevice, s) != hipSuccess)
                 return MLG_EHIP;
+            hipLaunchKernelGGL(k_asg_sim, dim3((maxn + SBM - 1) / SBM, (maxm + SBM - 1) / SBM, na), dim3(256), 0, s, ASG,
+                               MD, SS);
             const dim3 rows((maxm + 3) / 4, na), cols((maxn + 63) / 64, (maxm + CH - 1) / CH, na),
                 cfin((maxn + 255) / 256, na);
             hipLaunchKernelGGL(k_asg_rowlse, rows, dim3(256), 0, s, ASG, SS, RMAX, RLOG);

@@ -42,6 +42,34 @@ class RowGather:
         return self.out
 
 
+def balanced_pairs(pa, pb, world, rank, group=None):
+    """Pair-level load balance for the verification stage.  Each rank holds the
+    gate-accepted (query, match) pairs of its own query rows (int32 tensors, row-major
+    order); their number varies with the floor layout and the revisit pattern, so
+    verifying them where they were found leaves ranks idle.  All ranks all-gather the
+    lists (8 B per pair) and take the rank-th contiguous slice of the global,
+    rank-ordered list: the union of the slices is exactly the global list and slice
+    sizes differ by at most one.  Every keyframe's features are all-gathered before this
+    step, so any rank can verify any pair."""
+    if world == 1:
+        return pa, pb
+    dev = pa.device
+    n = torch.tensor([pa.numel()], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    pad = max(max(sizes), 1)
+    send = torch.zeros(2, pad, dtype=torch.int32, device=dev)
+    send[0, :pa.numel()] = pa
+    send[1, :pb.numel()] = pb
+    bufs = [torch.empty_like(send) for _ in range(world)]
+    dist.all_gather(bufs, send, group=group)
+    allp = torch.cat([b[:, :s] for b, s in zip(bufs, sizes)], dim=1)
+    total = allp.shape[1]
+    lo, hi = rank * total // world, (rank + 1) * total // world
+    return allp[0, lo:hi].contiguous(), allp[1, lo:hi].contiguous()
+
+
 def gather_objects_to_rank0(obj, world, rank, group=None):
     """Python objects (e.g. per-rank match arrays) collected on rank 0, in rank order."""
     if world == 1:

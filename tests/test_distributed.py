@@ -63,3 +63,33 @@ def test_shards_cover_exactly():
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
             assert sum(mdist.shard_sizes(n, w)) == n
+
+
+def _pairs_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(rank)
+    n = [7, 0, 23][rank]  # deliberately uneven (and one empty) per-rank pair lists
+    pa = torch.from_numpy((1000 * rank + np.arange(n)).astype(np.int32))
+    pb = torch.from_numpy(rng.integers(0, 100, n).astype(np.int32))
+    sa, sb = mdist.balanced_pairs(pa, pb, world, rank)
+    got = mdist.gather_objects_to_rank0((sa.numpy(), sb.numpy()), world, rank)
+    full = mdist.gather_objects_to_rank0((pa.numpy(), pb.numpy()), world, rank)
+    if rank == 0:
+        ga = np.concatenate([g[0] for g in got])
+        gb = np.concatenate([g[1] for g in got])
+        fa = np.concatenate([f[0] for f in full])
+        fb = np.concatenate([f[1] for f in full])
+        sizes = [len(g[0]) for g in got]
+        ok = np.array_equal(ga, fa) and np.array_equal(gb, fb) and max(sizes) - min(sizes) <= 1
+        with open(out_path, "w") as f:
+            f.write("ok" if ok else f"mismatch {sizes}")
+    dist.destroy_process_group()
+
+
+def test_balanced_pairs_partition_the_global_list(tmp_path):
+    """Verification pairs re-split across ranks: union == the rank-ordered global list,
+    slice sizes within one of each other (bench.py's multi-GPU verification stage)."""
+    out = str(tmp_path / "pairs.txt")
+    mp.spawn(_pairs_worker, args=(3, _free_port(), out), nprocs=3, join=True)
+    assert open(out).read() == "ok"

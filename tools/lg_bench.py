@@ -4,8 +4,8 @@
 
 SuperPoint features of bench.py's synthetic keyframes, then LightGlue on `pairs`
 random pairs in one call (bench.py's lg_chunk), timed with HIP events; prints the
-wall time per call, the profiled slots (LightGlue attention / projections+FFN) with
-achieved TFLOP/s, and a histogram of the layers run.
+wall time per call, the profiled slots (LightGlue attention, projections, fused FFN)
+with achieved TFLOP/s (TB/s for the HBM-bound FFN), and a histogram of the layers run.
 """
 import argparse
 import ctypes
@@ -46,7 +46,7 @@ def main():
     m, s, n, stop = lg.match_device(kp, ds, counts, pa, pb)  # warm-up
     torch.cuda.synchronize()
     L.mlg_prof_reset()
-    L.mlg_prof_enable((1 << 5) | (1 << 6))
+    L.mlg_prof_enable((1 << 5) | (1 << 6) | (1 << 8))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.iters):
@@ -57,12 +57,13 @@ def main():
     res = {"pairs": args.pairs, "mean_keypoints": float(counts.mean()), "no_prune": args.no_prune,
            "ms_per_call": round(e0.elapsed_time(e1) / args.iters, 2),
            "stop_hist": np.bincount(stop, minlength=10).tolist(), "matches_mean": float(n.float().mean())}
-    for slot, name in ((5, "attention"), (6, "proj_ffn")):
+    for slot, name in ((5, "attention"), (6, "qkv_proj"), (8, "ffn_fused")):
         ms, cnt_, work = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
         L.mlg_prof_read(slot, ctypes.byref(ms), ctypes.byref(cnt_))
         L.mlg_prof_read_work(slot, ctypes.byref(work))
+        rate = work.value / (ms.value * 1e9) if ms.value else None  # TFLOP/s, or TB/s for slot 8
         res[name] = {"ms_per_call": round(ms.value / args.iters, 2),
-                     "tflops": round(work.value / (ms.value * 1e9), 1) if ms.value else None}
+                     ("tb_per_s" if slot == 8 else "tflops"): round(rate, 2) if rate else None}
     print(json.dumps(res), flush=True)
 
 
