@@ -266,11 +266,16 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
     }
     __syncthreads();
 
-    // 3. x += GELU(..) . W2^T + b2 (f32); bf16 copy of x for the next projections
+    // 3. x += GELU(..) . W2^T + b2 (f32); bf16 copy of x for the next projections.
+    //    y = acc + b2 is staged in LDS ([64][256] f32 over the dead GELU tile, 16-B chunk
+    //    c of row r at c ^ (r & 15)), then each wave streams whole rows: 64 lanes x 16 B =
+    //    one 1-KiB f32 row of x read, updated and written, its 512-B bf16 copy written --
+    //    full-line HBM traffic instead of 16-B pieces of 32 rows per instruction.
     {
         f32x16 acc[2][MT];
         zero(acc);
         gemm_phase<2>(w.Wf2, 256, 64 * wave, 8, 0, lds, acc);
+        __syncthreads();  // every wave has read the GELU output
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -279,20 +284,28 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
                 const float4 b = *reinterpret_cast<const float4*>(s_bf2 + n);
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt) {
-                    const int m = m0 + 32 * mt + col;
-                    if (m >= M) continue;
+                    const int r = 32 * mt + col;
                     const f32x16& a = acc[t][mt];
-                    float4* px = reinterpret_cast<float4*>(X + (size_t)m * 256 + n);
-                    float4 x = *px;
-                    x.x += a[4 * g] + b.x;
-                    x.y += a[4 * g + 1] + b.y;
-                    x.z += a[4 * g + 2] + b.z;
-                    x.w += a[4 * g + 3] + b.w;
-                    *px = x;
-                    *reinterpret_cast<uint2*>(xcopy + (size_t)m * ldc + n) =
-                        make_uint2(pack_bf16x2(x.x, x.y), pack_bf16x2(x.z, x.w));
+                    *reinterpret_cast<float4*>(lds + r * 1024 + (((n >> 2) ^ (r & 15)) << 4)) =
+                        make_float4(a[4 * g] + b.x, a[4 * g + 1] + b.y, a[4 * g + 2] + b.z, a[4 * g + 3] + b.w);
                 }
             }
+        __syncthreads();
+#pragma unroll 4
+        for (int i = 0; i < R / NW; ++i) {
+            const int r = wave * (R / NW) + i, m = m0 + r;
+            if (m >= M) break;  // wave-uniform
+            const float4 y = *reinterpret_cast<const float4*>(lds + r * 1024 + ((lane ^ (r & 15)) << 4));
+            float4* px = reinterpret_cast<float4*>(X + (size_t)m * 256) + lane;
+            float4 x = *px;
+            x.x += y.x;
+            x.y += y.y;
+            x.z += y.z;
+            x.w += y.w;
+            *px = x;
+            *reinterpret_cast<uint2*>(xcopy + (size_t)m * ldc + 4 * lane) =
+                make_uint2(pack_bf16x2(x.x, x.y), pack_bf16x2(x.z, x.w));
+        }
     }
 }
 
