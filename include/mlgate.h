@@ -159,6 +159,14 @@ int mlg_op_attention_varlen(const uint16_t* Q, const uint16_t* K, const uint16_t
 int mlg_op_lg_ffn(const uint16_t* ctx, float* X, uint16_t* xcopy, int ldc, int M, const uint16_t* Wout,
                   const float* bout, const uint16_t* Wf1, const float* bf1, const float* ln_g, const float* ln_b,
                   const uint16_t* Wf2, const float* bf2, void* stream);
+/* LightGlue block projections (lg_proj.hip): self_block != 0: q, k, v = Wqkv x + b with
+ * rotary (ecos / esin f32 [Npad][32]) on q and k; else qk = to_qk x, v = to_v x.  xcopy
+ * bf16 [Npad][ldx] (cols 0..255), W k-step-major [16][768 | 512][16] with rows
+ * [q|k|v] x (head, 64) (self) or [qk | v]; outputs Q, K bf16 [4][Npad][64], Vt bf16
+ * [4][Npad/64][64][64]; rows with live[m] == 0 written as zeros.  Npad % 64 == 0. */
+int mlg_op_lg_proj(int self_block, const uint16_t* xcopy, int ldx, const uint16_t* W, const float* bias,
+                   const float* ecos, const float* esin, const uint8_t* live, uint16_t* Q, uint16_t* K, uint16_t* Vt,
+                   int Npad, void* stream);
 int mlg_op_preprocess_patches(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, int S,
                               uint16_t* patches, void* stream);
 
@@ -259,7 +267,8 @@ int mlg_superpoint(const mlg_sp_weights* w, const uint8_t* frames, int B, int H,
  * int32 [P]; stop_layer (host, optional): layers run per pair.  Synchronises `stream`
  * once per layer (early-stop / pruning decisions). */
 typedef struct mlg_lg_block {
-    const uint16_t* Wqkv; const float* bqkv;  /* self: Wqkv [768][256]; cross: [to_qk; to_v] [512][256] */
+    const uint16_t* Wqkv; const float* bqkv;  /* self: Wqkv [768][256] (rows as [q|k|v] x (head, 64));
+                                                 cross: [to_qk; to_v] [512][256]; k-step-major */
     const uint16_t* Wout; const float* bout;  /* out_proj / to_out [256][256]  } k-step-major: */
     const uint16_t* Wf1;  const float* bf1;   /* ffn.0 [512][512]             } W[n][k] at   */
     const float* ln_g;    const float* ln_b;  /* ffn.1 LayerNorm(512)                          */

@@ -398,6 +398,11 @@ int mlg_op_lg_ffn(const uint16_t* ctx, float* X, uint16_t* xcopy, int ldc, int M
     w.Wout = Wout; w.bout = bout; w.Wf1 = Wf1; w.bf1 = bf1; w.ln_g = ln_g; w.ln_b = ln_b; w.Wf2 = Wf2; w.bf2 = bf2;
     return mlg_lg_ffn(ctx, X, xcopy, ldc, M, w, (hipStream_t)stream);
 }
+int mlg_op_lg_proj(int self_block, const uint16_t* xcopy, int ldx, const uint16_t* W, const float* bias,
+                   const float* ecos, const float* esin, const uint8_t* live, uint16_t* Q, uint16_t* K, uint16_t* Vt,
+                   int Npad, void* stream) {
+    return mlg_lg_proj(self_block != 0, xcopy, ldx, W, bias, ecos, esin, live, Q, K, Vt, Npad, (hipStream_t)stream);
+}
 int mlg_op_preprocess_patches(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, int S,
                               uint16_t* patches, void* stream) {
     return mlg_preprocess_patches(frames, B, H, W, C, frame_stride, S, MLG_VIT_PATCH_K, 1, patches,

@@ -113,7 +113,7 @@ int mlg_superpoint_run(const mlg_sp_weights_i& w, const uint8_t* frames, int B, 
 
 // lightglue.hip -- LightGlue matcher over a ragged batch of pairs
 struct mlg_lg_block_i {
-    const bf16_t* Wqkv; const float* bqkv;  // self: [768][256]; cross: [to_qk; to_v] [512][256]
+    const bf16_t* Wqkv; const float* bqkv;  // self: [768][256]; cross: [to_qk; to_v] [512][256] (k-step-major)
     const bf16_t* Wout; const float* bout;  // [256][256]   } packed k-step-major,
     const bf16_t* Wf1;  const float* bf1;   // [512][512]   } [K/16][N][16] (lg_ffn.hip)
     const float* ln_g;  const float* ln_b;  // [512]
@@ -132,6 +132,10 @@ struct mlg_lg_weights_i {
 // xcopy [M][ldc] (cols 0..255; read as the GEMM operand, then rewritten); ctx bf16
 // [M][256] is the attention output.
 int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s);
+// lg_proj.hip -- LightGlue q/k/v projections (+ rotary for the self block) straight into
+// the attention operands; W packed k-step-major [16][768 | 512][16]; Npad % 64 == 0.
+int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,
+                const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s);
 size_t mlg_lightglue_ws_bytes(int P, int kmax);
 int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float* desc, const int32_t* counts, int kmax,
                       const int32_t* pa, const int32_t* pb, int P, float depth_conf, float width_conf,

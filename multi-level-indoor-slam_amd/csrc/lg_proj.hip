@@ -1,0 +1,165 @@
+// LightGlue block projections (upstream SelfBlock.Wqkv + rotary encoding, CrossBlock
+// to_qk / to_v; LightGlue(features='superpoint') as called by
+// LightGlue._detect_and_match_native, scripts/semantic_gating/geometric_verification.py:
+// 263-312) over the flat token layout, writing the attention operands directly:
+//   Q, K  bf16 [4 heads][Npad][64]                 (self: q, k rotated; cross: qk)
+//   V^T   bf16 [4][Npad / 64][64 d][64 keys]       (attention.hip's tiled V^T)
+// Rows outside live segments are written as zeros.
+//
+// One workgroup = 8 waves = 64 tokens x one 256-column part (q, k or v) of the
+// projection; the bf16 x tile [64][256] sits in LDS (XOR-swizzled 16-B chunks), the
+// weights stream from L2, packed k-step-major [16][N][16] so each wave-instruction
+// reads one contiguous 1 KiB, in a 4-step register ring.  Wave w owns output columns
+// 32 w .. +32 of the part for both 32-token m-tiles.  The q / k parts compute
+// C^T = W . X^T, which hands a lane 4 consecutive head dims of one token (the rotary
+// pairs are lane-local, one 8-B store per lane); the v part swaps the MFMA operands,
+// C = X . W^T, which hands a lane 4 consecutive tokens of one dim: one 8-B store into
+// the transposed V^T row, where the transposed product would need 4 scattered 2-B
+// stores.  Same fragments, operand order only.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int R = 64;      // tokens per workgroup
+constexpr int ROWB = 512;  // LDS bytes per token row: 256 bf16
+
+// chunk c (0..31) of row r at slot c ^ (r & 15): the 16 lanes of a ds_read_b128 lane
+// group (rows {0-3,12-15,20-27} + 32 k, one chunk) hit 16 distinct bank quads.
+__device__ __forceinline__ int xoff(int row, int chunk) { return row * ROWB + ((chunk ^ (row & 15)) << 4); }
+
+__device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+// acc[mt] over K = 256 (16 k-steps; step ks: LDS chunk 2 ks + hh, W slab ks).
+// SWAP: acc = X . W^T (lane col = output column), else acc = W . X^T (lane col = token).
+template <bool SWAP>
+__device__ __forceinline__ void proj_gemm(const bf16_t* __restrict__ wrow, size_t step, const char* lds,
+                                          f32x16 (&acc)[2]) {
+    const int lane = threadIdx.x & 63, col = lane & 31, hh = lane >> 5;
+    const char* xrow = lds + col * ROWB;
+    const int sw = col & 15;
+    bf16x8 wf[4], xa[2], xb[2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) wf[s] = ld16(wrow + s * step);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) xa[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + ((hh ^ sw) << 4));
+#pragma unroll 1
+    for (int kb = 0; kb < 4; ++kb) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int ks = 4 * kb + s;
+            const int cn = ((2 * min(ks + 1, 15) + hh) ^ sw) << 4;
+            bf16x8(&cur)[2] = (s & 1) ? xb : xa;
+            bf16x8(&nxt)[2] = (s & 1) ? xa : xb;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) nxt[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + cn);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+                acc[mt] = SWAP ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[mt], wf[s], acc[mt], 0, 0, 0)
+                               : __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s], cur[mt], acc[mt], 0, 0, 0);
+            // Wait states after the step's MFMAs: without them this kernel's schedule (the
+            // next step's fragment reads and address VALU landing in the registers the MFMAs
+            // just took as A / B) gave run-to-run different q (tests/test_kernels_gpu.py::
+            // test_lightglue_kernels_deterministic); the kernel is HBM-bound, they cost nothing
+            // measurable.
+            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+            wf[s] = ld16(wrow + min(ks + 4, 15) * step);
+            __builtin_amdgcn_sched_barrier(0);  // keep the refill here (lg_ffn.hip)
+        }
+    }
+}
+
+template <bool SELF>
+__global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcopy, int ldx,
+                                                const bf16_t* __restrict__ W, const float* __restrict__ bias,
+                                                const float* __restrict__ ecos, const float* __restrict__ esin,
+                                                const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
+                                                bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad) {
+    constexpr int N = SELF ? 768 : 512;
+    __shared__ __attribute__((aligned(16))) char lds[R * ROWB];
+    __shared__ float2 rot[SELF ? R : 1][32];  // (cos, sin) per token and frequency
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
+    const int m0 = blockIdx.x * R, part = blockIdx.y;
+    const bool is_v = part == (SELF ? 2 : 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int f = i * 512 + tid, row = f >> 5, c = f & 31;
+        *reinterpret_cast<uint4*>(lds + xoff(row, c)) =
+            *reinterpret_cast<const uint4*>(xcopy + (size_t)(m0 + row) * ldx + c * 8);
+        if (SELF && !is_v) {
+            const size_t e = (size_t)(m0 + row) * 32 + c;
+            rot[row][c] = make_float2(ecos[e], esin[e]);
+        }
+    }
+    __syncthreads();
+
+    const int nb = 256 * part + 32 * wave;  // first output column (row of W) of this wave
+    const bf16_t* wrow = W + (size_t)(nb + col) * 16 + 8 * hh;
+    f32x16 acc[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
+
+    if (!is_v) {
+        proj_gemm<false>(wrow, (size_t)N * 16, lds, acc);
+        bf16_t* dst = part == 0 ? Q : K;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = 32 * wave + 8 * g + 4 * hh;  // column within the part
+            const int h = n >> 6, d = n & 63;
+            const float4 b = *reinterpret_cast<const float4*>(bias + 256 * part + n);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                const int r = 32 * mt + col, m = m0 + r;
+                const f32x16& a = acc[mt];
+                float x0 = a[4 * g] + b.x, x1 = a[4 * g + 1] + b.y, x2 = a[4 * g + 2] + b.z, x3 = a[4 * g + 3] + b.w;
+                if (SELF) {  // t * cos + rotate_half(t) * sin, uncontracted as torch
+                    const float2 e0 = rot[r][d >> 1], e1 = rot[r][(d >> 1) + 1];
+                    const float r0 = __fadd_rn(__fmul_rn(x0, e0.x), __fmul_rn(-x1, e0.y));
+                    const float r1 = __fadd_rn(__fmul_rn(x1, e0.x), __fmul_rn(x0, e0.y));
+                    const float r2 = __fadd_rn(__fmul_rn(x2, e1.x), __fmul_rn(-x3, e1.y));
+                    const float r3 = __fadd_rn(__fmul_rn(x3, e1.x), __fmul_rn(x2, e1.y));
+                    x0 = r0; x1 = r1; x2 = r2; x3 = r3;
+                }
+                uint2 o = make_uint2(0u, 0u);
+                if (live[m]) o = make_uint2(pack_bf16x2(x0, x1), pack_bf16x2(x2, x3));
+                *reinterpret_cast<uint2*>(dst + ((size_t)h * Npad + m) * 64 + d) = o;
+            }
+        }
+    } else {
+        proj_gemm<true>(wrow, (size_t)N * 16, lds, acc);
+        const int n = 32 * wave + col, h = n >> 6, d = n & 63;
+        const float b = bias[256 * part + n];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                const int m = m0 + 32 * mt + 8 * g + 4 * hh;  // 4 consecutive tokens
+                const f32x16& a = acc[mt];
+                const uint32_t lv = *reinterpret_cast<const uint32_t*>(live + m);
+                const float v0 = (lv & 0xff) ? a[4 * g] + b : 0.f;
+                const float v1 = (lv & 0xff00) ? a[4 * g + 1] + b : 0.f;
+                const float v2 = (lv & 0xff0000) ? a[4 * g + 2] + b : 0.f;
+                const float v3 = (lv >> 24) ? a[4 * g + 3] + b : 0.f;
+                bf16_t* p = Vt + ((size_t)h * Npad + (m & ~63)) * 64 + (size_t)d * 64 + (m & 63);
+                *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+            }
+    }
+}
+
+}  // namespace
+
+int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,
+                const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s) {
+    if (Npad <= 0 || (Npad % R) || ldx < 256 || (ldx % 8)) return MLG_EINVAL;
+    if (self_block) {
+        hipLaunchKernelGGL(k_lg_proj<true>, dim3((unsigned)(Npad / R), 3), dim3(512), 0, s, xcopy, ldx, W, bias, ecos,
+                           esin, live, Q, K, Vt, Npad);
+    } else {
+        hipLaunchKernelGGL(k_lg_proj<false>, dim3((unsigned)(Npad / R), 2), dim3(512), 0, s, xcopy, ldx, W, bias,
+                           (const float*)nullptr, (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad);
+    }
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}

@@ -790,14 +790,15 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         // self block: projection + rotary + head split fused in the GEMM epilogue
         {
             MlgProfScope prof(6, s, 2.0 * live_tokens() * 768 * 256);
-            LG_TRY(mlg_gemm_lg_self(CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, LG_D, s));
+            LG_TRY(mlg_lg_proj(true, CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, s));
         }
         LG_TRY(attention(false));
         LG_TRY(ffn(w.self[i]));
         // cross block
         {
             MlgProfScope prof(6, s, 2.0 * live_tokens() * 512 * 256);
-            LG_TRY(mlg_gemm_lg_cross(CAT, 512, w.cross[i].Wqkv, w.cross[i].bqkv, LIVE, Q, VT, Npad, LG_D, s));
+            LG_TRY(mlg_lg_proj(false, CAT, 512, w.cross[i].Wqkv, w.cross[i].bqkv, nullptr, nullptr, LIVE, Q, nullptr, VT,
+                               Npad, s));
         }
         LG_TRY(attention(true));
         LG_TRY(ffn(w.cross[i]));

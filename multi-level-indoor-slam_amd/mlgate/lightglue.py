@@ -36,8 +36,8 @@ def qkv_row_order():
 
 def pack_kstep(w):
     """nn.Linear weight [N, K] -> k-step-major [K/16, N, 16] (the layout of the fused
-    block-tail kernel, csrc/lg_ffn.hip: a wave's 32 rows x 16 k of one MFMA step are one
-    contiguous 1 KiB)."""
+    block-tail and projection kernels, csrc/lg_ffn.hip / lg_proj.hip: a wave's 32 rows x
+    16 k of one MFMA step are one contiguous 1 KiB)."""
     w = np.asarray(w, np.float32)
     n, k = w.shape
     return np.ascontiguousarray(w.reshape(n, k // 16, 16).transpose(1, 0, 2))
@@ -74,14 +74,14 @@ class LightGlueGPU:
             p = f"transformers.{i}.self_attn."
             b = w.self_[i]
             perm = qkv_row_order()
-            b.Wqkv = self._t(np.asarray(sd[p + "Wqkv.weight"])[perm], bf)
+            b.Wqkv = self._t(pack_kstep(np.asarray(sd[p + "Wqkv.weight"])[perm]), bf)
             b.bqkv = self._t(np.asarray(sd[p + "Wqkv.bias"])[perm], f32)
             b.Wout = self._t(pack_kstep(sd[p + "out_proj.weight"]), bf)
             b.bout = self._t(sd[p + "out_proj.bias"], f32)
             self._ffn(b, sd, p)
             p = f"transformers.{i}.cross_attn."
             c = w.cross[i]
-            c.Wqkv = self._t(np.concatenate([sd[p + "to_qk.weight"], sd[p + "to_v.weight"]]), bf)
+            c.Wqkv = self._t(pack_kstep(np.concatenate([sd[p + "to_qk.weight"], sd[p + "to_v.weight"]])), bf)
             c.bqkv = self._t(np.concatenate([sd[p + "to_qk.bias"], sd[p + "to_v.bias"]]), f32)
             c.Wout = self._t(pack_kstep(sd[p + "to_out.weight"]), bf)
             c.bout = self._t(sd[p + "to_out.bias"], f32)

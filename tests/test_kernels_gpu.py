@@ -213,3 +213,86 @@ def test_lg_ffn_fused(dev, M):
     got = Xd.cpu()
     assert rel_err(got - X, ref - X) < 1e-2
     assert torch.equal(xc[:, :256].cpu(), bf16_bits(got))
+
+
+@pytest.mark.parametrize("self_block", [True, False])
+def test_lg_proj(dev, self_block):
+    """LightGlue projections (lg_proj.hip) vs float32 torch on the same bf16 operands:
+    q / k (+ rotary) in [4][Npad][64], v in the tiled V^T; dead rows zero."""
+    from mlgate.lightglue import pack_kstep
+    Npad, H = 192, 4
+    N = 768 if self_block else 512
+    g = torch.Generator().manual_seed(N)
+    x = bf16_bits(torch.randn(Npad, 256, generator=g))
+    W = bf16_bits(torch.randn(N, 256, generator=g) / 16)
+    b = torch.randn(N, generator=g) * 0.1
+    ang = torch.rand(Npad, 32, generator=g) * 6.3
+    ec, es = torch.cos(ang), torch.sin(ang)
+    live = (torch.rand(Npad, generator=g) > 0.2).to(torch.uint8)
+    xc = torch.zeros(Npad, 512, dtype=torch.bfloat16)
+    xc[:, :256] = x
+    d = {k: v.to(dev) for k, v in dict(xc=xc, b=b, ec=ec, es=es, live=live).items()}
+    Wd = torch.from_numpy(pack_kstep(W.float().numpy())).to(torch.bfloat16).to(dev)
+    Q = torch.full((H, Npad, 64), 7.0, dtype=torch.bfloat16, device=dev)
+    K = torch.full((H, Npad, 64), 7.0, dtype=torch.bfloat16, device=dev)
+    Vt = torch.full((H, Npad // 64, 64, 64), 7.0, dtype=torch.bfloat16, device=dev)
+    _native.check(_native.lib().mlg_op_lg_proj(int(self_block), P(d["xc"]), 512, P(Wd), P(d["b"]), P(d["ec"]),
+                                               P(d["es"]), P(d["live"]), P(Q), P(K), P(Vt), Npad, S(dev)), "lg_proj")
+    torch.cuda.synchronize()
+    y = x.float() @ W.float().T + b  # [Npad, N]
+    heads = lambda t: t.view(Npad, H, 64).transpose(0, 1)  # noqa: E731
+    m = live.bool()[None, :, None]
+    if self_block:
+        c2, s2 = ec.repeat_interleave(2, -1), es.repeat_interleave(2, -1)
+        rot = lambda t: t * c2 + torch.stack([-t[..., 1::2], t[..., 0::2]], -1).flatten(-2) * s2  # noqa: E731
+        refq, refk, refv = rot(heads(y[:, :256])), rot(heads(y[:, 256:512])), heads(y[:, 512:])
+        assert rel_err(K.float().cpu() * m, refk * m) < 1e-2
+        assert torch.all(K.float().cpu()[~m.expand_as(refk)] == 0)
+    else:
+        refq, refv = heads(y[:, :256]), heads(y[:, 256:])
+    assert rel_err(Q.float().cpu() * m, refq * m) < 1e-2
+    assert torch.all(Q.float().cpu()[~m.expand_as(refq)] == 0)
+    v = Vt.float().cpu().transpose(2, 3).reshape(H, Npad, 64)
+    assert rel_err(v * m, refv * m) < 1e-2
+    assert torch.all(v[~m.expand_as(refv)] == 0)
+
+
+def test_lightglue_kernels_deterministic(dev):
+    """The LightGlue projection, attention and fused block-tail kernels are bit-for-bit
+    deterministic run to run on the same inputs (no races, no order-dependent sums)."""
+    from mlgate.lightglue import pack_kstep
+    L = _native.lib()
+    Npad, H = 8192, 4
+    g = torch.Generator().manual_seed(11)
+    xc = torch.zeros(Npad, 512, dtype=torch.bfloat16)
+    xc[:, :256] = bf16_bits(torch.randn(Npad, 256, generator=g))
+    X = xc[:, :256].float().clone()
+    W = torch.from_numpy(pack_kstep((torch.randn(768, 256, generator=g) / 16).numpy())).to(torch.bfloat16)
+    b = torch.randn(768, generator=g) * 0.1
+    ang = torch.rand(Npad, 32, generator=g) * 6.3
+    live = (torch.rand(Npad, generator=g) > 0.1).to(torch.uint8)
+    d = {k: v.to(dev) for k, v in dict(xc=xc, W=W, b=b, ec=torch.cos(ang), es=torch.sin(ang), live=live).items()}
+    outs = []
+    for _ in range(3):
+        Q = torch.zeros(H, Npad, 64, dtype=torch.bfloat16, device=dev)
+        K = torch.zeros_like(Q)
+        Vt = torch.zeros(H, Npad // 64, 64, 64, dtype=torch.bfloat16, device=dev)
+        _native.check(L.mlg_op_lg_proj(1, P(d["xc"]), 512, P(d["W"]), P(d["b"]), P(d["ec"]), P(d["es"]),
+                                       P(d["live"]), P(Q), P(K), P(Vt), Npad, S(dev)), "proj")
+        tasks = torch.tensor([[s, 2048, s, 2048] for s in range(0, Npad, 2048)], dtype=torch.int32, device=dev)
+        oo = tasks[:, 0].contiguous()
+        O = torch.zeros(Npad, 256, dtype=torch.bfloat16, device=dev)
+        _native.check(L.mlg_op_attention_varlen(P(Q), P(K), P(Vt), P(O), 256, Npad, H, P(tasks), P(oo), len(tasks),
+                                                2048, S(dev)), "attn")
+        Xd, xcd = X.to(dev), d["xc"].clone()
+        w = {k: torch.from_numpy(pack_kstep((torch.randn(*s, generator=torch.Generator().manual_seed(5)) / 16)
+                                            .numpy())).to(torch.bfloat16).to(dev)
+             for k, s in (("o", (256, 256)), ("f1", (512, 512)), ("f2", (256, 512)))}
+        vec = {n: torch.full((n,), 0.01, device=dev) for n in (256, 512)}
+        _native.check(L.mlg_op_lg_ffn(P(O), P(Xd), P(xcd), 512, Npad, P(w["o"]), P(vec[256]), P(w["f1"]), P(vec[512]),
+                                      P(torch.ones(512, device=dev)), P(vec[512]), P(w["f2"]), P(vec[256]), S(dev)),
+                      "ffn")
+        torch.cuda.synchronize()
+        outs.append((Q.cpu(), K.cpu(), Vt.cpu(), O.cpu(), Xd.cpu()))
+    bad = [name for o in outs[1:] for name, a, r in zip("QKVOX", o, outs[0]) if not torch.equal(a, r)]
+    assert not bad, bad
