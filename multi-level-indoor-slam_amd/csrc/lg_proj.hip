@@ -57,12 +57,6 @@ __device__ __forceinline__ void proj_gemm(const bf16_t* __restrict__ wrow, size_
             for (int mt = 0; mt < 2; ++mt)
                 acc[mt] = SWAP ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[mt], wf[s], acc[mt], 0, 0, 0)
                                : __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s], cur[mt], acc[mt], 0, 0, 0);
-            // Wait states after the step's MFMAs: without them this kernel's schedule (the
-            // next step's fragment reads and address VALU landing in the registers the MFMAs
-            // just took as A / B) gave run-to-run different q (tests/test_kernels_gpu.py::
-            // test_lightglue_kernels_deterministic); the kernel is HBM-bound, they cost nothing
-            // measurable.
-            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
             wf[s] = ld16(wrow + min(ks + 4, 15) * step);
             __builtin_amdgcn_sched_barrier(0);  // keep the refill here (lg_ffn.hip)
         }
@@ -77,7 +71,6 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
                                                 bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad) {
     constexpr int N = SELF ? 768 : 512;
     __shared__ __attribute__((aligned(16))) char lds[R * ROWB];
-    __shared__ float2 rot[SELF ? R : 1][32];  // (cos, sin) per token and frequency
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
     const int m0 = blockIdx.x * R, part = blockIdx.y;
     const bool is_v = part == (SELF ? 2 : 1);
@@ -86,10 +79,6 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
         const int f = i * 512 + tid, row = f >> 5, c = f & 31;
         *reinterpret_cast<uint4*>(lds + xoff(row, c)) =
             *reinterpret_cast<const uint4*>(xcopy + (size_t)(m0 + row) * ldx + c * 8);
-        if (SELF && !is_v) {
-            const size_t e = (size_t)(m0 + row) * 32 + c;
-            rot[row][c] = make_float2(ecos[e], esin[e]);
-        }
     }
     __syncthreads();
 
@@ -102,6 +91,22 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
         for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
 
     if (!is_v) {
+        // rotary factors (cos, sin of frequencies d/2, d/2 + 1) of this lane's 2 tokens x 4
+        // head-dim groups, fetched before the GEMM so their latency hides under it.  Read
+        // straight from global: an LDS-staged copy of the tile's factors gave run-to-run
+        // different q / k on gfx950 (unexplained; tests/test_kernels_gpu.py::
+        // test_lightglue_kernels_deterministic).
+        float2 rc[2][4], rs[2][4];
+        if (SELF) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    const size_t eo = (size_t)(m0 + 32 * mt + col) * 32 + ((32 * wave + 8 * g + 4 * hh) & 63) / 2;
+                    rc[mt][g] = *reinterpret_cast<const float2*>(ecos + eo);
+                    rs[mt][g] = *reinterpret_cast<const float2*>(esin + eo);
+                }
+        }
         proj_gemm<false>(wrow, (size_t)N * 16, lds, acc);
         bf16_t* dst = part == 0 ? Q : K;
 #pragma unroll
@@ -115,7 +120,7 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
                 const f32x16& a = acc[mt];
                 float x0 = a[4 * g] + b.x, x1 = a[4 * g + 1] + b.y, x2 = a[4 * g + 2] + b.z, x3 = a[4 * g + 3] + b.w;
                 if (SELF) {  // t * cos + rotate_half(t) * sin, uncontracted as torch
-                    const float2 e0 = rot[r][d >> 1], e1 = rot[r][(d >> 1) + 1];
+                    const float2 e0 = make_float2(rc[mt][g].x, rs[mt][g].x), e1 = make_float2(rc[mt][g].y, rs[mt][g].y);
                     const float r0 = __fadd_rn(__fmul_rn(x0, e0.x), __fmul_rn(-x1, e0.y));
                     const float r1 = __fadd_rn(__fmul_rn(x1, e0.x), __fmul_rn(x0, e0.y));
                     const float r2 = __fadd_rn(__fmul_rn(x2, e1.x), __fmul_rn(-x3, e1.y));

@@ -17,4 +17,4 @@ for pass in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "pass $i ($pass) rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
-python3 "$REPO/tools/pmc_traffic.py" "$OUT" "$REPO/profiles/pmc_traffic.json"
+python3 "$REPO/tools/pmc_traffic.py" "$OUT" "$OUT/pmc_traffic.json"  # copy to profiles/ after the merge
