@@ -131,7 +131,19 @@ struct mlg_lg_weights_i {
 // LightGlue block over M token rows: X f32 [M][256] updated in place, its bf16 copy
 // xcopy [M][ldc] (cols 0..255; read as the GEMM operand, then rewritten); ctx bf16
 // [M][256] is the attention output.
-int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s);
+// Optional heads fused into the block tail's final row pass (lightglue.hip k_lg_conf
+// semantics): z = x . wm + bm -> lz = logsigmoid(z); with wc: conf = sigmoid(x . wc + bc),
+// flags = (conf < thr) | (sigmoid(z) > 1 - width || conf <= thr) << 1; dead rows
+// (rowseg < 0) get flags 0 and no lz.  wm == nullptr: off.
+struct mlg_lg_conf_i {
+    const int* rowseg;
+    const float* wc; const float* bc;
+    const float* wm; const float* bm;
+    float thr, width;
+    float* lz; uint8_t* flags;
+};
+int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s,
+               const mlg_lg_conf_i* conf = nullptr);
 // lg_proj.hip -- LightGlue q/k/v projections (+ rotary for the self block) straight into
 // the attention operands; W packed k-step-major [16][768 | 512][16]; Npad % 64 == 0.
 int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,

@@ -60,6 +60,10 @@ __device__ __forceinline__ float gelu_erf_fast(float x) {
     return 0.5f * x * (1.0f + e);
 }
 
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+// log(sigmoid(x)) = min(x, 0) - log1p(exp(-|x|))  (torch's stable form)
+__device__ __forceinline__ float logsigmoid_f(float x) { return fminf(x, 0.f) - log1pf(expf(-fabsf(x))); }
+
 // acc[t][mt] += W[n0 + 32 t + i][k] * T[32 mt + j][k] over K = 64 * nkb, with T the LDS
 // tile starting at 16-B chunk `chunk0` (k-step ks at chunk chunk0 + 2 ks + hh).  W is
 // packed k-step-major, [K/16][N][16] bf16 (mlgate.lightglue.pack_kstep), so the 32 rows
@@ -123,7 +127,8 @@ __device__ __forceinline__ void zero(f32x16 (&acc)[NT][MT]) {
 }
 
 __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ctx, float* __restrict__ X,
-                                                  bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w) {
+                                                  bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w,
+                                                  mlg_lg_conf_i cf) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_CAT];
     __shared__ float red[2][NW][R];
     // biases and LayerNorm affine, staged in LDS: epilogue reads never wait on VMEM
@@ -291,10 +296,19 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
                 }
             }
         __syncthreads();
-#pragma unroll 4
+        // Heads (cf.wm != nullptr): each lane keeps its 4-column partial dot of each of
+        // the wave's 16 rows; one reduce-scatter over the 64 lanes (8 + 4 + 2 + 1 + 1 + 1
+        // shuffles per head instead of 16 x 6) leaves every 4-lane group with one row's sum.
+        const bool heads = cf.wm != nullptr, conf = cf.wc != nullptr;
+        float4 wm4 = make_float4(0.f, 0.f, 0.f, 0.f), wc4 = wm4;
+        if (heads) wm4 = *reinterpret_cast<const float4*>(cf.wm + 4 * lane);
+        if (conf) wc4 = *reinterpret_cast<const float4*>(cf.wc + 4 * lane);
+        float pz[R / NW], pa[R / NW];
+#pragma unroll
         for (int i = 0; i < R / NW; ++i) {
             const int r = wave * (R / NW) + i, m = m0 + r;
-            if (m >= M) break;  // wave-uniform
+            pz[i] = pa[i] = 0.f;
+            if (m >= M) continue;  // wave-uniform
             const float4 y = *reinterpret_cast<const float4*>(lds + r * 1024 + ((lane ^ (r & 15)) << 4));
             float4* px = reinterpret_cast<float4*>(X + (size_t)m * 256) + lane;
             float4 x = *px;
@@ -305,16 +319,59 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
             *px = x;
             *reinterpret_cast<uint2*>(xcopy + (size_t)m * ldc + 4 * lane) =
                 make_uint2(pack_bf16x2(x.x, x.y), pack_bf16x2(x.z, x.w));
+            if (heads) pz[i] = x.x * wm4.x + x.y * wm4.y + x.z * wm4.z + x.w * wm4.w;
+            if (conf) pa[i] = x.x * wc4.x + x.y * wc4.y + x.z * wc4.z + x.w * wc4.w;
+        }
+        if (heads) {
+            // reduce-scatter: after the step over lane bit b the lane keeps the half of its
+            // rows selected by that bit; rows end up as row = 8 b5 + 4 b4 + 2 b3 + b2
+#pragma unroll
+            for (int half = 8, bit = 32; half >= 1; half >>= 1, bit >>= 1) {
+                const bool up = (lane & bit) != 0;
+#pragma unroll
+                for (int j = 0; j < half; ++j) {
+                    const float kz = up ? pz[half + j] : pz[j], sz = up ? pz[j] : pz[half + j];
+                    pz[j] = kz + __shfl_xor(sz, bit, 64);
+                    if (conf) {
+                        const float ka = up ? pa[half + j] : pa[j], sa = up ? pa[j] : pa[half + j];
+                        pa[j] = ka + __shfl_xor(sa, bit, 64);
+                    }
+                }
+            }
+            float z = pz[0], a = pa[0];
+            z += __shfl_xor(z, 2, 64);
+            z += __shfl_xor(z, 1, 64);
+            if (conf) {
+                a += __shfl_xor(a, 2, 64);
+                a += __shfl_xor(a, 1, 64);
+            }
+            const int r = wave * (R / NW) + (lane >> 2), m = m0 + r;
+            if ((lane & 3) == 0 && m < M) {  // one writer per row (k_lg_conf semantics)
+                z += cf.bm[0];
+                if (cf.rowseg[m] < 0) {
+                    if (conf) cf.flags[m] = 0;
+                } else {
+                    cf.lz[m] = logsigmoid_f(z);
+                    if (conf) {
+                        const float c = sigmoid_f(a + cf.bc[0]);
+                        const bool keep = sigmoid_f(z) > 1.f - cf.width || c <= cf.thr;
+                        cf.flags[m] = (uint8_t)((c < cf.thr) | (keep << 1));
+                    }
+                }
+            }
         }
     }
 }
 
 }  // namespace
 
-int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s) {
+int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s,
+               const mlg_lg_conf_i* conf) {
     if (M <= 0) return MLG_OK;
     if (ldc < 256 || (ldc % 8)) return MLG_EINVAL;
-    hipLaunchKernelGGL(k_lg_ffn, dim3((unsigned)((M + R - 1) / R)), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w);
+    mlg_lg_conf_i cf{};
+    if (conf) cf = *conf;
+    hipLaunchKernelGGL(k_lg_ffn, dim3((unsigned)((M + R - 1) / R)), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

@@ -22,11 +22,6 @@ namespace {
 
 constexpr int LG_D = 256, LG_H = 4, LG_L = 9;
 
-__device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(-x)); }
-__device__ __forceinline__ float logsigmoidf(float x) {
-    // log(sigmoid(x)) = min(x, 0) - log1p(exp(-|x|))  (torch's stable form)
-    return fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
-}
 
 struct Seg {
     int off, len, frame, pad;  // flat row offset, live tokens, source frame, unused
@@ -112,41 +107,8 @@ __global__ __launch_bounds__(256) void k_lg_init(const Seg* __restrict__ segs, c
 }
 
 // ------------------------------------------------------------------ confidences
-// One wave per live token: conf = sigmoid(x . wc + bc), z = x . wm + bm; lz = logsigmoid(z)
-// (the assignment's certainty term); flags[r] = (conf < thr) | keep << 1 with
-// keep = sigmoid(z) > 1 - width or conf <= thr.  wc == nullptr: only lz.
-__global__ __launch_bounds__(256) void k_lg_conf(const int* __restrict__ rowseg, int Npad, const float* __restrict__ x,
-                                                 const float* __restrict__ wc, const float* __restrict__ bc,
-                                                 const float* __restrict__ wm, const float* __restrict__ bm,
-                                                 float thr, float width_conf, float* __restrict__ lz,
-                                                 uint8_t* __restrict__ flags) {
-    const int lane = threadIdx.x & 63;
-    const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= Npad) return;
-    if (rowseg[r] < 0) {
-        if (lane == 0 && wc) flags[r] = 0;
-        return;
-    }
-    const float* xr = x + r * LG_D;
-    float a = 0.f, m = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const float v = xr[lane + 64 * j];
-        if (wc) a += v * wc[lane + 64 * j];
-        m += v * wm[lane + 64 * j];
-    }
-    m = wave_sum(m) + bm[0];
-    if (wc) a = wave_sum(a) + bc[0];
-    if (lane == 0) {
-        lz[r] = logsigmoidf(m);
-        if (wc) {
-            const float conf = sigmoidf(a);
-            const bool k = sigmoidf(m) > 1.f - width_conf || conf <= thr;
-            flags[r] = (uint8_t)((conf < thr) | (k << 1));
-        }
-    }
-}
-
+// Token confidence / matchability heads run inside the cross block's fused tail
+// (lg_ffn.hip, mlg_lg_conf_i): flags[r] = (conf < thr) | keep << 1, lz = logsigmoid(z).
 // stats[seg] = {#(conf < thr), #keep}: one workgroup per segment
 __global__ __launch_bounds__(256) void k_lg_segstats(const Seg* __restrict__ segs, const uint8_t* __restrict__ flags,
                                                      int* __restrict__ stats) {
@@ -729,16 +691,12 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         return mlg_attention_varlen(Q, cross ? Q : K, VT, CTX, LG_D, Npad, LG_H, TASKS + o, OUTOFF + o, nt, maxq, s);
     };
     // out_proj / to_out + FFN + residual, fused (lg_ffn.hip)
-    auto ffn = [&](const mlg_lg_block_i& bw) -> int {
+    // (conf: the layer's token-confidence / matchability heads, fused into the tail)
+    auto ffn = [&](const mlg_lg_block_i& bw, const mlg_lg_conf_i* conf) -> int {
         // algorithmic HBM bytes per live token: ctx + bf16 x in (512 + 512), f32 x read +
         // written (1024 + 1024), bf16 x copy written (512)
         MlgProfScope prof(8, s, 3584.0 * live_tokens());
-        return mlg_lg_ffn(CTX, X, CAT, 512, Npad, bw, s);
-    };
-    // matchability log-sigmoid of every live token (layer i's head)
-    auto certainty = [&](int i) {
-        hipLaunchKernelGGL(k_lg_conf, dim3((Npad + 3) / 4), dim3(256), 0, s, ROWSEG, Npad, X, (const float*)nullptr,
-                           (const float*)nullptr, w.wmatch[i], w.bmatch[i], 0.f, 0.f, LZ, KEEP);
+        return mlg_lg_ffn(CTX, X, CAT, 512, Npad, bw, s, conf);
     };
     // assignment + filter of the listed segment pairs (k = index of image a's segment)
     auto assign = [&](int i, const std::vector<size_t>& ks) -> int {
@@ -793,7 +751,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
             LG_TRY(mlg_lg_proj(true, CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, s));
         }
         LG_TRY(attention(false));
-        LG_TRY(ffn(w.self[i]));
+        LG_TRY(ffn(w.self[i], nullptr));
         // cross block
         {
             MlgProfScope prof(6, s, 2.0 * live_tokens() * 512 * 256);
@@ -801,18 +759,19 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
                                Npad, s));
         }
         LG_TRY(attention(true));
-        LG_TRY(ffn(w.cross[i]));
+        // layer i's heads on the updated tokens: matchability log-sigmoid (the assignment's
+        // certainty term) and, before the last layer, confidences + early-stop / prune flags
+        const bool last = i == LG_L - 1;
+        const mlg_lg_conf_i heads{ROWSEG, last ? nullptr : w.wconf[i], last ? nullptr : w.bconf[i], w.wmatch[i],
+                                  w.bmatch[i], last ? 0.f : conf_threshold(i), width_conf, LZ, KEEP};
+        LG_TRY(ffn(w.cross[i], &heads));
 
-        if (i == LG_L - 1) {
-            certainty(i);
+        if (last) {
             std::vector<size_t> ks;
             for (size_t k = 0; k < segs.size(); k += 2) ks.push_back(k);
             LG_TRY(assign(i, ks));
             break;
         }
-        const float thr = conf_threshold(i);
-        hipLaunchKernelGGL(k_lg_conf, dim3((Npad + 3) / 4), dim3(256), 0, s, ROWSEG, Npad, X, w.wconf[i], w.bconf[i],
-                           w.wmatch[i], w.bmatch[i], thr, width_conf, LZ, KEEP);
         hipLaunchKernelGGL(k_lg_segstats, dim3((unsigned)segs.size()), dim3(256), 0, s, SEGS, KEEP, STATS);
         MLG_LAUNCH_CHECK();
         if (hipMemcpyAsync(stats.data(), STATS, segs.size() * 2 * sizeof(int), hipMemcpyDeviceToHost, s) !=
