@@ -44,6 +44,23 @@ struct EpiBiasF32 {  // y = acc + b  -> f32
     }
 };
 
+// y = acc + b as a bf16 pair hi = bf16(y), lo = bf16(y - hi) (y = hi + lo to 2^-17),
+// k-step-major [N / 16][rows][16] so a 32-row MFMA fragment load is one contiguous
+// 1 KiB (LightGlue's assignment similarity, lightglue.hip k_asg_sim)
+struct EpiBiasSplitBF16 {
+    bf16_t* H; bf16_t* L; int rows; const float* bias;
+    __device__ void operator()(int m, int n, const f32x4& v) const {
+        const float4 b = *reinterpret_cast<const float4*>(bias + n);
+        const float y0 = v[0] + b.x, y1 = v[1] + b.y, y2 = v[2] + b.z, y3 = v[3] + b.w;
+        const uint32_t h01 = pack_bf16x2(y0, y1), h23 = pack_bf16x2(y2, y3);
+        const float r0 = y0 - __uint_as_float(h01 << 16), r1 = y1 - __uint_as_float(h01 & 0xffff0000u);
+        const float r2 = y2 - __uint_as_float(h23 << 16), r3 = y3 - __uint_as_float(h23 & 0xffff0000u);
+        const size_t o = ((size_t)(n >> 4) * rows + m) * 16 + (n & 15);
+        *reinterpret_cast<uint2*>(H + o) = make_uint2(h01, h23);
+        *reinterpret_cast<uint2*>(L + o) = make_uint2(pack_bf16x2(r0, r1), pack_bf16x2(r2, r3));
+    }
+};
+
 struct EpiBiasBF16 {  // y = acc + b  -> bf16
     bf16_t* C; int ldc; const float* bias;
     __device__ void operator()(int m, int n, const f32x4& v) const {
@@ -664,6 +681,11 @@ int mlg_gemm_f32out_variant(int variant, const bf16_t* A, const bf16_t* W, float
 int mlg_gemm_bias_f32_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, float* C, int ldc, int M,
                          int N, int K, hipStream_t s) {
     return launch(A, W, M, N, K, lda, K, EpiBiasF32{C, ldc, bias}, s);
+}
+int mlg_gemm_bias_split_bf16(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* H, bf16_t* L,
+                             int M, int N, int K, hipStream_t s) {
+    if (N % 16) return MLG_EINVAL;
+    return launch(A, W, M, N, K, lda, K, EpiBiasSplitBF16{H, L, M, bias}, s);
 }
 int mlg_gemm_bias_bf16_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* C, int ldc, int M,
                           int N, int K, hipStream_t s) {

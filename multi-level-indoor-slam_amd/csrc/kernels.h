@@ -32,6 +32,10 @@ int mlg_gemm_set_variant(int variant);
 // leading-dimension variants (A row stride lda, output row stride ldc / ldx)
 int mlg_gemm_bias_f32_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, float* C, int ldc, int M,
                          int N, int K, hipStream_t s);
+// C = A . W^T + bias split into bf16 hi / lo halves (C = hi + lo to 2^-17 relative),
+// stored k-step-major [N / 16][M][16] (LightGlue assignment operands)
+int mlg_gemm_bias_split_bf16(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* H, bf16_t* L,
+                             int M, int N, int K, hipStream_t s);
 int mlg_gemm_bias_bf16_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* C, int ldc, int M,
                           int N, int K, hipStream_t s);
 int mlg_gemm_residual_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* gamma, float* X,

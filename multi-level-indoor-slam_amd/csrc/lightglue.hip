@@ -211,35 +211,62 @@ __global__ void k_lg_live(const Seg* __restrict__ segs, int nseg, uint8_t* __res
 
 // ------------------------------------------------------------------ assignment
 // For every finishing pair a (table entry Asg): S = final_proj(x0) . final_proj(x1)^T
-// (f32; the two 1/4 scales applied here as one exact 1/16), the row / column
-// log_softmax terms (torch form (x - max) - log(sum exp(x - max))), and the row /
-// column argmax of  (s0 + s1) + (lz0 + lz1)  (first index on ties, as torch.max), then
-// the mutual filter.  Row / column statistics are indexed by layout row, so all
-// pairs share the buffers.  Grids carry the pair in blockIdx.y / z.
+// (the two 1/4 scales applied here as one exact 1/16), the row / column log_softmax
+// terms (torch form (x - max) - log(sum exp(x - max))), and the row / column argmax of
+// (s0 + s1) + (lz0 + lz1)  (first index on ties, as torch.max), then the mutual filter.
+// Row / column statistics are indexed by layout row, so all pairs share the buffers.
+// Tile grids carry the pair in blockIdx.z, line grids in blockIdx.y.
+//
+//   k_asg_sim      128 x 128 GEMM tile -> S (whole float4 rows) + the tile's partial
+//                  (max, sum exp) of every row and column, from the LDS-staged tile;
+//   k_asg_stats    combines the partials -> row / column (max, log sum exp);
+//   k_asg_arg      reads each 64 x 128 tile of S once -> per-tile best (score, index)
+//                  of every row and column;
+//   k_asg_argfinal combines them -> row argmax + value, column argmax.
+// S is written once and read once.
 struct Asg {
     int m, n, ra, rb;  // rows of image a / b, their first layout rows
     long soff;         // S offset (floats)
-    int pair, pad;
+    int pair, ld;      // pair index, S row stride (n rounded up to 4: float4 rows)
 };
 
-constexpr int CH = 256;  // rows per column-statistics chunk
+constexpr int SBM = 128;               // k_asg_sim tile (rows = columns)
+constexpr int TSS = SBM + 4;           // its LDS row stride: the 16 lanes of a b128 group (16 rows)
+                                       // and the 64 lanes of a b32 column read hit distinct banks
+constexpr int ARM = 64, ARN = 128;     // k_asg_arg tile
+constexpr int TSA = ARN + 8;           // its LDS row stride: b128 groups of 8 rows x 2 halves
 
-// S = MD[ra .. ra + m) . MD[rb .. rb + n)^T of every listed pair in ONE launch (grid.z =
-// pair; a per-pair launch left most of the chip idle on 2048 x 2048 x 256).  Exact-f32
-// v_mfma_f32_32x32x2_f32 (as upstream, which runs this einsum in float32); 128 x 128
-// tile, 2 x 2 waves of 64 x 64, K = 256 staged 16 at a time, transposed to [k][row].
-constexpr int SBM = 128, SBK = 16;
-__global__ __launch_bounds__(256, 2) void k_asg_sim(const Asg* __restrict__ tab, const float* __restrict__ MD,
-                                                    float* __restrict__ Sall) {
+// per-tile partials: part[((slot * 2 + dir) * tiles + t) * kmax + i]; dir 0 = rows
+// (t = 128-column tile), dir 1 = columns (t = row tile: 128 rows in k_asg_sim's
+// statistics, 64 in k_asg_arg's bests)
+__device__ __forceinline__ size_t part_at(int slot, int dir, int t, int i, int kmax) {
+    return ((size_t)(slot * 2 + dir) * ((kmax + ARM - 1) / ARM) + t) * kmax + i;
+}
+
+// S = MD[ra .. ra + m) . MD[rb .. rb + n)^T of every listed pair in ONE launch.  MD is
+// final_proj(x) (f32 accumulate) held as bf16 hi + lo halves (hi = bf16(y), lo =
+// bf16(y - hi), k-step-major [16][rows][16]; gemm_bf16.hip EpiBiasSplitBF16), and the
+// product is hi.hi + hi.lo + lo.hi on v_mfma_f32_32x32x16_bf16 with f32 accumulation:
+// operand error ~2^-17, dropped lo.lo ~2^-18 relative -- f32-class accuracy (upstream
+// runs this einsum in float32) at 3 bf16 MFMAs instead of 8 exact-f32 32x32x2 ones per
+// 16-deep k-step.  4 waves of 64 x 64; each wave streams its operand fragments straight
+// from L2 (one contiguous 1 KiB per wave-load), double-buffered one k-step ahead.
+__global__ __launch_bounds__(256, 2) void k_asg_sim(const Asg* __restrict__ tab, const bf16_t* __restrict__ MDH,
+                                                    const bf16_t* __restrict__ MDL, int rows,
+                                                    float* __restrict__ Sall, float2* __restrict__ part, int kmax) {
     const Asg a = tab[blockIdx.z];
     const int m0 = blockIdx.y * SBM, n0 = blockIdx.x * SBM;
     if (m0 >= a.m || n0 >= a.n) return;
-    __shared__ float As[SBK][SBM + 4];
-    __shared__ float Bs[SBK][SBM + 4];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ __attribute__((aligned(16))) float T[SBM * TSS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
     const int wm = wave >> 1, wn = wave & 1;
-    const float* A = MD + (size_t)a.ra * LG_D;
-    const float* B = MD + (size_t)a.rb * LG_D;
+    const size_t step = (size_t)rows * 16;
+    size_t ao[2], bo[2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+        ao[x] = (size_t)(a.ra + min(m0 + wm * 64 + 32 * x + col, a.m - 1)) * 16 + 8 * hh;
+        bo[x] = (size_t)(a.rb + min(n0 + wn * 64 + 32 * x + col, a.n - 1)) * 16 + 8 * hh;
+    }
     f32x16 acc[2][2];
 #pragma unroll
     for (int x = 0; x < 2; ++x)
@@ -247,207 +274,233 @@ __global__ __launch_bounds__(256, 2) void k_asg_sim(const Asg* __restrict__ tab,
         for (int y = 0; y < 2; ++y)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[x][y][r] = 0.f;
-    for (int k0 = 0; k0 < LG_D; k0 += SBK) {
+    bf16x8 ah[2][2], al[2][2], bh[2][2], bl[2][2];  // [buffer][x or y]
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int c = tid + i * 256, row = c >> 2, kq = (c & 3) * 4;
-            const float4 va = *reinterpret_cast<const float4*>(A + (size_t)min(m0 + row, a.m - 1) * LG_D + k0 + kq);
-            const float4 vb = *reinterpret_cast<const float4*>(B + (size_t)min(n0 + row, a.n - 1) * LG_D + k0 + kq);
-            As[kq][row] = va.x; As[kq + 1][row] = va.y; As[kq + 2][row] = va.z; As[kq + 3][row] = va.w;
-            Bs[kq][row] = vb.x; Bs[kq + 1][row] = vb.y; Bs[kq + 2][row] = vb.z; Bs[kq + 3][row] = vb.w;
-        }
-        __syncthreads();
+    for (int x = 0; x < 2; ++x) {
+        ah[0][x] = *reinterpret_cast<const bf16x8*>(MDH + ao[x]);
+        al[0][x] = *reinterpret_cast<const bf16x8*>(MDL + ao[x]);
+        bh[0][x] = *reinterpret_cast<const bf16x8*>(MDH + bo[x]);
+        bl[0][x] = *reinterpret_cast<const bf16x8*>(MDL + bo[x]);
+    }
 #pragma unroll
-        for (int kk = 0; kk < SBK; kk += 2) {
-            const int k = kk + (lane >> 5);
-            float fa[2], fb[2];
+    for (int ks = 0; ks < LG_D / 16; ++ks) {
+        const int cb = ks & 1, nb = cb ^ 1;
+        if (ks + 1 < LG_D / 16) {
+            const size_t o = (size_t)(ks + 1) * step;
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                fa[t] = As[k][wm * 64 + t * 32 + (lane & 31)];
-                fb[t] = Bs[k][wn * 64 + t * 32 + (lane & 31)];
+            for (int x = 0; x < 2; ++x) {
+                ah[nb][x] = *reinterpret_cast<const bf16x8*>(MDH + o + ao[x]);
+                al[nb][x] = *reinterpret_cast<const bf16x8*>(MDL + o + ao[x]);
+                bh[nb][x] = *reinterpret_cast<const bf16x8*>(MDH + o + bo[x]);
+                bl[nb][x] = *reinterpret_cast<const bf16x8*>(MDL + o + bo[x]);
             }
-#pragma unroll
-            for (int x = 0; x < 2; ++x)
-#pragma unroll
-                for (int y = 0; y < 2; ++y)
-                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[x], fb[y], acc[x][y], 0, 0, 0);
         }
-        __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);  // next step's loads stay ahead of this step's MFMAs
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int y = 0; y < 2; ++y) {
+                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb][x], bl[cb][y], acc[x][y], 0, 0, 0);
+                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cb][x], bh[cb][y], acc[x][y], 0, 0, 0);
+                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb][x], bh[cb][y], acc[x][y], 0, 0, 0);
+            }
     }
     // D[i][j]: col j = lane & 31, row i = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-    float* S = Sall + a.soff;
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
         for (int y = 0; y < 2; ++y) {
-            const int j = n0 + wn * 64 + y * 32 + (lane & 31);
-            if (j >= a.n) continue;
+            const int j = wn * 64 + y * 32 + col;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int i = m0 + wm * 64 + x * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-                if (i < a.m) S[(size_t)i * a.n + j] = acc[x][y][r];
-            }
+            for (int r = 0; r < 16; ++r)
+                T[(wm * 64 + x * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh) * TSS + j] = acc[x][y][r];
         }
-}
-
-__global__ __launch_bounds__(256) void k_asg_rowlse(const Asg* __restrict__ tab, const float* __restrict__ Sall,
-                                                    float* __restrict__ rmax, float* __restrict__ rlog) {
-    const Asg a = tab[blockIdx.y];
-    const int lane = threadIdx.x & 63;
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= a.m) return;
-    const float* row = Sall + a.soff + (size_t)i * a.n;
-    float mx = -INFINITY;
-    for (int j = lane; j < a.n; j += 64) mx = fmaxf(mx, row[j] * 0.0625f);
-    mx = wave_max(mx);
-    float s = 0.f;
-    for (int j = lane; j < a.n; j += 64) s += expf(row[j] * 0.0625f - mx);
-    s = wave_sum(s);
-    if (lane == 0) {
-        rmax[a.ra + i] = mx;
-        rlog[a.ra + i] = logf(s);
-    }
-}
-
-// per (64-column block, 256-row chunk): online (max, sum) of the column slice
-__global__ __launch_bounds__(256) void k_asg_colpart(const Asg* __restrict__ tab, const float* __restrict__ Sall,
-                                                     float2* __restrict__ part, int kmax) {
-    const Asg a = tab[blockIdx.z];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int j = blockIdx.x * 64 + lane, i0 = blockIdx.y * CH;
-    if ((int)blockIdx.x * 64 >= a.n || i0 >= a.m) return;
-    __shared__ float2 sp[4][64];
-    float mx = -INFINITY, sm = 0.f;
-    if (j < a.n)
-        for (int i = i0 + wave; i < min(a.m, i0 + CH); i += 4) {
-            const float v = Sall[a.soff + (size_t)i * a.n + j] * 0.0625f;
-            if (v > mx) {
-                sm = sm * expf(mx - v) + 1.f;
-                mx = v;
-            } else {
-                sm += expf(v - mx);
-            }
-        }
-    sp[wave][lane] = make_float2(mx, sm);
     __syncthreads();
-    if (wave == 0 && j < a.n) {
-        float M = sp[0][lane].x;
-        for (int w = 1; w < 4; ++w) M = fmaxf(M, sp[w][lane].x);
-        float S = 0.f;
-        for (int w = 0; w < 4; ++w)
-            if (sp[w][lane].y > 0.f) S += sp[w][lane].y * expf(sp[w][lane].x - M);
-        part[((size_t)blockIdx.z * (kmax / CH + 1) + blockIdx.y) * kmax + j] = make_float2(M, S);
+    const int mr = min(SBM, a.m - m0), nc = min(SBM, a.n - n0);
+    float* S = Sall + a.soff;
+#pragma unroll 4
+    for (int it = 0; it < SBM / 8; ++it) {
+        // ld is a multiple of 4 and columns n .. ld are scratch: whole float4s while c < nc
+        const int r = it * 8 + (tid >> 5), c = (tid & 31) * 4;
+        if (r < mr && c < nc)
+            *reinterpret_cast<float4*>(S + (size_t)(m0 + r) * a.ld + n0 + c) =
+                *reinterpret_cast<const float4*>(T + r * TSS + c);
     }
+    // partial softmax statistics: threads 0-127 one row each, 128-255 one column each;
+    // exp(v / 16 - mx) as exp2 of one FMA (v_exp_f32)
+    constexpr float L2E = 1.4426950408889634f;
+    const bool colw = tid >= SBM;
+    const int q = tid & (SBM - 1);
+    if (q >= (colw ? nc : mr)) return;
+    float mx = -INFINITY, sm = 0.f;
+    if (colw) {
+        for (int e = 0; e < mr; ++e) mx = fmaxf(mx, T[e * TSS + q]);
+        mx *= 0.0625f;
+        const float nm = -mx * L2E;
+        for (int e = 0; e < mr; ++e) sm += __builtin_amdgcn_exp2f(fmaf(T[e * TSS + q], 0.0625f * L2E, nm));
+    } else {
+        const float* p = T + q * TSS;
+        for (int e = 0; e < nc; e += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(p + e);
+            mx = fmaxf(mx, v.x);
+            if (e + 1 < nc) mx = fmaxf(mx, v.y);
+            if (e + 2 < nc) mx = fmaxf(mx, v.z);
+            if (e + 3 < nc) mx = fmaxf(mx, v.w);
+        }
+        mx *= 0.0625f;
+        const float nm = -mx * L2E;
+        for (int e = 0; e < nc; e += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(p + e);
+            sm += __builtin_amdgcn_exp2f(fmaf(v.x, 0.0625f * L2E, nm));
+            if (e + 1 < nc) sm += __builtin_amdgcn_exp2f(fmaf(v.y, 0.0625f * L2E, nm));
+            if (e + 2 < nc) sm += __builtin_amdgcn_exp2f(fmaf(v.z, 0.0625f * L2E, nm));
+            if (e + 3 < nc) sm += __builtin_amdgcn_exp2f(fmaf(v.w, 0.0625f * L2E, nm));
+        }
+    }
+    part[colw ? part_at(blockIdx.z, 1, blockIdx.y, n0 + q, kmax) : part_at(blockIdx.z, 0, blockIdx.x, m0 + q, kmax)] =
+        make_float2(mx, sm);
 }
 
-__global__ void k_asg_colfinal(const Asg* __restrict__ tab, const float2* __restrict__ part, int kmax,
-                               float* __restrict__ cmax, float* __restrict__ clog) {
+// row / column (max, log sum exp) from k_asg_sim's partials; grid (.., pairs, 2 dirs)
+__global__ __launch_bounds__(256) void k_asg_stats(const Asg* __restrict__ tab, const float2* __restrict__ part,
+                                                   int kmax, float* __restrict__ rmax, float* __restrict__ rlog,
+                                                   float* __restrict__ cmax, float* __restrict__ clog) {
     const Asg a = tab[blockIdx.y];
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= a.n) return;
-    const int nch = (a.m + CH - 1) / CH;
-    const float2* p = part + (size_t)blockIdx.y * (kmax / CH + 1) * kmax + j;
+    const int dir = blockIdx.z;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= (dir ? a.n : a.m)) return;
+    const int nt = ((dir ? a.m : a.n) + SBM - 1) / SBM;
+    const float2* p = part + part_at(blockIdx.y, dir, 0, i, kmax);
     float M = -INFINITY;
-    for (int c = 0; c < nch; ++c) M = fmaxf(M, p[(size_t)c * kmax].x);
+    for (int t = 0; t < nt; ++t) M = fmaxf(M, p[(size_t)t * kmax].x);
     float S = 0.f;
-    for (int c = 0; c < nch; ++c) S += p[(size_t)c * kmax].y * expf(p[(size_t)c * kmax].x - M);
-    cmax[a.rb + j] = M;
-    clog[a.rb + j] = logf(S);
+    for (int t = 0; t < nt; ++t) S += p[(size_t)t * kmax].y * expf(p[(size_t)t * kmax].x - M);
+    const int o = dir ? a.rb + i : a.ra + i;
+    (dir ? cmax : rmax)[o] = M;
+    (dir ? clog : rlog)[o] = logf(S);
 }
 
 __device__ __forceinline__ float lg_score(float v, float rm, float rl, float cm, float cl, float cert) {
     return (((v - rm) - rl) + ((v - cm) - cl)) + cert;
 }
 
-__global__ __launch_bounds__(256) void k_asg_rowarg(const Asg* __restrict__ tab, const float* __restrict__ Sall,
+// (score, index) a beats b: higher score, the lower index on ties
+__device__ __forceinline__ bool beats(float sa, int ia, float sb, int ib) { return sa > sb || (sa == sb && ia < ib); }
+
+// per-tile best (score, index) of every row and column of a 64 x 128 tile of S (4 tiles
+// in flight per CU so the HBM read of one overlaps the scoring of another): threads
+// 0-127 two per row (alternate float4 column chunks, combined by one shuffle), 128-255
+// one per column; each scans increasing indices with strict >, keeping the first index
+__global__ __launch_bounds__(256, 4) void k_asg_arg(const Asg* __restrict__ tab, const float* __restrict__ Sall,
                                                     const float* __restrict__ rmax, const float* __restrict__ rlog,
                                                     const float* __restrict__ cmax, const float* __restrict__ clog,
-                                                    const float* __restrict__ lz, int* __restrict__ arg,
-                                                    float* __restrict__ val) {
-    const Asg a = tab[blockIdx.y];
-    const int lane = threadIdx.x & 63;
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= a.m) return;
-    const float* row = Sall + a.soff + (size_t)i * a.n;
-    const float rm = rmax[a.ra + i], rl = rlog[a.ra + i], l0 = lz[a.ra + i];
+                                                    const float* __restrict__ lz, float2* __restrict__ part, int kmax) {
+    const Asg a = tab[blockIdx.z];
+    const int m0 = blockIdx.y * ARM, n0 = blockIdx.x * ARN;
+    if (m0 >= a.m || n0 >= a.n) return;
+    __shared__ __attribute__((aligned(16))) float T[ARM * TSA];
+    __shared__ float4 sr[ARM], sc[ARN];  // (max, log sum, log-sigmoid) of the tile's rows / columns
+    const int tid = threadIdx.x;
+    const int mr = min(ARM, a.m - m0), nc = min(ARN, a.n - n0);
+    const float* S = Sall + a.soff;
+#pragma unroll
+    for (int it = 0; it < ARM / 8; ++it) {
+        const int r = it * 8 + (tid >> 5), c = (tid & 31) * 4;
+        if (r < mr && c < nc)
+            *reinterpret_cast<float4*>(T + r * TSA + c) =
+                *reinterpret_cast<const float4*>(S + (size_t)(m0 + r) * a.ld + n0 + c);
+    }
+    if (tid < ARM) {
+        if (tid < mr) {
+            const int o = a.ra + m0 + tid;
+            sr[tid] = make_float4(rmax[o], rlog[o], lz[o], 0.f);
+        }
+    } else if (tid >= ARN) {
+        const int j = tid - ARN;
+        if (j < nc) {
+            const int o = a.rb + n0 + j;
+            sc[j] = make_float4(cmax[o], clog[o], lz[o], 0.f);
+        }
+    }
+    __syncthreads();
     float best = -INFINITY;
-    int bj = 0x7fffffff;
-    for (int j = lane; j < a.n; j += 64) {
-        const float v = lg_score(row[j] * 0.0625f, rm, rl, cmax[a.rb + j], clog[a.rb + j], l0 + lz[a.rb + j]);
-        if (v > best || (v == best && j < bj)) {
-            best = v;
-            bj = j;
+    int bi = 0x7fffffff;
+    if (tid < ARN) {
+        const int r = tid >> 1, h = tid & 1;
+        if (r < mr) {
+            const float4 me = sr[r];
+            const float* p = T + r * TSA;
+            for (int c = 4 * h; c < nc; c += 8) {
+                const float4 v = *reinterpret_cast<const float4*>(p + c);
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (c + k >= nc) break;
+                    const float4 ot = sc[c + k];
+                    const float s = lg_score(vv[k] * 0.0625f, me.x, me.y, ot.x, ot.y, me.z + ot.z);
+                    if (s > best) {
+                        best = s;
+                        bi = c + k;
+                    }
+                }
+            }
+        }
+        const float ob = __shfl_xor(best, 1, 64);
+        const int oi = __shfl_xor(bi, 1, 64);
+        if (beats(ob, oi, best, bi)) {
+            best = ob;
+            bi = oi;
+        }
+        if (h == 0 && r < mr)
+            part[part_at(blockIdx.z, 0, blockIdx.x, m0 + r, kmax)] =
+                make_float2(best, __int_as_float(bi == 0x7fffffff ? bi : n0 + bi));
+    } else {
+        const int j = tid - ARN;
+        if (j >= nc) return;
+        const float4 me = sc[j];
+        for (int e = 0; e < mr; ++e) {
+            const float4 ot = sr[e];
+            const float s = lg_score(T[e * TSA + j] * 0.0625f, ot.x, ot.y, me.x, me.y, ot.z + me.z);
+            if (s > best) {
+                best = s;
+                bi = e;
+            }
+        }
+        part[part_at(blockIdx.z, 1, blockIdx.y, n0 + j, kmax)] =
+            make_float2(best, __int_as_float(bi == 0x7fffffff ? bi : m0 + bi));
+    }
+}
+
+// row argmax + value, column argmax from the per-tile bests (tiles in increasing index
+// order, strict >: the first index on ties); grid (.., pairs, 2 dirs).  A line with no
+// finite score (NaN input) points at index 0 with value -inf.
+__global__ __launch_bounds__(256) void k_asg_argfinal(const Asg* __restrict__ tab, const float2* __restrict__ part,
+                                                      int kmax, int* __restrict__ arg, float* __restrict__ val) {
+    const Asg a = tab[blockIdx.y];
+    const int dir = blockIdx.z;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= (dir ? a.n : a.m)) return;
+    const int nt = dir ? (a.m + ARM - 1) / ARM : (a.n + ARN - 1) / ARN;
+    const float2* p = part + part_at(blockIdx.y, dir, 0, i, kmax);
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int t = 0; t < nt; ++t) {
+        const float2 c = p[(size_t)t * kmax];
+        if (c.x > best) {
+            best = c.x;
+            bi = __float_as_int(c.y);
         }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(best, o, 64);
-        const int oj = __shfl_xor(bj, o, 64);
-        if (ov > best || (ov == best && oj < bj)) {
-            best = ov;
-            bj = oj;
-        }
+    if (bi == 0x7fffffff) {
+        bi = 0;
+        best = -INFINITY;
     }
-    if (lane == 0) {
-        arg[a.ra + i] = bj;
+    if (dir) {
+        arg[a.rb + i] = bi;
+    } else {
+        arg[a.ra + i] = bi;
         val[a.ra + i] = best;
     }
-}
-
-__global__ __launch_bounds__(256) void k_asg_colargpart(const Asg* __restrict__ tab, const float* __restrict__ Sall,
-                                                        const float* __restrict__ rmax, const float* __restrict__ rlog,
-                                                        const float* __restrict__ cmax, const float* __restrict__ clog,
-                                                        const float* __restrict__ lz, float2* __restrict__ part,
-                                                        int kmax) {
-    const Asg a = tab[blockIdx.z];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int j = blockIdx.x * 64 + lane, i0 = blockIdx.y * CH;
-    if ((int)blockIdx.x * 64 >= a.n || i0 >= a.m) return;
-    __shared__ float sb[4][64];
-    __shared__ int si[4][64];
-    float best = -INFINITY;
-    int bi = 0x7fffffff;
-    if (j < a.n) {
-        const float cm = cmax[a.rb + j], cl = clog[a.rb + j], l1 = lz[a.rb + j];
-        for (int i = i0 + wave; i < min(a.m, i0 + CH); i += 4) {
-            const float v = lg_score(Sall[a.soff + (size_t)i * a.n + j] * 0.0625f, rmax[a.ra + i], rlog[a.ra + i], cm,
-                                     cl, lz[a.ra + i] + l1);
-            if (v > best || (v == best && i < bi)) {
-                best = v;
-                bi = i;
-            }
-        }
-    }
-    sb[wave][lane] = best;
-    si[wave][lane] = bi;
-    __syncthreads();
-    if (wave == 0 && j < a.n) {
-        for (int w = 1; w < 4; ++w)
-            if (sb[w][lane] > best || (sb[w][lane] == best && si[w][lane] < bi)) {
-                best = sb[w][lane];
-                bi = si[w][lane];
-            }
-        part[((size_t)blockIdx.z * (kmax / CH + 1) + blockIdx.y) * kmax + j] = make_float2(best, __int_as_float(bi));
-    }
-}
-
-__global__ void k_asg_colargfinal(const Asg* __restrict__ tab, const float2* __restrict__ part, int kmax,
-                                  int* __restrict__ arg) {
-    const Asg a = tab[blockIdx.y];
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= a.n) return;
-    const int nch = (a.m + CH - 1) / CH;
-    const float2* p = part + (size_t)blockIdx.y * (kmax / CH + 1) * kmax + j;
-    float best = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int c = 0; c < nch; ++c) {
-        const float2 q = p[(size_t)c * kmax];
-        const int qi = __float_as_int(q.y);
-        if (q.x > best || (q.x == best && qi < bi)) {
-            best = q.x;
-            bi = qi;
-        }
-    }
-    arg[a.rb + j] = bi;
 }
 
 // mutual nearest + exp(score) > th -> matches (ind0[i], ind1[m0[i]]) in row order.
@@ -545,10 +598,10 @@ LgLayout lg_layout(int P, int kmax) {
     L.clog = take(N * 4);
     L.arg = take(N * 4);
     L.val = take(N * 4);
-    L.part = take((size_t)L.asg_cap * (kmax / CH + 1) * kmax * sizeof(float2));
+    L.part = take((size_t)L.asg_cap * 2 * ((kmax + ARM - 1) / ARM) * kmax * sizeof(float2));
     L.asg = take((size_t)P * sizeof(Asg));
     L.norm = take((size_t)2 * P * sizeof(float4));
-    L.S = take((size_t)L.asg_cap * kmax * kmax * 4);
+    L.S = take((size_t)L.asg_cap * kmax * ((kmax + 3) & ~3) * 4);
     L.total = o;
     return L;
 }
@@ -602,7 +655,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     int4* TASKS = (int4*)(base + L.tasks);
     int* OUTOFF = (int*)(base + L.outoff);
     int4* MOVES = (int4*)(base + L.moves);
-    float* MD = (float*)(base + L.mdesc);
+    bf16_t* MDH = (bf16_t*)(base + L.mdesc);  // hi half, then the lo half
     float* RMAX = (float*)(base + L.rmax);
     float* RLOG = (float*)(base + L.rlog);
     float* CMAX = (float*)(base + L.cmax);
@@ -700,43 +753,45 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     };
     // assignment + filter of the listed segment pairs (k = index of image a's segment)
     auto assign = [&](int i, const std::vector<size_t>& ks) -> int {
-        // mdesc = final_proj(x) for every token; the 1/4 per side folds into S / 16
-        LG_TRY(mlg_gemm_bias_f32_ld(CAT, 512, w.Wfinal[i], w.bfinal[i], MD, LG_D, Npad, LG_D, LG_D, s));
+        // mdesc = final_proj(x) for every token, as bf16 hi + lo; the 1/4 per side folds into S / 16
+        LG_TRY(mlg_gemm_bias_split_bf16(CAT, 512, w.Wfinal[i], w.bfinal[i], MDH, MDH + (size_t)Npad * LG_D, Npad, LG_D,
+                                         LG_D, s));
+        // one table upload for all chunks (the per-layer statistics read-back orders its
+        // reuse), so chunks follow each other without a host round trip
+        h_asg.clear();
+        for (size_t c = 0; c < ks.size(); ++c) {
+            const Seg sa = segs[ks[c]], sb = segs[ks[c] + 1];
+            Asg a;
+            a.m = sa.len;
+            a.n = sb.len;
+            a.ra = sa.off;
+            a.rb = sb.off;
+            a.soff = (long)(c % L.asg_cap) * kmax * ((kmax + 3) & ~3);
+            a.pair = pair_of[ks[c] / 2];
+            a.ld = (sb.len + 3) & ~3;
+            h_asg.push_back(a);
+            if (stop_layer) stop_layer[a.pair] = i + 1;
+        }
+        if (hipMemcpyAsync(ASG, h_asg.data(), h_asg.size() * sizeof(Asg), hipMemcpyHostToDevice, s) != hipSuccess)
+            return MLG_EHIP;
         for (size_t c0 = 0; c0 < ks.size(); c0 += L.asg_cap) {
             const size_t c1 = std::min(ks.size(), c0 + L.asg_cap);
-            if (c0 > 0 && hipStreamSynchronize(s) != hipSuccess) return MLG_EHIP;  // h_asg reuse
-            h_asg.clear();
             int maxm = 0, maxn = 0;
             for (size_t c = c0; c < c1; ++c) {
-                const Seg sa = segs[ks[c]], sb = segs[ks[c] + 1];
-                Asg a;
-                a.m = sa.len;
-                a.n = sb.len;
-                a.ra = sa.off;
-                a.rb = sb.off;
-                a.soff = (long)(c - c0) * kmax * kmax;
-                a.pair = pair_of[ks[c] / 2];
-                a.pad = 0;
-                h_asg.push_back(a);
-                maxm = std::max(maxm, a.m);
-                maxn = std::max(maxn, a.n);
-                if (stop_layer) stop_layer[a.pair] = i + 1;
+                maxm = std::max(maxm, h_asg[c].m);
+                maxn = std::max(maxn, h_asg[c].n);
             }
-            const unsigned na = (unsigned)h_asg.size();
-            if (hipMemcpyAsync(ASG, h_asg.data(), na * sizeof(Asg), hipMemcpyHostToDevice, s) != hipSuccess)
-                return MLG_EHIP;
-            hipLaunchKernelGGL(k_asg_sim, dim3((maxn + SBM - 1) / SBM, (maxm + SBM - 1) / SBM, na), dim3(256), 0, s, ASG,
-                               MD, SS);
-            const dim3 rows((maxm + 3) / 4, na), cols((maxn + 63) / 64, (maxm + CH - 1) / CH, na),
-                cfin((maxn + 255) / 256, na);
-            hipLaunchKernelGGL(k_asg_rowlse, rows, dim3(256), 0, s, ASG, SS, RMAX, RLOG);
-            hipLaunchKernelGGL(k_asg_colpart, cols, dim3(256), 0, s, ASG, SS, PART, kmax);
-            hipLaunchKernelGGL(k_asg_colfinal, cfin, dim3(256), 0, s, ASG, PART, kmax, CMAX, CLOG);
-            hipLaunchKernelGGL(k_asg_rowarg, rows, dim3(256), 0, s, ASG, SS, RMAX, RLOG, CMAX, CLOG, LZ, ARG, VAL);
-            hipLaunchKernelGGL(k_asg_colargpart, cols, dim3(256), 0, s, ASG, SS, RMAX, RLOG, CMAX, CLOG, LZ, PART,
+            const unsigned na = (unsigned)(c1 - c0);
+            const Asg* tab = ASG + c0;
+            const dim3 stiles((maxn + SBM - 1) / SBM, (maxm + SBM - 1) / SBM, na),
+                atiles((maxn + ARN - 1) / ARN, (maxm + ARM - 1) / ARM, na),
+                lines((std::max(maxm, maxn) + 255) / 256, na, 2);
+            hipLaunchKernelGGL(k_asg_sim, stiles, dim3(256), 0, s, tab, MDH, MDH + (size_t)Npad * LG_D, Npad, SS, PART,
                                kmax);
-            hipLaunchKernelGGL(k_asg_colargfinal, cfin, dim3(256), 0, s, ASG, PART, kmax, ARG);
-            hipLaunchKernelGGL(k_lg_filter, dim3(na), dim3(256), 0, s, ASG, ARG, VAL, IND, filter_thr, kmax, matches,
+            hipLaunchKernelGGL(k_asg_stats, lines, dim3(256), 0, s, tab, PART, kmax, RMAX, RLOG, CMAX, CLOG);
+            hipLaunchKernelGGL(k_asg_arg, atiles, dim3(256), 0, s, tab, SS, RMAX, RLOG, CMAX, CLOG, LZ, PART, kmax);
+            hipLaunchKernelGGL(k_asg_argfinal, lines, dim3(256), 0, s, tab, PART, kmax, ARG, VAL);
+            hipLaunchKernelGGL(k_lg_filter, dim3(na), dim3(256), 0, s, tab, ARG, VAL, IND, filter_thr, kmax, matches,
                                mscores, nmatch);
             MLG_LAUNCH_CHECK();
         }

@@ -11,7 +11,7 @@ rc=$?; echo "rocprof rc=$rc"; grep pairs "$OUT/stdout.log"
 python3 - "$OUT" <<'PY'
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0]
-for r in list(csv.DictReader(open(f)))[:14]:
+for r in list(csv.DictReader(open(f)))[:24]:
     print(f"{float(r['TotalDurationNs'])/1e6:9.2f} ms {float(r['Percentage']):5.1f}% n={r['Calls']:>5} avg={float(r['AverageNs'])/1e3:8.1f}us {r['Name'][:90]}")
 PY
 exit $rc
