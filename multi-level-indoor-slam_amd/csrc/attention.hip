@@ -211,25 +211,157 @@ __device__ __forceinline__ float max3_raw(float a, float b, float c) {
     return r;
 }
 
-// Wide tile for the ragged (LightGlue) path: one workgroup = 4 waves = 256 query rows of
-// one (task, head); each wave owns 64 queries as two 32-column MFMA tiles, so every K and
-// V^T fragment read from LDS feeds two MFMAs (half the LDS bytes per FLOP of the 32-query
-// tile, whose LDS read rate equalled its MFMA rate).  VALU per score, the other bound of
-// a d = 64 attention: no key mask except on the last block; exponent as one fma + one
-// v_exp (log2 domain, 1/8 folded into the constant); row sums kept per lane half and
-// combined once at the end; the running max moves lazily -- P and the O / l
-// accumulators are rescaled only when some lane's block max exceeds its running max by
-// more than 2^8, so P <= 256 (exact softmax either way: numerator and denominator share
-// the same stale max).
-template <bool VTILED>
-__device__ __forceinline__ void attention_tile_q64(char* smem, const bf16_t* __restrict__ Qh,
-                                                   const bf16_t* __restrict__ Kh, const bf16_t* __restrict__ Vh,
-                                                   int vstride, int T, int nq, int qmax, int qblock,
-                                                   bf16_t* __restrict__ orow, int ldo) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, col = lane & 31;
-    const int Tpad = vstride;
-    const int qbase = qblock * 256 + wave * 64;
+// Software-pipelined wide tile for the ragged (LightGlue) path: one workgroup = 4 waves
+// = 256 query rows of one (task, head), one wave per SIMD, each wave 64 queries as two
+// 32-column MFMA tiles.  The softmax runs over 32-key half-blocks: while the VALU
+// exponentiates half-block h (scores computed one step earlier) and P_h V_h runs, the
+// MFMA pipe computes the scores of half-block h + 1, so every MFMA gap has independent
+// VALU work (a one-phase tile leaves the VALU idle during QK^T and the MFMA pipe idle
+// during the max / exp chain: 865 vs 936 TFLOP/s on bench.py's LightGlue stage).  Two 32-key score sets (64 VGPRs) are live.
+// VALU per score, the bound of a d = 64 attention: no key mask except in the last stage;
+// exponent as one fma + one v_exp (log2 domain, 1/8 folded into the constant); row sums
+// as f32 adds per lane half (a 16x16x32 ones-MFMA for them measured slower); the running
+// max moves lazily -- P and the O / l
+// accumulators are rescaled only when some lane's max grows by more than 2^8, so
+// P <= 256 (exact softmax either way: numerator and denominator share the stale max).
+// Softmax order is the textbook one: a half-block's max and the lazy rescale decision
+// precede its exponentials, and all earlier P V MFMAs have been
+// issued by then.
+// LDS, per 64-key stage: K ring of 3 (the current stage's K is still read for its second
+// half while K_{j+1} is read and K_{j+2} lands), V ring of 2; global loads issued at the
+// top of a stage land in LDS at its end, one barrier per stage.
+__device__ __forceinline__ float swap_max(float v) {  // max(v, v of lane ^ 32)
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float swap_sum(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+
+struct PipeCtx {
+    const bf16_t* Kh;
+    const bf16_t* Vh;
+    char* smem;
+    int T, nkb, gk_off, gv_off;
+    int sk0, sk1, sv0a, sv0b, sv1a, sv1b;
+    int koff[4];     // K fragment offset per 16-key step (chunk XOR depends on it only)
+    int voff[2][2][4];  // V^T fragment offsets [half][st][dt * 2 + lo/hi]
+};
+
+// S^T of one 32-key half-block (kt) of the K tile at kb: [qt] tiles
+__device__ __forceinline__ void qk_half(const char* kb, const PipeCtx& c, const bf16x8 (&qf)[2][4], int kt,
+                                        f32x16 (&s)[2]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { s[0][i] = 0.f; s[1][i] = 0.f; }
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + kt * 4096 + c.koff[st]);
+        s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[0][st], s[0], 0, 0, 0);
+        s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[1][st], s[1], 0, 0, 0);
+    }
+}
+
+// half-step H of stage j: consume `cur` (keys 64 j + 32 H ..), produce `nxt`.  kcur /
+// knext: K ring slots of stages j / j + 1; kw: slot for K_{j+2}.
+template <int H, bool LASTSTAGE>
+__device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)[2], const PipeCtx& c,
+                                          const bf16x8 (&qf)[2][4], f32x16 (&o)[2][2], float (&mrun)[2],
+                                          float (&lsum)[2][2], int kcur, int knext, int kw, uint4 (&stage)[4]) {
     constexpr float C = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
+    const int hh = (threadIdx.x & 63) >> 5;
+    if (!LASTSTAGE && H == 0) {  // K_{j+2} (clamped), V_{j+1} -> registers, into LDS at the stage end
+        const bf16_t* pk = c.Kh + (size_t)min(j + 2, c.nkb - 1) * (KB * 64) + c.gk_off;
+        stage[0] = *reinterpret_cast<const uint4*>(pk);
+        stage[1] = *reinterpret_cast<const uint4*>(pk + 32 * 64);
+        const bf16_t* pv = c.Vh + (size_t)(j + 1) * 4096 + c.gv_off;
+        stage[2] = *reinterpret_cast<const uint4*>(pv);
+        stage[3] = *reinterpret_cast<const uint4*>(pv + 32 * 64);
+    }
+    if (LASTSTAGE && (c.T & (KB - 1))) {  // partial last stage: mask keys >= T
+        const int key0 = j * KB + H * 32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (key >= c.T) { cur[0][r] = -INFINITY; cur[1][r] = -INFINITY; }
+        }
+    }
+    float mnew[2];
+    bool grow = false;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+        float bm = max3_raw(cur[qt][0], cur[qt][1], cur[qt][2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) bm = max3_raw(bm, cur[qt][r], cur[qt][r + 1]);
+        bm = fmaxf(bm, cur[qt][15]);
+        mnew[qt] = fmaxf(mrun[qt], swap_max(bm));
+        grow |= (mnew[qt] - mrun[qt]) * C > 8.0f;
+    }
+    if (__any(grow)) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+            const float alpha = __builtin_amdgcn_exp2f((mrun[qt] - mnew[qt]) * C);
+            lsum[qt][0] *= alpha;
+            lsum[qt][1] *= alpha;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { o[qt][0][i] *= alpha; o[qt][1][i] *= alpha; }
+            mrun[qt] = mnew[qt];
+        }
+    }
+    const float mc0 = mrun[0] * C, mc1 = mrun[1] * C;
+    // next half-block's scores on the MFMA pipe
+    const char* kring = c.smem;
+    if (!(LASTSTAGE && H == 1)) qk_half(kring + (H == 0 ? kcur : knext), c, qf, H ^ 1, nxt);
+    // P of this half-block [st][qt]: keys 16 st + 8 hh .. + 7, then O^T += V^T . P^T
+    const char* vb = c.smem + 3 * KTILE_BYTES + (j & 1) * VTILE_BYTES;
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+            const float mc = qt ? mc1 : mc0;
+            u32x4 w;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) {
+                const float p0 = __builtin_amdgcn_exp2f(fmaf(cur[qt][8 * st + 2 * jj], C, -mc));
+                const float p1 = __builtin_amdgcn_exp2f(fmaf(cur[qt][8 * st + 2 * jj + 1], C, -mc));
+                lsum[qt][0] += p0;
+                lsum[qt][1] += p1;
+                w[jj] = pack_bf16x2(p0, p1);
+            }
+            pf[st][qt] = __builtin_bit_cast(bf16x8, w);
+        }
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            const s16x4 lo = *reinterpret_cast<const s16x4*>(vb + c.voff[H][st][2 * dt]);
+            const s16x4 hi = *reinterpret_cast<const s16x4*>(vb + c.voff[H][st][2 * dt + 1]);
+            const bf16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st][0], o[0][dt], 0, 0, 0);
+            o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st][1], o[1][dt], 0, 0, 0);
+        }
+    }
+    if (!LASTSTAGE && H == 1) {
+        char* kwp = c.smem + kw;
+        char* vw = c.smem + 3 * KTILE_BYTES + ((j + 1) & 1) * VTILE_BYTES;
+        *reinterpret_cast<uint4*>(kwp + c.sk0) = stage[0];
+        *reinterpret_cast<uint4*>(kwp + c.sk1) = stage[1];
+        *reinterpret_cast<uint2*>(vw + c.sv0a) = make_uint2(stage[2].x, stage[2].y);
+        *reinterpret_cast<uint2*>(vw + c.sv0b) = make_uint2(stage[2].z, stage[2].w);
+        *reinterpret_cast<uint2*>(vw + c.sv1a) = make_uint2(stage[3].x, stage[3].y);
+        *reinterpret_cast<uint2*>(vw + c.sv1b) = make_uint2(stage[3].z, stage[3].w);
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __restrict__ Qh,
+                                                    const bf16_t* __restrict__ Kh, const bf16_t* __restrict__ Vh,
+                                                    int T, int nq, int qmax, int qblock, bf16_t* __restrict__ orow,
+                                                    int ldo) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, col = lane & 31;
+    const int qbase = qblock * 256 + wave * 64;
     bf16x8 qf[2][4];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
@@ -238,144 +370,74 @@ __device__ __forceinline__ void attention_tile_q64(char* smem, const bf16_t* __r
         for (int st = 0; st < 4; ++st)
             qf[qt][st] = *reinterpret_cast<const bf16x8*>(Qh + (size_t)qld * 64 + st * 16 + hh * 8);
     }
-
+    PipeCtx c;
+    c.Kh = Kh;
+    c.Vh = Vh;
+    c.smem = smem;
+    c.T = T;
+    c.nkb = (T + KB - 1) / KB;
     const int srow = tid >> 3, sch = tid & 7;
-    const int sk0 = k_off(srow, sch), sk1 = k_off(srow + 32, sch);
-    const int sv0a = v_off(srow, 2 * sch), sv0b = v_off(srow, 2 * sch + 1);
-    const int sv1a = v_off(srow + 32, 2 * sch), sv1b = v_off(srow + 32, 2 * sch + 1);
-    uint4 rk0, rk1, rv0, rv1;
-#define ATT_GLOAD(kb)                                                                        \
-    {                                                                                        \
-        rk0 = *reinterpret_cast<const uint4*>(Kh + (size_t)((kb) + srow) * 64 + sch * 8);      \
-        rk1 = *reinterpret_cast<const uint4*>(Kh + (size_t)((kb) + srow + 32) * 64 + sch * 8); \
-        if (VTILED) {                                                                          \
-            const bf16_t* vb_ = Vh + (size_t)((kb) >> 6) * 4096 + sch * 8;                    \
-            rv0 = *reinterpret_cast<const uint4*>(vb_ + srow * 64);                            \
-            rv1 = *reinterpret_cast<const uint4*>(vb_ + (srow + 32) * 64);                     \
-        } else {                                                                               \
-            rv0 = *reinterpret_cast<const uint4*>(Vh + (size_t)srow * Tpad + (kb) + sch * 8);  \
-            rv1 = *reinterpret_cast<const uint4*>(Vh + (size_t)(srow + 32) * Tpad + (kb) + sch * 8); \
-        }                                                                                      \
+    c.gk_off = srow * 64 + sch * 8;
+    c.gv_off = srow * 64 + sch * 8;
+    c.sk0 = k_off(srow, sch);
+    c.sk1 = k_off(srow + 32, sch);
+    c.sv0a = v_off(srow, 2 * sch);
+    c.sv0b = v_off(srow, 2 * sch + 1);
+    c.sv1a = v_off(srow + 32, 2 * sch);
+    c.sv1b = v_off(srow + 32, 2 * sch + 1);
+#pragma unroll
+    for (int st = 0; st < 4; ++st) c.koff[st] = k_off(col, 2 * st + hh);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {  // 8-B granule of keys 32 h + 16 st + 4 hh (+ 8)
+                c.voff[h][st][2 * dt] = v_off(dt * 32 + col, h * 8 + st * 4 + hh);
+                c.voff[h][st][2 * dt + 1] = v_off(dt * 32 + col, h * 8 + st * 4 + hh + 2);
+            }
+    {
+        const uint4 k0 = *reinterpret_cast<const uint4*>(Kh + c.gk_off);
+        const uint4 k1 = *reinterpret_cast<const uint4*>(Kh + c.gk_off + 32 * 64);
+        const uint4 v0 = *reinterpret_cast<const uint4*>(Vh + c.gv_off);
+        const uint4 v1 = *reinterpret_cast<const uint4*>(Vh + c.gv_off + 32 * 64);
+        const bf16_t* pk = Kh + (size_t)min(1, c.nkb - 1) * (KB * 64) + c.gk_off;
+        const uint4 k2 = *reinterpret_cast<const uint4*>(pk);
+        const uint4 k3 = *reinterpret_cast<const uint4*>(pk + 32 * 64);
+        *reinterpret_cast<uint4*>(smem + c.sk0) = k0;
+        *reinterpret_cast<uint4*>(smem + c.sk1) = k1;
+        *reinterpret_cast<uint4*>(smem + KTILE_BYTES + c.sk0) = k2;
+        *reinterpret_cast<uint4*>(smem + KTILE_BYTES + c.sk1) = k3;
+        char* vw = smem + 3 * KTILE_BYTES;
+        *reinterpret_cast<uint2*>(vw + c.sv0a) = make_uint2(v0.x, v0.y);
+        *reinterpret_cast<uint2*>(vw + c.sv0b) = make_uint2(v0.z, v0.w);
+        *reinterpret_cast<uint2*>(vw + c.sv1a) = make_uint2(v1.x, v1.y);
+        *reinterpret_cast<uint2*>(vw + c.sv1b) = make_uint2(v1.z, v1.w);
     }
-#define ATT_LSTORE(buf)                                                                      \
-    {                                                                                        \
-        char* kb_ = smem + (buf) * (KTILE_BYTES + VTILE_BYTES);                              \
-        char* vb_ = kb_ + KTILE_BYTES;                                                       \
-        *reinterpret_cast<uint4*>(kb_ + sk0) = rk0;                                          \
-        *reinterpret_cast<uint4*>(kb_ + sk1) = rk1;                                          \
-        *reinterpret_cast<uint2*>(vb_ + sv0a) = make_uint2(rv0.x, rv0.y);                    \
-        *reinterpret_cast<uint2*>(vb_ + sv0b) = make_uint2(rv0.z, rv0.w);                    \
-        *reinterpret_cast<uint2*>(vb_ + sv1a) = make_uint2(rv1.x, rv1.y);                    \
-        *reinterpret_cast<uint2*>(vb_ + sv1b) = make_uint2(rv1.z, rv1.w);                    \
-    }
-
+    __syncthreads();
+    f32x16 sA[2], sB[2];
+    qk_half(smem, c, qf, 0, sA);
     f32x16 o[2][2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) { o[0][0][i] = 0.f; o[0][1][i] = 0.f; o[1][0][i] = 0.f; o[1][1][i] = 0.f; }
-    float mrun[2] = {-INFINITY, -INFINITY}, lrun[2] = {0.f, 0.f};
-
-    const int nkb = (T + KB - 1) / KB;
-    ATT_GLOAD(0);
-    ATT_LSTORE(0);
-    __syncthreads();
-    int cur = 0;
-    for (int kb = 0; kb < nkb; ++kb) {
-        if (kb + 1 < nkb) { ATT_GLOAD((kb + 1) * KB); }
-        const char* kbase = smem + cur * (KTILE_BYTES + VTILE_BYTES);
-        const char* vbase = kbase + KTILE_BYTES;
-
-        f32x16 s[2][2];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { s[0][0][i] = 0.f; s[0][1][i] = 0.f; s[1][0][i] = 0.f; s[1][1][i] = 0.f; }
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbase + k_off(kt * 32 + col, 2 * st + hh));
-                s[0][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[0][st], s[0][kt], 0, 0, 0);
-                s[1][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[1][st], s[1][kt], 0, 0, 0);
-            }
-        const int key0 = kb * KB;
-        if (key0 + KB > T) {  // last, partial block: mask keys >= T
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int key = key0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                    if (key >= T) { s[0][kt][r] = -INFINITY; s[1][kt][r] = -INFINITY; }
-                }
-        }
-        float mnew[2];
-        bool grow = false;
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-            float bm = -INFINITY;
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) bm = max3_raw(bm, s[qt][kt][r], s[qt][kt][r + 1]);
-            bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-            mnew[qt] = fmaxf(mrun[qt], bm);
-            grow |= (mnew[qt] - mrun[qt]) * C > 8.0f;
-        }
-        if (__any(grow)) {
-#pragma unroll
-            for (int qt = 0; qt < 2; ++qt) {
-                const float alpha = __builtin_amdgcn_exp2f((mrun[qt] - mnew[qt]) * C);
-                lrun[qt] *= alpha;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) { o[qt][0][i] *= alpha; o[qt][1][i] *= alpha; }
-                mrun[qt] = mnew[qt];
-            }
-        }
-        // O^T += V^T . P^T; P of one 16-key step made right before its MFMAs (short live
-        // ranges); each V^T fragment feeds both query tiles
-        const float mc0 = mrun[0] * C, mc1 = mrun[1] * C;
-        float ps[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int st = 0; st < 2; ++st) {
-                bf16x8 pf[2];
-#pragma unroll
-                for (int qt = 0; qt < 2; ++qt) {
-                    const float mc = qt ? mc1 : mc0;
-#pragma unroll
-                    for (int j = 0; j < 8; j += 2) {
-                        const float p0 = __builtin_amdgcn_exp2f(fmaf(s[qt][kt][8 * st + j], C, -mc));
-                        const float p1 = __builtin_amdgcn_exp2f(fmaf(s[qt][kt][8 * st + j + 1], C, -mc));
-                        ps[qt][0] += p0;
-                        ps[qt][1] += p1;
-                        const uint32_t w = pack_bf16x2(p0, p1);
-                        pf[qt][j] = (short)(w & 0xffff);
-                        pf[qt][j + 1] = (short)(w >> 16);
-                    }
-                }
-                const int g0 = kt * 8 + st * 4 + hh;
-#pragma unroll
-                for (int dt = 0; dt < 2; ++dt) {
-                    const int d = dt * 32 + col;
-                    const uint2 lo = *reinterpret_cast<const uint2*>(vbase + v_off(d, g0));
-                    const uint2 hi = *reinterpret_cast<const uint2*>(vbase + v_off(d, g0 + 2));
-                    bf16x8 vf;
-                    vf[0] = (short)(lo.x & 0xffff); vf[1] = (short)(lo.x >> 16);
-                    vf[2] = (short)(lo.y & 0xffff); vf[3] = (short)(lo.y >> 16);
-                    vf[4] = (short)(hi.x & 0xffff); vf[5] = (short)(hi.x >> 16);
-                    vf[6] = (short)(hi.y & 0xffff); vf[7] = (short)(hi.y >> 16);
-                    o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[0], o[0][dt], 0, 0, 0);
-                    o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[1], o[1][dt], 0, 0, 0);
-                }
-            }
-        lrun[0] += ps[0][0] + ps[0][1];
-        lrun[1] += ps[1][0] + ps[1][1];
-        if (kb + 1 < nkb) { ATT_LSTORE(cur ^ 1); }
-        __syncthreads();
-        cur ^= 1;
+    float mrun[2] = {-INFINITY, -INFINITY};
+    float lsum[2][2] = {{0.f, 0.f}, {0.f, 0.f}};  // per lane half, two partial sums each
+    uint4 stage[4];
+    int k0 = 0, k1 = KTILE_BYTES, k2 = 2 * KTILE_BYTES;  // ring slots of K_j, K_{j+1}, K_{j+2}
+    for (int j = 0; j + 1 < c.nkb; ++j) {
+        pipe_half<0, false>(j, sA, sB, c, qf, o, mrun, lsum, k0, k1, k2, stage);
+        pipe_half<1, false>(j, sB, sA, c, qf, o, mrun, lsum, k0, k1, k2, stage);
+        const int t = k0;
+        k0 = k1;
+        k1 = k2;
+        k2 = t;
     }
+    pipe_half<0, true>(c.nkb - 1, sA, sB, c, qf, o, mrun, lsum, k0, k1, k2, stage);
+    pipe_half<1, true>(c.nkb - 1, sB, sA, c, qf, o, mrun, lsum, k0, k1, k2, stage);
 
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-        const float l = lrun[qt] + __shfl_xor(lrun[qt], 32, 64);
+        const float l = swap_sum(lsum[qt][0] + lsum[qt][1]);
         const int qrow = qbase + qt * 32 + col;
         if (qrow < nq) {
             const float inv = 1.0f / l;
@@ -392,8 +454,6 @@ __device__ __forceinline__ void attention_tile_q64(char* smem, const bf16_t* __r
                 }
         }
     }
-#undef ATT_GLOAD
-#undef ATT_LSTORE
 }
 
 // Ragged batch: task t attends query rows [q_off, q_off + q_len) to keys / values
@@ -405,13 +465,13 @@ __device__ __forceinline__ void attention_tile_q64(char* smem, const bf16_t* __r
 // 1-D grid of qblocks x heads x tasks (rounded up to a multiple of 8), dealt so that the
 // query blocks of one (task, head) -- which all stream the same K / V^T -- land on one
 // XCD (hardware deals linear block b to XCD b % 8) and share its L2.
-__global__ __launch_bounds__(256, 2) void k_attention_varlen(const bf16_t* __restrict__ Q,
+__global__ __launch_bounds__(256, 1) void k_attention_varlen(const bf16_t* __restrict__ Q,
                                                              const bf16_t* __restrict__ K,
                                                              const bf16_t* __restrict__ Vt, bf16_t* __restrict__ O,
                                                              int ldo, int Npad, const int4* __restrict__ tasks,
                                                              const int* __restrict__ out_off, int nqb, int heads,
                                                              int total) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_BYTES + VTILE_BYTES)];
+    __shared__ __attribute__((aligned(16))) char smem[3 * KTILE_BYTES + 2 * VTILE_BYTES];
     const int per_xcd = (int)gridDim.x >> 3;
     const int logical = ((int)blockIdx.x & 7) * per_xcd + ((int)blockIdx.x >> 3);
     if (logical >= total) return;
@@ -421,9 +481,9 @@ __global__ __launch_bounds__(256, 2) void k_attention_varlen(const bf16_t* __res
     const int4 tk = tasks[t];  // q_off, q_len, kv_off, kv_len
     if (qb * 256 >= tk.y || tk.w <= 0) return;
     const int qpad = (tk.y + 63) & ~63;
-    attention_tile_q64<true>(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
-                             Vt + ((size_t)h * Npad + tk.z) * 64, Npad, tk.w, tk.y, qpad, qb,
-                             O + (size_t)out_off[t] * ldo + h * 64, ldo);
+    attention_tile_pipe(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
+                        Vt + ((size_t)h * Npad + tk.z) * 64, tk.w, tk.y, qpad, qb, O + (size_t)out_off[t] * ldo + h * 64,
+                        ldo);
 }
 
 }  // namespace
