@@ -72,7 +72,15 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
     constexpr int N = SELF ? 768 : 512;
     __shared__ __attribute__((aligned(16))) char lds[R * ROWB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
-    const int m0 = blockIdx.x * R, part = blockIdx.y;
+    // 1-D grid, dealt so the parts (q, k, v / qk, v) of one token tile are consecutive
+    // workgroups of one XCD (hardware deals block b to XCD b % 8): the tile's x rows are
+    // then read from HBM once and from that XCD's L2 by the other parts (with the part in
+    // blockIdx.y every part re-read the whole of x from HBM)
+    constexpr int NPART = SELF ? 3 : 2;
+    const int per_xcd = (int)gridDim.x >> 3;
+    const int logical = ((int)blockIdx.x & 7) * per_xcd + ((int)blockIdx.x >> 3);
+    if (logical >= (Npad / R) * NPART) return;
+    const int m0 = (logical / NPART) * R, part = logical % NPART;
     const bool is_v = part == (SELF ? 2 : 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -158,12 +166,13 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
 int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,
                 const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s) {
     if (Npad <= 0 || (Npad % R) || ldx < 256 || (ldx % 8)) return MLG_EINVAL;
+    const unsigned grid = (unsigned)((((long)(Npad / R) * (self_block ? 3 : 2)) + 7) & ~7L);
     if (self_block) {
-        hipLaunchKernelGGL(k_lg_proj<true>, dim3((unsigned)(Npad / R), 3), dim3(512), 0, s, xcopy, ldx, W, bias, ecos,
-                           esin, live, Q, K, Vt, Npad);
+        hipLaunchKernelGGL(k_lg_proj<true>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin, live, Q, K,
+                           Vt, Npad);
     } else {
-        hipLaunchKernelGGL(k_lg_proj<false>, dim3((unsigned)(Npad / R), 2), dim3(512), 0, s, xcopy, ldx, W, bias,
-                           (const float*)nullptr, (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad);
+        hipLaunchKernelGGL(k_lg_proj<false>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, (const float*)nullptr,
+                           (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad);
     }
     MLG_LAUNCH_CHECK();
     return MLG_OK;
