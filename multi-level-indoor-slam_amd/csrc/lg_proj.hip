@@ -30,6 +30,14 @@ __device__ __forceinline__ int xoff(int row, int chunk) { return row * ROWB + ((
 
 __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+// Output staging image over the dead x tile: [4 heads][64 rows][64] bf16, 16-B chunk c of
+// row r at slot c ^ (r & 7).  Rows are tokens for q / k and head dims for V^T; either way
+// a head's 64 rows are ONE contiguous 8 KiB block of the destination, written as whole
+// 1 KiB pieces (per-lane 8-B stores at a 128-B row stride touched 32 lines each).
+__device__ __forceinline__ int stage_off(int h, int row, int e) {
+    return (h * 64 + row) * 128 + ((((e >> 3) ^ (row & 7))) << 4) + (e & 7) * 2;
+}
+
 // acc[mt] over K = 256 (16 k-steps; step ks: LDS chunk 2 ks + hh, W slab ks).
 // SWAP: acc = X . W^T (lane col = output column), else acc = W . X^T (lane col = token).
 template <bool SWAP>
@@ -116,7 +124,7 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
                 }
         }
         proj_gemm<false>(wrow, (size_t)N * 16, lds, acc);
-        bf16_t* dst = part == 0 ? Q : K;
+        __syncthreads();  // every wave has read the x tile
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int n = 32 * wave + 8 * g + 4 * hh;  // column within the part
@@ -137,11 +145,12 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
                 }
                 uint2 o = make_uint2(0u, 0u);
                 if (live[m]) o = make_uint2(pack_bf16x2(x0, x1), pack_bf16x2(x2, x3));
-                *reinterpret_cast<uint2*>(dst + ((size_t)h * Npad + m) * 64 + d) = o;
+                *reinterpret_cast<uint2*>(lds + stage_off(h, r, d)) = o;
             }
         }
     } else {
         proj_gemm<true>(wrow, (size_t)N * 16, lds, acc);
+        __syncthreads();  // every wave has read the x tile
         const int n = 32 * wave + col, h = n >> 6, d = n & 63;
         const float b = bias[256 * part + n];
 #pragma unroll
@@ -155,9 +164,18 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
                 const float v1 = (lv & 0xff00) ? a[4 * g + 1] + b : 0.f;
                 const float v2 = (lv & 0xff0000) ? a[4 * g + 2] + b : 0.f;
                 const float v3 = (lv >> 24) ? a[4 * g + 3] + b : 0.f;
-                bf16_t* p = Vt + ((size_t)h * Npad + (m & ~63)) * 64 + (size_t)d * 64 + (m & 63);
-                *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+                *reinterpret_cast<uint2*>(lds + stage_off(h, d, m & 63)) =
+                    make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
             }
+    }
+    __syncthreads();
+    // copy-out: per head one contiguous [64 rows][64] block at (h * Npad + m0) * 64
+    bf16_t* dst = is_v ? Vt : (part == 0 ? Q : K);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int L = p * 512 + tid, h = L >> 9, row = (L >> 3) & 63, c = L & 7;
+        *reinterpret_cast<uint4*>(dst + ((size_t)h * Npad + m0 + row) * 64 + c * 8) =
+            *reinterpret_cast<const uint4*>(lds + stage_off(h, row, 8 * c));
     }
 }
 
