@@ -435,24 +435,34 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
     pipe_half<0, true>(c.nkb - 1, sA, sB, c, qf, o, mrun, lsum, k0, k1, k2, stage);
     pipe_half<1, true>(c.nkb - 1, sB, sA, c, qf, o, mrun, lsum, k0, k1, k2, stage);
 
+    // O staged through LDS (the K / V rings are dead once every wave is past its last
+    // stage) as this wave's [64 queries][64 d] bf16, 16-B chunk c of row r at c ^ (r & 7),
+    // then written as whole 128-B row pieces: 8 rows per wave-instruction instead of 32
+    // rows x 16 B (the store tail of a row-per-lane epilogue is issue-bound)
+    __syncthreads();
+    char* st = smem + wave * (64 * 128);
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-        const float l = swap_sum(lsum[qt][0] + lsum[qt][1]);
-        const int qrow = qbase + qt * 32 + col;
-        if (qrow < nq) {
-            const float inv = 1.0f / l;
-            bf16_t* out = orow + (size_t)qrow * ldo;
+        const float inv = 1.0f / swap_sum(lsum[qt][0] + lsum[qt][1]);
+        const int r = qt * 32 + col;
 #pragma unroll
-            for (int dt = 0; dt < 2; ++dt)
+        for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int d = dt * 32 + 8 * g + 4 * hh;
-                    uint2 w;
-                    w.x = pack_bf16x2(o[qt][dt][4 * g] * inv, o[qt][dt][4 * g + 1] * inv);
-                    w.y = pack_bf16x2(o[qt][dt][4 * g + 2] * inv, o[qt][dt][4 * g + 3] * inv);
-                    *reinterpret_cast<uint2*>(out + d) = w;
-                }
-        }
+            for (int g = 0; g < 4; ++g) {
+                uint2 w;
+                w.x = pack_bf16x2(o[qt][dt][4 * g] * inv, o[qt][dt][4 * g + 1] * inv);
+                w.y = pack_bf16x2(o[qt][dt][4 * g + 2] * inv, o[qt][dt][4 * g + 3] * inv);
+                *reinterpret_cast<uint2*>(st + r * 128 + (((dt * 4 + g) ^ (r & 7)) << 4) + 8 * hh) = w;
+            }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const int r = p * 8 + (lane >> 3), c = lane & 7, qrow = qbase + r;
+        if (qrow < nq)
+            *reinterpret_cast<uint4*>(orow + (size_t)qrow * ldo + c * 8) =
+                *reinterpret_cast<const uint4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
     }
 }
 
