@@ -277,6 +277,13 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
     //    one 1-KiB f32 row of x read, updated and written, its 512-B bf16 copy written --
     //    full-line HBM traffic instead of 16-B pieces of 32 rows per instruction.
     {
+        // the residual rows this wave updates below, fetched now so their HBM latency
+        // hides under the ffn2 GEMM (rows past M clamped, never stored)
+        float4 xr[R / NW];
+#pragma unroll
+        for (int i = 0; i < R / NW; ++i)
+            xr[i] = reinterpret_cast<const float4*>(X + (size_t)min(m0 + wave * (R / NW) + i, M - 1) * 256)[lane];
+        __builtin_amdgcn_sched_barrier(0);
         f32x16 acc[2][MT];
         zero(acc);
         gemm_phase<2>(w.Wf2, 256, 64 * wave, 8, 0, lds, acc);
@@ -311,7 +318,7 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
             if (m >= M) continue;  // wave-uniform
             const float4 y = *reinterpret_cast<const float4*>(lds + r * 1024 + ((lane ^ (r & 15)) << 4));
             float4* px = reinterpret_cast<float4*>(X + (size_t)m * 256) + lane;
-            float4 x = *px;
+            float4 x = xr[i];
             x.x += y.x;
             x.y += y.y;
             x.z += y.z;
