@@ -135,88 +135,8 @@ struct EpiQKV {  // qkv -> Q, K bf16 [B, 12, Tpad, 64] and V^T bf16 [B, 12, 64, 
     }
 };
 
-// LightGlue self-attention projection.  Weight rows are permuted on the host from the
-// reference's (head, 64, 3) interleave to [q | k | v] x (head, 64), so a lane's 4
-// consecutive columns are 4 consecutive dims of one head: rotary pairs (2j, 2j+1) are
-// lane-local.  q, k: t*cos + rotate_half(t)*sin (uncontracted, as torch) -> Q / K
-// [4][Npad][64]; v -> V^T [4][64][Npad]; rows outside live segments written as zeros.
-struct EpiLgSelf {
-    bf16_t* Q; bf16_t* K; bf16_t* Vt; const float* bias; const float* ecos; const float* esin;
-    const uint8_t* live; int Npad;
-    __device__ void operator()(int m, int n, const f32x4& v) const {
-        const float4 b = *reinterpret_cast<const float4*>(bias + n);
-        const bool on = live[m] != 0;
-        float x0 = v[0] + b.x, x1 = v[1] + b.y, x2 = v[2] + b.z, x3 = v[3] + b.w;
-        const int which = n >> 8, c = n & 255, h = c >> 6, d = c & 63;
-        if (which < 2) {
-            const int j = d >> 1;
-            const float c0 = ecos[(size_t)m * 32 + j], s0 = esin[(size_t)m * 32 + j];
-            const float c1 = ecos[(size_t)m * 32 + j + 1], s1 = esin[(size_t)m * 32 + j + 1];
-            const float r0 = __fadd_rn(__fmul_rn(x0, c0), __fmul_rn(-x1, s0));
-            const float r1 = __fadd_rn(__fmul_rn(x1, c0), __fmul_rn(x0, s0));
-            const float r2 = __fadd_rn(__fmul_rn(x2, c1), __fmul_rn(-x3, s1));
-            const float r3 = __fadd_rn(__fmul_rn(x3, c1), __fmul_rn(x2, s1));
-            uint2 o = make_uint2(0u, 0u);
-            if (on) {
-                o.x = pack_bf16x2(r0, r1);
-                o.y = pack_bf16x2(r2, r3);
-            }
-            *reinterpret_cast<uint2*>((which == 0 ? Q : K) + ((size_t)h * Npad + m) * 64 + d) = o;
-        } else {
-            // V^T tiled per 64-key block: [h][m / 64][64 d][64 keys] (attention.hip)
-            bf16_t* p = Vt + (((size_t)h * Npad + (m & ~63)) * 64) + (size_t)d * 64 + (m & 63);
-            p[0] = on ? f32_to_bf16(x0) : (bf16_t)0;
-            p[64] = on ? f32_to_bf16(x1) : (bf16_t)0;
-            p[128] = on ? f32_to_bf16(x2) : (bf16_t)0;
-            p[192] = on ? f32_to_bf16(x3) : (bf16_t)0;
-        }
-    }
-};
 
-// LightGlue cross-attention projection [to_qk | to_v]: qk -> Q [4][Npad][64], v -> V^T.
-struct EpiLgCross {
-    bf16_t* Q; bf16_t* Vt; const float* bias; const uint8_t* live; int Npad;
-    __device__ void operator()(int m, int n, const f32x4& v) const {
-        const float4 b = *reinterpret_cast<const float4*>(bias + n);
-        const bool on = live[m] != 0;
-        const float x0 = v[0] + b.x, x1 = v[1] + b.y, x2 = v[2] + b.z, x3 = v[3] + b.w;
-        const int which = n >> 8, c = n & 255, h = c >> 6, d = c & 63;
-        if (which == 0) {
-            uint2 o = make_uint2(0u, 0u);
-            if (on) {
-                o.x = pack_bf16x2(x0, x1);
-                o.y = pack_bf16x2(x2, x3);
-            }
-            *reinterpret_cast<uint2*>(Q + ((size_t)h * Npad + m) * 64 + d) = o;
-        } else {
-            // V^T tiled per 64-key block: [h][m / 64][64 d][64 keys] (attention.hip)
-            bf16_t* p = Vt + (((size_t)h * Npad + (m & ~63)) * 64) + (size_t)d * 64 + (m & 63);
-            p[0] = on ? f32_to_bf16(x0) : (bf16_t)0;
-            p[64] = on ? f32_to_bf16(x1) : (bf16_t)0;
-            p[128] = on ? f32_to_bf16(x2) : (bf16_t)0;
-            p[192] = on ? f32_to_bf16(x3) : (bf16_t)0;
-        }
-    }
-};
 
-// X += acc + b (f32 residual stream) and its bf16 copy into C (the next GEMM's input)
-struct EpiResidualCopy {
-    float* X; int ldx; const float* bias; bf16_t* C; int ldc;
-    __device__ void operator()(int m, int n, const f32x4& v) const {
-        float4* p = reinterpret_cast<float4*>(X + (size_t)m * ldx + n);
-        const float4 b = *reinterpret_cast<const float4*>(bias + n);
-        float4 x = *p;
-        x.x += v[0] + b.x;
-        x.y += v[1] + b.y;
-        x.z += v[2] + b.z;
-        x.w += v[3] + b.w;
-        *p = x;
-        uint2 o;
-        o.x = pack_bf16x2(x.x, x.y);
-        o.y = pack_bf16x2(x.z, x.w);
-        *reinterpret_cast<uint2*>(C + (size_t)m * ldc + n) = o;
-    }
-};
 
 // relu(acc + b) -> bf16, columns >= nvalid dropped (N padded to the tile width)
 struct EpiBiasReluBF16 {
@@ -686,27 +606,6 @@ int mlg_gemm_bias_split_bf16(const bf16_t* A, int lda, const bf16_t* W, const fl
                              int M, int N, int K, hipStream_t s) {
     if (N % 16) return MLG_EINVAL;
     return launch(A, W, M, N, K, lda, K, EpiBiasSplitBF16{H, L, M, bias}, s);
-}
-int mlg_gemm_bias_bf16_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* C, int ldc, int M,
-                          int N, int K, hipStream_t s) {
-    return launch(A, W, M, N, K, lda, K, EpiBiasBF16{C, ldc, bias}, s);
-}
-int mlg_gemm_residual_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* gamma, float* X,
-                         int ldx, int M, int N, int K, hipStream_t s) {
-    return launch(A, W, M, N, K, lda, K, EpiResidual{X, ldx, bias, gamma}, s);
-}
-int mlg_gemm_lg_self(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* ecos,
-                     const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, int K_,
-                     hipStream_t s) {
-    return launch(A, W, Npad, 768, K_, lda, K_, EpiLgSelf{Q, K, Vt, bias, ecos, esin, live, Npad}, s);
-}
-int mlg_gemm_lg_cross(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const uint8_t* live, bf16_t* Q,
-                      bf16_t* Vt, int Npad, int K_, hipStream_t s) {
-    return launch(A, W, Npad, 512, K_, lda, K_, EpiLgCross{Q, Vt, bias, live, Npad}, s);
-}
-int mlg_gemm_residual_copy(const bf16_t* A, int lda, const bf16_t* W, const float* bias, float* X, int ldx, bf16_t* C,
-                           int ldc, int M, int N, int K_, hipStream_t s) {
-    return launch(A, W, M, N, K_, lda, K_, EpiResidualCopy{X, ldx, bias, C, ldc}, s);
 }
 int mlg_gemm_bias_relu_bf16(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* C, int ldc,
                             int nvalid, int M, int N, int K_, hipStream_t s) {

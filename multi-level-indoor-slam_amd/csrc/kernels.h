@@ -36,17 +36,6 @@ int mlg_gemm_bias_f32_ld(const bf16_t* A, int lda, const bf16_t* W, const float*
 // stored k-step-major [N / 16][M][16] (LightGlue assignment operands)
 int mlg_gemm_bias_split_bf16(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* H, bf16_t* L,
                              int M, int N, int K, hipStream_t s);
-int mlg_gemm_bias_bf16_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* C, int ldc, int M,
-                          int N, int K, hipStream_t s);
-int mlg_gemm_residual_ld(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* gamma, float* X,
-                         int ldx, int M, int N, int K, hipStream_t s);
-int mlg_gemm_lg_self(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* ecos,
-                     const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, int K_,
-                     hipStream_t s);
-int mlg_gemm_lg_cross(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const uint8_t* live, bf16_t* Q,
-                      bf16_t* Vt, int Npad, int K_, hipStream_t s);
-int mlg_gemm_residual_copy(const bf16_t* A, int lda, const bf16_t* W, const float* bias, float* X, int ldx, bf16_t* C,
-                           int ldc, int M, int N, int K_, hipStream_t s);
 int mlg_gemm_bias_relu_bf16(const bf16_t* A, int lda, const bf16_t* W, const float* bias, bf16_t* C, int ldc,
                             int nvalid, int M, int N, int K_, hipStream_t s);
 int mlg_gemm_bias_add_relu(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, float* X,

@@ -29,7 +29,7 @@ class _Weights(ctypes.Structure):
 def qkv_row_order():
     """Row permutation of SelfBlock.Wqkv from the reference's (head, 64, 3) interleave
     (``qkv.unflatten(-1, (heads, -1, 3))``) to [q | k | v] x (head, dim), the layout the
-    fused GEMM epilogue expects (csrc/gemm_bf16.hip EpiLgSelf)."""
+    projection kernel expects (csrc/lg_proj.hip: parts q, k, v of 256 columns each)."""
     s, h, d = np.meshgrid(np.arange(3), np.arange(4), np.arange(64), indexing="ij")
     return (h * 192 + d * 3 + s).reshape(-1)
 
