@@ -107,22 +107,6 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
         for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
 
     if (!is_v) {
-        // rotary factors (cos, sin of frequencies d/2, d/2 + 1) of this lane's 2 tokens x 4
-        // head-dim groups, fetched before the GEMM so their latency hides under it.  Read
-        // straight from global: an LDS-staged copy of the tile's factors gave run-to-run
-        // different q / k on gfx950 (unexplained; tests/test_kernels_gpu.py::
-        // test_lightglue_kernels_deterministic).
-        float2 rc[2][4], rs[2][4];
-        if (SELF) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    const size_t eo = (size_t)(m0 + 32 * mt + col) * 32 + ((32 * wave + 8 * g + 4 * hh) & 63) / 2;
-                    rc[mt][g] = *reinterpret_cast<const float2*>(ecos + eo);
-                    rs[mt][g] = *reinterpret_cast<const float2*>(esin + eo);
-                }
-        }
         proj_gemm<false>(wrow, (size_t)N * 16, lds, acc);
         __syncthreads();  // every wave has read the x tile
 #pragma unroll
@@ -136,7 +120,15 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
                 const f32x16& a = acc[mt];
                 float x0 = a[4 * g] + b.x, x1 = a[4 * g + 1] + b.y, x2 = a[4 * g + 2] + b.z, x3 = a[4 * g + 3] + b.w;
                 if (SELF) {  // t * cos + rotate_half(t) * sin, uncontracted as torch
-                    const float2 e0 = make_float2(rc[mt][g].x, rs[mt][g].x), e1 = make_float2(rc[mt][g].y, rs[mt][g].y);
+                    // (cos, sin) of frequencies d/2, d/2 + 1, read after the GEMM (held
+                    // across it they cost 32 VGPRs = one workgroup per CU less) straight
+                    // from global: an LDS-staged copy of the tile's factors gave run-to-run
+                    // different q / k on gfx950 (unexplained; tests/test_kernels_gpu.py::
+                    // test_lightglue_kernels_deterministic)
+                    const size_t eo = (size_t)m * 32 + (n & 63) / 2;
+                    const float2 rc = *reinterpret_cast<const float2*>(ecos + eo);
+                    const float2 rs = *reinterpret_cast<const float2*>(esin + eo);
+                    const float2 e0 = make_float2(rc.x, rs.x), e1 = make_float2(rc.y, rs.y);
                     const float r0 = __fadd_rn(__fmul_rn(x0, e0.x), __fmul_rn(-x1, e0.y));
                     const float r1 = __fadd_rn(__fmul_rn(x1, e0.x), __fmul_rn(x0, e0.y));
                     const float r2 = __fadd_rn(__fmul_rn(x2, e1.x), __fmul_rn(-x3, e1.y));
