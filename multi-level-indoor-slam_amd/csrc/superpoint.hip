@@ -288,6 +288,111 @@ __global__ void k_nms_final(float* __restrict__ s, const uint8_t* __restrict__ m
     s[i] = v;
 }
 
+// simple_nms(r = 4) + border + keep, fused: one workgroup per 32 x 64 output tile holds
+// its scores with a 5 r halo (the dependency radius of the initial max-pool and two
+// suppression rounds) in LDS and runs every max-pool (separable, -inf outside the image,
+// as max_pool2d's padding) and mask update there -- one read of the score map (3.7x
+// halo redundancy) and one write, instead of 16 full-resolution passes.  Out-of-place
+// (neighbouring tiles read the input halo).
+constexpr int NMS_TH = 32, NMS_TW = 64, NMS_HALO = 20;
+constexpr int NMS_LH = NMS_TH + 2 * NMS_HALO, NMS_LW = NMS_TW + 2 * NMS_HALO, NMS_N = NMS_LH * NMS_LW;
+
+template <typename T> struct Vec4;
+template <> struct Vec4<float> { typedef float4 type; };
+template <> struct Vec4<uint8_t> { typedef uchar4 type; };
+
+template <typename T>
+__device__ __forceinline__ T vmax_(T a, T b) { return a > b ? a : b; }
+
+// (2 R + 1) max filter of the tile, separable, R = 4: each thread produces 4 consecutive
+// outputs from 12 inputs held in registers (one vector read per 4 in x, column reads in
+// y).  Values outside the tile are -inf / 0 (never in a used output: see k_sp_nms).
+template <typename T>
+__device__ __forceinline__ void nms_pool4(const T* in, T* tmp, T* out, T lo) {
+    typedef typename Vec4<T>::type V;
+    constexpr int GX = NMS_LW / 4, GY = NMS_LH / 4;
+    for (int i = threadIdx.x; i < NMS_LH * GX; i += blockDim.x) {  // along x
+        const int y = i / GX, g = i - y * GX;
+        const V* row = reinterpret_cast<const V*>(in + y * NMS_LW);
+        const V c = row[g];
+        const V l = g > 0 ? row[g - 1] : V{lo, lo, lo, lo};
+        const V r = g + 1 < GX ? row[g + 1] : V{lo, lo, lo, lo};
+        const T v[12] = {l.x, l.y, l.z, l.w, c.x, c.y, c.z, c.w, r.x, r.y, r.z, r.w};
+        T o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            T m = v[k];
+#pragma unroll
+            for (int d = 1; d <= 8; ++d) m = vmax_(m, v[k + d]);
+            o[k] = m;
+        }
+        reinterpret_cast<V*>(tmp + y * NMS_LW)[g] = V{o[0], o[1], o[2], o[3]};
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < GY * NMS_LW; i += blockDim.x) {  // along y
+        const int g = i / NMS_LW, x = i - g * NMS_LW, y0 = 4 * g;
+        T v[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const int y = y0 - 4 + k;
+            v[k] = (y >= 0 && y < NMS_LH) ? tmp[y * NMS_LW + x] : lo;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            T m = v[k];
+#pragma unroll
+            for (int d = 1; d <= 8; ++d) m = vmax_(m, v[k + d]);
+            out[(y0 + k) * NMS_LW + x] = m;
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(512) void k_sp_nms(const float* __restrict__ sc, float* __restrict__ out, int B, int H,
+                                                int W, int border) {
+    __shared__ __attribute__((aligned(16))) char nms_smem[(size_t)NMS_N * (4 * 4 + 3)];  // 142 KB: one per CU
+    float* S = reinterpret_cast<float*>(nms_smem);
+    float* A = S + NMS_N;
+    float* Tm = A + NMS_N;
+    float* P = Tm + NMS_N;
+    uint8_t* MK = reinterpret_cast<uint8_t*>(P + NMS_N);
+    uint8_t* SP = MK + NMS_N;
+    uint8_t* TU = SP + NMS_N;
+    const int tx = blockIdx.x, ty = blockIdx.y, b = blockIdx.z;
+    const int ox = tx * NMS_TW - NMS_HALO, oy = ty * NMS_TH - NMS_HALO;
+    const float* img = sc + (size_t)b * H * W;
+    auto inside = [&](int i) {
+        const int y = i / NMS_LW + oy, x = i % NMS_LW + ox;
+        return y >= 0 && y < H && x >= 0 && x < W;
+    };
+    for (int i = threadIdx.x; i < NMS_N; i += blockDim.x) {
+        const int y = i / NMS_LW + oy, x = i % NMS_LW + ox;
+        S[i] = (y >= 0 && y < H && x >= 0 && x < W) ? img[(size_t)y * W + x] : -INFINITY;
+    }
+    __syncthreads();
+    nms_pool4(S, Tm, P, -INFINITY);  // max_mask = scores == max_pool(scores)
+    for (int i = threadIdx.x; i < NMS_N; i += blockDim.x) MK[i] = inside(i) && S[i] == P[i];
+    __syncthreads();
+    for (int it = 0; it < 2; ++it) {
+        nms_pool4(MK, TU, SP, (uint8_t)0);  // supp_mask = max_pool(max_mask) > 0
+        for (int i = threadIdx.x; i < NMS_N; i += blockDim.x) A[i] = inside(i) ? (SP[i] ? 0.f : S[i]) : -INFINITY;
+        __syncthreads();
+        nms_pool4(A, Tm, P, -INFINITY);  // new_max_mask = supp_scores == max_pool(supp_scores)
+        for (int i = threadIdx.x; i < NMS_N; i += blockDim.x)
+            MK[i] = MK[i] | (inside(i) && A[i] == P[i] && !SP[i]);
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < NMS_TH * NMS_TW; i += blockDim.x) {
+        const int ly = i / NMS_TW + NMS_HALO, lx = i % NMS_TW + NMS_HALO;
+        const int y = ly + oy, x = lx + ox;
+        if (y >= H || x >= W) continue;
+        const int l = ly * NMS_LW + lx;
+        float v = MK[l] ? S[l] : 0.f;
+        if (y < border || x < border || y >= H - border || x >= W - border) v = -1.f;
+        out[(size_t)b * H * W + (size_t)y * W + x] = v;
+    }
+}
+
 // ------------------------------------------------------------------ selection
 // One 1024-thread workgroup per frame.  Candidates (score > thr) are compacted in
 // raster order; if there are more than k, the k-th largest score is found by a 4-pass
@@ -606,26 +711,35 @@ int mlg_superpoint_run(const mlg_sp_weights_i& w, const uint8_t* frames, int B, 
     hipLaunchKernelGGL(k_sp_scores, dim3((M + 255) / 256), dim3(256), 0, s, logits, 128, w.b[8], B, h, wd, sc);
     MLG_LAUNCH_CHECK();
     // simple_nms
-    const long n = (long)B * H * W;
-    const dim3 g((unsigned)((n + 255) / 256)), t(256);
-    auto maxpool_f = [&](const float* in, float* out) {
-        hipLaunchKernelGGL(k_maxfilt<float>, g, t, 0, s, in, t1, B, H, W, nms_radius, 0);
-        hipLaunchKernelGGL(k_maxfilt<float>, g, t, 0, s, (const float*)t1, out, B, H, W, nms_radius, 1);
-    };
-    maxpool_f(sc, t0);
-    hipLaunchKernelGGL(k_nms_init, g, t, 0, s, sc, t0, mask, n);
-    for (int it = 0; it < 2; ++it) {
-        hipLaunchKernelGGL(k_maxfilt<uint8_t>, g, t, 0, s, mask, u1, B, H, W, nms_radius, 0);
-        hipLaunchKernelGGL(k_maxfilt<uint8_t>, g, t, 0, s, (const uint8_t*)u1, u0, B, H, W, nms_radius, 1);
-        hipLaunchKernelGGL(k_nms_supp, g, t, 0, s, sc, u0, t0, n);   // t0 = supp_scores
-        hipLaunchKernelGGL(k_maxfilt<float>, g, t, 0, s, (const float*)t0, t1, B, H, W, nms_radius, 0);
-        float* mp = (float*)ckey;  // scratch (candidates are written later)
-        hipLaunchKernelGGL(k_maxfilt<float>, g, t, 0, s, (const float*)t1, mp, B, H, W, nms_radius, 1);
-        hipLaunchKernelGGL(k_nms_update, g, t, 0, s, t0, mp, u0, mask, n);
+    const float* nms_out = sc;
+    if (nms_radius == 4) {  // fused (SuperPoint's default radius)
+        hipLaunchKernelGGL(k_sp_nms, dim3((unsigned)((W + NMS_TW - 1) / NMS_TW), (unsigned)((H + NMS_TH - 1) / NMS_TH),
+                                          (unsigned)B),
+                           dim3(512), 0, s, sc, t0, B, H, W, border);
+        MLG_LAUNCH_CHECK();
+        nms_out = t0;
+    } else {  // multi-pass at full resolution
+        const long n = (long)B * H * W;
+        const dim3 g((unsigned)((n + 255) / 256)), t(256);
+        auto maxpool_f = [&](const float* in, float* out) {
+            hipLaunchKernelGGL(k_maxfilt<float>, g, t, 0, s, in, t1, B, H, W, nms_radius, 0);
+            hipLaunchKernelGGL(k_maxfilt<float>, g, t, 0, s, (const float*)t1, out, B, H, W, nms_radius, 1);
+        };
+        maxpool_f(sc, t0);
+        hipLaunchKernelGGL(k_nms_init, g, t, 0, s, sc, t0, mask, n);
+        for (int it = 0; it < 2; ++it) {
+            hipLaunchKernelGGL(k_maxfilt<uint8_t>, g, t, 0, s, mask, u1, B, H, W, nms_radius, 0);
+            hipLaunchKernelGGL(k_maxfilt<uint8_t>, g, t, 0, s, (const uint8_t*)u1, u0, B, H, W, nms_radius, 1);
+            hipLaunchKernelGGL(k_nms_supp, g, t, 0, s, sc, u0, t0, n);   // t0 = supp_scores
+            hipLaunchKernelGGL(k_maxfilt<float>, g, t, 0, s, (const float*)t0, t1, B, H, W, nms_radius, 0);
+            float* mp = (float*)ckey;  // scratch (candidates are written later)
+            hipLaunchKernelGGL(k_maxfilt<float>, g, t, 0, s, (const float*)t1, mp, B, H, W, nms_radius, 1);
+            hipLaunchKernelGGL(k_nms_update, g, t, 0, s, t0, mp, u0, mask, n);
+        }
+        hipLaunchKernelGGL(k_nms_final, g, t, 0, s, sc, mask, B, H, W, border);
+        MLG_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(k_nms_final, g, t, 0, s, sc, mask, B, H, W, border);
-    MLG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_sp_select, dim3(B), dim3(SEL_T), 0, s, sc, H, W, det_thr, max_kp, ckey, cidx, kpts, kscores,
+    hipLaunchKernelGGL(k_sp_select, dim3(B), dim3(SEL_T), 0, s, nms_out, H, W, det_thr, max_kp, ckey, cidx, kpts, kscores,
                        count);
     MLG_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_sp_desc, dim3((unsigned)(((long)B * max_kp + 3) / 4)), dim3(256), 0, s, dmap, w.b[10], B, h,
