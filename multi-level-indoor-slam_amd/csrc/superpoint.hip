@@ -48,28 +48,38 @@ __global__ __launch_bounds__(256) void k_sp_conv1a(const uint8_t* __restrict__ f
         g[i / HALO][i % HALO] = v;
     }
     __syncthreads();
-    const int ty = threadIdx.x / TS, tx = threadIdx.x % TS;
-    const int y = y0 + ty, x = x0 + tx;
-    if (y >= H || x >= W) return;
-    float nb[9];
+    // thread -> 8 output channels (chunk t & 7) of one pixel per pass, 32 pixels per pass
+    // in raster order of the tile: a wave-instruction stores 8 consecutive pixels' whole
+    // 128-B channel vectors (1 KiB contiguous) instead of 16 B of 64 pixels
+    const int ch = threadIdx.x & 7;
+    float wr[8][9], br[8];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) nb[k] = g[ty + k / 3][tx + k % 3];
-    bf16_t* o = out + (((size_t)bz * H + y) * W + x) * 64;
+    for (int j = 0; j < 8; ++j) {
+        br[j] = sw[576 + 8 * ch + j];
 #pragma unroll
-    for (int c0 = 0; c0 < 64; c0 += 8) {
+        for (int k = 0; k < 9; ++k) wr[j][k] = sw[(8 * ch + j) * 9 + k];
+    }
+#pragma unroll 2
+    for (int pass = 0; pass < TS * TS / 32; ++pass) {
+        const int p = pass * 32 + (threadIdx.x >> 3), ty = p / TS, tx = p % TS;
+        const int y = y0 + ty, x = x0 + tx;
+        if (y >= H || x >= W) continue;
+        float nb[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) nb[k] = g[ty + k / 3][tx + k % 3];
         uint32_t pk[4];
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
-            float a0 = sw[576 + c0 + j], a1 = sw[576 + c0 + j + 1];
             float s0 = 0.f, s1 = 0.f;
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
-                s0 += sw[(c0 + j) * 9 + k] * nb[k];
-                s1 += sw[(c0 + j + 1) * 9 + k] * nb[k];
+                s0 += wr[j][k] * nb[k];
+                s1 += wr[j + 1][k] * nb[k];
             }
-            pk[j / 2] = pack_bf16x2(fmaxf(s0 + a0, 0.f), fmaxf(s1 + a1, 0.f));
+            pk[j / 2] = pack_bf16x2(fmaxf(s0 + br[j], 0.f), fmaxf(s1 + br[j + 1], 0.f));
         }
-        *reinterpret_cast<uint4*>(o + c0) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        *reinterpret_cast<uint4*>(out + (((size_t)bz * H + y) * W + x) * 64 + 8 * ch) =
+            make_uint4(pk[0], pk[1], pk[2], pk[3]);
     }
 }
 
