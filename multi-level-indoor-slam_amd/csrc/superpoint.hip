@@ -93,6 +93,8 @@ __global__ __launch_bounds__(512) void k_conv3x3(const bf16_t* __restrict__ in, 
     constexpr int NT = COUT_T / 16;       // N-tiles (output channels) per wave
     constexpr int STEPS = 9 * (CIN / KC);
     constexpr int HALO_BYTES = HALO * HALO * HS;
+    static_assert(POOL || TS * TS * COUT_T * 2 <= HALO_BYTES + 2 * COUT_T * (KC * 2 + 16),
+                  "output staging must fit in the (dead) halo + weight buffers");
     constexpr int B_BYTES = COUT_T * BS;
     __shared__ __attribute__((aligned(16))) char smem[HALO_BYTES + 2 * B_BYTES];
     char* sh = smem;
@@ -203,17 +205,28 @@ __global__ __launch_bounds__(512) void k_conv3x3(const bf16_t* __restrict__ in, 
                 o.y = pack_bf16x2(m[2], m[3]);
                 *reinterpret_cast<uint2*>(out + (((size_t)bz * (H / 2) + py) * (W / 2) + px) * Cout + c) = o;
             }
-        } else {
+        } else {  // stage the tile [256 px][COUT_T] (chunk c ^ (px & 7)) over the dead halo / weights
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
-                const int y = y0 + 2 * wave + r;
-                if (y < H && x < W) {
-                    uint2 o;
-                    o.x = pack_bf16x2(v[r][0], v[r][1]);
-                    o.y = pack_bf16x2(v[r][2], v[r][3]);
-                    *reinterpret_cast<uint2*>(out + (((size_t)bz * H + y) * W + x) * Cout + c) = o;
-                }
+                const int p = (2 * wave + r) * TS + col, cc = 2 * n + (kg >> 1);
+                uint2 o;
+                o.x = pack_bf16x2(v[r][0], v[r][1]);
+                o.y = pack_bf16x2(v[r][2], v[r][3]);
+                *reinterpret_cast<uint2*>(sh + p * (COUT_T * 2) + ((cc ^ (p & 7)) << 4) + 8 * (kg & 1)) = o;
             }
+        }
+    }
+    if (!POOL) {  // each pixel's COUT_T channels as whole 16-B chunks: a wave-instruction
+                  // stores 1 KiB of consecutive pixels' contiguous channel runs
+        __syncthreads();
+        constexpr int CPX = COUT_T / 8;  // 16-B chunks per pixel
+#pragma unroll
+        for (int it = 0; it < TS * TS * CPX / 512; ++it) {
+            const int L = it * 512 + tid, p = L / CPX, cc = L % CPX;
+            const int y = y0 + p / TS, xx = x0 + p % TS;
+            if (y < H && xx < W)
+                *reinterpret_cast<uint4*>(out + (((size_t)bz * H + y) * W + xx) * Cout + n0 + 8 * cc) =
+                    *reinterpret_cast<const uint4*>(sh + p * (COUT_T * 2) + ((cc ^ (p & 7)) << 4));
         }
     }
 }
