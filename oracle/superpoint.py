@@ -113,7 +113,7 @@ def detect(scores, desc, max_kp=2048, det_thr=0.001, nms_radius=4, border=4):
     return out
 
 
-def superpoint(sd, images_bgr, max_kp=2048, det_thr=0.001, emulate_bf16=True):
+def superpoint(sd, images_bgr, max_kp=2048, det_thr=0.001, emulate_bf16=True, nms_radius=4):
     gray = np.stack([bgr_to_gray_u8(im) for im in images_bgr]).astype(np.float32) / 255.0
     sc, desc = dense_maps(sd, torch.from_numpy(gray)[:, None], emulate_bf16)
-    return detect(sc, desc, max_kp, det_thr)
+    return detect(sc, desc, max_kp, det_thr, nms_radius)

@@ -97,3 +97,17 @@ def test_superpoint_gray_input_and_errors(dev, sd):
     assert np.array_equal(a["keypoints"], b["keypoints"])
     with pytest.raises(ValueError):
         sp.extract([np.zeros((60, 60, 3), np.uint8)])
+
+
+@pytest.mark.parametrize("h,w,nms", [(200, 344, 4), (200, 344, 3)])
+def test_superpoint_partial_tiles_and_radius(dev, sd, h, w, nms):
+    """Frame sizes that are not multiples of the fused NMS tile (32 x 64, with its 20-px
+    halo crossing the image border) and a non-default radius (the multi-pass path)."""
+    rng = np.random.default_rng(7)
+    imgs = [scene(rng, h, w)]
+    sp = SuperPointGPU(sd, device=str(dev), nms_radius=nms)
+    got = sp.extract(imgs)
+    ref = osp.superpoint(sd, imgs, max_kp=2048, det_thr=0.001, nms_radius=nms)
+    for g, o in zip(got, ref):
+        assert len(g["keypoints"]) == len(o["keypoints"])
+        _compare(g, o)
