@@ -247,7 +247,7 @@ def main():
     # ViT layer (3 / 9 / 12 N-tiles) then fill 256 CUs in whole waves (99.6 %).
     ap.add_argument("--batch", type=int, default=123)
     ap.add_argument("--sp-batch", type=int, default=64)
-    ap.add_argument("--lg-chunk", type=int, default=256)
+    ap.add_argument("--lg-chunk", type=int, default=1024)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--places", type=int, default=600)
     ap.add_argument("--verify", choices=["all", "none"], default="all")

@@ -39,7 +39,7 @@ def main():
         res[slot] = {"kernel": pat.rstrip("("), "dispatches": len(fetch), "fetch_bytes_per_launch": round(fb),
                      "write_bytes_per_launch": round(wb), "bytes_per_launch": round(fb + wb),
                      "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of "
-                               "tools/lg_bench.py --iters 1 (one 256-pair LightGlue call = bench.py's "
+                               "tools/lg_bench.py --iters 1 --pairs 1024 (one 1024-pair LightGlue call = bench.py's "
                                "lg_chunk); FETCH_SIZE x2 (gfx950)"}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
