@@ -200,11 +200,19 @@ __global__ void k_lg_live(const Seg* __restrict__ segs, int nseg, uint8_t* __res
                           int* __restrict__ rowseg, int Npad) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= Npad) return;
-    int sgi = -1;
-    for (int s = 0; s < nseg; ++s) {
-        const Seg sg = segs[s];
-        if (r >= sg.off && r < sg.off + sg.len) sgi = s;
+    // segments are in increasing offset order: binary search for the last one starting
+    // at or before r (a linear scan over every segment per row was quadratic)
+    int lo = 0, hi = nseg - 1, sgi = -1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        if (segs[mid].off <= r) {
+            sgi = mid;
+            lo = mid + 1;
+        } else {
+            hi = mid - 1;
+        }
     }
+    if (sgi >= 0 && r >= segs[sgi].off + segs[sgi].len) sgi = -1;
     live[r] = sgi >= 0;
     rowseg[r] = sgi;
 }
