@@ -12,18 +12,32 @@
 //             solver, error max(d1^2, d2^2) of the two point-to-epiline distances in
 //             pixels; 7 points: the 7-point model directly; 8..14 points: LMedS (as
 //             OpenCV does below 15 points); fewer than 7: no model.
-// OpenCV draws hypotheses adaptively from its own RNG; here a fixed budget of H
-// hypotheses per pair (counter-based RNG, seeded) is solved and scored in parallel
-// and the best model is the one with the most inliers (lowest hypothesis index on
-// ties), so results are deterministic.  Parity is on decisions.
+// RANSAC follows OpenCV's RANSACPointSetRegistrator::run (calib3d/ptsetreg.cpp) step
+// for step, restated so its sequential control flow runs in parallel:
+//   * the minimal samples are OpenCV's: cv::RNG((uint64)-1) (multiply-with-carry,
+//     coefficient 4164903690), getSubset's duplicate redraw and, for F, checkSubset's
+//     collinearity test (haveCollinearPoints, FLT_EPSILON) -- one thread per pair
+//     replays the RNG stream and writes the H = maxIters subsets;
+//   * every subset is solved and scored in parallel (one thread per hypothesis);
+//   * one thread per pair then scans the hypotheses in iteration order exactly as
+//     the sequential loop would: a model replaces the best iff its inlier count
+//     exceeds max(best, modelPoints - 1), and each replacement shrinks the iteration
+//     budget by RANSACUpdateNumIters(0.999, outlier ratio, modelPoints, niters), so
+//     hypotheses past the adaptive stop are ignored;
+//   * no model when no count exceeded modelPoints - 1 (OpenCV's maxGoodCount == 0).
+// The inlier count therefore equals OpenCV's for the same matches; only the order of
+// several solutions of one sample (solver-specific) can pick a different model among
+// equal counts.  LMedS (F, 8..14 matches) keeps a seeded counter-based sample stream.
 //
 // Pipeline (one pair = one segment of the flat match arrays):
-//   k_ransac_prep   : normalised double coordinates (+ Hartley transforms for F)
-//   k_ransac_hyp    : one thread per hypothesis: sample, solve (<= 10 models)
-//   k_ransac_score  : one thread per hypothesis: inlier count (or LMedS median) of
-//                     each model over the pair's points, staged in LDS
-//   k_ransac_select : one workgroup per pair: best model, inlier mask
-//   k_recover_pose  : one workgroup per pair: E -> [R|t] by cheirality on the inliers
+//   k_ransac_prep    : normalised double coordinates (+ Hartley transforms for F)
+//   k_ransac_subsets : one thread per pair: OpenCV's sample stream
+//   k_ransac_hyp     : one thread per hypothesis: solve (<= 10 models)
+//   k_ransac_score   : one thread per hypothesis: inlier count (or LMedS median) of
+//                      each model over the pair's points, staged in LDS
+//   k_ransac_select  : one workgroup per pair: OpenCV's sequential best-model scan,
+//                      inlier mask
+//   k_recover_pose   : one workgroup per pair: E -> [R|t] by cheirality on the inliers
 #include "common.h"
 #include "kernels.h"
 
@@ -465,6 +479,46 @@ RS_HD __forceinline__ uint64_t splitmix(uint64_t x) {
     return x ^ (x >> 31);
 }
 
+// cv::RNG (core/include/opencv2/core/operations.hpp): state' = (uint32)state * 4164903690
+// + (state >> 32); next() = (uint32)state'; uniform(a, b) = next() % (b - a) + a.
+struct CvRng {
+    uint64_t state;
+    RS_HD unsigned next() {
+        state = (uint64_t)(unsigned)state * 4164903690ull + (unsigned)(state >> 32);
+        return (unsigned)state;
+    }
+    RS_HD int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a)) + a; }
+};
+
+constexpr double RANSAC_CONFIDENCE = 0.999;  // findEssentialMat / findFundamentalMat prob
+constexpr int RANSAC_MAX_ATTEMPTS = 10000;   // getSubset(..., maxAttempts) in run()
+
+// RANSACUpdateNumIters (ptsetreg.cpp); cvRound = round half to even
+RS_HD int ransac_update_iters(double p, double ep, int model_points, int max_iters) {
+    p = fmin(fmax(p, 0.0), 1.0);
+    ep = fmin(fmax(ep, 0.0), 1.0);
+    double num = fmax(1.0 - p, 2.2250738585072014e-308);
+    double denom = 1.0 - pow(1.0 - ep, model_points);
+    if (denom < 2.2250738585072014e-308) return 0;
+    num = log(num);
+    denom = log(denom);
+    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
+}
+
+// haveCollinearPoints (fundam.cpp) for the last of `count` selected points
+RS_HD bool collinear_last(const float (*pt)[2], int count) {
+    const int i = count - 1;
+    for (int j = 0; j < i; ++j) {
+        const double dx1 = (double)(pt[j][0] - pt[i][0]), dy1 = (double)(pt[j][1] - pt[i][1]);
+        for (int k = 0; k < j; ++k) {
+            const double dx2 = (double)(pt[k][0] - pt[i][0]), dy2 = (double)(pt[k][1] - pt[i][1]);
+            if (fabs(dx2 * dy1 - dy2 * dx1) <= 1.1920928955078125e-07 * (fabs(dx1) + fabs(dy1) + fabs(dx2) + fabs(dy2)))
+                return true;
+        }
+    }
+    return false;
+}
+
 // per-pair parameters in workspace
 struct PairInfo {
     int start, count, mode;  // mode: 0 none, 1 E RANSAC, 2 F RANSAC, 3 F LMedS, 4 F direct (7 pts), 5 E direct (5 pts)
@@ -567,8 +621,54 @@ RS_HD void denorm_F(const double* Fn, const double* T1, const double* T2, double
     for (int k = 0; k < 9; ++k) F[k] *= nrm;
 }
 
+// OpenCV's sample stream for pair p (modes 1 / 2): subsets of iterations 0..nsub-1.
+// getSubset: draw modelPoints indices with cv::RNG, redrawing duplicates; for F the
+// whole subset is redrawn while checkSubset (collinear points in either image) fails,
+// up to 10000 attempts; an iteration whose getSubset fails ends the loop.
+__global__ __launch_bounds__(64) void k_ransac_subsets(const PairInfo* __restrict__ info, int P, int H,
+                                                       const float* __restrict__ kp1, const float* __restrict__ kp2,
+                                                       int32_t* __restrict__ subsets, int32_t* __restrict__ nsub) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const PairInfo pi = info[p];
+    if (pi.mode != 1 && pi.mode != 2) {
+        nsub[p] = 0;
+        return;
+    }
+    const int m = pi.mode == 1 ? 5 : 7;
+    CvRng rng{~0ull};
+    int32_t* out = subsets + (size_t)p * H * 7;
+    int it = 0;
+    for (; it < H; ++it) {
+        int idx[7];
+        float a[7][2], b[7][2];
+        int iters = 0, i = 0;
+        for (; iters < RANSAC_MAX_ATTEMPTS; ++iters) {
+            for (i = 0; i < m;) {
+                int v;
+                for (;;) {
+                    v = idx[i] = rng.uniform(0, pi.count);
+                    int j = 0;
+                    for (; j < i; ++j)
+                        if (v == idx[j]) break;
+                    if (j == i) break;
+                }
+                a[i][0] = kp1[2 * (pi.start + v)]; a[i][1] = kp1[2 * (pi.start + v) + 1];
+                b[i][0] = kp2[2 * (pi.start + v)]; b[i][1] = kp2[2 * (pi.start + v) + 1];
+                ++i;
+            }
+            if (m == 7 && (collinear_last(a, 7) || collinear_last(b, 7))) continue;
+            break;
+        }
+        if (!(i == m && iters < RANSAC_MAX_ATTEMPTS)) break;
+        for (int j = 0; j < m; ++j) out[it * 7 + j] = idx[j];
+    }
+    nsub[p] = it;
+}
+
 __global__ __launch_bounds__(64) void k_ransac_hyp(const PairInfo* __restrict__ info, const double4* __restrict__ ptsn,
-                                                   int H, uint64_t seed, double* __restrict__ models,
+                                                   int H, uint64_t seed, const int32_t* __restrict__ subsets,
+                                                   const int32_t* __restrict__ nsub, double* __restrict__ models,
                                                    int8_t* __restrict__ nsol) {
     const int p = blockIdx.y;
     const int h = blockIdx.x * blockDim.x + threadIdx.x;
@@ -587,6 +687,12 @@ __global__ __launch_bounds__(64) void k_ransac_hyp(const PairInfo* __restrict__ 
     uint64_t st = splitmix(seed ^ (uint64_t)h * 0x632BE59BD9B4E019ull);
     if (direct) {
         for (int i = 0; i < m; ++i) idx[i] = i;
+    } else if (pi.mode == 1 || pi.mode == 2) {
+        if (h >= nsub[p]) {
+            nsol[(size_t)p * H + h] = 0;
+            return;
+        }
+        for (int i = 0; i < m; ++i) idx[i] = subsets[((size_t)p * H + h) * 7 + i];
     } else {
         for (int i = 0; i < m; ++i) {
             int v;
@@ -852,7 +958,8 @@ __global__ __launch_bounds__(256) void k_ransac_select(const PairInfo* __restric
                                                        const double4* __restrict__ ptsn,
                                                        const double4* __restrict__ ptsr, int H,
                                                        const double* __restrict__ models,
-                                                       const float* __restrict__ score, double* __restrict__ model_out,
+                                                       const float* __restrict__ score, const int8_t* __restrict__ nsol,
+                                                       const int32_t* __restrict__ nsub, double* __restrict__ model_out,
                                                        uint8_t* __restrict__ mask, int32_t* __restrict__ inliers,
                                                        int32_t* __restrict__ status) {
     const int p = blockIdx.x, tid = threadIdx.x;
@@ -862,22 +969,46 @@ __global__ __launch_bounds__(256) void k_ransac_select(const PairInfo* __restric
     __shared__ double Mb[9];
     __shared__ int cnt_sh;
     const int total = H * MAXSOL;
-    float best = -INFINITY;
-    int bidx = 0x7fffffff;
-    for (int i = tid; i < total; i += 256) {
-        const float v = score[(size_t)p * total + i];
-        if (v > best || (v == best && i < bidx)) { best = v; bidx = i; }
-    }
-    bs[tid] = best;
-    bi[tid] = bidx;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (tid < o) {
-            const float v = bs[tid + o];
-            const int ii = bi[tid + o];
-            if (v > bs[tid] || (v == bs[tid] && ii < bi[tid])) { bs[tid] = v; bi[tid] = ii; }
+    if (pi.mode == 1 || pi.mode == 2) {
+        // OpenCV's sequential loop over iterations 0 .. niters-1 (niters shrinks as better
+        // models arrive); one thread: at most H * MAXSOL comparisons
+        if (tid == 0) {
+            const int mp = pi.mode == 1 ? 5 : 7;
+            const int ns_it = nsub[p];
+            int niters = H, max_good = 0, bidx = -1;
+            for (int it = 0; it < niters && it < ns_it; ++it) {
+                const int ns = nsol[(size_t)p * H + it];
+                for (int s = 0; s < ns; ++s) {
+                    const int g = (int)score[(size_t)p * total + it * MAXSOL + s];
+                    if (g > max(max_good, mp - 1)) {
+                        max_good = g;
+                        bidx = it * MAXSOL + s;
+                        niters = ransac_update_iters(RANSAC_CONFIDENCE, (double)(pi.count - g) / pi.count, mp, niters);
+                    }
+                }
+            }
+            bs[0] = bidx >= 0 ? (float)max_good : -INFINITY;
+            bi[0] = bidx >= 0 ? bidx : 0;
         }
         __syncthreads();
+    } else {
+        float best = -INFINITY;
+        int bidx = 0x7fffffff;
+        for (int i = tid; i < total; i += 256) {
+            const float v = score[(size_t)p * total + i];
+            if (v > best || (v == best && i < bidx)) { best = v; bidx = i; }
+        }
+        bs[tid] = best;
+        bi[tid] = bidx;
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if (tid < o) {
+                const float v = bs[tid + o];
+                const int ii = bi[tid + o];
+                if (v > bs[tid] || (v == bs[tid] && ii < bi[tid])) { bs[tid] = v; bi[tid] = ii; }
+            }
+            __syncthreads();
+        }
     }
     const bool have = pi.mode != 0 && bs[0] > -INFINITY;
     if (!have) {
@@ -991,7 +1122,7 @@ __global__ __launch_bounds__(256) void k_recover_pose(const float* __restrict__ 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct RsLayout {
-    size_t info, ptsn, ptsr, models, nsol, score, total;
+    size_t info, ptsn, ptsr, models, nsol, score, subsets, nsub, total;
 };
 
 RsLayout rs_layout(int P, long S_total, int H) {
@@ -1002,7 +1133,9 @@ RsLayout rs_layout(int P, long S_total, int H) {
     L.models = L.ptsr + align256(sizeof(double4) * (size_t)S_total);
     L.nsol = L.models + align256(sizeof(double) * 9 * MAXSOL * (size_t)P * H);
     L.score = L.nsol + align256((size_t)P * H);
-    L.total = L.score + align256(sizeof(float) * MAXSOL * (size_t)P * H);
+    L.subsets = L.score + align256(sizeof(float) * MAXSOL * (size_t)P * H);
+    L.nsub = L.subsets + align256(sizeof(int32_t) * 7 * (size_t)P * H);
+    L.total = L.nsub + align256(sizeof(int32_t) * (size_t)P);
     return L;
 }
 
@@ -1026,15 +1159,20 @@ int mlg_ransac_run(const float* kp1, const float* kp2, const int32_t* offs, int 
     double* models = (double*)(w + L.models);
     int8_t* nsol = (int8_t*)(w + L.nsol);
     float* score = (float*)(w + L.score);
+    int32_t* subsets = (int32_t*)(w + L.subsets);
+    int32_t* nsub = (int32_t*)(w + L.nsub);
     hipLaunchKernelGGL(k_ransac_prep, dim3(P), dim3(256), 0, s, kp1, kp2, offs, K, k_stride, thr, info, ptsn, ptsr);
     MLG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ransac_hyp, dim3((H + 63) / 64, P), dim3(64), 0, s, info, ptsn, H, seed, models, nsol);
+    hipLaunchKernelGGL(k_ransac_subsets, dim3((P + 63) / 64), dim3(64), 0, s, info, P, H, kp1, kp2, subsets, nsub);
+    MLG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ransac_hyp, dim3((H + 63) / 64, P), dim3(64), 0, s, info, ptsn, H, seed, subsets, nsub,
+                       models, nsol);
     MLG_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_ransac_score, dim3((H + 255) / 256, P), dim3(256), 0, s, info, ptsn, ptsr, H, models, nsol,
                        score);
     MLG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ransac_select, dim3(P), dim3(256), 0, s, info, ptsn, ptsr, H, models, score, model_out, mask,
-                       inliers, status);
+    hipLaunchKernelGGL(k_ransac_select, dim3(P), dim3(256), 0, s, info, ptsn, ptsr, H, models, score, nsol, nsub, model_out,
+                       mask, inliers, status);
     MLG_LAUNCH_CHECK();
     if (pose && K) {
         hipLaunchKernelGGL(k_recover_pose, dim3(P), dim3(256), 0, s, kp1, kp2, offs, K, k_stride, model_out, mask, pose,

@@ -1,7 +1,13 @@
-"""ctypes binding of libmlgate.so -- the C ABI declared in include/mlgate.h.
+"""Bindings of the native libraries.
 
-The library is the only compute path of this package: there is no CPU or eager
-PyTorch fallback.  ``lib()`` raises if the shared object is missing, and
+  * ``ops()`` -- the PyTorch-ROCm custom operators ``torch.ops.mlgate.*``
+    (libmlgate_torch.so, csrc/torch_ops.cpp: TORCH_LIBRARY(mlgate) over the C ABI).
+    Every compute call of the mlgate package goes through them.
+  * ``lib()`` -- ctypes view of libmlgate.so, the C ABI declared in include/mlgate.h,
+    kept for the op-level kernel tests and the ABI export checks.
+
+The libraries are the only compute path of this package: there is no CPU or eager
+PyTorch fallback.  ``ops()`` / ``lib()`` raise if a shared object is missing, and
 ``require_device()`` raises if no HIP device is visible.
 """
 import ctypes
@@ -9,6 +15,10 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmlgate.so")
+TORCH_LIB_PATH = os.path.join(_HERE, "libmlgate_torch.so")
+OPS = ("vit_forward_into", "knn_gate", "knn_query", "row_normalize", "similarity", "xcorr_score", "superpoint",
+       "lightglue", "ransac_epipolar", "recover_pose", "resnet50", "pillow_resize_224", "plane_ransac", "proximity",
+       "prof_enable", "prof_reset", "prof_read")
 # A/B tooling only (tools/*_bench.py): load another build of the same library
 _LIB_OVERRIDE = os.environ.get("MLGATE_LIB_AB")
 if _LIB_OVERRIDE:
@@ -81,6 +91,7 @@ EXPORTS = {
 }
 
 _lib = None
+_ops = None
 
 
 class MlgateError(RuntimeError):
@@ -105,6 +116,20 @@ def lib():
     return _lib
 
 
+def ops():
+    """torch.ops.mlgate, after loading libmlgate_torch.so (built by __graft_entry__.build)."""
+    global _ops
+    if _ops is None:
+        import torch
+        if not os.path.exists(TORCH_LIB_PATH):
+            raise MlgateError(f"{TORCH_LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                              "g.build()'`")
+        lib()  # the C ABI library the operators link against
+        torch.ops.load_library(TORCH_LIB_PATH)
+        _ops = torch.ops.mlgate
+    return _ops
+
+
 def check(rc, what=""):
     if rc != 0:
         msg = lib().mlg_strerror(rc).decode()
@@ -120,7 +145,7 @@ def require_device(device="cuda"):
                           "Use device='cuda' (PyTorch-ROCm's name for the HIP device).")
     if not torch.cuda.is_available():
         raise MlgateError("no HIP device visible: mlgate's kernels need an MI355X (gfx950)")
-    lib()
+    ops()
     return dev
 
 

@@ -54,9 +54,12 @@ class SemanticLoopClosureGate:
         return c
 
     def decide(self, query_idx, match_idx) -> np.ndarray:
-        """Vectorised verdicts (True = accept) for index arrays; does not touch the stats."""
+        """Vectorised verdicts (True = accept) for index arrays; does not touch the stats.
+        Computed as the negation of the reference's rejection test |qf - mf| > limit, so a
+        NaN label (which never satisfies it) is accepted, as in gate_candidate."""
         f = np.asarray(self.floor_labels)
-        return np.abs(f[np.asarray(query_idx)] - f[np.asarray(match_idx)]) <= self._limit()
+        with np.errstate(invalid='ignore'):
+            return ~(np.abs(f[np.asarray(query_idx)] - f[np.asarray(match_idx)]) > self._limit())
 
     def gate_candidates(self, candidates: List[Tuple[int, int, float]]) -> Tuple[List, List]:
         if len(candidates) == 0:

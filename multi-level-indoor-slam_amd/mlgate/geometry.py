@@ -13,7 +13,7 @@ import torch
 
 from . import _native
 
-DEFAULT_HYPOTHESES = 1024
+DEFAULT_HYPOTHESES = 1000  # OpenCV's maxIters for findEssentialMat / findFundamentalMat
 
 
 @dataclass
@@ -54,27 +54,10 @@ def epipolar_ransac_device(k1, k2, offs, K=None, k_stride=0, threshold=3.0, hypo
     Returns device tensors (model [P, 9] f64, mask [S] u8, inliers [P] i32, pose [P, 16] f64 or None,
     status [P] i32).
     """
-    P = int(offs.numel()) - 1
-    S = int(k1.shape[0])
-    dev = k1.device
-    L = _native.lib()
-    nbytes = L.mlg_ransac_workspace_bytes(P, S, int(hypotheses))
-    if nbytes == 0:
-        raise ValueError(f"bad RANSAC shape (pairs {P}, matches {S}, hypotheses {hypotheses})")
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    model = torch.empty(P, 9, dtype=torch.float64, device=dev)
-    mask = torch.empty(max(S, 1), dtype=torch.uint8, device=dev)
-    inl = torch.empty(P, dtype=torch.int32, device=dev)
-    status = torch.empty(P, dtype=torch.int32, device=dev)
-    pose = torch.empty(P, 16, dtype=torch.float64, device=dev) if (with_pose and K is not None) else None
-    rc = L.mlg_ransac_epipolar(_native.ptr(k1), _native.ptr(k2), _native.ptr(offs), P, S,
-                               _native.ptr(K) if K is not None else None, int(k_stride), float(threshold),
-                               int(hypotheses), int(seed) & ((1 << 64) - 1), _native.ptr(ws), nbytes,
-                               _native.ptr(model), _native.ptr(mask), _native.ptr(inl),
-                               _native.ptr(pose) if pose is not None else None, _native.ptr(status),
-                               _native.stream_of(dev))
-    _native.check(rc, "mlg_ransac_epipolar")
-    return model, mask[:S], inl, pose, status
+    model, mask, inl, pose, status = _native.ops().ransac_epipolar(
+        k1.contiguous(), k2.contiguous(), offs.contiguous(), K, int(k_stride), float(threshold), int(hypotheses),
+        int(seed) & ((1 << 63) - 1), bool(with_pose))
+    return model, mask, inl, (pose if pose.numel() else None), status
 
 
 def epipolar_ransac(pairs_k1: Sequence[np.ndarray], pairs_k2: Sequence[np.ndarray], K=None, threshold: float = 3.0,
@@ -113,13 +96,8 @@ def recover_pose(kpts1, kpts2, K, inlier_mask, E, device: str = "cuda") -> Optio
         return None
     dev = _native.require_device(device)
     k1, k2, offs = _flat([kpts1], [kpts2])
-    # keep every device buffer referenced until the launch has been queued and synced
-    bufs = [torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-            for a in (k1, k2, offs, np.asarray(K, np.float64).reshape(9), np.asarray(E, np.float64).reshape(9),
-                      mask.astype(np.uint8))]
-    pose = torch.empty(1, 16, dtype=torch.float64, device=dev)
-    rc = _native.lib().mlg_recover_pose(_native.ptr(bufs[0]), _native.ptr(bufs[1]), _native.ptr(bufs[2]), 1,
-                                        _native.ptr(bufs[3]), 0, _native.ptr(bufs[4]), _native.ptr(bufs[5]),
-                                        _native.ptr(pose), _native.stream_of(dev))
-    _native.check(rc, "mlg_recover_pose")
-    return pose.cpu().numpy().reshape(4, 4)
+    k1, k2, offs = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (k1, k2, offs))
+    K = torch.from_numpy(np.asarray(K, np.float64).reshape(9).copy()).to(dev)
+    E = torch.from_numpy(np.asarray(E, np.float64).reshape(9).copy()).to(dev)
+    m = torch.from_numpy(mask.astype(np.uint8)).to(dev)
+    return _native.ops().recover_pose(k1, k2, offs, K, 0, E, m).cpu().numpy().reshape(4, 4)

@@ -36,17 +36,8 @@ class FloorEstimate:
 def ground_plane_ransac_device(pts, offs, iterations, threshold, seed=0):
     """pts device f32 [N, 3], offs device int32 [S + 1] -> device (plane f64 [S, 4], ratio f64 [S],
     inliers int32 [S])."""
-    S = int(offs.numel()) - 1
-    dev = pts.device
-    L = _native.lib()
-    nb = L.mlg_plane_ransac_workspace_bytes(S, int(iterations))
-    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
-    plane = torch.empty(S, 4, dtype=torch.float64, device=dev)
-    ratio = torch.empty(S, dtype=torch.float64, device=dev)
-    inl = torch.empty(S, dtype=torch.int32, device=dev)
-    _native.check(L.mlg_plane_ransac(_native.ptr(pts), _native.ptr(offs), S, int(iterations), int(seed), float(threshold),
-                                     _native.ptr(ws), nb, _native.ptr(plane), _native.ptr(ratio), _native.ptr(inl),
-                                     _native.stream_of(dev)), "mlg_plane_ransac")
+    plane, ratio, inl = _native.ops().plane_ransac(pts.contiguous(), offs.contiguous(), int(iterations),
+                                                   int(seed) & ((1 << 63) - 1), float(threshold))
     return plane, ratio, inl
 
 

@@ -1,0 +1,284 @@
+"""The full semantic loop-closure gate (BASELINE configs[3]).
+
+No reference module chains the gate's stages; SURVEY.md §3.5 defines the harness from
+the reference's public APIs, and this module is that harness:
+
+  1. floor labels  IMUFloorDetector.detect_elevator_events / assign_floor_labels
+                   (floor_detector.py:63-156), or labels given per keyframe;
+  2. descriptors   SemanticPlaceRecognition('cricavpr').add_image per keyframe
+                   (place_recognition.py:843-849; here one batched add_images);
+  3. retrieval     find_loop_closures(enable_floor_gating, k) (:851-911);
+  4. verification  SemanticGeometricVerifier.verify_with_semantics on every retrieved
+                   match with is_valid (geometric_verification.py:688-734; batched);
+  5. gate          SemanticLoopClosureGate(floor_labels).gate_candidates on the
+                   geometrically valid pairs (loop_closure_gate.py:105-126).
+
+The false-loop-closure rejection count is the sum of four terms:
+retrieval matches with PlaceMatch.is_valid False (place_recognition.py:896-899),
+verifier skips on a floor mismatch (geometric_verification.py:709-710), verifier
+invalid results (:729-732) and the gate's rejected_cross_floor (loop_closure_gate.py:
+91-98).
+
+Two front ends run the same kernels:
+  * ``FullSemanticGate`` composes the drop-in classes (PlaceMatch / MatchResult /
+    LoopClosureCandidate objects, the reference's stats dicts);
+  * ``DeviceGate`` is the same chain on device arrays, frame-sharded over ranks (one
+    process per GPU, RCCL all-gathers; bench.py's step).  Its decisions and counts are
+    those of FullSemanticGate (tests/test_pipeline_gpu.py).
+"""
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from .floors import IMUFloorDetector
+from .gate import LoopClosureCandidate, SemanticLoopClosureGate
+from .verify import MatchResult, SemanticGeometricVerifier
+from .vpr import PlaceMatch, SemanticPlaceRecognition
+
+
+@dataclass
+class RejectionCount:
+    """The four terms of the false-loop-closure rejection count."""
+    retrieval_floor_rejected: int = 0   # PlaceMatch.is_valid == False
+    skipped_floor_mismatch: int = 0     # SemanticGeometricVerifier skip branch
+    verifier_invalid: int = 0           # geometric verification failed
+    gate_rejected_cross_floor: int = 0  # SemanticLoopClosureGate rejections
+
+    @property
+    def total(self) -> int:
+        return (self.retrieval_floor_rejected + self.skipped_floor_mismatch + self.verifier_invalid
+                + self.gate_rejected_cross_floor)
+
+    def as_dict(self) -> Dict[str, int]:
+        return {'retrieval_floor_rejected': self.retrieval_floor_rejected,
+                'skipped_floor_mismatch': self.skipped_floor_mismatch,
+                'verifier_invalid': self.verifier_invalid,
+                'gate_rejected_cross_floor': self.gate_rejected_cross_floor, 'total': self.total}
+
+
+@dataclass
+class GateReport:
+    floor_labels: np.ndarray
+    events: list
+    matches: List[PlaceMatch]
+    verified: List[PlaceMatch]          # matches sent to the verifier, in emission order
+    results: List[MatchResult]          # one per verified match
+    accepted: List[LoopClosureCandidate]
+    rejected: List[LoopClosureCandidate]
+    retrieval_stats: Dict
+    verifier_stats: Dict
+    gate_stats: Dict
+    rejections: RejectionCount = field(default_factory=RejectionCount)
+
+
+def floor_labels_from_imu(timestamps, imu, start_floor=5, detector_kwargs=None):
+    """(labels, events) from an IMU log (t, ax, ay, az) -- floor_detector.py:63-156."""
+    det = IMUFloorDetector(**(detector_kwargs or {}))
+    t, ax, ay, az = imu[:4]
+    events = det.detect_elevator_events(np.asarray(t), np.asarray(ax), np.asarray(ay), np.asarray(az))
+    return det.assign_floor_labels(np.asarray(timestamps), start_floor=start_floor), events
+
+
+class FullSemanticGate:
+    """IMU floors -> CricaVPR descriptors -> floor-gated kNN -> semantic geometric
+    verification -> floor gate, composed from the drop-in API."""
+
+    def __init__(self, vpr_method: str = 'cricavpr', matcher_type: str = 'lightglue', device: str = 'cuda',
+                 similarity_threshold: float = 0.5, min_time_gap: float = 10.0, k: int = 10, min_inliers: int = 20,
+                 min_inlier_ratio: float = 0.25, strict_mode: bool = True, retrieval_floor_gating: bool = True,
+                 verifier_floor_gating: bool = True, verify_rejected: bool = False, start_floor: int = 5,
+                 imu_detector_kwargs: Optional[Dict] = None):
+        self.vpr_method, self.matcher_type, self.device = vpr_method, matcher_type, device
+        self.similarity_threshold, self.min_time_gap, self.k = similarity_threshold, min_time_gap, k
+        self.min_inliers, self.min_inlier_ratio, self.strict_mode = min_inliers, min_inlier_ratio, strict_mode
+        self.retrieval_floor_gating = retrieval_floor_gating
+        self.verifier_floor_gating = verifier_floor_gating
+        self.verify_rejected = verify_rejected  # also send is_valid == False matches to the verifier
+        self.start_floor = start_floor
+        self.imu_detector_kwargs = imu_detector_kwargs
+        self.spr = None
+        self.verifier = None
+        self.gate = None
+
+    def run(self, images, timestamps, K: Optional[np.ndarray] = None, floor_labels=None, imu=None) -> GateReport:
+        """images: uint8 [N, H, W, C] device tensor or N numpy images; timestamps [N];
+        floor labels given, or derived from ``imu`` = (t, ax, ay, az)."""
+        import torch
+        timestamps = np.asarray(timestamps, np.float64)
+        events = []
+        if floor_labels is None:
+            if imu is None:
+                raise ValueError("need floor_labels or an IMU log")
+            floor_labels, events = floor_labels_from_imu(timestamps, imu, self.start_floor, self.imu_detector_kwargs)
+        floor_labels = np.asarray(floor_labels)
+        self.spr = SemanticPlaceRecognition(self.vpr_method, self.device, self.similarity_threshold,
+                                            self.min_time_gap)
+        if isinstance(images, torch.Tensor):
+            frames = images
+        else:
+            frames = torch.from_numpy(np.ascontiguousarray(np.stack([np.asarray(im, np.uint8) for im in images])))
+        frames = frames.to(torch.device(self.device))
+        labels = [int(f) if np.issubdtype(type(f), np.integer) else f for f in floor_labels.tolist()]
+        self.spr.add_images(frames, timestamps.tolist(), labels)
+        matches = self.spr.find_loop_closures(enable_floor_gating=self.retrieval_floor_gating, k=self.k)
+        to_verify = [m for m in matches if m.is_valid or self.verify_rejected]
+        self.verifier = SemanticGeometricVerifier(self.matcher_type, self.device, self.min_inliers,
+                                                  self.min_inlier_ratio, enable_floor_gating=self.verifier_floor_gating)
+        pairs = [(m.query_idx, m.match_idx) for m in to_verify]
+        results = self.verifier.verify_with_semantics_batch(frames, pairs,
+                                                            [(labels[a], labels[b]) for a, b in pairs], K, pairs)
+        self.gate = SemanticLoopClosureGate(floor_labels, strict_mode=self.strict_mode)
+        accepted, rejected = self.gate.gate_candidates(
+            [(m.query_idx, m.match_idx, m.similarity) for m, r in zip(to_verify, results) if r.is_valid])
+        vstats = self.verifier.get_statistics()
+        gstats = self.gate.get_stats()
+        counts = RejectionCount(retrieval_floor_rejected=sum(1 for m in matches if not m.is_valid),
+                                skipped_floor_mismatch=vstats['skipped_floor_mismatch'],
+                                verifier_invalid=vstats['invalid'],
+                                gate_rejected_cross_floor=gstats['rejected_cross_floor'])
+        return GateReport(floor_labels=floor_labels, events=events, matches=matches, verified=to_verify,
+                          results=results, accepted=accepted, rejected=rejected,
+                          retrieval_stats=self.spr.get_statistics(matches), verifier_stats=vstats,
+                          gate_stats=gstats, rejections=counts)
+
+
+class DeviceGate:
+    """The same chain on device arrays for a frame-sharded sequence: rank r of W owns
+    keyframes [r N / W, (r + 1) N / W) -- its frames, ViT forwards and SuperPoint
+    features -- and the query rows of the same range.  Exchange steps (RCCL over
+    xGMI): the [N, 768] descriptor all-gather before retrieval, the SuperPoint feature
+    all-gather before verification, and an 8-B-per-pair all-gather that re-balances the
+    gate-accepted pairs across ranks (mlgate.distributed.balanced_pairs).
+
+    One ``step()`` gates the whole sequence once and returns per-rank counts; the
+    caller all-reduces them (bench.py)."""
+
+    def __init__(self, frames, timestamps, floor_labels, world=1, rank=0, device='cuda', k=10,
+                 similarity_threshold=0.5, min_time_gap=10.0, strict_mode=True, retrieval_floor_gating=True,
+                 verifier_floor_gating=True, verify=True, K=None, min_inliers=20, min_inlier_ratio=0.25,
+                 vit_batch=123, sp_batch=64, lg_chunk=1024, max_keypoints=2048, vit_state_dict=None):
+        import torch
+        from . import distributed as mdist
+        from .lightglue import LightGlueGPU
+        from .superpoint import SuperPointGPU
+        from .vit import VitB14
+        from .weights import EMBED, synthetic_state_dict
+        self.torch, self.mdist = torch, mdist
+        self.dev = torch.device(device)
+        self.world, self.rank = world, rank
+        N = self.N = len(timestamps)
+        self.lo, self.hi = mdist.shard(N, world, rank)
+        self.n_local = self.hi - self.lo
+        if frames.shape[0] != self.n_local:
+            raise ValueError(f"rank {rank} owns {self.n_local} keyframes, got {frames.shape[0]} frames")
+        self.frames = frames
+        self.k, self.thr, self.gap = int(k), float(similarity_threshold), float(min_time_gap)
+        self.limit = 0 if strict_mode else 1
+        self.retrieval_floor_gating, self.verifier_floor_gating = retrieval_floor_gating, verifier_floor_gating
+        self.min_inliers, self.min_inlier_ratio = min_inliers, min_inlier_ratio
+        self.sp_batch, self.lg_chunk, self.kp = sp_batch, lg_chunk, max_keypoints
+        self.t_all = torch.as_tensor(np.asarray(timestamps, np.float64), device=self.dev)
+        self.labels = np.asarray(floor_labels)
+        codes = np.asarray(self.labels, np.int64)
+        if not np.array_equal(codes, self.labels):
+            raise ValueError("DeviceGate takes integer floor labels")
+        self.f_all = torch.as_tensor(codes, device=self.dev)
+        self.hf_all = torch.ones(N, dtype=torch.uint8, device=self.dev)
+        sd = vit_state_dict if vit_state_dict is not None else synthetic_state_dict(0)
+        self.eng = VitB14(sd, device=self.dev, max_batch=vit_batch)
+        self.gather = mdist.RowGather(N, EMBED, world, self.dev)
+        self.desc_loc = (self.gather.out[self.lo:self.hi] if world == 1
+                         else torch.empty(self.n_local, EMBED, device=self.dev))
+        self.local_feats = torch.empty(self.n_local, self.eng.n_local, EMBED, dtype=torch.float32, device=self.dev)
+        self.totals = torch.zeros(2, dtype=torch.int64, device=self.dev)
+        self.verify = verify
+        if verify:
+            KP = max_keypoints
+            self.sp = SuperPointGPU(device=self.dev, max_num_keypoints=KP)
+            self.lg = LightGlueGPU(device=self.dev)
+            self.g_kp = mdist.RowGather(N, KP * 2, world, self.dev)
+            self.g_ds = mdist.RowGather(N, KP * 256, world, self.dev)
+            self.g_cnt = mdist.RowGather(N, 1, world, self.dev, dtype=torch.int32)
+            if world == 1:
+                self.kp_loc, self.ds_loc, self.cnt_loc = self.g_kp.out, self.g_ds.out, self.g_cnt.out
+            else:
+                self.kp_loc = torch.empty(self.n_local, KP * 2, device=self.dev)
+                self.ds_loc = torch.empty(self.n_local, KP * 256, device=self.dev)
+                self.cnt_loc = torch.empty(self.n_local, 1, dtype=torch.int32, device=self.dev)
+            Kc = np.asarray(K if K is not None else np.eye(3), np.float64)
+            self.K = torch.from_numpy(Kc.reshape(9).copy()).to(self.dev) if K is not None else None
+        self.last = {}
+
+    def step(self):
+        """Gate the sequence once.  Returns this rank's counts (dict of ints): matches,
+        the four rejection terms, pairs verified, pairs geometrically valid, accepted."""
+        torch = self.torch
+        from . import geometry, retrieval
+        self.eng.forward_into(self.frames, self.desc_loc, self.local_feats)
+        if self.world > 1:
+            self.gather(self.desc_loc)  # RCCL all-gather of the descriptors over xGMI
+        self.totals.zero_()
+        idx, sim, valid, count = retrieval.knn_gate(self.gather.out, self.t_all, self.f_all, self.hf_all, self.gap,
+                                                    self.thr, self.k, self.retrieval_floor_gating, q0=self.lo,
+                                                    Q=self.n_local, totals=self.totals)
+        k = idx.shape[1]
+        live = torch.arange(k, device=self.dev)[None, :] < count[:, None].long()
+        out = {"matches": int(count.sum()), "retrieval_floor_rejected": 0, "skipped_floor_mismatch": 0,
+               "verifier_invalid": 0, "gate_rejected_cross_floor": 0, "pairs_verified": 0, "verified_valid": 0,
+               "accepted": 0}
+        # PlaceMatch.is_valid == False: emitted but floor-rejected
+        out["retrieval_floor_rejected"] = int((live & (valid == 0)).sum())
+        if not self.verify:
+            return out
+        # SuperPoint once per keyframe (the reference re-extracts per pair), cached in HBM
+        for b0 in range(0, self.n_local, self.sp_batch):
+            b1 = min(self.n_local, b0 + self.sp_batch)
+            kp, _, ds, _, cnt = self.sp.extract_device(self.frames[b0:b1])
+            self.kp_loc[b0:b1].copy_(kp.view(b1 - b0, -1))
+            self.ds_loc[b0:b1].copy_(ds.view(b1 - b0, -1))
+            self.cnt_loc[b0:b1, 0].copy_(cnt)
+        if self.world > 1:
+            self.g_kp(self.kp_loc)
+            self.g_ds(self.ds_loc)
+            self.g_cnt(self.cnt_loc)
+        kp_all = self.g_kp.out.view(self.N, self.kp, 2)
+        ds_all = self.g_ds.out.view(self.N, self.kp, 256)
+        counts = self.g_cnt.out.view(-1).cpu().numpy()
+        # matches handed to verify_with_semantics (is_valid ones), skip rule on floors
+        qs, js = torch.nonzero(live & (valid != 0), as_tuple=True)
+        pa_t, pb_t = (qs + self.lo).to(torch.int32), idx[qs, js].to(torch.int32)
+        if self.verifier_floor_gating:
+            same = self.f_all[pa_t.long()] == self.f_all[pb_t.long()]
+            out["skipped_floor_mismatch"] = int((~same).sum())
+            pa_t, pb_t = pa_t[same], pb_t[same]
+        # pair-level load balance across ranks (features are all-gathered, so any rank
+        # can verify any pair; the union of the slices is the global pair list)
+        pa_t, pb_t = self.mdist.balanced_pairs(pa_t, pb_t, self.world, self.rank)
+        pa, pb = pa_t.cpu().numpy(), pb_t.cpu().numpy()
+        n_valid = gate_rej = 0
+        for c0 in range(0, len(pa), self.lg_chunk):
+            ca, cb = pa[c0:c0 + self.lg_chunk], pb[c0:c0 + self.lg_chunk]
+            m, _, n, _ = self.lg.match_device(kp_all, ds_all, counts, ca, cb)
+            # matched keypoints -> one batched RANSAC (+ recoverPose when K is given)
+            P = len(ca)
+            lv = torch.arange(self.kp, device=self.dev)[None, :] < n[:, None]
+            pi, si = torch.nonzero(lv, as_tuple=True)
+            ta = torch.from_numpy(ca).to(self.dev).long()
+            tb = torch.from_numpy(cb).to(self.dev).long()
+            k1 = kp_all[ta[pi], m[pi, si, 0].long()].contiguous()
+            k2 = kp_all[tb[pi], m[pi, si, 1].long()].contiguous()
+            offs = torch.zeros(P + 1, dtype=torch.int32, device=self.dev)
+            offs[1:] = torch.cumsum(n, 0)
+            _, _, inl, _, _ = geometry.epipolar_ransac_device(k1, k2, offs, self.K, 0, 3.0)
+            ratio = inl.double() / n.clamp(min=1).double()
+            ok = (n >= 5) & (inl >= self.min_inliers) & (ratio >= self.min_inlier_ratio)
+            n_valid += int(ok.sum())
+            # the floor gate on the geometrically valid pairs
+            gate_rej += int((ok & ((self.f_all[ta] - self.f_all[tb]).abs() > self.limit)).sum())
+        out["pairs_verified"] = len(pa)
+        out["verified_valid"] = n_valid
+        out["verifier_invalid"] = len(pa) - n_valid
+        out["gate_rejected_cross_floor"] = gate_rej
+        out["accepted"] = n_valid - gate_rej
+        return out

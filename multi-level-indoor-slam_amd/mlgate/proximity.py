@@ -65,27 +65,13 @@ def proximity_candidates_device(pos, floor=None, distance_threshold=2.0, min_tim
     """
     N = int(pos.shape[0])
     nrows = N - row0 if nrows is None else int(nrows)
-    dev = pos.device
-    L = _native.lib()
-    nbytes = L.mlg_proximity_workspace_bytes(N, nrows)
-    if nbytes == 0:
+    if N > 65536 or not 0 <= row0 <= N or nrows < 0 or row0 + nrows > N:
         raise ValueError(f"proximity search supports up to 65536 poses and a row range inside [0, N) "
                          f"(N={N}, row0={row0}, nrows={nrows})")
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    totals = torch.empty(2, dtype=torch.int64, device=dev)
-    fptr = _native.ptr(floor) if floor is not None else None
-    args = (_native.ptr(pos), fptr, N, int(row0), nrows, float(distance_threshold), int(min_time_gap),
-            int(bool(strict_mode)))
-    s = _native.stream_of(dev)
-    _native.check(L.mlg_proximity_count(*args, _native.ptr(ws), nbytes, _native.ptr(totals), s),
-                  "mlg_proximity_count")
+    pairs, dist, valid, totals = _native.ops().proximity(pos.contiguous(), floor, int(row0), nrows,
+                                                         float(distance_threshold), int(min_time_gap),
+                                                         bool(strict_mode))
     total, accepted = (int(v) for v in totals.cpu())
-    pairs = torch.empty(max(total, 1), 2, dtype=torch.int32, device=dev)
-    dist = torch.empty(max(total, 1), dtype=torch.float64, device=dev)
-    valid = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
-    if total:
-        _native.check(L.mlg_proximity_emit(*args, _native.ptr(ws), nbytes, _native.ptr(pairs), _native.ptr(dist),
-                                           _native.ptr(valid), s), "mlg_proximity_emit")
     return pairs[:total], dist[:total], valid[:total], total, accepted
 
 

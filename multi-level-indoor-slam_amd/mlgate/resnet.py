@@ -3,8 +3,6 @@ the path MixVPR / SALAD actually execute in the reference, the torchvision ResNe
 fallback of MixVPR._load_fallback_model / extract_descriptor
 (scripts/semantic_gating/place_recognition.py:248-306).
 """
-import ctypes
-
 import numpy as np
 import torch
 
@@ -13,13 +11,7 @@ from .weights import RESNET_STAGES, resolve_resnet50_state_dict
 
 BN_EPS = 1e-5
 
-
-class _Block(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("w1", "b1", "w2", "b2", "w3", "b3", "wd", "bd")]
-
-
-class _Weights(ctypes.Structure):
-    _fields_ = [("stem_w", ctypes.c_void_p), ("stem_b", ctypes.c_void_p), ("blocks", _Block * 16)]
+BLOCK_ORDER = ("w1", "b1", "w2", "b2", "w3", "b3", "wd", "bd")  # mlg_rn_block field order
 
 
 def fold_bn(w, sd, p):
@@ -42,39 +34,36 @@ class ResNet50GPU:
             state_dict, self.weights_source = resolve_resnet50_state_dict(weights_path, seed)
         else:
             self.weights_source = "given"
-        self._keep = []
         self._w = self._pack(state_dict)
-        self._ws = None
 
     def _t(self, a, dtype):
-        t = torch.as_tensor(np.ascontiguousarray(a, np.float32)).to(dtype).contiguous().to(self.device)
-        self._keep.append(t)
-        return t.data_ptr()
+        return torch.as_tensor(np.ascontiguousarray(a, np.float32)).to(dtype).contiguous().to(self.device)
 
     def _pack(self, sd):
         bf, f32 = torch.bfloat16, torch.float32
-        w = _Weights()
         sw, sb = fold_bn(sd["conv1.weight"], sd, "bn1")
-        w.stem_w = self._t(sw.transpose(0, 2, 3, 1).reshape(64, 147), f32)  # [co][ky][kx][c]
-        w.stem_b = self._t(sb, f32)
+        w = [self._t(sw.transpose(0, 2, 3, 1).reshape(64, 147), f32),  # [co][ky][kx][c]
+             self._t(sb, f32)]
+        empty = torch.empty(0, dtype=bf, device=self.device)
         cin, k = 64, 0
         for li, (width, blocks, _) in enumerate(RESNET_STAGES, 1):
             wpad = max(width, 128)
             for bi in range(blocks):
                 p = f"layer{li}.{bi}."
-                blk = w.blocks[k]
+                blk = {"wd": empty, "bd": empty.float()}
                 w1, b1 = fold_bn(np.asarray(sd[p + "conv1.weight"]).reshape(width, cin), sd, p + "bn1")
                 w2, b2 = fold_bn(sd[p + "conv2.weight"], sd, p + "bn2")
                 w2 = w2.transpose(0, 2, 3, 1).reshape(width, 9 * width)  # k = tap * width + c
                 pad = lambda a: np.concatenate([a, np.zeros((wpad - a.shape[0],) + a.shape[1:], np.float32)])  # noqa
-                blk.w1, blk.b1 = self._t(pad(w1), bf), self._t(pad(b1[:, None])[:, 0], f32)
-                blk.w2, blk.b2 = self._t(pad(w2), bf), self._t(pad(b2[:, None])[:, 0], f32)
+                blk["w1"], blk["b1"] = self._t(pad(w1), bf), self._t(pad(b1[:, None])[:, 0], f32)
+                blk["w2"], blk["b2"] = self._t(pad(w2), bf), self._t(pad(b2[:, None])[:, 0], f32)
                 w3, b3 = fold_bn(np.asarray(sd[p + "conv3.weight"]).reshape(4 * width, width), sd, p + "bn3")
-                blk.w3, blk.b3 = self._t(w3, bf), self._t(b3, f32)
+                blk["w3"], blk["b3"] = self._t(w3, bf), self._t(b3, f32)
                 if bi == 0:
                     wd, bd = fold_bn(np.asarray(sd[p + "downsample.0.weight"]).reshape(4 * width, cin), sd,
                                      p + "downsample.1")
-                    blk.wd, blk.bd = self._t(wd, bf), self._t(bd, f32)
+                    blk["wd"], blk["bd"] = self._t(wd, bf), self._t(bd, f32)
+                w += [blk[f] for f in BLOCK_ORDER]
                 cin = 4 * width
                 k += 1
         return w
@@ -85,15 +74,4 @@ class ResNet50GPU:
             raise ValueError("frames must be uint8")
         if frames.dim() == 3:
             frames = frames[..., None]
-        frames = frames.contiguous()
-        B, H, W, C = frames.shape
-        L = _native.lib()
-        nbytes = L.mlg_resnet50_workspace_bytes(B, H, W)
-        if self._ws is None or self._ws.numel() < nbytes:
-            self._ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-        out = torch.empty(B, int(descriptor_dim), dtype=torch.float32, device=self.device)
-        rc = L.mlg_resnet50_forward(ctypes.byref(self._w), _native.ptr(frames), B, H, W, C, H * W * C,
-                                    int(descriptor_dim), _native.ptr(self._ws), self._ws.numel(), _native.ptr(out),
-                                    _native.stream_of(self.device))
-        _native.check(rc, "mlg_resnet50_forward")
-        return out
+        return _native.ops().resnet50(frames.contiguous(), self._w, int(descriptor_dim))

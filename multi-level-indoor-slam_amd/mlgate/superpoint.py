@@ -3,8 +3,6 @@ LightGlue._detect_and_match_native (scripts/semantic_gating/geometric_verificati
 263-312) -- ``SuperPoint(max_num_keypoints=2048, detection_threshold=0.001)`` on
 ``cv2.cvtColor(img, COLOR_BGR2GRAY) / 255`` -- for a batch of keyframes at once.
 """
-import ctypes
-
 import numpy as np
 import torch
 
@@ -15,10 +13,6 @@ DESC_DIM = 256
 _ORDER = ["conv1b", "conv2a", "conv2b", "conv3a", "conv3b", "conv4a", "conv4b", "convPa", "convPb", "convDa",
           "convDb"]
 
-
-class _SpWeights(ctypes.Structure):
-    _fields_ = [("conv1a_w", ctypes.c_void_p), ("conv1a_b", ctypes.c_void_p), ("w", ctypes.c_void_p * 11),
-                ("b", ctypes.c_void_p * 11)]
 
 
 def pack_weights(sd, device):
@@ -54,13 +48,9 @@ class SuperPointGPU:
         self.nms_radius = int(nms_radius)
         self.border = int(remove_borders)
         self._t = pack_weights(state_dict, self.device)
-        self._w = _SpWeights()
-        self._w.conv1a_w = self._t["conv1a.w"].data_ptr()
-        self._w.conv1a_b = self._t["conv1a.b"].data_ptr()
-        for i, n in enumerate(_ORDER):
-            self._w.w[i] = self._t[f"{n}.w"].data_ptr()
-            self._w.b[i] = self._t[f"{n}.b"].data_ptr()
-        self._ws = None
+        # mlg_sp_weights order: conv1a w, b; the 11 bf16 weights; their 11 biases
+        self._w = ([self._t["conv1a.w"], self._t["conv1a.b"]] + [self._t[f"{n}.w"] for n in _ORDER]
+                   + [self._t[f"{n}.b"] for n in _ORDER])
 
     def extract_device(self, frames, with_bf16=False):
         """frames: device uint8 [B, H, W, C] -> device (kpts [B, K, 2], scores [B, K], desc [B, K, 256],
@@ -69,27 +59,9 @@ class SuperPointGPU:
             raise ValueError("frames must be uint8 [B, H, W, C] or [B, H, W]")
         if frames.dim() == 3:
             frames = frames[..., None]
-        frames = frames.contiguous()
-        B, H, W, C = frames.shape
-        L = _native.lib()
-        nbytes = L.mlg_superpoint_workspace_bytes(B, H, W)
-        if nbytes == 0:
-            raise ValueError(f"SuperPoint needs H, W >= 16 and multiples of 8 (got {H}x{W})")
-        if self._ws is None or self._ws.numel() < nbytes:
-            self._ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
-        K = self.max_kp
-        kp = torch.zeros(B, K, 2, dtype=torch.float32, device=self.device)
-        sc = torch.zeros(B, K, dtype=torch.float32, device=self.device)
-        ds = torch.empty(B, K, DESC_DIM, dtype=torch.float32, device=self.device)
-        db = torch.empty(B, K, DESC_DIM, dtype=torch.bfloat16, device=self.device) if with_bf16 else None
-        cnt = torch.empty(B, dtype=torch.int32, device=self.device)
-        rc = L.mlg_superpoint(ctypes.byref(self._w), _native.ptr(frames), B, H, W, C, H * W * C, self.det_thr, K,
-                              self.nms_radius, self.border, _native.ptr(self._ws), self._ws.numel(),
-                              _native.ptr(kp), _native.ptr(sc), _native.ptr(ds),
-                              _native.ptr(db) if db is not None else None, _native.ptr(cnt),
-                              _native.stream_of(self.device))
-        _native.check(rc, "mlg_superpoint")
-        return kp, sc, ds, db, cnt
+        kp, sc, ds, db, cnt = _native.ops().superpoint(frames.contiguous(), self._w, self.det_thr, self.max_kp,
+                                                       self.nms_radius, self.border, bool(with_bf16))
+        return kp, sc, ds, (db if with_bf16 else None), cnt
 
     def extract(self, images):
         """List of HxW[x3] uint8 numpy images (same size) -> list of dicts with numpy

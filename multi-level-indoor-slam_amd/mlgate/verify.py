@@ -165,6 +165,10 @@ class SuperGlue(BaseFeatureMatcher):
         self._load_model()
         return self._fallback.detect_and_match(image1, image2)
 
+    def detect_and_match_batch(self, frames, pairs):
+        self._load_model()
+        return self._fallback.detect_and_match_batch(frames, pairs)
+
 
 class LoFTR(BaseFeatureMatcher):
     """geometric_verification.py:424-526.  Without kornia the reference falls back to
@@ -187,6 +191,10 @@ class LoFTR(BaseFeatureMatcher):
     def detect_and_match(self, image1, image2):
         self._load_model()
         return self._fallback.detect_and_match(image1, image2)
+
+    def detect_and_match_batch(self, frames, pairs):
+        self._load_model()
+        return self._fallback.detect_and_match_batch(frames, pairs)
 
 
 _MATCHERS = {'lightglue': LightGlue, 'superglue': SuperGlue, 'loftr': LoFTR}
@@ -257,26 +265,29 @@ class GeometricVerifier:
                      indices: Optional[List[Tuple[int, int]]] = None) -> List[MatchResult]:
         """Same results as verifying each pair in turn (geometric_verification.py:636-662),
         computed as one batched SuperPoint + LightGlue + RANSAC pass when the images
-        share a shape."""
+        share a shape (every matcher has a batched path; SuperGlue / LoFTR through the
+        LightGlue fallback the reference resolves them to)."""
         if not image_pairs:
             return []
-        shapes = {np.shape(im) for pair in image_pairs for im in pair}
-        m = self.matcher
-        if len(shapes) == 1 and hasattr(m, "detect_and_match_batch") or (
-                hasattr(m, "_fallback") and len(shapes) == 1):
-            mm = getattr(m, "_fallback", None) if not hasattr(m, "detect_and_match_batch") else m
-            if mm is None:
-                m._load_model()
-                mm = m._fallback
-            dev = torch.device(mm.device)
+        if len({np.shape(im) for pair in image_pairs for im in pair}) == 1:
             frames = torch.from_numpy(np.stack([np.asarray(im, np.uint8) for pair in image_pairs for im in pair]))
-            matched = mm.detect_and_match_batch(frames.to(dev), [(2 * i, 2 * i + 1) for i in range(len(image_pairs))])
-            return self.verify_matches_batch([(a, b) for a, b, _ in matched], K, indices)
+            frames = frames.to(torch.device(self.matcher.device))
+            return self.verify_frames_batch(frames, [(2 * i, 2 * i + 1) for i in range(len(image_pairs))], K, indices)
         out = []
         for i, (a, b) in enumerate(image_pairs):
             q, mi = indices[i] if indices is not None else (i, i)
             out.append(self.verify(a, b, K, q, mi))
         return out
+
+    def verify_frames_batch(self, frames, pairs: List[Tuple[int, int]], K: Optional[np.ndarray] = None,
+                            indices: Optional[List[Tuple[int, int]]] = None) -> List[MatchResult]:
+        """verify() for pairs (a, b) of device-resident keyframes frames[a], frames[b]
+        (uint8 [F, H, W, C]): SuperPoint once per distinct keyframe, LightGlue over all
+        pairs in one ragged call, one batched RANSAC + recoverPose, the decision rule."""
+        if not pairs:
+            return []
+        matched = self.matcher.detect_and_match_batch(frames, pairs)
+        return self.verify_matches_batch([(a, b) for a, b, _ in matched], K, indices)
 
 
 class SemanticGeometricVerifier(GeometricVerifier):
@@ -297,6 +308,28 @@ class SemanticGeometricVerifier(GeometricVerifier):
         self.stats['verified'] += 1
         self.stats['valid' if res.is_valid else 'invalid'] += 1
         return res
+
+    def verify_with_semantics_batch(self, frames, pairs: List[Tuple[int, int]], floors: List[Tuple[int, int]],
+                                    K: Optional[np.ndarray] = None,
+                                    indices: Optional[List[Tuple[int, int]]] = None) -> List[MatchResult]:
+        """verify_with_semantics for many pairs (a, b) of device-resident keyframes with
+        their floor labels (f_a, f_b): the same skip rule, results and counters as calling
+        it pair by pair in this order; the pairs that are not skipped are verified in one
+        batched pass (verify_frames_batch)."""
+        n = len(pairs)
+        idx = list(indices) if indices is not None else [(0, 0)] * n
+        skip = [self.enable_floor_gating and f1 != f2 for f1, f2 in floors]
+        run = [i for i in range(n) if not skip[i]]
+        res = self.verify_frames_batch(frames, [pairs[i] for i in run], K, [idx[i] for i in run])
+        out = [_rejected(*idx[i]) if skip[i] else None for i in range(n)]
+        for i, r in zip(run, res):
+            out[i] = r
+        self.stats['skipped_floor_mismatch'] += sum(skip)
+        self.stats['verified'] += len(run)
+        n_valid = sum(1 for r in res if r.is_valid)
+        self.stats['valid'] += n_valid
+        self.stats['invalid'] += len(run) - n_valid
+        return out
 
     def get_statistics(self) -> Dict:
         total = self.stats['verified'] + self.stats['skipped_floor_mismatch']

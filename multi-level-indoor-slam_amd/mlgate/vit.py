@@ -7,7 +7,6 @@ from ONE forward (the reference runs the identical forward twice per add_image, 
 for the descriptor and once for the local features).  Frames go in as uint8
 [B, H, W, C] device tensors; everything up to the float32 descriptors stays in HBM.
 """
-import ctypes
 import math
 
 import numpy as np
@@ -18,17 +17,9 @@ from . import _native
 from .weights import DEPTH, EMBED, PATCH
 
 PATCH_K = 768  # 3*14*14 = 588 patch inputs zero-padded to 12 K-tiles of 64 (include/mlgate.h)
-P = ctypes.c_void_p
-
-
-class _Block(ctypes.Structure):
-    _fields_ = [(n, P) for n in ("norm1_w", "norm1_b", "qkv_w", "qkv_b", "proj_w", "proj_b", "ls1", "norm2_w",
-                                 "norm2_b", "fc1_w", "fc1_b", "fc2_w", "fc2_b", "ls2")]
-
-
-class _Weights(ctypes.Structure):
-    _fields_ = [("patch_w", P), ("patch_b", P), ("cls", P), ("pos", P), ("blocks", _Block * DEPTH),
-                ("norm_w", P), ("norm_b", P)]
+BLOCK_ORDER = ("norm1_w", "norm1_b", "qkv_w", "qkv_b", "proj_w", "proj_b", "ls1", "norm2_w", "norm2_b", "fc1_w",
+               "fc1_b", "fc2_w", "fc2_b", "ls2")  # mlg_vit_block field order
+BF16_FIELDS = {"qkv_w", "proj_w", "fc1_w", "fc2_w"}  # GEMM weights; everything else float32
 
 
 def resample_pos_embed(pos_embed, grid):
@@ -57,59 +48,42 @@ class VitB14:
         self.n_local = self.n_patches - 1  # tokens 2.. of get_intermediate_layers (CLS + patch 0 dropped)
         self.max_batch = max_batch
         self.flags = (1 if pool == "mean" else 0) | (0 if swap_rb else 2)  # MLG_VIT_POOL_MEAN / KEEP_CHANNELS
-        self._keep = []
         self._w = self._pack(state_dict)
-        self._ws_bytes = _native.lib().mlg_vit_workspace_bytes(max_batch, image_size)
-        self._ws = torch.empty(self._ws_bytes, dtype=torch.uint8, device=self.device)
 
     # ------------------------------------------------------------ weights
     def _dev(self, a, dtype):
         t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
-        t = t.to(self.device, torch.float32).to(dtype).contiguous()
-        self._keep.append(t)
-        return ctypes.c_void_p(t.data_ptr())
+        return t.to(self.device, torch.float32).to(dtype).contiguous()
 
     def _pack(self, sd):
+        """Device tensors in mlg_vit_weights order (torch.ops.mlgate.vit_forward_into)."""
         f32, bf = torch.float32, torch.bfloat16
-        w = _Weights()
         pw = torch.as_tensor(np.asarray(sd["patch_embed.proj.weight"], np.float32)).reshape(EMBED, -1)
-        w.patch_w = self._dev(F.pad(pw, (0, PATCH_K - pw.shape[1])), bf)
-        w.patch_b = self._dev(sd["patch_embed.proj.bias"], f32)
-        w.cls = self._dev(np.asarray(sd["cls_token"], np.float32).reshape(EMBED), f32)
         pos = torch.as_tensor(np.asarray(sd["pos_embed"], np.float32)).to(self.device)
-        w.pos = self._dev(resample_pos_embed(pos, self.grid).reshape(-1, EMBED), f32)
+        w = [self._dev(F.pad(pw, (0, PATCH_K - pw.shape[1])), bf), self._dev(sd["patch_embed.proj.bias"], f32),
+             self._dev(np.asarray(sd["cls_token"], np.float32).reshape(EMBED), f32),
+             self._dev(resample_pos_embed(pos, self.grid).reshape(-1, EMBED), f32)]
+        names = {"norm1_w": "norm1.weight", "norm1_b": "norm1.bias", "qkv_w": "attn.qkv.weight",
+                 "qkv_b": "attn.qkv.bias", "proj_w": "attn.proj.weight", "proj_b": "attn.proj.bias",
+                 "ls1": "ls1.gamma", "norm2_w": "norm2.weight", "norm2_b": "norm2.bias", "fc1_w": "mlp.fc1.weight",
+                 "fc1_b": "mlp.fc1.bias", "fc2_w": "mlp.fc2.weight", "fc2_b": "mlp.fc2.bias", "ls2": "ls2.gamma"}
         for i in range(DEPTH):
-            p, b = f"blocks.{i}.", w.blocks[i]
-            b.norm1_w, b.norm1_b = self._dev(sd[p + "norm1.weight"], f32), self._dev(sd[p + "norm1.bias"], f32)
-            b.qkv_w, b.qkv_b = self._dev(sd[p + "attn.qkv.weight"], bf), self._dev(sd[p + "attn.qkv.bias"], f32)
-            b.proj_w, b.proj_b = self._dev(sd[p + "attn.proj.weight"], bf), self._dev(sd[p + "attn.proj.bias"], f32)
-            b.ls1 = self._dev(sd[p + "ls1.gamma"], f32)
-            b.norm2_w, b.norm2_b = self._dev(sd[p + "norm2.weight"], f32), self._dev(sd[p + "norm2.bias"], f32)
-            b.fc1_w, b.fc1_b = self._dev(sd[p + "mlp.fc1.weight"], bf), self._dev(sd[p + "mlp.fc1.bias"], f32)
-            b.fc2_w, b.fc2_b = self._dev(sd[p + "mlp.fc2.weight"], bf), self._dev(sd[p + "mlp.fc2.bias"], f32)
-            b.ls2 = self._dev(sd[p + "ls2.gamma"], f32)
-        w.norm_w, w.norm_b = self._dev(sd["norm.weight"], f32), self._dev(sd["norm.bias"], f32)
+            for f in BLOCK_ORDER:
+                w.append(self._dev(sd[f"blocks.{i}." + names[f]], bf if f in BF16_FIELDS else f32))
+        w += [self._dev(sd["norm.weight"], f32), self._dev(sd["norm.bias"], f32)]
         return w
 
     # ------------------------------------------------------------ forward
-    def forward_into(self, frames, desc_out, local_out=None, stream=None):
+    def forward_into(self, frames, desc_out, local_out=None):
         """frames: uint8 [B, H, W, C] device tensor (C = 1, 3 BGR or 4 BGRA; or [B, H, W]).
-        Writes float32 descriptors [B, 768] (and local features [B, n_local, 768])."""
+        Writes float32 descriptors [B, 768] (and local features [B, n_local, 768]);
+        torch.ops.mlgate.vit_forward_into on the current stream."""
         if frames.dim() == 3:
             frames = frames.unsqueeze(-1)
         if frames.dtype != torch.uint8 or frames.device.type != "cuda":
             raise TypeError("frames must be a uint8 tensor on the HIP device")
-        frames = frames.contiguous()
-        B, H, W, C = frames.shape
-        st = stream if stream is not None else _native.stream_of(self.device)
-        L = _native.lib()
-        for b0 in range(0, B, self.max_batch):
-            nb = min(self.max_batch, B - b0)
-            lo = ctypes.c_void_p(local_out[b0].data_ptr()) if local_out is not None else None
-            rc = L.mlg_vit_forward(ctypes.byref(self._w), ctypes.c_void_p(frames[b0].data_ptr()), nb, H, W, C,
-                                   H * W * C, self.image_size, self.flags, _native.ptr(self._ws), self._ws_bytes,
-                                   ctypes.c_void_p(desc_out[b0].data_ptr()), lo, st)
-            _native.check(rc, "mlg_vit_forward")
+        _native.ops().vit_forward_into(frames.contiguous(), self._w, self.image_size, self.flags, self.max_batch,
+                                       desc_out, local_out)
 
     def forward(self, frames, with_local=False):
         B = frames.shape[0]

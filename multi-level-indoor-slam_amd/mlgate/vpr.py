@@ -11,9 +11,8 @@ behaviour as the reference; the compute runs on the mlgate HIP kernels:
   * retrieval (find_loop_closures / query / pairwise similarities / cross-correlation
     rerank) -> mlg_knn_gate / mlg_knn_query / mlg_xcorr_score.
   * MixVPR / SALAD -> the reference resolves both to a torchvision ResNet-50 GAP
-    fallback (place_recognition.py:241-306, 370-378); that network is not built on HIP
-    yet, so their extract_descriptor raises.  Descriptors can still be injected into
-    ``.descriptors`` (as the reference's own demo does, :1020) and retrieved on the GPU.
+    fallback (place_recognition.py:241-306, 370-378); here that network runs on the
+    GPU (mlgate.resnet: Pillow-exact resize, HIP stem, MFMA bottlenecks, GAP, zero-pad).
 
 Weights: the hub checkpoint cannot be fetched offline.  ``pretrained_path`` (or
 MLGATE_DINOV2_WEIGHTS) may point at a local hub-format dinov2_vitb14 state_dict;
@@ -52,6 +51,43 @@ class PlaceDescriptor:
 def _torch():
     import torch
     return torch
+
+
+def _device_frames(images, device):
+    """uint8 [B, H, W, C] on the device from a device / host tensor or a list of images."""
+    torch = _torch()
+    if isinstance(images, torch.Tensor):
+        t = images if images.dim() == 4 else images.unsqueeze(-1)
+        if t.dtype != torch.uint8:
+            raise ValueError("frames must be uint8")
+        return t.to(device).contiguous()
+    return torch.from_numpy(_as_frames(images)).to(device)
+
+
+def floor_codes(labels):
+    """Integer codes with the reference's equality semantics for the floor check
+    ``query_floor == match_floor`` (place_recognition.py:896-899): labels that compare
+    equal in Python share a code (1 and 1.0 included), every NaN gets its own code
+    (NaN != NaN), None marks "no label" (has = 0)."""
+    codes = np.zeros(len(labels), np.int64)
+    has = np.ones(len(labels), np.uint8)
+    seen = {}
+    nxt = 0
+    for i, f in enumerate(labels):
+        if f is None:
+            has[i] = 0
+            continue
+        if isinstance(f, (float, np.floating)) and f != f:
+            codes[i] = nxt
+            nxt += 1
+            continue
+        key = f.item() if isinstance(f, np.generic) else f
+        c = seen.get(key)
+        if c is None:
+            c = seen[key] = nxt
+            nxt += 1
+        codes[i] = c
+    return codes, has
 
 
 def _as_frames(images):
@@ -109,10 +145,35 @@ class BasePlaceRecognition:
         return np.vstack([d.descriptor for d in self.descriptors])
 
     def _device_matrix(self):
+        """Device float32 [N, D] mirror of ``self.descriptors``.  Callers may append to (or
+        replace entries of) the public list directly, as the reference allows
+        (place_recognition.py:1020); the mirror tracks the descriptor arrays by identity
+        and uploads only rows whose array object changed (appends upload only the new
+        rows).  In-place edits of a descriptor array's values are not seen: replace the
+        PlaceDescriptor (or its array) instead."""
         torch = _torch()
         dev = _native.require_device(self.device)
-        X = np.ascontiguousarray(self.build_descriptor_matrix(), dtype=np.float32)
-        return torch.from_numpy(X).to(dev), dev
+        arrs = [d.descriptor for d in self.descriptors]
+        ids = [id(a) for a in arrs]
+        m = getattr(self, '_mirror', None)
+        D = int(np.asarray(arrs[0]).size) if arrs else 0
+        if m is None or m['dev'] != dev or m['D'] != D or m['buf'].shape[0] < len(arrs):
+            cap = max(len(arrs), 64, 0 if m is None else 2 * m['buf'].shape[0])
+            buf = torch.empty(cap, D, dtype=torch.float32, device=dev)
+            m = self._mirror = {'dev': dev, 'D': D, 'buf': buf, 'ids': [], 'keep': []}
+        old = m['ids']
+        stale = [i for i in range(len(ids)) if i >= len(old) or old[i] != ids[i]]
+        if stale:
+            lo = stale[0]
+            if len(stale) == len(ids) - lo:  # one contiguous tail: a single upload
+                rows = np.ascontiguousarray(np.stack([np.asarray(a, np.float32).reshape(-1) for a in arrs[lo:]]))
+                m['buf'][lo:len(ids)].copy_(torch.from_numpy(rows))
+            else:
+                for i in stale:
+                    m['buf'][i].copy_(torch.from_numpy(np.ascontiguousarray(arrs[i], dtype=np.float32).reshape(-1)))
+        m['ids'] = ids
+        m['keep'] = arrs  # hold the arrays so their ids stay unique while mirrored
+        return m['buf'][:len(ids)], dev
 
     def compute_all_pairwise_similarities(self) -> np.ndarray:
         """N x N cosine similarities (float32), computed on the device."""
@@ -143,6 +204,8 @@ class BasePlaceRecognition:
         tq = torch.tensor([float('nan') if timestamp is None else float(timestamp)], dtype=torch.float64,
                           device=dev)
         q = torch.from_numpy(np.asarray(qd, np.float32).reshape(1, -1)).to(dev)
+        if k > retrieval.MAX_K and len(self.descriptors) > retrieval.MAX_K:
+            raise ValueError(f"k={k} exceeds the device top-k limit of {retrieval.MAX_K}")
         kk = max(1, min(k, len(self.descriptors), retrieval.MAX_K))
         idx, sim, cnt = retrieval.knn_query(db, q, t_db, tq, min_time_gap if timestamp is not None else 0.0, kk)
         c = int(cnt[0]) if k > 0 else 0
@@ -176,8 +239,7 @@ class _ResNetFallback(BasePlaceRecognition):
 
     def extract_descriptors(self, images) -> np.ndarray:
         self._load_model()
-        torch = _torch()
-        frames = torch.from_numpy(_as_frames(images)).to(self._net.device)
+        frames = _device_frames(images, self._net.device)
         return self._net.forward_device(frames, self.descriptor_dim).cpu().numpy()
 
     def extract_descriptor(self, image: np.ndarray) -> np.ndarray:
@@ -221,10 +283,8 @@ class _DinoEngineMixin:
         return self._vit
 
     def _forward(self, images, with_local=False):
-        torch = _torch()
         eng = self._engine()
-        frames = torch.from_numpy(_as_frames(images)).to(eng.device)
-        return eng.forward(frames, with_local=with_local)
+        return eng.forward(_device_frames(images, eng.device), with_local=with_local)
 
     def extract_descriptors(self, images) -> np.ndarray:
         return self._forward(images).cpu().numpy()
@@ -343,16 +403,17 @@ class SemanticPlaceRecognition:
             return []
         torch = _torch()
         from . import retrieval
-        X, dev = self.vpr._device_matrix()
-        t = torch.tensor([float(d.timestamp) for d in descs], dtype=torch.float64, device=dev)
-        fl = torch.tensor([0 if d.floor_label is None else int(d.floor_label) for d in descs], dtype=torch.int64,
-                          device=dev)
-        hf = torch.tensor([d.floor_label is not None for d in descs], dtype=torch.uint8, device=dev)
         if k <= 0:
             return []
-        kk = min(k, retrieval.MAX_K)
-        if k > retrieval.MAX_K and n - 1 > retrieval.MAX_K:
+        # a row ranks all n entries (its own included when min_time_gap <= 0)
+        if k > retrieval.MAX_K and n > retrieval.MAX_K:
             raise ValueError(f"k={k} exceeds the device top-k limit of {retrieval.MAX_K}")
+        kk = min(k, retrieval.MAX_K)
+        X, dev = self.vpr._device_matrix()
+        t = torch.tensor([float(d.timestamp) for d in descs], dtype=torch.float64, device=dev)
+        codes, has = floor_codes([d.floor_label for d in descs])
+        fl = torch.from_numpy(codes).to(dev)
+        hf = torch.from_numpy(has).to(dev)
         out = retrieval.knn_gate(X, t, fl, hf, self.min_time_gap, self.similarity_threshold, kk,
                                  enable_floor_gating)
         q, m, sim, valid = retrieval.flatten_matches(*out)

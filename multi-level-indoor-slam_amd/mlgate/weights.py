@@ -10,6 +10,7 @@ The reference fetches ``torch.hub.load('facebookresearch/dinov2', 'dinov2_vitb14
     Descriptors from synthetic weights are meaningful for throughput and parity
     testing only, not for place recognition.
 """
+import functools
 import os
 
 import numpy as np
@@ -92,15 +93,59 @@ SUPERPOINT_LAYERS = [("conv1a", 1, 64, 3), ("conv1b", 64, 64, 3), ("conv2a", 64,
                      ("convDa", 128, 256, 3), ("convDb", 256, 256, 1)]
 
 
-def superpoint_state_dict(seed=0):
-    """Seeded float32 SuperPoint weights (He-normal convs, small biases), LightGlue key names."""
+def superpoint_state_dict(seed=0, whiten=True):
+    """Seeded float32 SuperPoint weights (He-normal convs, small biases), LightGlue key names.
+
+    With ``whiten`` the descriptor head convDb (1x1, 256 -> 256) is set to the
+    (regularised) whitening transform of convDa's responses on a few seeded synthetic
+    scenes instead of random numbers.  Untrained ReLU features share one dominant
+    direction (descriptor cosine ~0.9 between unrelated points), which leaves LightGlue
+    nothing to match; whitened descriptors are decorrelated (cosine ~0 between
+    unrelated points, > 0.95 between the same scene point in two views), so a revisit
+    produces true correspondences -- the property a trained SuperPoint has."""
+    return {k: v.copy() for k, v in _superpoint_sd(int(seed), bool(whiten)).items()}
+
+
+@functools.lru_cache(maxsize=4)
+def _superpoint_sd(seed, whiten):
     rng = np.random.default_rng(seed)
     sd = {}
     for name, cin, cout, k in SUPERPOINT_LAYERS:
         std = np.float32((2.0 / (cin * k * k)) ** 0.5)
         sd[f"{name}.weight"] = rng.standard_normal((cout, cin, k, k), dtype=np.float32) * std
         sd[f"{name}.bias"] = rng.standard_normal((cout,), dtype=np.float32) * np.float32(0.01)
+    if whiten:
+        sd["convDb.weight"], sd["convDb.bias"] = _whitening_head(sd, seed)
     return sd
+
+
+def _whitening_head(sd, seed, n_scenes=4, reg=1e-2):
+    """convDb = C^(-1/2) (eigenvalues floored at reg * max), bias = -C^(-1/2) mu, where mu / C
+    are the mean / covariance of convDa's ReLU outputs over the descriptor grid of
+    `n_scenes` seeded synthetic keyframes.  One-time weight construction on the CPU."""
+    import torch
+    import torch.nn.functional as F
+    from . import synthetic
+    imgs = []
+    for i in range(n_scenes):
+        base = synthetic.scene(50_000 + 97 * seed + i).astype(np.int16)
+        noise = np.random.default_rng(seed * 131 + i).integers(0, 30, base.shape)
+        imgs.append(np.clip(base + noise, 0, 255))
+    bgr = np.stack(imgs).astype(np.int32)
+    gray = ((bgr[..., 0] * 1868 + bgr[..., 1] * 9617 + bgr[..., 2] * 4899 + 8192) >> 14).astype(np.float32) / 255.0
+    w = {k: torch.from_numpy(v) for k, v in sd.items()}
+    with torch.no_grad():
+        x = torch.from_numpy(gray)[:, None]
+        for name in ("conv1a", "conv1b", "conv2a", "conv2b", "conv3a", "conv3b", "conv4a", "conv4b"):
+            x = torch.relu(F.conv2d(x, w[name + ".weight"], w[name + ".bias"], padding=1))
+            if name in ("conv1b", "conv2b", "conv3b"):
+                x = F.max_pool2d(x, 2, 2)
+        c = torch.relu(F.conv2d(x, w["convDa.weight"], w["convDa.bias"], padding=1))
+    Z = c.permute(0, 2, 3, 1).reshape(-1, c.shape[1]).double().numpy()
+    mu = Z.mean(0)
+    ev, V = np.linalg.eigh(np.cov(Z.T))
+    Wh = (V / np.sqrt(np.maximum(ev, 0) + reg * ev.max())) @ V.T
+    return Wh.astype(np.float32).reshape(256, 256, 1, 1), (-(Wh @ mu)).astype(np.float32)
 
 
 def load_superpoint_state_dict(path):

@@ -249,3 +249,112 @@ def synthetic_pair(rng, n_in, n_out, noise_px=0.5, K=ISEC_K, size=(720, 540), ro
 def rotation_angle_deg(Ra, Rb):
     c = (np.trace(Ra.T @ Rb) - 1) / 2
     return float(np.rad2deg(np.arccos(np.clip(c, -1, 1))))
+
+
+# --- OpenCV's RANSAC loop (calib3d/ptsetreg.cpp RANSACPointSetRegistrator::run) ------
+class CvRng:
+    """cv::RNG: multiply-with-carry, state' = (uint32)state * 4164903690 + (state >> 32)."""
+
+    def __init__(self, state=(1 << 64) - 1):
+        self.state = state
+
+    def next(self):
+        s = self.state
+        self.state = ((s & 0xFFFFFFFF) * 4164903690 + (s >> 32)) & ((1 << 64) - 1)
+        return self.state & 0xFFFFFFFF
+
+    def uniform(self, a, b):
+        return a if a == b else self.next() % (b - a) + a
+
+
+def update_num_iters(p, ep, model_points, max_iters):
+    """RANSACUpdateNumIters (ptsetreg.cpp); cvRound rounds half to even."""
+    p = min(max(p, 0.0), 1.0)
+    ep = min(max(ep, 0.0), 1.0)
+    num = max(1.0 - p, np.finfo(np.float64).tiny)
+    denom = 1.0 - (1.0 - ep) ** model_points
+    if denom < np.finfo(np.float64).tiny:
+        return 0
+    num, denom = np.log(num), np.log(denom)
+    return max_iters if (denom >= 0 or -num >= max_iters * (-denom)) else int(np.rint(num / denom))
+
+
+def _collinear_last(pts):
+    """haveCollinearPoints (fundam.cpp) for the last selected point (float32 coordinates)."""
+    pts = np.asarray(pts, np.float32)
+    i = len(pts) - 1
+    for j in range(i):
+        dx1, dy1 = float(pts[j, 0] - pts[i, 0]), float(pts[j, 1] - pts[i, 1])
+        for k in range(j):
+            dx2, dy2 = float(pts[k, 0] - pts[i, 0]), float(pts[k, 1] - pts[i, 1])
+            if abs(dx2 * dy1 - dy2 * dx1) <= np.finfo(np.float32).eps * (abs(dx1) + abs(dy1) + abs(dx2) + abs(dy2)):
+                return True
+    return False
+
+
+def cv_ransac(k1, k2, K=None, thr=3.0, confidence=0.999, max_iters=1000):
+    """cv2.findEssentialMat(k1, k2, K, RANSAC, confidence, thr) when K is given, else
+    cv2.findFundamentalMat(k1, k2, FM_RANSAC, thr, confidence) for >= 15 matches:
+    OpenCV's sample stream (cv::RNG((uint64)-1), getSubset with duplicate redraw and,
+    for F, the collinearity checkSubset), a model replaces the best iff its inlier
+    count exceeds max(best, modelPoints - 1), each replacement shrinks the budget by
+    RANSACUpdateNumIters.  Returns (model 3x3 or None, bool mask, inlier count)."""
+    k1 = np.asarray(k1, np.float32)
+    k2 = np.asarray(k2, np.float32)
+    n = len(k1)
+    if K is not None:
+        m = 5
+        p1, p2 = normalize(k1, K), normalize(k2, K)
+        t = thr / ((K[0, 0] + K[1, 1]) / 2)
+        t2 = np.float32(t * t)
+
+        def solve(idx):
+            return five_point(p1[idx], p2[idx])
+
+        def err(M):
+            return sampson_error(M, p1, p2)
+    else:
+        m = 7
+        if n < 15:
+            raise NotImplementedError("fewer than 15 matches: OpenCV switches FM_RANSAC to LMedS")
+        t2 = np.float32(thr * thr)
+
+        def solve(idx):
+            return seven_point(k1[idx].astype(np.float64), k2[idx].astype(np.float64))
+
+        def err(M):
+            return epiline_error(M, k1, k2)
+    if n < m:
+        return None, np.zeros(n, bool), 0
+    if n == m:
+        sols = solve(np.arange(m))
+        return (sols[0] if sols else None), np.ones(n, bool) if sols else np.zeros(n, bool), (n if sols else 0)
+    rng = CvRng()
+    niters, max_good, best, best_mask = max_iters, 0, None, np.zeros(n, bool)
+    it = 0
+    while it < niters:
+        found = False
+        for _attempt in range(10000):
+            idx = []
+            for _i in range(m):
+                while True:
+                    v = rng.uniform(0, n)
+                    if v not in idx:
+                        break
+                idx.append(v)
+            if m == 7 and (_collinear_last(k1[idx]) or _collinear_last(k2[idx])):
+                continue
+            found = True
+            break
+        if not found:
+            break
+        for M in solve(np.array(idx)):
+            mask = err(M) <= t2
+            g = int(mask.sum())
+            if g > max(max_good, m - 1):
+                max_good, best, best_mask = g, M, mask
+                niters = update_num_iters(confidence, (n - g) / n, m, niters)
+        it += 1
+    if max_good == 0:
+        return None, np.zeros(n, bool), 0
+    return best, best_mask, max_good

@@ -186,3 +186,29 @@ def test_library_exports_every_header_symbol():
     assert L.mlg_vit_workspace_bytes(64, 322) > 0
     assert L.mlg_vit_workspace_bytes(64, 300) == 0
     assert L.mlg_strerror(-1).decode().startswith("invalid")
+
+
+def test_torch_ops_registered():
+    """libmlgate_torch.so loads without a GPU and registers every torch.ops.mlgate operator
+    the package calls, each with a CUDA (= HIP on ROCm) kernel."""
+    import torch
+    ops = _native.ops()
+    for name in _native.OPS:
+        op = getattr(ops, name)
+        assert op.default._schema.name == f"mlgate::{name}"
+    for name in _native.OPS:
+        if not name.startswith("prof_"):
+            assert torch._C._dispatch_has_kernel_for_dispatch_key(f"mlgate::{name}", "CUDA"), name
+    # no CPU kernel: the ops fail loudly on host tensors instead of falling back
+    with pytest.raises(NotImplementedError):
+        ops.row_normalize(torch.ones(2, 4))
+
+
+def test_package_calls_compute_only_through_torch_ops():
+    """No module of the package calls the C ABI through ctypes (only _native does, for the
+    op-level tests); compute goes through torch.ops.mlgate."""
+    pkg = os.path.join(ROOT, "multi-level-indoor-slam_amd", "mlgate")
+    for f in os.listdir(pkg):
+        if f.endswith(".py") and f != "_native.py":
+            src = open(os.path.join(pkg, f)).read()
+            assert "_native.lib()" not in src and "import ctypes" not in src, f
