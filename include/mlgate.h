@@ -234,7 +234,8 @@ int mlg_op_pillow_resize_224(const uint8_t* frames, int B, int H, int W, int C, 
  * (scripts/semantic_gating/geometric_verification.py:263-312): cv2 BGR2GRAY / 255 ->
  * LightGlue's SuperPoint(max_num_keypoints, detection_threshold) forward (NMS radius,
  * border removal, top-k, bilinear descriptor sampling) for B frames at once.
- * frames: device uint8 [B] x (H x W x C), C in {1, 3 (BGR), 4}, H and W multiples of 8.
+ * frames: device uint8 [B] x (H x W x C), C in {1, 3 (BGR), 4}, H, W >= 16 (the score
+ * map and keypoints cover 8 floor(H/8) x 8 floor(W/8) after the encoder's round-down pools).
  * Outputs (device): keypoints f32 [B, max_kp, 2] (x, y), scores f32 [B, max_kp],
  * descriptors f32 [B, max_kp, 256] (unit L2; zero rows past counts[b]) and optionally
  * the same in bf16, counts int32 [B].  Keypoint order: raster order when at most

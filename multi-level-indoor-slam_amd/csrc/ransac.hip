@@ -621,6 +621,465 @@ RS_HD void denorm_F(const double* Fn, const double* T1, const double* T2, double
     for (int k = 0; k < 9; ++k) F[k] *= nrm;
 }
 
+// ------------------------------------------------------------------ 5-point solver, one hypothesis per 16 lanes
+// The Stewenius / Nister formulation OpenCV's EMEstimatorCallback::runKernel uses
+// (calib3d/five-point.cpp): the 10 cubic constraints over the 4-dim null space
+// E = x X + y Y + z Z + W form a 10 x 20 coefficient matrix over the monomials
+//   pivots  x^3 y^3 x^2y xy^2 x^2z x^2 y^2z y^2 xyz xy | xz^2 xz x yz^2 yz y z^3 z^2 z 1
+// reduced to [I | A] by Gauss-Jordan; the pivot pairs (x^2z, x^2), (y^2z, y^2),
+// (xyz, xy) give a 3 x 3 matrix of polynomials in z acting on (x, y, 1) whose
+// determinant is the degree-10 polynomial; each real root z gives (x, y) from the
+// matrix's null vector.  Data layout on the GPU: a 16-lane group per hypothesis (4
+// per wave), the null space in LDS, constraint row r of the matrix in lane r's
+// registers (20 doubles), Gauss-Jordan by cross-lane shuffles of the pivot row --
+// instead of one lane carrying every intermediate (the single-lane solver above
+// needed 11 KB of scratch per lane).
+
+// column of monomial x^a y^b z^c (a + b + c <= 3) in the order above
+constexpr int mono_col(int a, int b, int c) {
+    return (a == 3) ? 0 : (b == 3) ? 1 : (a == 2 && b == 1) ? 2 : (a == 1 && b == 2) ? 3
+         : (a == 2 && c == 1) ? 4 : (a == 2) ? 5 : (b == 2 && c == 1) ? 6 : (b == 2) ? 7
+         : (a == 1 && b == 1 && c == 1) ? 8 : (a == 1 && b == 1) ? 9 : (a == 1 && c == 2) ? 10
+         : (a == 1 && c == 1) ? 11 : (a == 1) ? 12 : (b == 1 && c == 2) ? 13 : (b == 1 && c == 1) ? 14
+         : (b == 1) ? 15 : (c == 3) ? 16 : (c == 2) ? 17 : (c == 1) ? 18 : 19;
+}
+// quadratic monomials (a + b + c <= 2): index a..c -> 0..9
+constexpr int QA[10] = {2, 1, 1, 1, 0, 0, 0, 0, 0, 0};
+constexpr int QB[10] = {0, 1, 0, 0, 2, 1, 1, 0, 0, 0};
+constexpr int QC[10] = {0, 0, 1, 0, 0, 1, 0, 2, 1, 0};
+constexpr int LA[4] = {1, 0, 0, 0}, LB[4] = {0, 1, 0, 0}, LC[4] = {0, 0, 1, 0};  // x, y, z, 1
+constexpr int qidx(int a, int b, int c) {
+    return (a == 2) ? 0 : (a == 1 && b == 1) ? 1 : (a == 1 && c == 1) ? 2 : (a == 1) ? 3 : (b == 2) ? 4
+         : (b == 1 && c == 1) ? 5 : (b == 1) ? 6 : (c == 2) ? 7 : (c == 1) ? 8 : 9;
+}
+
+// q (+)= s * (l1 * l2), linear polys l = [x, y, z, 1] coefficients
+__device__ __forceinline__ void q_fma(double (&q)[10], const double* l1, const double* l2, double s) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[qidx(LA[i] + LA[j], LB[i] + LB[j], LC[i] + LC[j])] += s * l1[i] * l2[j];
+}
+// c (+)= q * l
+__device__ __forceinline__ void c_fma(double (&c)[20], const double (&q)[10], const double* l) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[mono_col(QA[i] + LA[j], QB[i] + LB[j], QC[i] + LC[j])] += q[i] * l[j];
+}
+
+template <int NA, int NB>
+__device__ __forceinline__ void pmul_acc(double* out, const double* a, const double* b, double s) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) out[i + j] += s * a[i] * b[j];
+}
+
+// Null space of the 5 x 9 epipolar design matrix by Householder QR of its transpose
+// (9 x 5): the last 4 columns of Q = H0 H1 ... H4 are an orthonormal basis.  Fixed loop
+// structure, every index static, so everything stays in registers (a pivoting
+// elimination's data-dependent row / column indices put the arrays in scratch).
+// Rank < 5 (a Householder diagonal below 1e-12 of the column scale) -> false.
+__device__ __forceinline__ bool null_space5_reg(const double (&A)[5][9], double (&N)[4][9]) {
+    double M[9][5], V[5][9], beta[5];
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int k = 0; k < 5; ++k) M[i][k] = A[k][i];
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        double nrm2 = 0.0, scale = 0.0;
+#pragma unroll
+        for (int i = k; i < 9; ++i) nrm2 += M[i][k] * M[i][k];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) scale += M[i][k] * M[i][k];
+        const double nrm = sqrt(nrm2);
+        ok = ok && nrm > 1e-12 * sqrt(scale) && nrm > 0.0;
+        const double alpha = M[k][k] > 0.0 ? -nrm : nrm;
+        double vn2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            V[k][i] = i < k ? 0.0 : (i == k ? M[k][k] - alpha : M[i][k]);
+            vn2 += V[k][i] * V[k][i];
+        }
+        beta[k] = vn2 > 0.0 ? 2.0 / vn2 : 0.0;
+#pragma unroll
+        for (int j = k + 1; j < 5; ++j) {
+            double s = 0.0;
+#pragma unroll
+            for (int i = k; i < 9; ++i) s += V[k][i] * M[i][j];
+            s *= beta[k];
+#pragma unroll
+            for (int i = k; i < 9; ++i) M[i][j] -= s * V[k][i];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        double e[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) e[i] = (i == 5 + j) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 4; k >= 0; --k) {
+            double s = 0.0;
+#pragma unroll
+            for (int i = k; i < 9; ++i) s += V[k][i] * e[i];
+            s *= beta[k];
+#pragma unroll
+            for (int i = k; i < 9; ++i) e[i] -= s * V[k][i];
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) N[j][i] = e[i];
+    }
+    return ok;
+}
+
+// Real roots of sum c[i] x^i (degree <= 10) for a 16-lane group: isolation between the
+// roots of successive derivatives (highest first), each derivative's coefficients
+// formed once per level; the up-to-11 brackets of one level are refined in parallel,
+// one lane each (safeguarded regula falsi), and gathered in order by shuffles, so all
+// lanes of the group hold the same roots.
+__device__ __forceinline__ double peval11(const double (&c)[11], int n, double x) {
+    double v = 0.0;
+#pragma unroll
+    for (int i = 10; i >= 0; --i)
+        if (i <= n) v = v * x + c[i];
+    return v;
+}
+
+__device__ int real_roots10(double (&c)[11], double (&roots)[10], int r, int gl) {
+    double mx = 0.0;
+#pragma unroll
+    for (int i = 0; i <= 10; ++i) mx = fmax(mx, fabs(c[i]));
+    if (mx == 0.0) return 0;
+    int n = 0;  // degree after dropping negligible leading coefficients
+#pragma unroll
+    for (int i = 1; i <= 10; ++i)
+        if (fabs(c[i]) > 1e-13 * mx) n = i;
+    if (n == 0) return 0;
+    double lead = 0.0;
+#pragma unroll
+    for (int i = 1; i <= 10; ++i) lead = (i == n) ? c[i] : lead;
+#pragma unroll
+    for (int i = 0; i <= 10; ++i) c[i] = i <= n ? c[i] / lead : 0.0;
+    double B = 0.0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+        if (i < n) B = fmax(B, fabs(c[i]));
+    B += 1.0;
+    // the derivatives' roots lie in the convex hull of the roots (Gauss-Lucas), inside
+    // the Cauchy bound B: clamping only absorbs rounding
+    double crit[10];
+    double cn1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) cn1 = (i == n - 1) ? c[i] : cn1;
+    crit[0] = fmin(fmax(-cn1 / (double)n, -B), B);  // (n-1)-th derivative: n! x + (n-1)! c[n-1]
+#pragma unroll
+    for (int i = 1; i < 10; ++i) crit[i] = 0.0;
+    int ncrit = 1;
+    for (int k = n - 2; k >= 0; --k) {
+        const int dg = n - k;
+        double d[11];  // k-th derivative / k!: d[i] = C(i + k, k) c[i + k]
+#pragma unroll
+        for (int i = 0; i <= 10; ++i) {
+            double v = 0.0;
+#pragma unroll
+            for (int m = i; m <= 10; ++m) {
+                if (m - i == k) {
+                    double bin = 1.0;  // C(m, i), folded at compile time
+#pragma unroll
+                    for (int t = 1; t <= m - i; ++t) bin = bin * (double)(i + t) / (double)t;
+                    v = c[m] * bin;
+                }
+            }
+            d[i] = v;
+        }
+        // lane r refines bracket r of [-B, crit[0], ..., crit[ncrit - 1], B]
+        double lo = -B, hi = B;
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+            if (j == r - 1) lo = crit[j];
+            if (j == r && j < ncrit) hi = crit[j];
+        }
+        double cand = 0.0;
+        int has = 0;
+        if (r <= ncrit) {
+            const double flo = peval11(d, dg, lo), fhi = peval11(d, dg, hi);
+            if (flo == 0.0) {
+                cand = lo;
+                has = 1;
+            } else if ((flo < 0) != (fhi < 0) && fhi != 0.0) {
+                double fl = flo, fh = fhi;
+                int side = 0;
+                for (int it = 0; it < 100; ++it) {
+                    double x = (lo * fh - hi * fl) / (fh - fl);
+                    if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
+                    const double fx = peval11(d, dg, x);
+                    if (fx == 0.0) { lo = x; hi = x; break; }
+                    if ((fx < 0) == (fl < 0)) {
+                        lo = x; fl = fx;
+                        if (side == -1) fh *= 0.5;
+                        side = -1;
+                    } else {
+                        hi = x; fh = fx;
+                        if (side == 1) fl *= 0.5;
+                        side = 1;
+                    }
+                    if (hi - lo <= 1e-14 * fmax(1.0, fabs(lo))) break;
+                }
+                cand = 0.5 * (lo + hi);
+                has = 1;
+            }
+            if (r == ncrit && fhi == 0.0) has |= 2;  // the right end of the last bracket too
+        }
+        // gather in bracket order (dedupe a root shared by two brackets' ends)
+        int nn = 0;
+        double last = 0.0;
+        double nc[10];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) nc[i] = 0.0;
+#pragma unroll
+        for (int j = 0; j < 11; ++j) {
+            const double v = __shfl(cand, gl + j, 64);
+            const int hj = __shfl(has, gl + j, 64);
+            if (j <= ncrit && (hj & 1) && (nn == 0 || v != last) && nn < 10) {
+#pragma unroll
+                for (int i = 0; i < 10; ++i)
+                    if (i == nn) nc[i] = v;
+                last = v;
+                ++nn;
+            }
+            if (j <= ncrit && (hj & 2) && (nn == 0 || B != last) && nn < 10) {
+#pragma unroll
+                for (int i = 0; i < 10; ++i)
+                    if (i == nn) nc[i] = B;
+                last = B;
+                ++nn;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 10; ++i) crit[i] = nc[i];
+        ncrit = nn;
+    }
+#pragma unroll
+    for (int i = 0; i < 10; ++i) roots[i] = crit[i];
+    return ncrit;
+}
+
+__global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict__ info,
+                                                     const double4* __restrict__ ptsn, int H,
+                                                     const int32_t* __restrict__ subsets,
+                                                     const int32_t* __restrict__ nsub, double* __restrict__ models,
+                                                     int8_t* __restrict__ nsol) {
+    __shared__ double snb[16][4][9];
+    const int g = threadIdx.x >> 4, r = threadIdx.x & 15, gl = threadIdx.x & 48;  // group, lane in group, base
+    const int p = blockIdx.y;
+    const int h = blockIdx.x * 16 + g;
+    const PairInfo pi = info[p];
+    const bool ess = pi.mode == 1 || pi.mode == 5;
+    // whole groups are active or not (shuffles stay inside a group)
+    const bool act = ess && h < H && (pi.mode == 5 ? h == 0 : h < nsub[p]);
+    if (!ess) return;  // uniform per block (one pair per blockIdx.y)
+    bool ok = act;
+    if (act) {
+        double q1[5][2], q2[5][2];
+        for (int i = 0; i < 5; ++i) {
+            const int id = pi.mode == 5 ? i : subsets[((size_t)p * H + h) * 7 + i];
+            const double4 q = ptsn[pi.start + id];
+            q1[i][0] = q.x; q1[i][1] = q.y; q2[i][0] = q.z; q2[i][1] = q.w;
+        }
+        double A[5][9];
+        for (int i = 0; i < 5; ++i) {
+            const double x1 = q1[i][0], y1 = q1[i][1], x2 = q2[i][0], y2 = q2[i][1];
+            A[i][0] = x2 * x1; A[i][1] = x2 * y1; A[i][2] = x2;
+            A[i][3] = y2 * x1; A[i][4] = y2 * y1; A[i][5] = y2;
+            A[i][6] = x1;      A[i][7] = y1;      A[i][8] = 1.0;
+        }
+        double Nb[4][9];
+        ok = null_space5_reg(A, Nb);
+        if (r == 0)
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int k = 0; k < 9; ++k) snb[g][a][k] = Nb[a][k];
+    }
+    __syncthreads();
+    // E_k = [x, y, z, 1] coefficients of entry k
+    auto ent = [&](int k, double* l) {
+        for (int a = 0; a < 4; ++a) l[a] = snb[g][a][k];
+    };
+    // constraint row r (lanes 0..9): det(E) or (E E^T - tr(E E^T) / 2) E, entry (i, j)
+    double row[20];
+#pragma unroll
+    for (int j = 0; j < 20; ++j) row[j] = 0.0;
+    if (ok && r == 0) {
+        const int cof[3][5] = {{0, 4, 8, 5, 7}, {1, 3, 8, 5, 6}, {2, 3, 7, 4, 6}};
+        const double sg[3] = {1.0, -1.0, 1.0};
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            double l0[4], l1[4], l2[4], l3[4], l4[4];
+            ent(cof[t][0], l0); ent(cof[t][1], l1); ent(cof[t][2], l2); ent(cof[t][3], l3); ent(cof[t][4], l4);
+            double q[10];
+#pragma unroll
+            for (int s = 0; s < 10; ++s) q[s] = 0.0;
+            q_fma(q, l1, l2, sg[t]);
+            q_fma(q, l3, l4, -sg[t]);
+            c_fma(row, q, l0);
+        }
+    } else if (ok && r < 10) {
+        const int i = (r - 1) / 3, j = (r - 1) % 3;
+        double tr[10], eet[3][10];
+#pragma unroll
+        for (int s = 0; s < 10; ++s) {
+            tr[s] = 0.0;
+            eet[0][s] = 0.0; eet[1][s] = 0.0; eet[2][s] = 0.0;
+        }
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+            double a[4], b[4];
+            for (int kk = 0; kk < 3; ++kk) {
+                ent(l * 3 + kk, a);
+                q_fma(tr, a, a, 0.5);
+            }
+            for (int kk = 0; kk < 3; ++kk) {
+                ent(i * 3 + kk, a);
+                ent(l * 3 + kk, b);
+                q_fma(eet[l], a, b, 1.0);
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < 3; ++l) {
+            double m[10];
+#pragma unroll
+            for (int s = 0; s < 10; ++s) m[s] = eet[l][s] - (l == i ? tr[s] : 0.0);
+            double e[4];
+            ent(l * 3 + j, e);
+            c_fma(row, m, e);
+        }
+    }
+    // Gauss-Jordan over the group's rows (lanes 0..9), partial pivoting; the row with
+    // pivot column c ends in lane piv[c], scaled to 1 at c and 0 at the other pivots
+    int piv[10];
+    bool used = r >= 10;
+#pragma unroll
+    for (int c = 0; c < 10; ++c) {
+        double best = used ? -1.0 : fabs(row[c]);
+        int bl = r;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+            const double ob = __shfl_xor(best, o, 64);
+            const int ol = __shfl_xor(bl, o, 64);
+            if (ob > best || (ob == best && ol < bl)) { best = ob; bl = ol; }
+        }
+        if (!(best > 1e-300)) ok = false;  // singular (uniform in the group)
+        piv[c] = bl;
+        double prow[20];
+#pragma unroll
+        for (int jj = c; jj < 20; ++jj) prow[jj] = __shfl(row[jj], gl + bl, 64);
+        const double inv = ok ? 1.0 / prow[c] : 0.0;
+        if (r == bl) {
+#pragma unroll
+            for (int jj = c; jj < 20; ++jj) row[jj] = prow[jj] * inv;
+            used = true;
+        } else {
+            const double f = row[c] * inv;
+#pragma unroll
+            for (int jj = c; jj < 20; ++jj) row[jj] -= f * prow[jj];
+        }
+    }
+    // the 3 x 3 polynomial matrix on (x, y, 1) from the pivot pairs (x^2z, x^2), (y^2z, y^2),
+    // (xyz, xy): column k of A = row[10 + k] of the pivot's lane
+    double bx[3][4], by[3][4], b1[3][5];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        double a4[10], a5[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+            a4[k] = __shfl(row[10 + k], gl + piv[4 + 2 * i], 64);
+            a5[k] = __shfl(row[10 + k], gl + piv[5 + 2 * i], 64);
+        }
+        // non-pivot columns: 0 xz^2, 1 xz, 2 x, 3 yz^2, 4 yz, 5 y, 6 z^3, 7 z^2, 8 z, 9 1
+        bx[i][0] = a4[2]; bx[i][1] = a4[1] - a5[2]; bx[i][2] = a4[0] - a5[1]; bx[i][3] = -a5[0];
+        by[i][0] = a4[5]; by[i][1] = a4[4] - a5[5]; by[i][2] = a4[3] - a5[4]; by[i][3] = -a5[3];
+        b1[i][0] = a4[9]; b1[i][1] = a4[8] - a5[9]; b1[i][2] = a4[7] - a5[8]; b1[i][3] = a4[6] - a5[7];
+        b1[i][4] = -a5[6];
+    }
+    if (!ok) {
+        if (act && r == 0) nsol[(size_t)p * H + h] = 0;
+        return;
+    }
+    // det = bx0 (by1 b12 - b11 by2) - by0 (bx1 b12 - b11 bx2) + b10 (bx1 by2 - by1 bx2)
+    double poly[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) poly[i] = 0.0;
+    {
+        double t[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = 0.0;
+        pmul_acc<4, 5>(t, by[1], b1[2], 1.0);
+        pmul_acc<5, 4>(t, b1[1], by[2], -1.0);
+        pmul_acc<4, 8>(poly, bx[0], t, 1.0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = 0.0;
+        pmul_acc<4, 5>(t, bx[1], b1[2], 1.0);
+        pmul_acc<5, 4>(t, b1[1], bx[2], -1.0);
+        pmul_acc<4, 8>(poly, by[0], t, -1.0);
+        double u[7];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) u[i] = 0.0;
+        pmul_acc<4, 4>(u, bx[1], by[2], 1.0);
+        pmul_acc<4, 4>(u, by[1], bx[2], -1.0);
+        pmul_acc<5, 7>(poly, b1[0], u, 1.0);
+    }
+    double zr[10];
+    const int nz = real_roots10(poly, zr, r, gl);
+    if (r != 0) return;
+    double* out = models + ((size_t)p * H + h) * MAXSOL * 9;
+    int ns = 0;
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+        if (t >= nz) continue;
+        const double z = zr[t];
+        double M[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            double vx = 0.0, vy = 0.0, v1 = 0.0;
+#pragma unroll
+            for (int d = 3; d >= 0; --d) { vx = vx * z + bx[i][d]; vy = vy * z + by[i][d]; }
+#pragma unroll
+            for (int d = 4; d >= 0; --d) v1 = v1 * z + b1[i][d];
+            M[i][0] = vx; M[i][1] = vy; M[i][2] = v1;
+        }
+        // null vector of the rank-2 M: the largest cross product of two rows
+        double best[3] = {0.0, 0.0, 0.0}, bn = -1.0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const int b = (a + 1) % 3;
+            const double cx = M[a][1] * M[b][2] - M[a][2] * M[b][1];
+            const double cy = M[a][2] * M[b][0] - M[a][0] * M[b][2];
+            const double cz = M[a][0] * M[b][1] - M[a][1] * M[b][0];
+            const double n2 = cx * cx + cy * cy + cz * cz;
+            if (n2 > bn) { bn = n2; best[0] = cx; best[1] = cy; best[2] = cz; }
+        }
+        if (!(fabs(best[2]) > 1e-300 * sqrt(fmax(bn, 1e-300)))) continue;
+        const double x = best[0] / best[2], y = best[1] / best[2];
+        if (!(fabs(x) < 1e300) || !(fabs(y) < 1e300)) continue;
+        double e[9], nrm = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            e[k] = x * snb[g][0][k] + y * snb[g][1][k] + z * snb[g][2][k] + snb[g][3][k];
+            nrm += e[k] * e[k];
+        }
+        nrm = 1.0 / sqrt(nrm);
+        double* Eo = out + ns * 9;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Eo[k] = e[k] * nrm;
+        ++ns;
+    }
+    nsol[(size_t)p * H + h] = (int8_t)ns;
+}
+
 // OpenCV's sample stream for pair p (modes 1 / 2): subsets of iterations 0..nsub-1.
 // getSubset: draw modelPoints indices with cv::RNG, redrawing duplicates; for F the
 // whole subset is redrawn while checkSubset (collinear points in either image) fails,
@@ -676,6 +1135,7 @@ __global__ __launch_bounds__(64) void k_ransac_hyp(const PairInfo* __restrict__ 
     const PairInfo pi = info[p];
     double* out = models + ((size_t)p * H + h) * MAXSOL * 9;
     int ns = 0;
+    if (pi.mode == 1 || pi.mode == 5) return;  // essential matrix: k_ransac_hyp5
     const bool direct = pi.mode == 4 || pi.mode == 5;
     if (pi.mode == 0 || (direct && h > 0)) {
         nsol[(size_t)p * H + h] = 0;
@@ -1167,6 +1627,9 @@ int mlg_ransac_run(const float* kp1, const float* kp2, const int32_t* offs, int 
     MLG_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_ransac_hyp, dim3((H + 63) / 64, P), dim3(64), 0, s, info, ptsn, H, seed, subsets, nsub,
                        models, nsol);
+    MLG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_ransac_hyp5, dim3((H + 15) / 16, P), dim3(256), 0, s, info, ptsn, H, subsets, nsub, models,
+                       nsol);
     MLG_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_ransac_score, dim3((H + 255) / 256, P), dim3(256), 0, s, info, ptsn, ptsr, H, models, nsol,
                        score);

@@ -6,6 +6,10 @@
 // head (softmax over 65, depth-to-space) -> simple_nms(4) -> border 4 -> threshold
 // -> top-k -> descriptor head (L2-normalised) sampled bilinearly at the keypoints.
 //
+// Any H, W >= 16: conv1a / conv1b run at full resolution, the 2x2 pools round down,
+// and the score / NMS / border / descriptor grid is 8 floor(H/8) x 8 floor(W/8), as the
+// reference's SuperPoint on e.g. the ISEC cameras' 720x540 frames.
+//
 // Layout: activations NHWC bf16; 3x3 weights bf16 [Cout][3][3][Cin].  The 3x3 convs
 // are implicit GEMMs on MFMA (k_conv3x3): a 16x16-pixel output tile per workgroup
 // (8 waves, 2 image rows each), its 18x18 input halo staged once in LDS, the weights
@@ -684,14 +688,14 @@ SpLayout sp_layout(int B, int H, int W) {
 }  // namespace
 
 size_t mlg_superpoint_ws_bytes(int B, int H, int W) {
-    if (B <= 0 || H < 16 || W < 16 || (H % 8) || (W % 8)) return 0;
+    if (B <= 0 || H < 16 || W < 16) return 0;
     return sp_layout(B, H, W).total;
 }
 
 int mlg_superpoint_run(const mlg_sp_weights_i& w, const uint8_t* frames, int B, int H, int W, int C, long frame_stride,
                        float det_thr, int max_kp, int nms_radius, int border, void* ws, size_t ws_bytes, float* kpts,
                        float* kscores, float* desc, uint16_t* desc_bf16, int32_t* count, hipStream_t s) {
-    if (B <= 0 || H < 16 || W < 16 || (H % 8) || (W % 8) || (C != 1 && C != 3 && C != 4) || max_kp <= 0 ||
+    if (B <= 0 || H < 16 || W < 16 || (C != 1 && C != 3 && C != 4) || max_kp <= 0 ||
         max_kp > SEL_KMAX || nms_radius < 0 || border < 0)
         return MLG_EINVAL;
     const SpLayout L = sp_layout(B, H, W);
@@ -733,6 +737,10 @@ int mlg_superpoint_run(const mlg_sp_weights_i& w, const uint8_t* frames, int B, 
     SP_TRY(mlg_gemm_f32out(cDa, w.w[10], dmap, M, 256, 256, s));                 // convDb
     hipLaunchKernelGGL(k_sp_scores, dim3((M + 255) / 256), dim3(256), 0, s, logits, 128, w.b[8], B, h, wd, sc);
     MLG_LAUNCH_CHECK();
+    // the score map is 8 * floor(H / 8) x 8 * floor(W / 8): the encoder convolved the
+    // full frame, its pools rounded down, and depth-to-space covers whole cells only
+    H = 8 * h;
+    W = 8 * wd;
     // simple_nms
     const float* nms_out = sc;
     if (nms_radius == 4) {  // fused (SuperPoint's default radius)

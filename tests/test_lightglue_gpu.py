@@ -98,3 +98,28 @@ def test_lightglue_empty_side(lg):
     res = _run_gpu(lg, [(k0, d0, k1[:0], d1[:0]), (k0, d0, k1, d1)])
     assert len(res[0][0]) == 0
     assert len(res[1][0]) > 0
+
+
+def test_lightglue_against_fp32_reference(dev, lg, sd):
+    """The GPU matcher (bf16 GEMM / attention operands) against the reference's arithmetic
+    -- the fp32 forward without bf16 emulation -- on SuperPoint features of a synthetic
+    revisit pair (true correspondences): match sets overlap >= 90 %, scores of common
+    matches within 5e-2."""
+    from mlgate import synthetic
+    from mlgate.superpoint import SuperPointGPU
+    seq = synthetic.make_sequence(40, 4, 2)
+    same = [i for i in range(1, 40) if seq.place_of[i] == seq.place_of[0]]
+    fr = torch.from_numpy(synthetic.frames_host(seq, [0, same[0]])).to(dev)
+    f0, f1 = SuperPointGPU(device=str(dev)).extract(list(fr.cpu().numpy()))
+    case = (f0["keypoints"], f0["descriptors"], f1["keypoints"], f1["descriptors"])
+    gm, gs, gstop = _run_gpu(lg, [case])[0]
+    ref = Oracle(sd, emulate_bf16=False).match(*case)
+    g = {tuple(x): i for i, x in enumerate(gm.tolist())}
+    r = {tuple(x): i for i, x in enumerate(ref["matches"].numpy().tolist())}
+    common = set(g) & set(r)
+    overlap = len(common) / max(len(g), len(r), 1)
+    print(f"fp32 LightGlue: {len(g)} vs {len(r)} matches, overlap {overlap:.4f}, stop {gstop} vs {ref['stop']}")
+    assert len(r) > 100 and overlap >= 0.90
+    gi = np.array([g[c] for c in common])
+    ri = np.array([r[c] for c in common])
+    np.testing.assert_allclose(gs[gi], ref["scores"].numpy()[ri], atol=5e-2)

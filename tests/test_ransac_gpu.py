@@ -36,15 +36,16 @@ def test_ransac_masks_match_oracle_and_truth(dev, use_k):
         om = G.inlier_mask(r.model, k1, k2, K if use_k else None, 3.0)
         assert np.array_equal(r.mask, om)
         assert r.inliers == int(om.sum())
-        # (3) against the true model.  Plain RANSAC over minimal samples (as OpenCV's)
-        # lands within a few percent of the true inlier set when inliers dominate; at
-        # 50 % outliers the 7-point F hypotheses are rarer and noisier, so only a
-        # weaker bound holds there (OpenCV's RANSAC has the same limitation).
+        # (3) against the true model.  OpenCV's RANSAC (restated exactly: adaptive stop
+        # at confidence 0.999, no refinement) keeps the first minimal-sample model good
+        # enough to end the loop, so its mask lands within a few percent of the true
+        # inlier set when inliers dominate (7-point F models are the noisier); at 50 %
+        # outliers only a weaker bound holds.
         truth = G.essential_from_pose(R, t) if use_k else G.fundamental_from_pose(R, t, K)
         tm = G.inlier_mask(truth, k1, k2, K if use_k else None, 3.0)
         if inl.mean() >= 0.6 or (use_k and inl.mean() >= 0.4):
-            assert np.sum(r.mask != tm) <= max(2, 0.03 * len(k1)), (np.sum(r.mask != tm), len(k1))
-            assert np.sum(r.mask & inl) >= 0.95 * inl.sum()
+            assert np.sum(r.mask != tm) <= max(2, (0.03 if use_k else 0.06) * len(k1)), (np.sum(r.mask != tm), len(k1))
+            assert np.sum(r.mask & inl) >= (0.95 if use_k else 0.9) * inl.sum()
         elif inl.mean() >= 0.4:
             assert np.sum(r.mask & inl) >= 0.6 * inl.sum()
             assert np.sum(r.mask & ~tm) <= 0.05 * len(k1)
@@ -57,8 +58,9 @@ def test_recover_pose_close_to_truth(dev):
     res = geometry.epipolar_ransac([p[0] for p in pairs], [p[1] for p in pairs], K, 3.0, device=str(dev))
     for (k1, k2, R, t, inl), r in zip(pairs, res):
         assert r.pose is not None
-        # E from a noisy minimal sample (0.5 px): pose within a few degrees of truth
-        assert G.rotation_angle_deg(r.pose[:3, :3], R) < 2.5
+        # E from a noisy minimal sample (0.5 px), no refinement (as OpenCV): pose within
+        # a few degrees of truth
+        assert G.rotation_angle_deg(r.pose[:3, :3], R) < 5.0
         assert np.degrees(np.arccos(np.clip(r.pose[:3, 3] @ t, -1, 1))) < 10.0
         # the GPU pose of the returned E equals the oracle's recoverPose of that E
         good, Ro, to = G.recover_pose(r.model, k1[r.mask], k2[r.mask], K)
@@ -138,3 +140,19 @@ def test_verifier_decisions_batched_vs_single(dev):
         assert b.is_valid == (n_in >= 20 and ratio >= 0.25)
         truth_valid = inl.sum() >= 20 and inl.sum() / len(k1) >= 0.25
         assert b.is_valid == truth_valid
+
+
+@pytest.mark.parametrize("use_k", [True, False])
+def test_ransac_follows_opencv_loop(dev, use_k):
+    """The GPU runs OpenCV's RANSACPointSetRegistrator::run: cv::RNG((uint64)-1) sample
+    stream, strict-improvement updates, RANSACUpdateNumIters stop.  The numpy
+    restatement of that loop (oracle.geometry.cv_ransac) must reach the same inlier count
+    -- up to points within rounding of the threshold under the two solvers' slightly
+    different minimal-sample models (<= 0.3 %)."""
+    specs = [(300, 100), (150, 150), (800, 200), (60, 40), (1000, 30), (30, 300)]
+    pairs = _pairs(31 if use_k else 32, specs)
+    res = geometry.epipolar_ransac([p[0] for p in pairs], [p[1] for p in pairs], K if use_k else None, 3.0,
+                                   device=str(dev))
+    for (k1, k2, *_), r in zip(pairs, res):
+        _, mask, n_in = G.cv_ransac(k1, k2, K if use_k else None, 3.0)
+        assert abs(r.inliers - n_in) <= max(1, 0.003 * len(k1)), (len(k1), r.inliers, n_in)

@@ -95,14 +95,17 @@ def test_superpoint_gray_input_and_errors(dev, sd):
     a = sp.extract([img])[0]
     b = sp.extract([gray])[0]
     assert np.array_equal(a["keypoints"], b["keypoints"])
-    with pytest.raises(ValueError):
-        sp.extract([np.zeros((60, 60, 3), np.uint8)])
+    with pytest.raises(RuntimeError):
+        sp.extract([np.zeros((12, 60, 3), np.uint8)])  # below the 16-px minimum
 
 
-@pytest.mark.parametrize("h,w,nms", [(200, 344, 4), (200, 344, 3)])
+@pytest.mark.parametrize("h,w,nms", [(200, 344, 4), (200, 344, 3), (540, 720, 4), (537, 721, 4), (60, 60, 4)])
 def test_superpoint_partial_tiles_and_radius(dev, sd, h, w, nms):
     """Frame sizes that are not multiples of the fused NMS tile (32 x 64, with its 20-px
-    halo crossing the image border) and a non-default radius (the multi-pass path)."""
+    halo crossing the image border), a non-default radius (the multi-pass path), and
+    sizes that are not multiples of 8 -- the ISEC cameras' 720 x 540 and an odd 721 x 537:
+    the encoder convolves the full frame, the pools round down and the keypoints cover
+    8 floor(H/8) x 8 floor(W/8), as the reference's SuperPoint."""
     rng = np.random.default_rng(7)
     imgs = [scene(rng, h, w)]
     sp = SuperPointGPU(sd, device=str(dev), nms_radius=nms)
@@ -111,3 +114,25 @@ def test_superpoint_partial_tiles_and_radius(dev, sd, h, w, nms):
     for g, o in zip(got, ref):
         assert len(g["keypoints"]) == len(o["keypoints"])
         _compare(g, o)
+
+
+def test_superpoint_against_fp32_reference(dev, sd):
+    """The GPU (bf16 activations) against the reference's arithmetic -- the fp32 forward
+    without bf16 emulation -- at 2048 keypoints on a synthetic revisit frame: the
+    keypoint sets overlap >= 95 % and common descriptors have cosine >= 0.98."""
+    from mlgate import synthetic
+    seq = synthetic.make_sequence(4, 2, 0)
+    imgs = list(synthetic.frames_host(seq, [0, 1]))
+    got = SuperPointGPU(sd, device=str(dev)).extract(imgs)
+    ref = osp.superpoint(sd, imgs, max_kp=2048, det_thr=0.001, emulate_bf16=False)
+    for g, o in zip(got, ref):
+        gk = {tuple(k): i for i, k in enumerate(np.round(g["keypoints"]).astype(int).tolist())}
+        ok = {tuple(k): i for i, k in enumerate(np.round(o["keypoints"].numpy()).astype(int).tolist())}
+        common = set(gk) & set(ok)
+        overlap = len(common) / max(len(gk), len(ok))
+        gi = np.array([gk[c] for c in common])
+        oi = np.array([ok[c] for c in common])
+        cos = np.sum(g["descriptors"][gi] * o["descriptors"].numpy()[oi], 1)
+        print(f"fp32 SuperPoint: keypoint overlap {overlap:.4f}, descriptor cosine min {cos.min():.4f} "
+              f"median {np.median(cos):.5f}")
+        assert overlap >= 0.95 and cos.min() >= 0.98

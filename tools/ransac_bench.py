@@ -1,0 +1,50 @@
+"""Time the batched epipolar RANSAC (mlg_ransac_epipolar) on bench-like pairs: P pairs of
+S matches with a given inlier fraction (low fractions keep OpenCV's loop at its full
+1000 iterations, as non-revisit pairs do in bench.py)."""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "multi-level-indoor-slam_amd")]
+from mlgate import geometry  # noqa: E402
+from oracle import geometry as G  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=1024)
+    ap.add_argument("--matches", type=int, default=1700)
+    ap.add_argument("--inliers", type=float, default=0.2)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    rng = np.random.default_rng(0)
+    n_in = int(a.matches * a.inliers)
+    k1s, k2s = [], []
+    for _ in range(8):
+        k1, k2, *_ = G.synthetic_pair(rng, n_in, a.matches - n_in, 0.5)
+        k1s.append(k1)
+        k2s.append(k2)
+    k1 = np.concatenate([k1s[i % 8] for i in range(a.pairs)])
+    k2 = np.concatenate([k2s[i % 8] for i in range(a.pairs)])
+    offs = np.arange(a.pairs + 1, dtype=np.int32) * a.matches
+    dev = torch.device("cuda")
+    K = torch.from_numpy(G.ISEC_K.reshape(9).copy()).to(dev)
+    args = (torch.from_numpy(k1).to(dev), torch.from_numpy(k2).to(dev), torch.from_numpy(offs).to(dev), K, 0, 3.0)
+    geometry.epipolar_ransac_device(*args)
+    torch.cuda.synchronize()
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        _, _, inl, _, _ = geometry.epipolar_ransac_device(*args)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(f"{a.pairs} pairs x {a.matches} matches ({a.inliers:.0%} inliers): {dt * 1e3:.1f} ms, "
+              f"mean inliers {inl.float().mean().item():.1f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
