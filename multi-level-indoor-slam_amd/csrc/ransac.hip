@@ -457,6 +457,27 @@ RS_HD __forceinline__ float err_sampson(const double* E, double x1, double y1, d
     return (float)(r * r / (ex0 * ex0 + ex1 * ex1 + et0 * et0 + et1 * et1));
 }
 
+// err_sampson(E, ...) <= t2f without the division on almost every point: with
+// hi = the midpoint between t2f and the next float (the largest value that still
+// rounds to <= t2f, ties to even), (float)(num / den) <= t2f iff num / den < hi (or ==
+// hi with an even t2f).  Points whose num clears hi * den by a relative 1e-12 are
+// decided by one multiply; the rest take the exact division, so the verdict is the
+// same bit for bit.
+RS_HD __forceinline__ bool sampson_inlier(const double* E, double x1, double y1, double x2, double y2, float t2f,
+                                          double hi) {
+    const double ex0 = E[0] * x1 + E[1] * y1 + E[2];
+    const double ex1 = E[3] * x1 + E[4] * y1 + E[5];
+    const double ex2 = E[6] * x1 + E[7] * y1 + E[8];
+    const double et0 = E[0] * x2 + E[3] * y2 + E[6];
+    const double et1 = E[1] * x2 + E[4] * y2 + E[7];
+    const double r = x2 * ex0 + y2 * ex1 + ex2;
+    const double num = r * r, den = ex0 * ex0 + ex1 * ex1 + et0 * et0 + et1 * et1;
+    const double lim = hi * den;
+    if (num < lim * (1.0 - 1e-12)) return true;
+    if (num > lim * (1.0 + 1e-12)) return false;
+    return (float)(num / den) <= t2f;
+}
+
 // max of the squared point-to-epiline distances in pixels (FMEstimatorCallback).
 RS_HD __forceinline__ float err_epiline(const double* F, double x1, double y1, double x2, double y2) {
     double a = F[0] * x1 + F[1] * y1 + F[2];
@@ -735,19 +756,12 @@ __device__ __forceinline__ bool null_space5_reg(const double (&A)[5][9], double 
     return ok;
 }
 
-// Real roots of sum c[i] x^i (degree <= 10) for a 16-lane group: isolation between the
-// roots of successive derivatives (highest first), each derivative's coefficients
-// formed once per level; the up-to-11 brackets of one level are refined in parallel,
-// one lane each (safeguarded regula falsi), and gathered in order by shuffles, so all
-// lanes of the group hold the same roots.
-__device__ __forceinline__ double peval11(const double (&c)[11], int n, double x) {
-    double v = 0.0;
-#pragma unroll
-    for (int i = 10; i >= 0; --i)
-        if (i <= n) v = v * x + c[i];
-    return v;
-}
-
+// Real roots of sum c[i] x^i (degree <= 10) for a 16-lane group: all roots at once by
+// Aberth-Ehrlich iteration, lane i refining estimate z_i (complex) with the others'
+// estimates gathered by shuffles (cubic convergence, no brackets -- OpenCV's
+// solvePoly is the related Durand-Kerner iteration); estimates with a negligible
+// imaginary part are the real roots, polished by two real Newton steps and
+// gathered in lane order, so every lane of the group holds the same list.
 __device__ int real_roots10(double (&c)[11], double (&roots)[10], int r, int gl) {
     double mx = 0.0;
 #pragma unroll
@@ -763,108 +777,96 @@ __device__ int real_roots10(double (&c)[11], double (&roots)[10], int r, int gl)
     for (int i = 1; i <= 10; ++i) lead = (i == n) ? c[i] : lead;
 #pragma unroll
     for (int i = 0; i <= 10; ++i) c[i] = i <= n ? c[i] / lead : 0.0;
-    double B = 0.0;
-#pragma unroll
-    for (int i = 0; i < 10; ++i)
-        if (i < n) B = fmax(B, fabs(c[i]));
-    B += 1.0;
-    // the derivatives' roots lie in the convex hull of the roots (Gauss-Lucas), inside
-    // the Cauchy bound B: clamping only absorbs rounding
-    double crit[10];
-    double cn1 = 0.0;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) cn1 = (i == n - 1) ? c[i] : cn1;
-    crit[0] = fmin(fmax(-cn1 / (double)n, -B), B);  // (n-1)-th derivative: n! x + (n-1)! c[n-1]
-#pragma unroll
-    for (int i = 1; i < 10; ++i) crit[i] = 0.0;
-    int ncrit = 1;
-    for (int k = n - 2; k >= 0; --k) {
-        const int dg = n - k;
-        double d[11];  // k-th derivative / k!: d[i] = C(i + k, k) c[i + k]
-#pragma unroll
-        for (int i = 0; i <= 10; ++i) {
-            double v = 0.0;
-#pragma unroll
-            for (int m = i; m <= 10; ++m) {
-                if (m - i == k) {
-                    double bin = 1.0;  // C(m, i), folded at compile time
-#pragma unroll
-                    for (int t = 1; t <= m - i; ++t) bin = bin * (double)(i + t) / (double)t;
-                    v = c[m] * bin;
-                }
-            }
-            d[i] = v;
-        }
-        // lane r refines bracket r of [-B, crit[0], ..., crit[ncrit - 1], B]
-        double lo = -B, hi = B;
+    // start on a circle of the roots' geometric-mean modulus |c0|^(1/n)
+    const double R = fmax(pow(fabs(c[0]), 1.0 / n), 1e-6);
+    const double ang = 6.283185307179586 * r / n + 0.4;
+    double zr = R * cos(ang), zi = R * sin(ang);
+    bool done = r >= n;
+    for (int it = 0; it < 60; ++it) {
+        // every lane of the group takes part in the gathers (converged ones included)
+        double xr_[10], xi_[10];
 #pragma unroll
         for (int j = 0; j < 10; ++j) {
-            if (j == r - 1) lo = crit[j];
-            if (j == r && j < ncrit) hi = crit[j];
+            xr_[j] = __shfl(zr, gl + j, 64);
+            xi_[j] = __shfl(zi, gl + j, 64);
         }
-        double cand = 0.0;
-        int has = 0;
-        if (r <= ncrit) {
-            const double flo = peval11(d, dg, lo), fhi = peval11(d, dg, hi);
-            if (flo == 0.0) {
-                cand = lo;
-                has = 1;
-            } else if ((flo < 0) != (fhi < 0) && fhi != 0.0) {
-                double fl = flo, fh = fhi;
-                int side = 0;
-                for (int it = 0; it < 100; ++it) {
-                    double x = (lo * fh - hi * fl) / (fh - fl);
-                    if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
-                    const double fx = peval11(d, dg, x);
-                    if (fx == 0.0) { lo = x; hi = x; break; }
-                    if ((fx < 0) == (fl < 0)) {
-                        lo = x; fl = fx;
-                        if (side == -1) fh *= 0.5;
-                        side = -1;
-                    } else {
-                        hi = x; fh = fx;
-                        if (side == 1) fl *= 0.5;
-                        side = 1;
-                    }
-                    if (hi - lo <= 1e-14 * fmax(1.0, fabs(lo))) break;
+        if (!done) {
+            // p(z), p'(z) by Horner (complex)
+            double pr = 0.0, pi_ = 0.0, dr = 0.0, di = 0.0;
+#pragma unroll
+            for (int i = 10; i >= 0; --i) {
+                if (i <= n) {
+                    const double ndr = dr * zr - di * zi + pr, ndi = dr * zi + di * zr + pi_;
+                    dr = ndr; di = ndi;
+                    const double npr = pr * zr - pi_ * zi + c[i], npi = pr * zi + pi_ * zr;
+                    pr = npr; pi_ = npi;
                 }
-                cand = 0.5 * (lo + hi);
-                has = 1;
             }
-            if (r == ncrit && fhi == 0.0) has |= 2;  // the right end of the last bracket too
+            // w = p / p'
+            const double dd = dr * dr + di * di;
+            double wr, wi;
+            if (dd > 0.0) {
+                wr = (pr * dr + pi_ * di) / dd;
+                wi = (pi_ * dr - pr * di) / dd;
+            } else {
+                wr = 1e-3 * R; wi = 1e-3 * R;  // stationary point: nudge
+            }
+            // s = sum_{j != i} 1 / (z_i - z_j) as one fraction num / den
+            double nr_ = 0.0, ni_ = 0.0, er = 1.0, ei = 0.0;
+#pragma unroll
+            for (int j = 0; j < 10; ++j) {
+                if (j != r && j < n) {
+                    const double ar = zr - xr_[j], ai = zi - xi_[j];
+                    const double tr = nr_ * ar - ni_ * ai + er, ti = nr_ * ai + ni_ * ar + ei;
+                    nr_ = tr; ni_ = ti;
+                    const double ur = er * ar - ei * ai, ui = er * ai + ei * ar;
+                    er = ur; ei = ui;
+                }
+            }
+            // denominator 1 - w s = (den - w num) / den;  step = w den / (den - w num)
+            const double qr = er - (wr * nr_ - wi * ni_), qi = ei - (wr * ni_ + wi * nr_);
+            const double mr = wr * er - wi * ei, mi = wr * ei + wi * er;
+            const double qq = qr * qr + qi * qi;
+            double sr = wr, si = wi;
+            if (qq > 0.0 && isfinite(qq)) {
+                sr = (mr * qr + mi * qi) / qq;
+                si = (mi * qr - mr * qi) / qq;
+            }
+            zr -= sr;
+            zi -= si;
+            done = sr * sr + si * si <= 1e-30 * (zr * zr + zi * zi) + 1e-300;
         }
-        // gather in bracket order (dedupe a root shared by two brackets' ends)
-        int nn = 0;
-        double last = 0.0;
-        double nc[10];
-#pragma unroll
-        for (int i = 0; i < 10; ++i) nc[i] = 0.0;
-#pragma unroll
-        for (int j = 0; j < 11; ++j) {
-            const double v = __shfl(cand, gl + j, 64);
-            const int hj = __shfl(has, gl + j, 64);
-            if (j <= ncrit && (hj & 1) && (nn == 0 || v != last) && nn < 10) {
-#pragma unroll
-                for (int i = 0; i < 10; ++i)
-                    if (i == nn) nc[i] = v;
-                last = v;
-                ++nn;
-            }
-            if (j <= ncrit && (hj & 2) && (nn == 0 || B != last) && nn < 10) {
-#pragma unroll
-                for (int i = 0; i < 10; ++i)
-                    if (i == nn) nc[i] = B;
-                last = B;
-                ++nn;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 10; ++i) crit[i] = nc[i];
-        ncrit = nn;
+        if (__all(done)) break;
     }
+    // real roots: negligible imaginary part; polish on the real polynomial
+    bool real = r < n && fabs(zi) <= 1e-7 * fmax(1.0, fabs(zr));
+    double x = zr;
+    if (real) {
 #pragma unroll
-    for (int i = 0; i < 10; ++i) roots[i] = crit[i];
-    return ncrit;
+        for (int pass = 0; pass < 2; ++pass) {
+            double f = 0.0, df = 0.0;
+#pragma unroll
+            for (int i = 10; i >= 0; --i)
+                if (i <= n) { df = df * x + f; f = f * x + c[i]; }
+            if (df != 0.0) {
+                const double xn = x - f / df;
+                if (isfinite(xn)) x = xn;
+            }
+        }
+    }
+    int nn = 0;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        const double v = __shfl(x, gl + j, 64);
+        const int isr = __shfl((int)real, gl + j, 64);
+        if (isr) {
+#pragma unroll
+            for (int i = 0; i < 10; ++i)
+                if (i == nn) roots[i] = v;
+            ++nn;
+        }
+    }
+    return nn;
 }
 
 __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict__ info,
@@ -905,6 +907,10 @@ __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict_
                 for (int k = 0; k < 9; ++k) snb[g][a][k] = Nb[a][k];
     }
     __syncthreads();
+#if defined(RS_ABLATE) && RS_ABLATE == 3
+    if (act && r == 0) nsol[(size_t)p * H + h] = 0;
+    return;
+#endif
     // E_k = [x, y, z, 1] coefficients of entry k
     auto ent = [&](int k, double* l) {
         for (int a = 0; a < 4; ++a) l[a] = snb[g][a][k];
@@ -1009,6 +1015,10 @@ __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict_
         if (act && r == 0) nsol[(size_t)p * H + h] = 0;
         return;
     }
+#if defined(RS_ABLATE) && RS_ABLATE == 2
+    if (r == 0) nsol[(size_t)p * H + h] = (int8_t)(bx[0][0] > 1e300);
+    return;
+#endif
     // det = bx0 (by1 b12 - b11 by2) - by0 (bx1 b12 - b11 bx2) + b10 (bx1 by2 - by1 bx2)
     double poly[11];
 #pragma unroll
@@ -1033,6 +1043,10 @@ __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict_
         pmul_acc<5, 7>(poly, b1[0], u, 1.0);
     }
     double zr[10];
+#if defined(RS_ABLATE) && RS_ABLATE == 1
+    if (r == 0) nsol[(size_t)p * H + h] = (int8_t)(poly[3] > 1e300);
+    return;
+#endif
     const int nz = real_roots10(poly, zr, r, gl);
     if (r != 0) return;
     double* out = models + ((size_t)p * H + h) * MAXSOL * 9;
@@ -1207,6 +1221,8 @@ __global__ __launch_bounds__(256) void k_ransac_score(const PairInfo* __restrict
     int cnt[MAXSOL];
     for (int s = 0; s < MAXSOL; ++s) cnt[s] = 0;
     const float t2 = (float)pi.thr2;
+    // midpoint between t2 and the next float up; exactly representable in double
+    const double t2_hi = 0.5 * ((double)t2 + (double)nextafterf(t2, INFINITY));
     const double* mh = models + ((size_t)p * H + (h < H ? h : 0)) * MAXSOL * 9;
     if (pi.mode == 3) {
         // LMedS: fewer than 15 points; median of the errors per model
@@ -1242,7 +1258,7 @@ __global__ __launch_bounds__(256) void k_ransac_score(const PairInfo* __restrict
             if (ess) {
                 for (int i = 0; i < cn; ++i) {
                     const double4 q = sp[i];
-                    c += err_sampson(M, q.x, q.y, q.z, q.w) <= t2;
+                    c += sampson_inlier(M, q.x, q.y, q.z, q.w, t2, t2_hi);
                 }
             } else {
                 for (int i = 0; i < cn; ++i) {

@@ -16,13 +16,19 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmlgate.so")
 TORCH_LIB_PATH = os.path.join(_HERE, "libmlgate_torch.so")
-OPS = ("vit_forward_into", "knn_gate", "knn_query", "row_normalize", "similarity", "xcorr_score", "superpoint",
-       "lightglue", "ransac_epipolar", "recover_pose", "resnet50", "pillow_resize_224", "plane_ransac", "proximity",
-       "prof_enable", "prof_reset", "prof_read")
 # A/B tooling only (tools/*_bench.py): load another build of the same library
 _LIB_OVERRIDE = os.environ.get("MLGATE_LIB_AB")
 if _LIB_OVERRIDE:
     LIB_PATH = _LIB_OVERRIDE
+# A/B tooling only: a directory holding another build of both libraries
+_DIR_OVERRIDE = os.environ.get("MLGATE_LIB_DIR")
+if _DIR_OVERRIDE:
+    LIB_PATH = os.path.join(_DIR_OVERRIDE, "libmlgate.so")
+    TORCH_LIB_PATH = os.path.join(_DIR_OVERRIDE, "libmlgate_torch.so")
+OPS = ("vit_forward_into", "knn_gate", "knn_query", "row_normalize", "similarity", "xcorr_score", "superpoint",
+       "lightglue", "ransac_epipolar", "recover_pose", "resnet50", "pillow_resize_224", "plane_ransac", "proximity",
+       "prof_enable", "prof_reset", "prof_read")
+
 
 c_int, c_long, c_size_t, c_float, c_double, c_void_p = (
     ctypes.c_int, ctypes.c_long, ctypes.c_size_t, ctypes.c_float, ctypes.c_double, ctypes.c_void_p)
