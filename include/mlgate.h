@@ -100,6 +100,12 @@ int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, 
  * totals uint64[2] (+= valid, rejected) or NULL.  1 <= k <= 256.
  */
 size_t mlg_knn_workspace_bytes(int N, int D, int Q);
+/* Workspace for a given k, for mlg_knn_gate (query = 0) or mlg_knn_query (query = 1):
+ * for k <= 32 and D % 4 == 0 the scan is fused -- tiles of S stream through LDS into
+ * per-row top-k lists, no [Q, N] matrix -- and needs only the normalised rows and
+ * Q * splits * (8 k + 4) B of partial lists; otherwise = mlg_knn_workspace_bytes.
+ * mlg_knn_workspace_bytes(N, D, Q) is always sufficient. */
+size_t mlg_knn_workspace_bytes_k(int N, int D, int Q, int k, int query);
 int mlg_knn_gate(const float* desc, int N, int D, const double* t, const int64_t* floor, const uint8_t* has_floor,
                  double min_gap, float thr, int k, int gating, int q0, int Q, void* workspace,
                  size_t workspace_bytes, int32_t* idx, float* sim, uint8_t* valid, int32_t* count,

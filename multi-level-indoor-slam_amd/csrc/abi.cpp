@@ -177,16 +177,36 @@ size_t mlg_knn_workspace_bytes(int N, int D, int Q) {
     return align_up((size_t)N * D * 4) + align_up((size_t)Q * D * 4) + align_up((size_t)Q * N * 4);
 }
 
+// k <= 32 and D % 4 == 0 take the fused scan (no [Q, N] matrix): normalised rows plus
+// the per-split partial lists
+static bool knn_fused(int D, int k) { return k >= 1 && k <= 32 && D % 4 == 0; }
+
+// fused layouts: gate = Xn | partial lists; query = Xn | Qn | partial lists
+size_t mlg_knn_workspace_bytes_k(int N, int D, int Q, int k, int query) {
+    if (N <= 0 || D <= 0 || Q <= 0) return 0;
+    if (!knn_fused(D, k)) return mlg_knn_workspace_bytes(N, D, Q);
+    return align_up((size_t)N * D * 4) + (query ? align_up((size_t)Q * D * 4) : 0) +
+           align_up(mlg_knn_fused_ws_bytes(Q, N, k));
+}
+
 int mlg_knn_gate(const float* desc, int N, int D, const double* t, const int64_t* floor, const uint8_t* has_floor,
                  double min_gap, float thr, int k, int gating, int q0, int Q, void* workspace,
                  size_t workspace_bytes, int32_t* idx, float* sim, uint8_t* valid, int32_t* count,
                  unsigned long long* totals, void* stream) {
     if (!desc || !t || !workspace || N <= 0 || D <= 0 || Q <= 0 || q0 < 0 || q0 + Q > N) return MLG_EINVAL;
     if (gating && (!floor || !has_floor)) return MLG_EINVAL;
-    if (mlg_knn_workspace_bytes(N, D, Q) > workspace_bytes) return MLG_ENOMEM;
     hipStream_t s = (hipStream_t)stream;
     float* Xn = (float*)workspace;
     float* S = (float*)((char*)workspace + align_up((size_t)N * D * 4) + align_up((size_t)Q * D * 4));
+    if (knn_fused(D, k)) {
+        if (mlg_knn_workspace_bytes_k(N, D, Q, k, 0) > workspace_bytes) return MLG_ENOMEM;
+        TRY(mlg_row_normalize_wave(desc, Xn, N, D, nullptr, s));
+        void* part = (char*)workspace + align_up((size_t)N * D * 4);
+        return mlg_knn_fused(Xn + (size_t)q0 * D, Q, Xn, N, D, t + q0, t, gating ? floor + q0 : nullptr,
+                             gating ? has_floor + q0 : nullptr, gating ? floor : nullptr, gating ? has_floor : nullptr,
+                             min_gap, thr, k, gating, part, idx, sim, valid, count, totals, s);
+    }
+    if (mlg_knn_workspace_bytes(N, D, Q) > workspace_bytes) return MLG_ENOMEM;
     TRY(mlg_row_normalize(desc, Xn, N, D, nullptr, s));
     TRY(mlg_similarity_f32(Xn + (size_t)q0 * D, Q, Xn, N, D, S, N, s));
     TRY(mlg_topk_gate(S, N, N, Q, t + q0, t, gating ? floor + q0 : nullptr, gating ? has_floor + q0 : nullptr,
@@ -199,11 +219,18 @@ int mlg_knn_query(const float* db, int N, int D, const float* qdesc, int Q, cons
                   const double* t_query, double min_gap, int k, void* workspace, size_t workspace_bytes,
                   int32_t* idx, float* sim, int32_t* count, void* stream) {
     if (!db || !qdesc || !t_db || !t_query || !workspace || N <= 0 || D <= 0 || Q <= 0) return MLG_EINVAL;
-    if (mlg_knn_workspace_bytes(N, D, Q) > workspace_bytes) return MLG_ENOMEM;
     hipStream_t s = (hipStream_t)stream;
     float* Xn = (float*)workspace;
     float* Qn = (float*)((char*)workspace + align_up((size_t)N * D * 4));
     float* S = (float*)((char*)Qn + align_up((size_t)Q * D * 4));
+    if (knn_fused(D, k)) {
+        if (mlg_knn_workspace_bytes_k(N, D, Q, k, 1) > workspace_bytes) return MLG_ENOMEM;
+        TRY(mlg_row_normalize_wave(db, Xn, N, D, nullptr, s));
+        TRY(mlg_row_normalize_wave(qdesc, Qn, Q, D, nullptr, s));
+        return mlg_knn_fused(Qn, Q, Xn, N, D, t_query, t_db, nullptr, nullptr, nullptr, nullptr, min_gap, -INFINITY,
+                             k, 0, S, idx, sim, nullptr, count, nullptr, s);
+    }
+    if (mlg_knn_workspace_bytes(N, D, Q) > workspace_bytes) return MLG_ENOMEM;
     TRY(mlg_row_normalize(db, Xn, N, D, nullptr, s));
     TRY(mlg_row_normalize(qdesc, Qn, Q, D, nullptr, s));
     TRY(mlg_similarity_f32(Qn, Q, Xn, N, D, S, N, s));

@@ -74,6 +74,14 @@ int mlg_topk_gate(const float* S, int lds, int N, int Q, const double* tq, const
                   int gating, int32_t* idx, float* sim, uint8_t* valid, int32_t* count, unsigned long long* totals,
                   hipStream_t s);
 int mlg_xcorr_reduce(const float* C, int n1, int n2, float* out, hipStream_t s);
+// fused kNN (k <= 32): no [Q, N] matrix; workspace mlg_knn_fused_ws_bytes(Q, N, k)
+int mlg_row_normalize_wave(const float* X, float* Xn, int N, int D, float* norms, hipStream_t s);
+int mlg_knn_fused_splits(int Q, int N);
+size_t mlg_knn_fused_ws_bytes(int Q, int N, int k);
+int mlg_knn_fused(const float* Xq, int Q, const float* Xd, int N, int D, const double* tq, const double* tdb,
+                  const int64_t* fq, const uint8_t* hfq, const int64_t* fdb, const uint8_t* hfdb, double min_gap,
+                  float thr, int k, int gating, void* ws, int32_t* idx, float* sim, uint8_t* valid, int32_t* count,
+                  unsigned long long* totals, hipStream_t s);
 
 // proximity.hip -- trajectory-proximity candidates + floor gate
 bool mlg_proximity_shape_ok(int N, int row0, int nrows);

@@ -14,6 +14,19 @@
 //                    (similarity desc, index desc), drop sim < thr, floor-consistency
 //                    bit (gating && both labels present -> floor_i == floor_j), and
 //                    integer totals of valid / rejected matches.
+// Fused path (k <= 32, the default): no [Q, N] similarity matrix ever reaches HBM.
+//   k_row_norm_wave  the same numpy-exact norm, one wave per row: the leaves of numpy's
+//                    pairwise tree summed in parallel by lanes, combined in tree order.
+//   k_knn_scan       64 query rows x one column split per workgroup: 64 x 128 tiles of
+//                    S = Xn_q . Xn^T on the exact-f32 MFMA (the same k order as
+//                    k_sim_f32, so the same bits), staged in LDS, and streamed into
+//                    per-row top-k lists held across the lanes of a wave (lane l = rank
+//                    l): a candidate that beats the row's k-th is inserted by one
+//                    ballot + shuffle, so after the first tile almost every value is
+//                    rejected by one compare.  Writes each row's sorted partial list.
+//   k_knn_merge      per row: merges the column splits' lists, floor bit, totals.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -239,6 +252,291 @@ __global__ __launch_bounds__(64) void k_topk_gate(const float* __restrict__ S, i
     }
 }
 
+// ---------------------------------------------------------- fused path ----
+// numpy pairwise-sum tree of one 8192-element chunk: leaves (<= 128 elements) in order.
+// Each lane walks the same DFS; lane L sums leaves L, L + 64, ... (pairwise_leaf, the
+// exact leaf order) into LDS; lane 0 then combines them in the tree's order.
+__device__ float pairwise_sumsq_wave(const float* a, int n, float* leaf) {
+    const int lane = threadIdx.x & 63;
+    // pass 1: enumerate leaves, lane-parallel sums
+    {
+        int st_off[16], st_n[16], sp = 0, li = 0;
+        st_off[0] = 0; st_n[0] = n;
+        while (sp >= 0) {
+            const int o = st_off[sp], m = st_n[sp];
+            --sp;
+            if (m <= 128) {
+                if ((li & 63) == lane) leaf[li] = pairwise_leaf(a + o, m);
+                ++li;
+            } else {
+                int n2 = m / 2;
+                n2 -= n2 % 8;
+                ++sp; st_off[sp] = o + n2; st_n[sp] = m - n2;  // right after left
+                ++sp; st_off[sp] = o; st_n[sp] = n2;
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    float ret = 0.f;
+    if (lane == 0) {  // pass 2: post-order combine, leaves consumed in order
+        int st_off[16], st_n[16], st_state[16];
+        float st_val[16];
+        int sp = 0, li = 0;
+        st_off[0] = 0; st_n[0] = n; st_state[0] = 0;
+        while (sp >= 0) {
+            const int o = st_off[sp], m = st_n[sp];
+            if (m <= 128) {
+                ret = leaf[li++];
+                --sp;
+            } else {
+                int n2 = m / 2;
+                n2 -= n2 % 8;
+                if (st_state[sp] == 0) {
+                    st_state[sp] = 1;
+                    ++sp; st_off[sp] = o; st_n[sp] = n2; st_state[sp] = 0;
+                } else if (st_state[sp] == 1) {
+                    st_val[sp] = ret;
+                    st_state[sp] = 2;
+                    ++sp; st_off[sp] = o + n2; st_n[sp] = m - n2; st_state[sp] = 0;
+                } else {
+                    ret = __fadd_rn(st_val[sp], ret);
+                    --sp;
+                }
+            }
+        }
+    }
+    return __shfl(ret, 0, 64);
+}
+
+__global__ __launch_bounds__(256) void k_row_norm_wave(const float* __restrict__ X, float* __restrict__ Xn, int N,
+                                                       int D, float* __restrict__ norms) {
+    __shared__ float leaf[4][128];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i = blockIdx.x * 4 + wave;
+    if (i >= N) return;  // wave-uniform
+    const float* x = X + (size_t)i * D;
+    float acc = 0.f;
+    for (int c0 = 0; c0 < D; c0 += 8192) {
+        const float p = pairwise_sumsq_wave(x + c0, min(8192, D - c0), leaf[wave]);
+        acc = c0 == 0 ? p : __fadd_rn(acc, p);
+    }
+    const float nrm = __fsqrt_rn(acc);
+    if (norms && lane == 0) norms[i] = nrm;
+    const float den = __fadd_rn(nrm, 1e-8f);
+    float* y = Xn + (size_t)i * D;
+    for (int j = lane; j < D; j += 64) y[j] = __fdiv_rn(x[j], den);
+}
+
+constexpr int FR = 64;    // query rows per workgroup
+constexpr int FC = 128;   // database columns per tile
+constexpr int FKMAX = 32;  // fused path: k <= 32 (a list rank per lane)
+
+// Row lists in registers: lane l holds rank l of each of the wave's 16 rows.
+__global__ __launch_bounds__(256, 2) void k_knn_scan(const float* __restrict__ Xq, int Q, const float* __restrict__ Xd,
+                                                     int N, int D, const double* __restrict__ tq,
+                                                     const double* __restrict__ tdb, double min_gap, float thr, int k,
+                                                     int cols_per_split, int nsplit_arg, float* __restrict__ part_v,
+                                                     int32_t* __restrict__ part_i, int32_t* __restrict__ part_n) {
+    __shared__ float As[SBK][FR + 4];
+    __shared__ float Bs[SBK][FC + 4];
+    __shared__ float St[FR][FC + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // 1-D grid dealt XCD-major: block b runs on XCD b % 8; its local index i = b / 8 walks
+    // the row blocks of one column split before the next split, so each XCD streams its
+    // own splits' database rows and keeps them in its L2
+    const int nrb = (Q + FR - 1) / FR, nsplit = nsplit_arg;
+    const int xcd = (int)blockIdx.x & 7, i8 = (int)blockIdx.x >> 3;
+    const int split = xcd + 8 * (i8 / nrb);
+    if (split >= nsplit) return;
+    const int r0 = (i8 % nrb) * FR;
+    const int cb = split * cols_per_split, ce = min(N, cb + cols_per_split);
+    if (cb >= ce) {
+        for (int q = 0; q < 16; ++q) {
+            const int row = r0 + wave * 16 + q;
+            if (row < Q && lane == 0) part_n[(size_t)row * nsplit + split] = 0;
+        }
+        return;
+    }
+    float lv[16];
+    int li[16], cnt[16];
+    double ti[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        lv[q] = -INFINITY;
+        li[q] = -1;
+        cnt[q] = 0;
+        ti[q] = tq[min(r0 + wave * 16 + q, Q - 1)];
+    }
+    for (int c0 = cb; c0 < ce; c0 += FC) {
+        f32x16 acc[2];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
+        // stage 64 rows (A) and 128 columns (B) x 16 k, transposed to [k][row]; the next
+        // k-step's values are fetched into registers while this one's MFMAs run
+        const float* srcs[3];
+        int rows_[3], kqs[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int c = tid + i * 256, isA = c < 256;
+            const int cc = isA ? c : c - 256;
+            rows_[i] = cc >> 2;
+            kqs[i] = (cc & 3) * 4;
+            srcs[i] = isA ? Xq + (size_t)min(r0 + rows_[i], Q - 1) * D : Xd + (size_t)min(c0 + rows_[i], N - 1) * D;
+        }
+        auto fetch = [&](int k0, float (&tv)[3][4]) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const int kq = kqs[i];
+                if (k0 + kq + 3 < D) {
+                    const float4 v = *reinterpret_cast<const float4*>(srcs[i] + k0 + kq);
+                    tv[i][0] = v.x; tv[i][1] = v.y; tv[i][2] = v.z; tv[i][3] = v.w;
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) tv[i][u] = k0 + kq + u < D ? srcs[i][k0 + kq + u] : 0.f;
+                }
+            }
+        };
+        auto put = [&](const float (&tv)[3][4]) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (i == 0) As[kqs[i] + u][rows_[i]] = tv[i][u];
+                    else Bs[kqs[i] + u][rows_[i]] = tv[i][u];
+                }
+        };
+        float tv[3][4];
+        fetch(0, tv);
+        put(tv);
+        __syncthreads();
+        for (int k0 = 0; k0 < D; k0 += SBK) {
+            const bool more = k0 + SBK < D;
+            if (more) fetch(k0 + SBK, tv);
+#pragma unroll
+            for (int kk = 0; kk < SBK; kk += 2) {
+                const int kx = kk + (lane >> 5);
+                const float b = Bs[kx][wave * 32 + (lane & 31)];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+                    acc[mt] = __builtin_amdgcn_mfma_f32_32x32x2f32(As[kx][mt * 32 + (lane & 31)], b, acc[mt], 0, 0, 0);
+            }
+            __syncthreads();
+            if (more) {
+                put(tv);
+                __syncthreads();
+            }
+        }
+        // D[i][j]: column j = lane & 31 (of this wave's 32), row i = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                St[mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)][wave * 32 + (lane & 31)] = acc[mt][r];
+        __syncthreads();
+        // stream the tile into the wave's 16 row lists (lane: columns c0 + lane, c0 + 64 + lane)
+        double tj[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) tj[h] = tdb[min(c0 + lane + 64 * h, N - 1)];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int row = wave * 16 + q;
+            const float kv = __shfl(lv[q], k - 1, 64);
+            const int ki = __shfl(li[q], k - 1, 64);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = lane + 64 * h, j = c0 + c;
+                const float v = St[row][c];
+                bool pass = j < ce && !(fabs(tj[h] - ti[q]) < min_gap) && !(v < thr) && v > -INFINITY;
+                pass = pass && (cnt[q] < k || before(v, j, kv, ki));
+                unsigned long long m = __ballot(pass);
+                while (m) {
+                    const int src_l = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const float cv = __shfl(v, src_l, 64);
+                    const int cj = __shfl(j, src_l, 64);
+                    // rank of the candidate: entries before it
+                    const bool bef = lane < cnt[q] && before(lv[q], li[q], cv, cj);
+                    const int pos = __popcll(__ballot(bef));
+                    if (pos < k) {
+                        const float up_v = __shfl_up(lv[q], 1, 64);
+                        const int up_i = __shfl_up(li[q], 1, 64);
+                        if (lane == pos) { lv[q] = cv; li[q] = cj; }
+                        else if (lane > pos) { lv[q] = up_v; li[q] = up_i; }
+                        cnt[q] = min(cnt[q] + 1, k);
+                    }
+                }
+            }
+        }
+        __syncthreads();  // St is rewritten by the next tile
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int row = r0 + wave * 16 + q;
+        if (row >= Q) continue;  // wave-uniform
+        const size_t base = ((size_t)row * nsplit + split) * k;
+        if (lane < k) {
+            part_v[base + lane] = lv[q];
+            part_i[base + lane] = li[q];
+        }
+        if (lane == 0) part_n[(size_t)row * nsplit + split] = cnt[q];
+    }
+}
+
+// Merge the column splits' sorted lists of each row (one wave per row): k rounds of a
+// wave argmax over the lists' heads; then the floor bit and the totals, as k_topk_gate.
+__global__ __launch_bounds__(64) void k_knn_merge(const float* __restrict__ part_v, const int32_t* __restrict__ part_i,
+                                                  const int32_t* __restrict__ part_n, int nsplit, int Q,
+                                                  const int64_t* __restrict__ fq, const uint8_t* __restrict__ hfq,
+                                                  const int64_t* __restrict__ fdb, const uint8_t* __restrict__ hfdb,
+                                                  int k, int gating, int32_t* __restrict__ idx_out,
+                                                  float* __restrict__ sim_out, uint8_t* __restrict__ valid_out,
+                                                  int32_t* __restrict__ count_out,
+                                                  unsigned long long* __restrict__ totals) {
+    const int lane = threadIdx.x, r = blockIdx.x;
+    if (r >= Q) return;
+    // lane s < nsplit walks list s
+    const bool own = lane < nsplit;
+    const size_t base = ((size_t)r * nsplit + lane) * k;
+    const int n = own ? part_n[(size_t)r * nsplit + lane] : 0;
+    int ptr = 0;
+    int emitted = 0, nvalid = 0;
+    const bool hf_i = gating && hfq[r] != 0;
+    const int64_t fi = gating ? fq[r] : 0;
+    for (int step = 0; step < k; ++step) {
+        float bv = ptr < n ? part_v[base + ptr] : -INFINITY;
+        int bi = ptr < n ? part_i[base + ptr] : -1;
+        const int mine = bi;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(bv, o, 64);
+            const int oi = __shfl_xor(bi, o, 64);
+            if (oi >= 0 && (bi < 0 || before(ov, oi, bv, bi))) { bv = ov; bi = oi; }
+        }
+        if (bi < 0) break;
+        if (mine == bi) ++ptr;  // indices are distinct across splits
+        if (lane == 0) {
+            bool ok = true;
+            if (hf_i && hfdb[bi]) ok = fi == fdb[bi];
+            idx_out[(size_t)r * k + emitted] = bi;
+            sim_out[(size_t)r * k + emitted] = bv;
+            if (valid_out) valid_out[(size_t)r * k + emitted] = ok;
+            nvalid += ok;
+        }
+        ++emitted;
+    }
+    if (lane == 0) {
+        count_out[r] = emitted;
+        if (totals) {
+            atomicAdd(totals + 0, (unsigned long long)nvalid);
+            atomicAdd(totals + 1, (unsigned long long)(emitted - nvalid));
+        }
+    }
+}
+
 // CricaVPR.compute_cross_correlation_score reduction: given C [n1, n2],
 // score = sqrt(mean_i max_j C + ... ) -- one workgroup, fixed reduction order.
 __global__ __launch_bounds__(256) void k_xcorr_reduce(const float* __restrict__ C, int n1, int n2,
@@ -305,6 +603,51 @@ int mlg_topk_gate(const float* S, int lds, int N, int Q, const double* tq, const
 int mlg_xcorr_reduce(const float* C, int n1, int n2, float* out, hipStream_t s) {
     if (n1 <= 0 || n2 <= 0) return MLG_EINVAL;
     hipLaunchKernelGGL(k_xcorr_reduce, dim3(1), dim3(256), 0, s, C, n1, n2, out);
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}
+
+int mlg_row_normalize_wave(const float* X, float* Xn, int N, int D, float* norms, hipStream_t s) {
+    if (N <= 0 || D <= 0) return MLG_EINVAL;
+    hipLaunchKernelGGL(k_row_norm_wave, dim3((N + 3) / 4), dim3(256), 0, s, X, Xn, N, D, norms);
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}
+
+size_t mlg_knn_fused_ws_bytes(int Q, int N, int k) {
+    const int nsplit = mlg_knn_fused_splits(Q, N);
+    return (size_t)Q * nsplit * ((size_t)k * 8 + 4) + 256;
+}
+
+int mlg_knn_fused_splits(int Q, int N) {
+    // a multiple of the 8 XCDs; each split's database rows (<= ~2 MB) fit an XCD's 4 MB
+    // L2; at least 512 workgroups (256 CUs x 2) when the rows allow
+    const int rb = (Q + FR - 1) / FR;
+    const long split_bytes_cap = 2L << 20;
+    int ns = 8;
+    while (ns < 64 && ((long)N * 768 * 4 / ns > split_bytes_cap || (long)rb * ns < 512)) ns += 8;
+    return ns;
+}
+
+int mlg_knn_fused(const float* Xq, int Q, const float* Xd, int N, int D, const double* tq, const double* tdb,
+                  const int64_t* fq, const uint8_t* hfq, const int64_t* fdb, const uint8_t* hfdb, double min_gap,
+                  float thr, int k, int gating, void* ws, int32_t* idx, float* sim, uint8_t* valid, int32_t* count,
+                  unsigned long long* totals, hipStream_t s) {
+    if (Q <= 0 || N <= 0 || D <= 0 || (D % 4) || k <= 0 || k > FKMAX) return MLG_EINVAL;
+    if (gating && (!fq || !hfq || !fdb || !hfdb)) return MLG_EINVAL;
+    const int nsplit = mlg_knn_fused_splits(Q, N);
+    const int tiles = (N + FC - 1) / FC;
+    const int cps = ((tiles + nsplit - 1) / nsplit) * FC;
+    float* pv = (float*)ws;
+    int32_t* pi = (int32_t*)(pv + (size_t)Q * nsplit * k);
+    int32_t* pn = pi + (size_t)Q * nsplit * k;
+    const int nrb = (Q + FR - 1) / FR;
+    const int grid = 8 * nrb * ((nsplit + 7) / 8);
+    hipLaunchKernelGGL(k_knn_scan, dim3(grid), dim3(256), 0, s, Xq, Q, Xd, N, D, tq, tdb, min_gap, thr, k, cps, nsplit,
+                       pv, pi, pn);
+    MLG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_knn_merge, dim3(Q), dim3(64), 0, s, pv, pi, pn, nsplit, Q, fq, hfq, fdb, hfdb, k, gating, idx,
+                       sim, valid, count, totals);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

@@ -675,8 +675,9 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     float* SS = (float*)(base + L.S);
 
     // Host tables below are uploaded with hipMemcpyAsync on `s` and only rewritten after
-    // the stream has been synchronised (the per-layer statistics read-back), so the
-    // pageable sources outlive every copy that reads them.
+    // the stream has been synchronised (the per-layer statistics read-back, and one final
+    // synchronisation before returning), so the pageable sources outlive every copy that
+    // reads them.
     std::vector<Seg> segs;
     std::vector<int> pair_of;  // pair index per active segment pair
     std::vector<int> orig_total(P);
@@ -908,5 +909,8 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         if (!segs.empty()) LG_TRY(upload_layout());
         stats.assign(segs.size() * 2, 0);
     }
+    // the last assignment's table (h_asg) and possibly a final layout upload are pageable
+    // copies still queued on s: they must complete before the vectors go out of scope
+    if (hipStreamSynchronize(s) != hipSuccess) return MLG_EHIP;
     return MLG_OK;
 }

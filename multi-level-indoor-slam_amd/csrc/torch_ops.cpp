@@ -131,7 +131,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> knn_gate(const Tensor& desc, const Te
     auto o = desc.options();
     Tensor idx = at::empty({Q, k}, o.dtype(at::kInt)), sim = at::empty({Q, k}, o.dtype(at::kFloat));
     Tensor valid = at::empty({Q, k}, o.dtype(at::kByte)), count = at::empty({Q}, o.dtype(at::kInt));
-    Tensor ws = workspace(mlg_knn_workspace_bytes((int)N, (int)D, (int)Q), desc);
+    Tensor ws = workspace(mlg_knn_workspace_bytes_k((int)N, (int)D, (int)Q, (int)k, 0), desc);
     check_rc(mlg_knn_gate(cp<float>(desc), (int)N, (int)D, cp<double>(t), cp<int64_t>(floor), cp<uint8_t>(has_floor),
                           min_gap, (float)thr, (int)k, gating ? 1 : 0, (int)q0, (int)Q, ws.data_ptr(),
                           (size_t)ws.numel(), mp<int32_t>(idx), mp<float>(sim), mp<uint8_t>(valid), mp<int32_t>(count),
@@ -154,7 +154,7 @@ std::tuple<Tensor, Tensor, Tensor> knn_query(const Tensor& db, const Tensor& q, 
     auto o = db.options();
     Tensor idx = at::empty({Q, k}, o.dtype(at::kInt)), sim = at::empty({Q, k}, o.dtype(at::kFloat));
     Tensor count = at::empty({Q}, o.dtype(at::kInt));
-    Tensor ws = workspace(mlg_knn_workspace_bytes((int)N, (int)D, (int)Q), db);
+    Tensor ws = workspace(mlg_knn_workspace_bytes_k((int)N, (int)D, (int)Q, (int)k, 1), db);
     check_rc(mlg_knn_query(cp<float>(db), (int)N, (int)D, cp<float>(q), (int)Q, cp<double>(t_db), cp<double>(t_q),
                            min_gap, (int)k, ws.data_ptr(), (size_t)ws.numel(), mp<int32_t>(idx), mp<float>(sim),
                            mp<int32_t>(count), stream_of(db)),

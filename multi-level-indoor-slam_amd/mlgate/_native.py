@@ -40,6 +40,7 @@ EXPORTS = {
     "mlg_vit_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_long, c_int, c_int, c_void_p,
                                 c_size_t, c_void_p, c_void_p, c_void_p]),
     "mlg_knn_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mlg_knn_workspace_bytes_k": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "mlg_knn_gate": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_float, c_int,
                              c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p]),

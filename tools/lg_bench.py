@@ -20,10 +20,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "multi-level-indoor-slam_amd"))
 sys.path.insert(0, ROOT)
 
-from mlgate import _native  # noqa: E402
+from mlgate import _native, synthetic  # noqa: E402
 from mlgate.lightglue import LightGlueGPU  # noqa: E402
 from mlgate.superpoint import SuperPointGPU  # noqa: E402
-import bench  # noqa: E402
 
 
 def main():
@@ -34,7 +33,8 @@ def main():
     ap.add_argument("--no-prune", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    frames = bench.make_frames(np.arange(args.frames), max(2, args.frames // 4), dev)
+    seq = synthetic.make_sequence(args.frames, max(2, args.frames // 4), 0)
+    frames = synthetic.frames_device(seq, np.arange(args.frames), dev)
     kp, _, ds, _, cnt = SuperPointGPU(device=dev, max_num_keypoints=2048).extract_device(frames)
     counts = cnt.cpu().numpy()
     rng = np.random.default_rng(0)
