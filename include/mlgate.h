@@ -156,21 +156,6 @@ int mlg_op_attention(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, u
 int mlg_op_attention_varlen(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, uint16_t* O, int ldo, int Npad,
                             int heads, const int32_t* tasks, const int32_t* out_off, int ntasks, int max_q,
                             void* stream);
-/* The fixed-shift form LightGlue runs (default; mlg_set_lightglue_fixed_shift): Q and K
- * carry the softmax scale in exp2 units (q' k'^T = q k^T log2(e) / 8, as
- * mlg_op_lg_proj_scaled writes them with qk_scale = sqrt(log2(e) / 8)) and knb f32
- * [heads][Npad/64] holds each 64-key block's largest key norm |k'|.  Each query's softmax
- * shift is then the bound |q'| max|k'| - 64 (no running max, no rescaling); a tile whose
- * scores all lie more than 2^60 below it re-runs with the online max.  Same softmax. */
-int mlg_op_attention_varlen_shifted(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, uint16_t* O, int ldo,
-                                    int Npad, int heads, const int32_t* tasks, const int32_t* out_off, int ntasks,
-                                    int max_q, const float* knb, void* stream);
-/* LightGlue attention path: 1 = fixed-shift (default), 0 = online max.  Returns the
- * previous setting. */
-int mlg_set_lightglue_fixed_shift(int on);
-/* Diagnostic: fixed-shift attention tiles that re-ran with the online max since the last
- * reset (synchronous read; reset != 0 zeroes the counter). */
-unsigned mlg_attention_fallback_count(int reset);
 /* Fused LightGlue block tail (SelfBlock / CrossBlock after the attention):
  * msg = ctx Wout^T + bout; X += Wf2 GELU(LN(Wf1 [bf16(X) | bf16(msg)] + bf1)) + bf2 for M token
  * rows; X f32 [M][256] in place; xcopy [M][ldc] cols 0..255 holds bf16(X) on entry (the
@@ -188,12 +173,6 @@ int mlg_op_lg_ffn(const uint16_t* ctx, float* X, uint16_t* xcopy, int ldc, int M
 int mlg_op_lg_proj(int self_block, const uint16_t* xcopy, int ldx, const uint16_t* W, const float* bias,
                    const float* ecos, const float* esin, const uint8_t* live, uint16_t* Q, uint16_t* K, uint16_t* Vt,
                    int Npad, void* stream);
-/* Same, with q and k multiplied by qk_scale before their bf16 rounding, and (knb != NULL)
- * knb f32 [4][Npad/64] = per head and 64-token tile the largest norm of the bf16 key rows
- * (self: k; cross: qk) -- the bound mlg_op_attention_varlen_shifted takes. */
-int mlg_op_lg_proj_scaled(int self_block, const uint16_t* xcopy, int ldx, const uint16_t* W, const float* bias,
-                          const float* ecos, const float* esin, const uint8_t* live, uint16_t* Q, uint16_t* K,
-                          uint16_t* Vt, int Npad, float qk_scale, float* knb, void* stream);
 int mlg_op_preprocess_patches(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, int S,
                               uint16_t* patches, void* stream);
 

@@ -416,20 +416,7 @@ int mlg_op_attention_varlen(const uint16_t* Q, const uint16_t* K, const uint16_t
                             int heads, const int32_t* tasks, const int32_t* out_off, int ntasks, int max_q,
                             void* stream) {
     return mlg_attention_varlen(Q, K, Vt, O, ldo, Npad, heads, reinterpret_cast<const int4*>(tasks), out_off, ntasks,
-                                max_q, nullptr, (hipStream_t)stream);
-}
-int mlg_op_attention_varlen_shifted(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, uint16_t* O, int ldo,
-                                    int Npad, int heads, const int32_t* tasks, const int32_t* out_off, int ntasks,
-                                    int max_q, const float* knb, void* stream) {
-    if (!knb) return MLG_EINVAL;
-    return mlg_attention_varlen(Q, K, Vt, O, ldo, Npad, heads, reinterpret_cast<const int4*>(tasks), out_off, ntasks,
-                                max_q, knb, (hipStream_t)stream);
-}
-unsigned mlg_attention_fallback_count(int reset) { return mlg_attention_fallbacks(reset != 0); }
-int mlg_set_lightglue_fixed_shift(int on) {
-    const int prev = g_lg_fixed_shift;
-    g_lg_fixed_shift = on != 0;
-    return prev;
+                                max_q, (hipStream_t)stream);
 }
 int mlg_op_lg_ffn(const uint16_t* ctx, float* X, uint16_t* xcopy, int ldc, int M, const uint16_t* Wout,
                   const float* bout, const uint16_t* Wf1, const float* bf1, const float* ln_g, const float* ln_b,
@@ -441,14 +428,7 @@ int mlg_op_lg_ffn(const uint16_t* ctx, float* X, uint16_t* xcopy, int ldc, int M
 int mlg_op_lg_proj(int self_block, const uint16_t* xcopy, int ldx, const uint16_t* W, const float* bias,
                    const float* ecos, const float* esin, const uint8_t* live, uint16_t* Q, uint16_t* K, uint16_t* Vt,
                    int Npad, void* stream) {
-    return mlg_lg_proj(self_block != 0, xcopy, ldx, W, bias, ecos, esin, live, Q, K, Vt, Npad, 1.f, nullptr,
-                       (hipStream_t)stream);
-}
-int mlg_op_lg_proj_scaled(int self_block, const uint16_t* xcopy, int ldx, const uint16_t* W, const float* bias,
-                          const float* ecos, const float* esin, const uint8_t* live, uint16_t* Q, uint16_t* K,
-                          uint16_t* Vt, int Npad, float qk_scale, float* knb, void* stream) {
-    return mlg_lg_proj(self_block != 0, xcopy, ldx, W, bias, ecos, esin, live, Q, K, Vt, Npad, qk_scale, knb,
-                       (hipStream_t)stream);
+    return mlg_lg_proj(self_block != 0, xcopy, ldx, W, bias, ecos, esin, live, Q, K, Vt, Npad, (hipStream_t)stream);
 }
 int mlg_op_preprocess_patches(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, int S,
                               uint16_t* patches, void* stream) {

@@ -248,59 +248,35 @@ struct PipeCtx {
     char* smem;
     int T, nkb, gk_off, gv_off;
     int sk0, sk1, sv0a, sv0b, sv1a, sv1b;
-    int kdma[2];        // K LDS-DMA: per-lane source element offset within a 64-key block
-    unsigned lds_base;  // LDS byte address of smem (M0 of the K DMAs)
     int koff[4];     // K fragment offset per 16-key step (chunk XOR depends on it only)
     int voff[2][2][4];  // V^T fragment offsets [half][st][dt * 2 + lo/hi]
 };
 
-// S^T of one 32-key half-block (kt) of the K tile at kb: [qt] tiles.  SHIFTED: a fifth
-// k-step of constant operands -- a ones column on the keys (kone) against each query's
-// -m (qm, bf16) -- leaves s = q'.k' - m ready for exp2.  (Seeding the chains' C operand
-// with -m instead took 32 more VGPRs, and the register squeeze sank the K prefetch to
-// the end of the stage, exposing its latency; the shift's bf16 rounding is one constant
-// per query, which the softmax cancels.)
-template <bool SHIFTED>
+// S^T of one 32-key half-block (kt) of the K tile at kb: [qt] tiles
 __device__ __forceinline__ void qk_half(const char* kb, const PipeCtx& c, const bf16x8 (&qf)[2][4], int kt,
-                                        const bf16x8& kone, const bf16x8 (&qm)[2], f32x16 (&s)[2]) {
+                                        f32x16 (&s)[2]) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) { s[0][i] = 0.f; s[1][i] = 0.f; }
-    bf16x8 kf[4];  // all four fragments in flight before the first MFMA waits on one
-#pragma unroll
-    for (int st = 0; st < 4; ++st) kf[st] = *reinterpret_cast<const bf16x8*>(kb + kt * 4096 + c.koff[st]);
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
-        s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[st], qf[0][st], s[0], 0, 0, 0);
-        s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[st], qf[1][st], s[1], 0, 0, 0);
-    }
-    if (SHIFTED) {  // last in the chain: a loop-invariant first step would be hoisted into
-                    // 32 registers of -m (the seeding this replaces)
-        s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kone, qm[0], s[0], 0, 0, 0);
-        s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kone, qm[1], s[1], 0, 0, 0);
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + kt * 4096 + c.koff[st]);
+        s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[0][st], s[0], 0, 0, 0);
+        s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[1][st], s[1], 0, 0, 0);
     }
 }
 
 // half-step H of stage j: consume `cur` (keys 64 j + 32 H ..), produce `nxt`.  kcur /
-// knext: K ring slots of stages j / j + 1; kw: slot for K_{j+2}.  C: score -> exp2 units.
-// FAST: scores arrive as q'.k' - m in exp2 units (shift k-step, fixed shift m per query):
-// no running max, no rescale, no per-score fma -- p = exp2(s) directly.
-template <int H, bool LASTSTAGE, bool FAST>
+// knext: K ring slots of stages j / j + 1; kw: slot for K_{j+2}.
+template <int H, bool LASTSTAGE>
 __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)[2], const PipeCtx& c,
                                           const bf16x8 (&qf)[2][4], f32x16 (&o)[2][2], float (&mrun)[2],
-                                          float (&lsum)[2][2], int kcur, int knext, int kw, uint4 (&stage)[4],
-                                          float C, const bf16x8& kone, const bf16x8 (&qm)[2]) {
+                                          float (&lsum)[2][2], int kcur, int knext, int kw, uint4 (&stage)[4]) {
+    constexpr float C = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
     const int hh = (threadIdx.x & 63) >> 5;
     if (!LASTSTAGE && H == 0) {  // K_{j+2} (clamped), V_{j+1} -> registers, into LDS at the stage end
-        // K_{j+2} by LDS-DMA straight into ring slot kw (no staging registers: held across
-        // the stage they were what the register squeeze sank to its end); slot kw (K_{j-1})
-        // was last read before the previous stage's barrier
-        const bf16_t* pk = c.Kh + (size_t)min(j + 2, c.nkb - 1) * (KB * 64);
-        const int w2 = (threadIdx.x >> 6) * 2;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-            asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(pk + c.kdma[i]),
-                         "{m0}"(c.lds_base + kw + (w2 + i) * 1024)
-                         : "memory");
+        const bf16_t* pk = c.Kh + (size_t)min(j + 2, c.nkb - 1) * (KB * 64) + c.gk_off;
+        stage[0] = *reinterpret_cast<const uint4*>(pk);
+        stage[1] = *reinterpret_cast<const uint4*>(pk + 32 * 64);
         const bf16_t* pv = c.Vh + (size_t)(j + 1) * 4096 + c.gv_off;
         stage[2] = *reinterpret_cast<const uint4*>(pv);
         stage[3] = *reinterpret_cast<const uint4*>(pv + 32 * 64);
@@ -313,46 +289,34 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
             if (key >= c.T) { cur[0][r] = -INFINITY; cur[1][r] = -INFINITY; }
         }
     }
-    if (!FAST) {
-        float mnew[2];
-        bool grow = false;
+    float mnew[2];
+    bool grow = false;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+        float bm = max3_raw(cur[qt][0], cur[qt][1], cur[qt][2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) bm = max3_raw(bm, cur[qt][r], cur[qt][r + 1]);
+        bm = fmaxf(bm, cur[qt][15]);
+        mnew[qt] = fmaxf(mrun[qt], swap_max(bm));
+        grow |= (mnew[qt] - mrun[qt]) * C > 8.0f;
+    }
+    if (__any(grow)) {
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
-            float bm = max3_raw(cur[qt][0], cur[qt][1], cur[qt][2]);
+            const float alpha = __builtin_amdgcn_exp2f((mrun[qt] - mnew[qt]) * C);
+            lsum[qt][0] *= alpha;
+            lsum[qt][1] *= alpha;
 #pragma unroll
-            for (int r = 3; r < 15; r += 2) bm = max3_raw(bm, cur[qt][r], cur[qt][r + 1]);
-            bm = fmaxf(bm, cur[qt][15]);
-            mnew[qt] = fmaxf(mrun[qt], swap_max(bm));
-            grow |= (mnew[qt] - mrun[qt]) * C > 8.0f;
-        }
-        if (__any(grow)) {
-#pragma unroll
-            for (int qt = 0; qt < 2; ++qt) {
-                const float alpha = __builtin_amdgcn_exp2f((mrun[qt] - mnew[qt]) * C);
-                lsum[qt][0] *= alpha;
-                lsum[qt][1] *= alpha;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) { o[qt][0][i] *= alpha; o[qt][1][i] *= alpha; }
-                mrun[qt] = mnew[qt];
-            }
+            for (int i = 0; i < 16; ++i) { o[qt][0][i] *= alpha; o[qt][1][i] *= alpha; }
+            mrun[qt] = mnew[qt];
         }
     }
     const float mc0 = mrun[0] * C, mc1 = mrun[1] * C;
-    // this half-block's V^T fragments, read ahead of the score MFMAs they then hide under
-    const char* vb = c.smem + 3 * KTILE_BYTES + (j & 1) * VTILE_BYTES;
-    bf16x8 vfr[2][2];
-#pragma unroll
-    for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-            const s16x4 lo = *reinterpret_cast<const s16x4*>(vb + c.voff[H][st][2 * dt]);
-            const s16x4 hi = *reinterpret_cast<const s16x4*>(vb + c.voff[H][st][2 * dt + 1]);
-            vfr[st][dt] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-        }
     // next half-block's scores on the MFMA pipe
     const char* kring = c.smem;
-    if (!(LASTSTAGE && H == 1)) qk_half<FAST>(kring + (H == 0 ? kcur : knext), c, qf, H ^ 1, kone, qm, nxt);
+    if (!(LASTSTAGE && H == 1)) qk_half(kring + (H == 0 ? kcur : knext), c, qf, H ^ 1, nxt);
     // P of this half-block [st][qt]: keys 16 st + 8 hh .. + 7, then O^T += V^T . P^T
+    const char* vb = c.smem + 3 * KTILE_BYTES + (j & 1) * VTILE_BYTES;
     bf16x8 pf[2][2];
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
@@ -362,9 +326,8 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
             u32x4 w;
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
-                const float p0 = __builtin_amdgcn_exp2f(FAST ? cur[qt][8 * st + 2 * jj] : fmaf(cur[qt][8 * st + 2 * jj], C, -mc));
-                const float p1 =
-                    __builtin_amdgcn_exp2f(FAST ? cur[qt][8 * st + 2 * jj + 1] : fmaf(cur[qt][8 * st + 2 * jj + 1], C, -mc));
+                const float p0 = __builtin_amdgcn_exp2f(fmaf(cur[qt][8 * st + 2 * jj], C, -mc));
+                const float p1 = __builtin_amdgcn_exp2f(fmaf(cur[qt][8 * st + 2 * jj + 1], C, -mc));
                 lsum[qt][0] += p0;
                 lsum[qt][1] += p1;
                 w[jj] = pack_bf16x2(p0, p1);
@@ -373,7 +336,9 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
         }
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
-            const bf16x8 vf = vfr[st][dt];
+            const s16x4 lo = *reinterpret_cast<const s16x4*>(vb + c.voff[H][st][2 * dt]);
+            const s16x4 hi = *reinterpret_cast<const s16x4*>(vb + c.voff[H][st][2 * dt + 1]);
+            const bf16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
             o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st][0], o[0][dt], 0, 0, 0);
             o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st][1], o[1][dt], 0, 0, 0);
         }
@@ -381,27 +346,20 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
     if (!LASTSTAGE && H == 1) {
         char* kwp = c.smem + kw;
         char* vw = c.smem + 3 * KTILE_BYTES + ((j + 1) & 1) * VTILE_BYTES;
-        (void)kwp;
+        *reinterpret_cast<uint4*>(kwp + c.sk0) = stage[0];
+        *reinterpret_cast<uint4*>(kwp + c.sk1) = stage[1];
         *reinterpret_cast<uint2*>(vw + c.sv0a) = make_uint2(stage[2].x, stage[2].y);
         *reinterpret_cast<uint2*>(vw + c.sv0b) = make_uint2(stage[2].z, stage[2].w);
         *reinterpret_cast<uint2*>(vw + c.sv1a) = make_uint2(stage[3].x, stage[3].y);
         *reinterpret_cast<uint2*>(vw + c.sv1b) = make_uint2(stage[3].z, stage[3].w);
-        __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): this wave's K DMAs have landed
         __syncthreads();
     }
 }
 
-// FAST (kbn != NULL): Q and K carry the exp2-unit scale, kbn[b] is the largest key norm of
-// 64-key block b of the segment; each query's shift is m = |q'| max_j |k'_j| - 64, an upper
-// bound of its scores less 64 (Cauchy-Schwarz), so every p <= 2^64 and no running max is
-// needed.  Returns true, without writing O, if some query's denominator came out below
-// 2^-60 (its scores lie far below the bound: precision would suffer) -- the caller then
-// runs the online-max tile instead.  Both paths compute the same softmax.
-template <bool FAST>
-__device__ __forceinline__ bool attention_tile_pipe(char* smem, const bf16_t* __restrict__ Qh,
+__device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __restrict__ Qh,
                                                     const bf16_t* __restrict__ Kh, const bf16_t* __restrict__ Vh,
                                                     int T, int nq, int qmax, int qblock, bf16_t* __restrict__ orow,
-                                                    int ldo, float C, const float* __restrict__ kbn) {
+                                                    int ldo) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, col = lane & 31;
     const int qbase = qblock * 256 + wave * 64;
     bf16x8 qf[2][4];
@@ -423,14 +381,6 @@ __device__ __forceinline__ bool attention_tile_pipe(char* smem, const bf16_t* __
     c.gv_off = srow * 64 + sch * 8;
     c.sk0 = k_off(srow, sch);
     c.sk1 = k_off(srow + 32, sch);
-    // DMA piece i of wave w fills LDS rows 8 (2 w + i) .. + 8 lane-linearly: lane l lands in
-    // row r = 8 (2 w + i) + l / 8, slot l % 8, which k_off maps to chunk (l % 8) ^ ((r >> 1) & 7)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int r = 8 * (2 * wave + i) + (lane >> 3);
-        c.kdma[i] = r * 64 + (((lane & 7) ^ ((r >> 1) & 7)) << 3);
-    }
-    c.lds_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
     c.sv0a = v_off(srow, 2 * sch);
     c.sv0b = v_off(srow, 2 * sch + 1);
     c.sv1a = v_off(srow + 32, 2 * sch);
@@ -464,36 +414,9 @@ __device__ __forceinline__ bool attention_tile_pipe(char* smem, const bf16_t* __
         *reinterpret_cast<uint2*>(vw + c.sv1a) = make_uint2(v1.x, v1.y);
         *reinterpret_cast<uint2*>(vw + c.sv1b) = make_uint2(v1.z, v1.w);
     }
-    bf16x8 kone, qm[2];
-    if (FAST) {
-        const u32x4 one = {hh == 0 ? 0x3f80u : 0u, 0u, 0u, 0u};  // bf16 1.0 at k = 64
-        kone = __builtin_bit_cast(bf16x8, one);
-        float kmax = 0.f;
-        for (int b = lane; b < c.nkb; b += 64) kmax = fmaxf(kmax, kbn[b]);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) kmax = fmaxf(kmax, __shfl_xor(kmax, o, 64));
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-            float q2 = 0.f;
-#pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                const u32x4 w = __builtin_bit_cast(u32x4, qf[qt][st]);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float a = __uint_as_float(w[e] << 16), b = __uint_as_float(w[e] & 0xffff0000u);
-                    q2 = fmaf(a, a, fmaf(b, b, q2));
-                }
-            }
-            q2 += __shfl_xor(q2, 32, 64);
-            // bound with a 2^-16 relative margin for the f32 rounding of norms and dots
-            const float m = sqrtf(q2) * kmax * (1.f + 0x1p-16f) - 64.f;
-            const u32x4 w = {hh == 0 ? (uint32_t)pack_bf16x2(-m, 0.f) : 0u, 0u, 0u, 0u};
-            qm[qt] = __builtin_bit_cast(bf16x8, w);
-        }
-    }
     __syncthreads();
     f32x16 sA[2], sB[2];
-    qk_half<FAST>(smem, c, qf, 0, kone, qm, sA);
+    qk_half(smem, c, qf, 0, sA);
     f32x16 o[2][2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) { o[0][0][i] = 0.f; o[0][1][i] = 0.f; o[1][0][i] = 0.f; o[1][1][i] = 0.f; }
@@ -502,32 +425,25 @@ __device__ __forceinline__ bool attention_tile_pipe(char* smem, const bf16_t* __
     uint4 stage[4];
     int k0 = 0, k1 = KTILE_BYTES, k2 = 2 * KTILE_BYTES;  // ring slots of K_j, K_{j+1}, K_{j+2}
     for (int j = 0; j + 1 < c.nkb; ++j) {
-        pipe_half<0, false, FAST>(j, sA, sB, c, qf, o, mrun, lsum, k0, k1, k2, stage, C, kone, qm);
-        pipe_half<1, false, FAST>(j, sB, sA, c, qf, o, mrun, lsum, k0, k1, k2, stage, C, kone, qm);
+        pipe_half<0, false>(j, sA, sB, c, qf, o, mrun, lsum, k0, k1, k2, stage);
+        pipe_half<1, false>(j, sB, sA, c, qf, o, mrun, lsum, k0, k1, k2, stage);
         const int t = k0;
         k0 = k1;
         k1 = k2;
         k2 = t;
     }
-    pipe_half<0, true, FAST>(c.nkb - 1, sA, sB, c, qf, o, mrun, lsum, k0, k1, k2, stage, C, kone, qm);
-    pipe_half<1, true, FAST>(c.nkb - 1, sB, sA, c, qf, o, mrun, lsum, k0, k1, k2, stage, C, kone, qm);
-    float lrow[2];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) lrow[qt] = swap_sum(lsum[qt][0] + lsum[qt][1]);
-    if (FAST) {
-        const bool bad = !(lrow[0] >= 0x1p-60f) || !(lrow[1] >= 0x1p-60f);
-        if (__syncthreads_or(bad)) return true;  // also the barrier before the LDS reuse below
-    }
+    pipe_half<0, true>(c.nkb - 1, sA, sB, c, qf, o, mrun, lsum, k0, k1, k2, stage);
+    pipe_half<1, true>(c.nkb - 1, sB, sA, c, qf, o, mrun, lsum, k0, k1, k2, stage);
 
     // O staged through LDS (the K / V rings are dead once every wave is past its last
     // stage) as this wave's [64 queries][64 d] bf16, 16-B chunk c of row r at c ^ (r & 7),
     // then written as whole 128-B row pieces: 8 rows per wave-instruction instead of 32
     // rows x 16 B (the store tail of a row-per-lane epilogue is issue-bound)
-    if (!FAST) __syncthreads();
+    __syncthreads();
     char* st = smem + wave * (64 * 128);
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-        const float inv = 1.0f / lrow[qt];
+        const float inv = 1.0f / swap_sum(lsum[qt][0] + lsum[qt][1]);
         const int r = qt * 32 + col;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
@@ -548,10 +464,7 @@ __device__ __forceinline__ bool attention_tile_pipe(char* smem, const bf16_t* __
             *reinterpret_cast<uint4*>(orow + (size_t)qrow * ldo + c * 8) =
                 *reinterpret_cast<const uint4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
     }
-    return false;
 }
-
-__device__ unsigned g_attn_fallbacks;  // fixed-shift tiles re-run with the online max
 
 // Ragged batch: task t attends query rows [q_off, q_off + q_len) to keys / values
 // [kv_off, kv_off + kv_len) of a flat token layout (offsets multiples of 64, rows
@@ -567,7 +480,7 @@ __global__ __launch_bounds__(256, 1) void k_attention_varlen(const bf16_t* __res
                                                              const bf16_t* __restrict__ Vt, bf16_t* __restrict__ O,
                                                              int ldo, int Npad, const int4* __restrict__ tasks,
                                                              const int* __restrict__ out_off, int nqb, int heads,
-                                                             int total, const float* __restrict__ knb) {
+                                                             int total) {
     __shared__ __attribute__((aligned(16))) char smem[3 * KTILE_BYTES + 2 * VTILE_BYTES];
     const int per_xcd = (int)gridDim.x >> 3;
     const int logical = ((int)blockIdx.x & 7) * per_xcd + ((int)blockIdx.x >> 3);
@@ -578,33 +491,12 @@ __global__ __launch_bounds__(256, 1) void k_attention_varlen(const bf16_t* __res
     const int4 tk = tasks[t];  // q_off, q_len, kv_off, kv_len
     if (qb * 256 >= tk.y || tk.w <= 0) return;
     const int qpad = (tk.y + 63) & ~63;
-    const bf16_t* Qh = Q + ((size_t)h * Npad + tk.x) * 64;
-    const bf16_t* Kh = K + ((size_t)h * Npad + tk.z) * 64;
-    const bf16_t* Vh = Vt + ((size_t)h * Npad + tk.z) * 64;
-    bf16_t* orow = O + (size_t)out_off[t] * ldo + h * 64;
-    if (knb) {  // scores pre-scaled to exp2 units; fixed shift from the norm bound
-        if (attention_tile_pipe<true>(smem, Qh, Kh, Vh, tk.w, tk.y, qpad, qb, orow, ldo, 1.f,
-                                      knb + (size_t)h * (Npad / 64) + tk.z / 64)) {
-            if (threadIdx.x == 0) atomicAdd(&g_attn_fallbacks, 1u);
-            attention_tile_pipe<false>(smem, Qh, Kh, Vh, tk.w, tk.y, qpad, qb, orow, ldo, 1.f, nullptr);
-        }
-    } else {
-        attention_tile_pipe<false>(smem, Qh, Kh, Vh, tk.w, tk.y, qpad, qb, orow, ldo, 0.125f * 1.4426950408889634f,
-                                   nullptr);
-    }
+    attention_tile_pipe(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
+                        Vt + ((size_t)h * Npad + tk.z) * 64, tk.w, tk.y, qpad, qb, O + (size_t)out_off[t] * ldo + h * 64,
+                        ldo);
 }
 
 }  // namespace
-
-unsigned mlg_attention_fallbacks(bool reset) {
-    unsigned v = 0;
-    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_attn_fallbacks), sizeof(v)) != hipSuccess) return 0;
-    if (reset) {
-        const unsigned z = 0;
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_fallbacks), &z, sizeof(z));
-    }
-    return v;
-}
 
 int mlg_attention(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int B, int T, int Tpad,
                   hipStream_t s) {
@@ -616,8 +508,7 @@ int mlg_attention(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O,
 }
 
 int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,
-                         const int4* tasks, const int* out_off, int ntasks, int max_q, const float* knb,
-                         hipStream_t s) {
+                         const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s) {
     if (ntasks <= 0) return MLG_OK;
     if (Npad % 64 || heads <= 0 || max_q <= 0) return MLG_EINVAL;
     const int nqb = (max_q + 255) / 256;
@@ -625,7 +516,7 @@ int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf1
     if (total > (1L << 30)) return MLG_EINVAL;
     const int grid = (int)((total + 7) & ~7L);
     hipLaunchKernelGGL(k_attention_varlen, dim3(grid), dim3(256), 0, s, Q, K, Vt, O, ldo, Npad, tasks, out_off, nqb,
-                       heads, (int)total, knb);
+                       heads, (int)total);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

@@ -40,13 +40,8 @@ int mlg_gemm_bias_relu_bf16(const bf16_t* A, int lda, const bf16_t* W, const flo
                             int nvalid, int M, int N, int K_, hipStream_t s);
 int mlg_gemm_bias_add_relu(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, float* X,
                            int ldx, bf16_t* C, int M, int N, int K_, hipStream_t s);
-extern int g_lg_fixed_shift;
-unsigned mlg_attention_fallbacks(bool reset);  // fixed-shift tiles re-run online (diagnostic)  // lightglue.hip: fixed-shift attention (mlg_set_lightglue_fixed_shift)
-// knb != NULL: Q / K pre-scaled to exp2 units (lg_proj qk_scale = sqrt(log2 e / 8)) and
-// knb [heads][Npad / 64] the per-64-key-block largest key norm (lg_proj): fixed-shift path
 int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,
-                         const int4* tasks, const int* out_off, int ntasks, int max_q, const float* knb,
-                         hipStream_t s);
+                         const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s);
 int mlg_gemm_bias_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,
                        hipStream_t s);
 int mlg_gemm_bias_gelu_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,
@@ -153,8 +148,7 @@ int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const
 // lg_proj.hip -- LightGlue q/k/v projections (+ rotary for the self block) straight into
 // the attention operands; W packed k-step-major [16][768 | 512][16]; Npad % 64 == 0.
 int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,
-                const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, float qk_scale,
-                float* knb, hipStream_t s);
+                const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s);
 size_t mlg_lightglue_ws_bytes(int P, int kmax);
 int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float* desc, const int32_t* counts, int kmax,
                       const int32_t* pa, const int32_t* pb, int P, float depth_conf, float width_conf,

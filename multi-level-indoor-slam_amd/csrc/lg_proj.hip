@@ -16,11 +16,6 @@
 // C = X . W^T, which hands a lane 4 consecutive tokens of one dim: one 8-B store into
 // the transposed V^T row, where the transposed product would need 4 scattered 2-B
 // stores.  Same fragments, operand order only.
-// qk_scale multiplies q and k before their bf16 rounding (the attention's 1/8 * log2 e,
-// split as sqrt over q and k, so the scores arrive in exp2 units); with knb != NULL the
-// key part (self: k, cross: qk) also writes, per head and 64-token tile, the largest
-// Euclidean norm of its bf16 key rows, knb[h][m0 / 64] -- the attention's softmax shift
-// bound (attention.hip, k_attention_varlen fast path).
 #include "common.h"
 #include "kernels.h"
 
@@ -81,11 +76,9 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
                                                 const bf16_t* __restrict__ W, const float* __restrict__ bias,
                                                 const float* __restrict__ ecos, const float* __restrict__ esin,
                                                 const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
-                                                bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad,
-                                                float qk_scale, float* __restrict__ knb) {
+                                                bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad) {
     constexpr int N = SELF ? 768 : 512;
     __shared__ __attribute__((aligned(16))) char lds[R * ROWB];
-    __shared__ float nsq[8][R];  // per wave: squared norm of its 32 key dims per token
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
     // 1-D grid, dealt so the parts (q, k, v / qk, v) of one token tile are consecutive
     // workgroups of one XCD (hardware deals block b to XCD b % 8): the tile's x rows are
@@ -113,11 +106,9 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
 
-    const bool key_part = knb != nullptr && part == (SELF ? 1 : 0);
     if (!is_v) {
         proj_gemm<false>(wrow, (size_t)N * 16, lds, acc);
         __syncthreads();  // every wave has read the x tile
-        float ss[2] = {0.f, 0.f};  // squared norm of this lane's 16 rounded dims per m-tile
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int n = 32 * wave + 8 * g + 4 * hh;  // column within the part
@@ -145,23 +136,8 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
                     x0 = r0; x1 = r1; x2 = r2; x3 = r3;
                 }
                 uint2 o = make_uint2(0u, 0u);
-                if (live[m])
-                    o = make_uint2(pack_bf16x2(__fmul_rn(x0, qk_scale), __fmul_rn(x1, qk_scale)),
-                                   pack_bf16x2(__fmul_rn(x2, qk_scale), __fmul_rn(x3, qk_scale)));
-                if (key_part) {
-                    const float y0 = __uint_as_float(o.x << 16), y1 = __uint_as_float(o.x & 0xffff0000u);
-                    const float y2 = __uint_as_float(o.y << 16), y3 = __uint_as_float(o.y & 0xffff0000u);
-                    ss[mt] = __fadd_rn(ss[mt], __fadd_rn(__fadd_rn(__fmul_rn(y0, y0), __fmul_rn(y1, y1)),
-                                                         __fadd_rn(__fmul_rn(y2, y2), __fmul_rn(y3, y3))));
-                }
+                if (live[m]) o = make_uint2(pack_bf16x2(x0, x1), pack_bf16x2(x2, x3));
                 *reinterpret_cast<uint2*>(lds + stage_off(h, r, d)) = o;
-            }
-        }
-        if (key_part) {
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                const float t = __fadd_rn(ss[mt], __shfl_xor(ss[mt], 32, 64));
-                if (hh == 0) nsq[wave][32 * mt + col] = t;
             }
         }
     } else {
@@ -185,12 +161,6 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
             }
     }
     __syncthreads();
-    if (key_part && wave < 4) {  // wave h: the tile's largest key norm of head h
-        float nrm = __fsqrt_rn(__fadd_rn(nsq[2 * wave][lane], nsq[2 * wave + 1][lane]));
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) nrm = fmaxf(nrm, __shfl_xor(nrm, o, 64));
-        if (lane == 0) knb[(size_t)wave * (Npad / R) + m0 / R] = nrm;
-    }
     // copy-out: per head one contiguous [64 rows][64] block at (h * Npad + m0) * 64
     bf16_t* dst = is_v ? Vt : (part == 0 ? Q : K);
 #pragma unroll
@@ -204,16 +174,15 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
 }  // namespace
 
 int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,
-                const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, float qk_scale,
-                float* knb, hipStream_t s) {
+                const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s) {
     if (Npad <= 0 || (Npad % R) || ldx < 256 || (ldx % 8)) return MLG_EINVAL;
     const unsigned grid = (unsigned)((((long)(Npad / R) * (self_block ? 3 : 2)) + 7) & ~7L);
     if (self_block) {
         hipLaunchKernelGGL(k_lg_proj<true>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin, live, Q, K,
-                           Vt, Npad, qk_scale, knb);
+                           Vt, Npad);
     } else {
         hipLaunchKernelGGL(k_lg_proj<false>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, (const float*)nullptr,
-                           (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad, qk_scale, knb);
+                           (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad);
     }
     MLG_LAUNCH_CHECK();
     return MLG_OK;

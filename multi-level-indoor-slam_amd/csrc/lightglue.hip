@@ -18,8 +18,6 @@
 #include "common.h"
 #include "kernels.h"
 
-int g_lg_fixed_shift = 1;
-
 namespace {
 
 constexpr int LG_D = 256, LG_H = 4, LG_L = 9;
@@ -564,7 +562,7 @@ size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct LgLayout {
     size_t x, cat, ecos, esin, ind, x2, cat2, ecos2, esin2, ind2, Q, K, Vt, ctx, hf, hb, live, rowseg, lz, keep,
-        stats, segs, tasks, outoff, moves, mdesc, rmax, rlog, cmax, clog, arg, val, part, asg, norm, knb, S, total;
+        stats, segs, tasks, outoff, moves, mdesc, rmax, rlog, cmax, clog, arg, val, part, asg, norm, S, total;
     int asg_cap;
 };
 
@@ -596,7 +594,6 @@ LgLayout lg_layout(int P, int kmax) {
     L.rowseg = take(N * 4);
     L.lz = take(N * 4);
     L.keep = take(N);
-    L.knb = take((size_t)LG_H * (N / 64) * 4);
     L.stats = take((size_t)2 * P * 2 * 4);
     L.segs = take((size_t)2 * P * sizeof(Seg));
     L.tasks = take((size_t)4 * P * sizeof(int4));  // self tasks, then cross tasks
@@ -662,7 +659,6 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     float* LZ = (float*)(base + L.lz);
     uint8_t* KEEP = (uint8_t*)(base + L.keep);
     int* STATS = (int*)(base + L.stats);
-    float* KNB = (float*)(base + L.knb);  // per head and 64-key block: largest key norm
     Seg* SEGS = (Seg*)(base + L.segs);
     int4* TASKS = (int4*)(base + L.tasks);
     int* OUTOFF = (int*)(base + L.outoff);
@@ -754,8 +750,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
             work += 4.0 * LG_H * 64 * (cross ? 2 * a * b : a * a + b * b);
         }
         MlgProfScope prof(5, s, work);
-        return mlg_attention_varlen(Q, cross ? Q : K, VT, CTX, LG_D, Npad, LG_H, TASKS + o, OUTOFF + o, nt, maxq,
-                                    g_lg_fixed_shift ? KNB : nullptr, s);
+        return mlg_attention_varlen(Q, cross ? Q : K, VT, CTX, LG_D, Npad, LG_H, TASKS + o, OUTOFF + o, nt, maxq, s);
     };
     // out_proj / to_out + FFN + residual, fused (lg_ffn.hip)
     // (conf: the layer's token-confidence / matchability heads, fused into the tail)
@@ -812,16 +807,12 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         return MLG_OK;
     };
 
-    // fixed-shift attention: q and k leave the projections in exp2 units (1/8 * log2 e,
-    // split as a square root over the two), with per-block key norms for the shift bound
-    const float qk_scale = g_lg_fixed_shift ? sqrtf(0.125f * 1.4426950408889634f) : 1.f;
     std::vector<int> stats(segs.size() * 2);
     for (int i = 0; i < LG_L && !segs.empty(); ++i) {
         // self block: projection + rotary + head split fused in the GEMM epilogue
         {
             MlgProfScope prof(6, s, 2.0 * live_tokens() * 768 * 256);
-            LG_TRY(mlg_lg_proj(true, CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, qk_scale,
-                               g_lg_fixed_shift ? KNB : nullptr, s));
+            LG_TRY(mlg_lg_proj(true, CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, s));
         }
         LG_TRY(attention(false));
         LG_TRY(ffn(w.self[i], nullptr));
@@ -829,7 +820,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         {
             MlgProfScope prof(6, s, 2.0 * live_tokens() * 512 * 256);
             LG_TRY(mlg_lg_proj(false, CAT, 512, w.cross[i].Wqkv, w.cross[i].bqkv, nullptr, nullptr, LIVE, Q, nullptr, VT,
-                               Npad, qk_scale, g_lg_fixed_shift ? KNB : nullptr, s));
+                               Npad, s));
         }
         LG_TRY(attention(true));
         // layer i's heads on the updated tokens: matchability log-sigmoid (the assignment's

@@ -87,13 +87,8 @@ EXPORTS = {
     "mlg_op_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_op_attention_varlen": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                                         c_void_p, c_int, c_int, c_void_p]),
-    "mlg_op_attention_varlen_shifted": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
-                                                c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "mlg_op_lg_ffn": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 8 + [c_void_p]),
     "mlg_op_lg_proj": (c_int, [c_int, c_void_p, c_int] + [c_void_p] * 8 + [c_int, c_void_p]),
-    "mlg_op_lg_proj_scaled": (c_int, [c_int, c_void_p, c_int] + [c_void_p] * 8 + [c_int, c_float, c_void_p, c_void_p]),
-    "mlg_set_lightglue_fixed_shift": (c_int, [c_int]),
-    "mlg_attention_fallback_count": (ctypes.c_uint, [c_int]),
     "mlg_op_preprocess_patches": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_long, c_int, c_void_p,
                                           c_void_p]),
     "mlg_prof_enable": (c_int, [c_int]),

@@ -22,10 +22,7 @@ on CUDA (scaled_dot_product_attention), point pruning while a side has more than
     reached, filter_matches (mutual nearest, exp(score) > 0.1).
 ``emulate_bf16`` rounds every GEMM input (weights and activations) and the attention
 operands to bfloat16 as the GPU kernels consume them, so GPU-vs-oracle differences
-reduce to summation order.  With ``fixed_shift`` (the kernels' default attention form,
-mlg_set_lightglue_fixed_shift) q and k are rounded after multiplication by
-sqrt(log2(e) / 8), as the projection kernel writes them (scores in exp2 units); the
-softmax itself is shift-invariant, so only that rounding point differs.
+reduce to summation order.
 """
 import numpy as np
 import torch
@@ -57,10 +54,9 @@ def rotate_half(x):
 
 
 class Oracle:
-    def __init__(self, sd, emulate_bf16=True, fixed_shift=True):
+    def __init__(self, sd, emulate_bf16=True):
         self.sd = {k: torch.as_tensor(np.asarray(v, np.float32)) for k, v in sd.items()}
         self.bf = emulate_bf16
-        self.fixed_shift = fixed_shift
 
     def lin(self, x, name):
         w, b = self.sd[name + ".weight"], self.sd[name + ".bias"]
@@ -73,13 +69,8 @@ class Oracle:
         return x + self.lin(h, p + ".ffn.3")
 
     def attn(self, q, k, v):
-        if self.bf and self.fixed_shift:
-            c = float(np.sqrt(np.float32(0.125 * 1.4426950408889634)))
-            q, k, v = _q(q * c, True), _q(k * c, True), _q(v, True)
-            s = (q @ k.transpose(-1, -2)) * float(np.log(2.0))
-        else:
-            q, k, v = (_q(t, self.bf) for t in (q, k, v))
-            s = (q @ k.transpose(-1, -2)) / HD ** 0.5
+        q, k, v = (_q(t, self.bf) for t in (q, k, v))
+        s = (q @ k.transpose(-1, -2)) / HD ** 0.5
         p = torch.softmax(s, -1)
         return _q(p, self.bf) @ v if self.bf else p @ v
 

@@ -148,33 +148,17 @@ def test_preprocess_bit_exact(dev, shape):
         assert torch.count_nonzero(got[:, 588:].float()) == 0
 
 
-QK_SCALE = float(np.sqrt(np.float32(0.125 * 1.4426950408889634)))  # sqrt(log2(e) / 8), f32
-
-
-def key_block_norms(K):
-    """[H, Npad, 64] -> [H, Npad / 64] largest row norm per 64-row block (f32)."""
-    n = K.float().pow(2).sum(-1).sqrt()
-    return n.view(K.shape[0], -1, 64).amax(-1).contiguous()
-
-
-@pytest.mark.parametrize("mode", ["online", "shifted", "fallback"])
 @pytest.mark.parametrize("lens", [(64, 70), (1, 200, 3, 129), (700, 650, 2048, 1900), (300, 17)])
-def test_attention_varlen(dev, lens, mode):
-    """LightGlue's ragged self / cross attention (k_attention_varlen) vs float32 softmax.
-    online: softmax(q k^T / 8) with the running max.  shifted (LightGlue's default): q, k
-    pre-scaled to exp2 units, each query shifted by its Cauchy-Schwarz bound from the
-    per-block key norms.  fallback: norms inflated 10^4 x, so every tile's denominator
-    underflows the 2^-60 guard and re-runs with the online max -- same softmax."""
+def test_attention_varlen(dev, lens):
+    """LightGlue's ragged self / cross attention (k_attention_varlen) vs float32 softmax."""
     H = 4
     lens = np.array(lens)
     offs = np.concatenate([[0], np.cumsum((lens + 63) // 64 * 64)])
     Npad = int(offs[-1])
     g = torch.Generator().manual_seed(int(lens.sum()))
-    sc = 1.0 if mode == "online" else QK_SCALE
-    Q = bf16_bits(torch.randn(H, Npad, 64, generator=g) * 1.5 * sc)
-    K = bf16_bits(torch.randn(H, Npad, 64, generator=g) * 1.5 * sc)
+    Q = bf16_bits(torch.randn(H, Npad, 64, generator=g) * 1.5)
+    K = bf16_bits(torch.randn(H, Npad, 64, generator=g) * 1.5)
     V = bf16_bits(torch.randn(H, Npad, 64, generator=g))
-    knb = key_block_norms(K) * (1e4 if mode == "fallback" else 1.0)
     Vt = V.view(H, Npad // 64, 64, 64).transpose(2, 3).contiguous()
     tasks, outs = [], []
     for i in range(len(lens)):  # self, then cross with the next segment
@@ -183,24 +167,18 @@ def test_attention_varlen(dev, lens, mode):
         tasks += [(offs[i], lens[i], offs[j], lens[j])]
     O = torch.zeros(2, Npad, H * 64, dtype=torch.bfloat16, device=dev)
     L = _native.lib()
-    Qd, Kd, Vd, kd = Q.to(dev), K.to(dev), Vt.to(dev), knb.to(dev)  # alive until the launches have run
+    Qd, Kd, Vd = Q.to(dev), K.to(dev), Vt.to(dev)  # kept alive until the launches have run
     for kind in range(2):
         T = torch.tensor(np.array(tasks[kind::2], np.int32), device=dev)
         OO = torch.tensor(np.array([t[0] for t in tasks[kind::2]], np.int32), device=dev)
-        if mode == "online":
-            _native.check(L.mlg_op_attention_varlen(P(Qd), P(Kd), P(Vd), P(O[kind]), H * 64, Npad, H, P(T), P(OO),
-                                                    len(T), int(lens.max()), S(dev)), "attn varlen")
-        else:
-            _native.check(L.mlg_op_attention_varlen_shifted(P(Qd), P(Kd), P(Vd), P(O[kind]), H * 64, Npad, H, P(T),
-                                                            P(OO), len(T), int(lens.max()), P(kd), S(dev)),
-                          "attn varlen shifted")
+        _native.check(L.mlg_op_attention_varlen(P(Qd), P(Kd), P(Vd), P(O[kind]), H * 64, Npad, H, P(T), P(OO),
+                                                len(T), int(lens.max()), S(dev)), "attn varlen")
         torch.cuda.synchronize()
     torch.cuda.synchronize()
     O = O.float().cpu()
     for n, (qo, ql, ko, kl) in enumerate(tasks):
         q, k, v = Q[:, qo:qo + ql].float(), K[:, ko:ko + kl].float(), V[:, ko:ko + kl].float()
-        logits = q @ k.transpose(1, 2) / 8.0 if mode == "online" else q @ k.transpose(1, 2) * float(np.log(2.0))
-        ref = (torch.softmax(logits, -1) @ v).transpose(0, 1).reshape(ql, H * 64)
+        ref = (torch.softmax(q @ k.transpose(1, 2) / 8.0, -1) @ v).transpose(0, 1).reshape(ql, H * 64)
         got = O[n % 2, qo:qo + ql]
         assert rel_err(got, ref) < 1e-2, (n, rel_err(got, ref))
 
@@ -237,13 +215,10 @@ def test_lg_ffn_fused(dev, M):
     assert torch.equal(xc[:, :256].cpu(), bf16_bits(got))
 
 
-@pytest.mark.parametrize("scaled", [False, True])
 @pytest.mark.parametrize("self_block", [True, False])
-def test_lg_proj(dev, self_block, scaled):
+def test_lg_proj(dev, self_block):
     """LightGlue projections (lg_proj.hip) vs float32 torch on the same bf16 operands:
-    q / k (+ rotary) in [4][Npad][64], v in the tiled V^T; dead rows zero.  scaled: q and k
-    multiplied by sqrt(log2(e) / 8) before rounding, and the per-block largest key norm of
-    the bf16 keys (self: k, cross: qk) written for the fixed-shift attention."""
+    q / k (+ rotary) in [4][Npad][64], v in the tiled V^T; dead rows zero."""
     from mlgate.lightglue import pack_kstep
     Npad, H = 192, 4
     N = 768 if self_block else 512
@@ -261,33 +236,20 @@ def test_lg_proj(dev, self_block, scaled):
     Q = torch.full((H, Npad, 64), 7.0, dtype=torch.bfloat16, device=dev)
     K = torch.full((H, Npad, 64), 7.0, dtype=torch.bfloat16, device=dev)
     Vt = torch.full((H, Npad // 64, 64, 64), 7.0, dtype=torch.bfloat16, device=dev)
-    knb = torch.full((H, Npad // 64), -1.0, device=dev)
-    if scaled:
-        _native.check(_native.lib().mlg_op_lg_proj_scaled(int(self_block), P(d["xc"]), 512, P(Wd), P(d["b"]),
-                                                          P(d["ec"]), P(d["es"]), P(d["live"]), P(Q), P(K), P(Vt), Npad,
-                                                          QK_SCALE, P(knb), S(dev)), "lg_proj")
-    else:
-        _native.check(_native.lib().mlg_op_lg_proj(int(self_block), P(d["xc"]), 512, P(Wd), P(d["b"]), P(d["ec"]),
-                                                   P(d["es"]), P(d["live"]), P(Q), P(K), P(Vt), Npad, S(dev)),
-                      "lg_proj")
+    _native.check(_native.lib().mlg_op_lg_proj(int(self_block), P(d["xc"]), 512, P(Wd), P(d["b"]), P(d["ec"]),
+                                               P(d["es"]), P(d["live"]), P(Q), P(K), P(Vt), Npad, S(dev)), "lg_proj")
     torch.cuda.synchronize()
-    if scaled:  # the norms of exactly the bf16 keys written (f32 sums: to rounding)
-        keys = K if self_block else Q
-        assert torch.allclose(knb.cpu(), key_block_norms(keys.cpu()), rtol=1e-5, atol=0)
-    else:
-        assert torch.all(knb.cpu() == -1.0)
-    sc = QK_SCALE if scaled else 1.0
     y = x.float() @ W.float().T + b  # [Npad, N]
     heads = lambda t: t.view(Npad, H, 64).transpose(0, 1)  # noqa: E731
     m = live.bool()[None, :, None]
     if self_block:
         c2, s2 = ec.repeat_interleave(2, -1), es.repeat_interleave(2, -1)
         rot = lambda t: t * c2 + torch.stack([-t[..., 1::2], t[..., 0::2]], -1).flatten(-2) * s2  # noqa: E731
-        refq, refk, refv = rot(heads(y[:, :256])) * sc, rot(heads(y[:, 256:512])) * sc, heads(y[:, 512:])
+        refq, refk, refv = rot(heads(y[:, :256])), rot(heads(y[:, 256:512])), heads(y[:, 512:])
         assert rel_err(K.float().cpu() * m, refk * m) < 1e-2
         assert torch.all(K.float().cpu()[~m.expand_as(refk)] == 0)
     else:
-        refq, refv = heads(y[:, :256]) * sc, heads(y[:, 256:])
+        refq, refv = heads(y[:, :256]), heads(y[:, 256:])
     assert rel_err(Q.float().cpu() * m, refq * m) < 1e-2
     assert torch.all(Q.float().cpu()[~m.expand_as(refq)] == 0)
     v = Vt.float().cpu().transpose(2, 3).reshape(H, Npad, 64)
@@ -315,14 +277,13 @@ def test_lightglue_kernels_deterministic(dev):
         Q = torch.zeros(H, Npad, 64, dtype=torch.bfloat16, device=dev)
         K = torch.zeros_like(Q)
         Vt = torch.zeros(H, Npad // 64, 64, 64, dtype=torch.bfloat16, device=dev)
-        knb = torch.zeros(H, Npad // 64, device=dev)
-        _native.check(L.mlg_op_lg_proj_scaled(1, P(d["xc"]), 512, P(d["W"]), P(d["b"]), P(d["ec"]), P(d["es"]),
-                                              P(d["live"]), P(Q), P(K), P(Vt), Npad, QK_SCALE, P(knb), S(dev)), "proj")
+        _native.check(L.mlg_op_lg_proj(1, P(d["xc"]), 512, P(d["W"]), P(d["b"]), P(d["ec"]), P(d["es"]),
+                                       P(d["live"]), P(Q), P(K), P(Vt), Npad, S(dev)), "proj")
         tasks = torch.tensor([[s, 2048, s, 2048] for s in range(0, Npad, 2048)], dtype=torch.int32, device=dev)
         oo = tasks[:, 0].contiguous()
         O = torch.zeros(Npad, 256, dtype=torch.bfloat16, device=dev)
-        _native.check(L.mlg_op_attention_varlen_shifted(P(Q), P(K), P(Vt), P(O), 256, Npad, H, P(tasks), P(oo),
-                                                        len(tasks), 2048, P(knb), S(dev)), "attn")
+        _native.check(L.mlg_op_attention_varlen(P(Q), P(K), P(Vt), P(O), 256, Npad, H, P(tasks), P(oo), len(tasks),
+                                                2048, S(dev)), "attn")
         Xd, xcd = X.to(dev), d["xc"].clone()
         w = {k: torch.from_numpy(pack_kstep((torch.randn(*s, generator=torch.Generator().manual_seed(5)) / 16)
                                             .numpy())).to(torch.bfloat16).to(dev)
@@ -332,6 +293,6 @@ def test_lightglue_kernels_deterministic(dev):
                                       P(torch.ones(512, device=dev)), P(vec[512]), P(w["f2"]), P(vec[256]), S(dev)),
                       "ffn")
         torch.cuda.synchronize()
-        outs.append((Q.cpu(), K.cpu(), Vt.cpu(), knb.cpu(), O.cpu(), Xd.cpu()))
-    bad = [name for o in outs[1:] for name, a, r in zip("QKVNOX", o, outs[0]) if not torch.equal(a, r)]
+        outs.append((Q.cpu(), K.cpu(), Vt.cpu(), O.cpu(), Xd.cpu()))
+    bad = [name for o in outs[1:] for name, a, r in zip("QKVOX", o, outs[0]) if not torch.equal(a, r)]
     assert not bad, bad

@@ -31,7 +31,6 @@ def main():
     ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--no-prune", action="store_true")
-    ap.add_argument("--online", action="store_true", help="online-max attention instead of the fixed shift")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     seq = synthetic.make_sequence(args.frames, max(2, args.frames // 4), 0)
@@ -44,7 +43,6 @@ def main():
     kw = dict(depth_confidence=-1, width_confidence=-1) if args.no_prune else {}
     lg = LightGlueGPU(device=dev, **kw)
     L = _native.lib()
-    L.mlg_set_lightglue_fixed_shift(0 if args.online else 1)
     m, s, n, stop = lg.match_device(kp, ds, counts, pa, pb)  # warm-up
     torch.cuda.synchronize()
     L.mlg_prof_reset()
@@ -56,12 +54,9 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     L.mlg_prof_enable(0)
-    fallbacks = L.mlg_attention_fallback_count(1)
     res = {"pairs": args.pairs, "mean_keypoints": float(counts.mean()), "no_prune": args.no_prune,
-           "attention_form": "online" if args.online else "fixed-shift",
            "ms_per_call": round(e0.elapsed_time(e1) / args.iters, 2),
-           "stop_hist": np.bincount(stop, minlength=10).tolist(), "matches_mean": float(n.float().mean()),
-           "fallback_tiles": int(fallbacks)}
+           "stop_hist": np.bincount(stop, minlength=10).tolist(), "matches_mean": float(n.float().mean())}
     for slot, name in ((5, "attention"), (6, "qkv_proj"), (8, "ffn_fused")):
         ms, cnt_, work = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
         L.mlg_prof_read(slot, ctypes.byref(ms), ctypes.byref(cnt_))
