@@ -320,6 +320,56 @@ int mlg_ransac_epipolar(const float* kp1, const float* kp2, const int32_t* offse
 int mlg_recover_pose(const float* kp1, const float* kp2, const int32_t* offsets, int P, const double* K,
                      int k_stride, const double* E, const uint8_t* mask, double* pose, void* stream);
 
+/* ------------------------------------------------------------------ LoFTR --
+ * Replaces LoFTR.detect_and_match (geometric_verification.py:458-526):
+ * kornia.feature.LoFTR(pretrained='indoor') on cv2 BGR2GRAY / 255 frames whose H and W
+ * are multiples of 8.  Weights are device pointers prepared on the host
+ * (mlgate/loftr.py): eval BatchNorm folded into the convs, the 196-channel stages
+ * zero-padded to 256, conv weights bf16 [Cout][k * k * Cin] with k index = tap * Cin + c.
+ * conv_w order: layer1.{0,1}.conv{1,2} (0-3); layer2.0.conv1, .conv2, .downsample,
+ * layer2.1.conv1, .conv2 (4-8); the same for layer3 (9-13); layer3_outconv,
+ * layer2_outconv, layer2_outconv2.0 (+BN), layer2_outconv2.3 (14-17); layer1_outconv,
+ * layer1_outconv2.0 (+BN), layer1_outconv2.3 (18-20).  conv_b: folded BN bias or NULL. */
+#define MLG_LOFTR_NCONV 21
+typedef struct {
+    const uint16_t* w;      /* [3d][d] rows q | k | v (no bias) */
+    const uint16_t* wmerge; /* [d][d] */
+    const uint16_t* w1;     /* mlp.0 [2d][2d] */
+    const uint16_t* w2;     /* mlp.2 [d][2d] */
+    const float *ln1_g, *ln1_b, *ln2_g, *ln2_b;
+} mlg_loftr_layer;
+typedef struct {
+    const float* stem_w; /* conv1 7x7 (BN folded) f32 [49][128] */
+    const float* stem_b; /* [128] */
+    const uint16_t* conv_w[MLG_LOFTR_NCONV];
+    const float* conv_b[MLG_LOFTR_NCONV];
+    mlg_loftr_layer coarse[8]; /* d 256, self / cross alternating */
+    mlg_loftr_layer fine[2];   /* d 128 */
+    const uint16_t* down_w;    /* fine_preprocess.down_proj [128][256] */
+    const float* down_b;
+    const uint16_t* merge_wf;  /* merge_feat weight columns 0..127 (window features) [128][128] */
+    const uint16_t* merge_wc;  /* merge_feat weight columns 128..255 (coarse context) [128][128] */
+    const float* merge_b;
+} mlg_loftr_weights;
+/* Backbone for B frames uint8 [B, H, W, C] (C = 3 BGR, 4 BGRA or 1 gray; frame_stride
+ * bytes): coarse f32 [B, H/8 * W/8, 256] (1/8 map, row-major cells) and fine f32
+ * [B, H/2 * W/2, 128].  H, W >= 32, multiples of 8. */
+size_t mlg_loftr_features_ws_bytes(int B, int H, int W);
+int mlg_loftr_features(const mlg_loftr_weights* w, const uint8_t* frames, int B, int H, int W, int C,
+                       long frame_stride, void* workspace, size_t workspace_bytes, float* coarse, float* fine,
+                       void* stream);
+/* Matching of P pairs (frames pa[p], pb[p]: HOST int32 arrays indexing coarse / fine):
+ * coarse transformer, dual-softmax coarse matches (conf > 0.2, 2-cell border, mutual
+ * nearest), fine refinement.  pe: position encoding f32 [H/8 * W/8, 256] (device).
+ * Outputs (device): counts int32 [P]; for pair p, match k < counts[p] (row order of the
+ * coarse cell in frame pa[p]): kpts0 / kpts1 f32 [P, L, 2] at [p * L + k], conf f32
+ * [P, L] (L = H/8 * W/8).  Synchronises the stream (the fine stage is sized by the
+ * coarse counts). */
+size_t mlg_loftr_match_ws_bytes(int P, int H, int W);
+int mlg_loftr_match(const mlg_loftr_weights* w, const float* coarse, const float* fine, int H, int W,
+                    const int32_t* pa, const int32_t* pb, int P, const float* pe, void* workspace,
+                    size_t workspace_bytes, int32_t* counts, float* kpts0, float* kpts1, float* conf, void* stream);
+
 /* ------------------------------------------------------------- profiling --
  * Per-launch HIP-event timing of selected kernels, recorded on the stream the kernel
  * is launched on, with the algorithmic work of each launch (FLOPs; HBM bytes for slot

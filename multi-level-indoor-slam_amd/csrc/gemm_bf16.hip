@@ -170,6 +170,35 @@ struct EpiBiasAddRelu {
     }
 };
 
+// Generic conv / linear epilogue (LoFTR, loftr.hip): y = acc (+ bias) (+ R[m, n]), then
+// act 1 = ReLU, 2 = LeakyReLU(0.01), 3 = elu + 1 on columns < act_cols; stored as f32
+// (X, ldx) and / or bf16 (C, ldc), either may be null.
+struct EpiConv {
+    const float* bias; const float* R; int ldr; float* X; int ldx; bf16_t* C; int ldc; int act; int act_cols;
+    __device__ void operator()(int m, int n, const f32x4& v) const {
+        float y[4] = {v[0], v[1], v[2], v[3]};
+        if (bias) {
+            const float4 b = *reinterpret_cast<const float4*>(bias + n);
+            y[0] += b.x; y[1] += b.y; y[2] += b.z; y[3] += b.w;
+        }
+        if (R) {
+            const float4 r = *reinterpret_cast<const float4*>(R + (size_t)m * ldr + n);
+            y[0] += r.x; y[1] += r.y; y[2] += r.z; y[3] += r.w;
+        }
+        if (act && n < act_cols) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (act == 1) y[i] = fmaxf(y[i], 0.f);
+                else if (act == 2) y[i] = y[i] > 0.f ? y[i] : 0.01f * y[i];
+                else y[i] = (y[i] > 0.f ? y[i] : expf(y[i]) - 1.f) + 1.f;  // elu(y) + 1, as torch
+            }
+        }
+        if (X) *reinterpret_cast<float4*>(X + (size_t)m * ldx + n) = make_float4(y[0], y[1], y[2], y[3]);
+        if (C) *reinterpret_cast<uint2*>(C + (size_t)m * ldc + n) =
+            make_uint2(pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3]));
+    }
+};
+
 struct EpiPatch {  // patch tokens: X[b, 1 + p, :] = acc + b + pos[1 + p]
     float* X; const float* bias; const float* pos; int P;  // P = patches per image
     __device__ void operator()(int m, int n, const f32x4& v) const {
@@ -614,6 +643,11 @@ int mlg_gemm_bias_relu_bf16(const bf16_t* A, int lda, const bf16_t* W, const flo
 int mlg_gemm_bias_add_relu(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, float* X,
                            int ldx, bf16_t* C, int M, int N, int K_, hipStream_t s) {
     return launch(A, W, M, N, K_, lda, K_, EpiBiasAddRelu{R, X, ldx, C, bias}, s);
+}
+int mlg_gemm_conv(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, int ldr, float* X,
+                  int ldx, bf16_t* C, int ldc, int act, int act_cols, int M, int N, int K_, hipStream_t s) {
+    if ((!X && !C) || act < 0 || act > 3) return MLG_EINVAL;
+    return launch(A, W, M, N, K_, lda, K_, EpiConv{bias, R, ldr, X, ldx, C, ldc, act, act_cols}, s);
 }
 int mlg_gemm_set_variant(int variant) {
     if (variant < 1 || variant > 4) return MLG_EINVAL;

@@ -40,6 +40,10 @@ int mlg_gemm_bias_relu_bf16(const bf16_t* A, int lda, const bf16_t* W, const flo
                             int nvalid, int M, int N, int K_, hipStream_t s);
 int mlg_gemm_bias_add_relu(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, float* X,
                            int ldx, bf16_t* C, int M, int N, int K_, hipStream_t s);
+// y = A . W^T (+ bias) (+ R) -> act (1 relu, 2 leaky 0.01, 3 elu + 1 on cols < act_cols)
+// -> f32 X and / or bf16 C (LoFTR convs on im2col rows and its transformer linears)
+int mlg_gemm_conv(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, int ldr, float* X,
+                  int ldx, bf16_t* C, int ldc, int act, int act_cols, int M, int N, int K_, hipStream_t s);
 int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,
                          const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s);
 int mlg_gemm_bias_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,

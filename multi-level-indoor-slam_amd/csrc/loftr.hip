@@ -1,0 +1,926 @@
+// LoFTR detector-free matching (kornia.feature.LoFTR(pretrained='indoor') as the
+// reference's LoFTR.detect_and_match runs it, scripts/semantic_gating/
+// geometric_verification.py:458-526; semantics restated in oracle/loftr.py).
+//
+// Features, once per keyframe (mlg_loftr_features), NHWC throughout:
+//   k_lf_stem     cv2 BGR2GRAY (fixed point) / 255 -> conv 7x7/2 (1 -> 128, BN folded) +
+//                 ReLU on the VALU (0.96 GFLOP per 640x480 frame); f32 + bf16 copy
+//   k_lf_im2col   3x3 / 1x1 patches (pad 1 / 0, stride 1 / 2) as bf16 GEMM rows,
+//                 k = tap * C + c
+//   mlg_gemm_conv every other conv of ResNetFPN_8_2 as a bf16 MFMA GEMM (gemm_bf16.hip,
+//                 persistent 256x256 LDS-DMA tiles), bias (folded BN) + shortcut + ReLU /
+//                 LeakyReLU fused in the epilogue; 196-channel stages zero-padded to 256
+//   k_lf_up_add   FPN merge: lateral + bilinear x2 upsample (align_corners=True) -> bf16
+// Matching, per batch of pairs (mlg_loftr_match):
+//   coarse tokens x = feat + PE in a side-major f32 residual stream [2][P][L][256] with
+//   its bf16 copy in the first half of the MLP input rows CAT [.., 512]; per layer:
+//     q, k, v  one GEMM (self) or two (cross: q from x, k / v from the source side),
+//              elu + 1 fused on q, k;
+//     k_lf_kv    per (segment, head): KV = sum_s phi(k_s)^T (v_s / L), ksum = sum_s phi(k_s)
+//                (tokens staged through LDS, fixed summation order);
+//     k_lf_apply per (token, head): msg = (phi(q) KV) / (phi(q) . ksum + 1e-6) * L -> bf16;
+//     merge GEMM -> k_lf_ln (norm1) -> bf16 into CAT's second half; MLP GEMMs
+//     (512 -> 512 ReLU, 512 -> 256); k_lf_ln_res: x += norm2(.), new bf16 copy;
+//   dual softmax: S = f0 . f1^T on the exact-f32 MFMA (knn.hip), sim = S / 256 / 0.1;
+//   k_lf_rowstats / k_lf_colstats (max, sum exp); k_lf_rowbest (row max of conf, first
+//   argmax) / k_lf_colmax (column max of conf) with conf recomputed identically in both;
+//   k_lf_select: conf > 0.2, 2-cell border, mutual max, compacted in row order;
+//   fine: k_lf_windows gathers the 5x5 windows (stride 4, zero padding) of the 1/2 maps
+//   as bf16, down_proj / merge_feat as GEMMs (the coarse half of merge_feat applied
+//   once per match, added to its 25 tokens), the same layer code over 25-token
+//   segments (d 128, 8 heads x 16), k_lf_fine_match: softmax(center . window /
+//   sqrt(128)), spatial expectation on the [-1, 1] grid, keypoints.
+#include <math.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+#include "../../include/mlgate.h"
+
+namespace {
+
+constexpr int STEM_C = 128;
+
+// ------------------------------------------------------------------ stem ----
+// One workgroup = 8 output rows x 16 output columns x 128 channels; thread (c, half)
+// computes rows 4 half .. + 4 of channel c.  The gray input tile (21 x 37 px) is staged
+// in LDS (broadcast reads), the folded 7x7 weights [49][128] read per tap.
+__global__ __launch_bounds__(256) void k_lf_stem(const uint8_t* __restrict__ frames, long frame_stride, int H, int W,
+                                                 int C, const float* __restrict__ w, const float* __restrict__ bias,
+                                                 float* __restrict__ xf, bf16_t* __restrict__ xb) {
+    __shared__ float tile[21][37];
+    const int Ho = H / 2, Wo = W / 2;
+    const int b = blockIdx.z, oy0 = blockIdx.y * 8, ox0 = blockIdx.x * 16;
+    const uint8_t* img = frames + (size_t)b * frame_stride;
+    for (int e = threadIdx.x; e < 21 * 37; e += 256) {
+        const int ty = e / 37, tx = e % 37;
+        const int iy = 2 * oy0 - 3 + ty, ix = 2 * ox0 - 3 + tx;
+        float v = 0.f;
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+            const uint8_t* p = img + ((size_t)iy * W + ix) * C;
+            const int g = C >= 3 ? (p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + 8192) >> 14 : p[0];
+            v = (float)g / 255.0f;
+        }
+        tile[ty][tx] = v;
+    }
+    __syncthreads();
+    const int c = threadIdx.x & 127, half = threadIdx.x >> 7;
+    float acc[4][16];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) acc[r][x] = 0.f;
+    for (int ky = 0; ky < 7; ++ky)
+        for (int kx = 0; kx < 7; ++kx) {
+            const float wv = w[(ky * 7 + kx) * STEM_C + c];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int x = 0; x < 16; ++x) acc[r][x] = fmaf(tile[2 * (4 * half + r) + ky][2 * x + kx], wv, acc[r][x]);
+        }
+    const float bc = bias[c];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int oy = oy0 + 4 * half + r;
+        if (oy >= Ho) continue;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const int ox = ox0 + x;
+            if (ox >= Wo) continue;
+            const float y = fmaxf(acc[r][x] + bc, 0.f);
+            const size_t o = (((size_t)b * Ho + oy) * Wo + ox) * STEM_C + c;
+            xf[o] = y;
+            xb[o] = f32_to_bf16(y);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- im2col ----
+// out[(b, oy, ox)][tap * C + c] for a k x k (k = 1 or 3) conv with padding k / 2 and
+// stride s over bf16 NHWC [B, H, W, C]; 8 channels (16 B) per thread.
+__global__ void k_lf_im2col(const bf16_t* __restrict__ in, int B, int H, int W, int C, int k, int s,
+                            bf16_t* __restrict__ out) {
+    const int Ho = (H + s - 1) / s, Wo = (W + s - 1) / s, C8 = C / 8, taps = k * k;
+    const long total = (long)B * Ho * Wo * taps * C8;
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const int c8 = (int)(e % C8);
+    long r = e / C8;
+    const int tap = (int)(r % taps);
+    r /= taps;
+    const int ox = (int)(r % Wo), oy = (int)((r / Wo) % Ho), b = (int)(r / ((long)Wo * Ho));
+    const int pad = k / 2, iy = oy * s - pad + tap / k, ix = ox * s - pad + tap % k;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+        v = *reinterpret_cast<const uint4*>(in + (((size_t)b * H + iy) * W + ix) * C + c8 * 8);
+    *reinterpret_cast<uint4*>(out + (size_t)r * taps * C + tap * C + c8 * 8) = v;
+}
+
+// ---------------------------------------------------------------- FPN add ---
+// out_bf16[b, y, x, c] = lat[b, y, x, c] + bilinear_x2(src)[b, y, x, c]  (align_corners:
+// source index = dst * (in - 1) / (out - 1) in f32, as torch's upsample_bilinear2d)
+__global__ void k_lf_up_add(const float* __restrict__ lat, const float* __restrict__ src, int B, int h, int w, int C,
+                            bf16_t* __restrict__ out) {
+    const int Ho = 2 * h, Wo = 2 * w;
+    const long total = (long)B * Ho * Wo * C;
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= total) return;
+    const int c = (int)(e % C);
+    long r = e / C;
+    const int x = (int)(r % Wo), y = (int)((r / Wo) % Ho), b = (int)(r / ((long)Wo * Ho));
+    const float sh = Ho > 1 ? (float)(h - 1) / (float)(Ho - 1) : 0.f;
+    const float sw = Wo > 1 ? (float)(w - 1) / (float)(Wo - 1) : 0.f;
+    const float fy = sh * (float)y, fx = sw * (float)x;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = y0 < h - 1 ? y0 + 1 : y0, x1 = x0 < w - 1 ? x0 + 1 : x0;
+    const float ly1 = fy - (float)y0, lx1 = fx - (float)x0, ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+    const float* s0 = src + ((size_t)b * h * w) * C + c;
+    const float v00 = s0[((size_t)y0 * w + x0) * C], v01 = s0[((size_t)y0 * w + x1) * C];
+    const float v10 = s0[((size_t)y1 * w + x0) * C], v11 = s0[((size_t)y1 * w + x1) * C];
+    const float up = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+    out[e] = f32_to_bf16(lat[e] + up);
+}
+
+// ------------------------------------------------------- tokens + PE --------
+// x[row] = feat[frame(row)][t] + pe[t] (f32) and bf16 copy into cat[row][0..255]
+__global__ void k_lf_tokens(const float* __restrict__ coarse, const int32_t* __restrict__ frame_of, int L,
+                            const float* __restrict__ pe, float* __restrict__ x, bf16_t* __restrict__ cat, int rows) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (row, 4 channels)
+    if (e >= (long)rows * 64) return;
+    const int row = (int)(e / 64), c4 = (int)(e % 64), seg = row / L, t = row - seg * L;
+    const float4 f = reinterpret_cast<const float4*>(coarse + ((size_t)frame_of[seg] * L + t) * 256)[c4];
+    const float4 p = reinterpret_cast<const float4*>(pe + (size_t)t * 256)[c4];
+    const float4 y = make_float4(f.x + p.x, f.y + p.y, f.z + p.z, f.w + p.w);
+    reinterpret_cast<float4*>(x + (size_t)row * 256)[c4] = y;
+    reinterpret_cast<uint2*>(cat + (size_t)row * 512)[c4] = make_uint2(pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w));
+}
+
+// ------------------------------------------------------ linear attention ----
+// per (segment, head): KV[dk][dv] = sum_s phik[s][dk] * (v[s][dv] / L), ksum[dk] = sum_s
+// phik[s][dk]; phik / v rows of segment g start at (g * L + s) * ld + col offset.  Thread
+// (dk, dv-quad) of a 256-thread group; tokens staged 64 at a time through LDS.
+template <int DH>
+__global__ __launch_bounds__(256) void k_lf_kv(const float* __restrict__ k, const float* __restrict__ v, int ldk,
+                                               int ldv, int L, int heads, const int32_t* __restrict__ kseg,
+                                               float* __restrict__ KV, float* __restrict__ ksum) {
+    __shared__ float sk[64][DH + 1], sv[64][DH + 1];
+    const int g = blockIdx.x / heads, h = blockIdx.x % heads;
+    const int src = kseg ? kseg[g] : g;
+    constexpr int NQ = DH * DH / 4;  // (dk, quad) items
+    const int tid = threadIdx.x;
+    float acc[(NQ + 255) / 256][4] = {};
+    float ks = 0.f;
+    const float invL = 1.0f / (float)L;
+    for (int s0 = 0; s0 < L; s0 += 64) {
+        const int n = min(64, L - s0);
+        __syncthreads();
+        for (int e = tid; e < 64 * DH; e += 256) {
+            const int s = e / DH, d = e % DH;
+            float a = 0.f, b = 0.f;
+            if (s < n) {
+                const size_t row = (size_t)src * L + s0 + s;
+                a = k[row * ldk + h * DH + d];
+                b = v[row * ldv + h * DH + d] / (float)L;
+            }
+            sk[s][d] = a;
+            sv[s][d] = b;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < (NQ + 255) / 256; ++it) {
+            const int q = tid + 256 * it;
+            if (q >= NQ) break;
+            const int dk = q / (DH / 4), dv = (q % (DH / 4)) * 4;
+            for (int s = 0; s < n; ++s) {
+                const float a = sk[s][dk];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[it][j] = fmaf(a, sv[s][dv + j], acc[it][j]);
+            }
+        }
+        if (tid < DH)
+            for (int s = 0; s < n; ++s) ks += sk[s][tid];
+    }
+    (void)invL;
+#pragma unroll
+    for (int it = 0; it < (NQ + 255) / 256; ++it) {
+        const int q = tid + 256 * it;
+        if (q >= NQ) break;
+        const int dk = q / (DH / 4), dv = (q % (DH / 4)) * 4;
+        float* o = KV + (((size_t)g * heads + h) * DH + dk) * DH + dv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = acc[it][j];
+    }
+    if (tid < DH) ksum[((size_t)g * heads + h) * DH + tid] = ks;
+}
+
+// msg[row][h * DH + dv] = (sum_dk phiq[dk] KV[dk][dv]) * (1 / (phiq . ksum + 1e-6)) * L
+template <int DH>
+__global__ __launch_bounds__(256) void k_lf_apply(const float* __restrict__ q, int ldq, const float* __restrict__ KV,
+                                                  const float* __restrict__ ksum, int L, int heads, long rows,
+                                                  bf16_t* __restrict__ msg) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (row, head)
+    if (e >= rows * heads) return;
+    const long row = e / heads;
+    const int h = (int)(e % heads);
+    const long g = row / L;
+    const float* qr = q + row * ldq + h * DH;
+    const float* kv = KV + ((size_t)g * heads + h) * DH * DH;
+    const float* ks = ksum + ((size_t)g * heads + h) * DH;
+    float qv[DH];
+    float z = 0.f;
+#pragma unroll
+    for (int d = 0; d < DH; ++d) {
+        qv[d] = qr[d];
+        z = fmaf(qv[d], ks[d], z);
+    }
+    const float zi = 1.0f / (z + 1e-6f);
+    bf16_t* o = msg + row * (heads * DH) + h * DH;
+#pragma unroll
+    for (int dv = 0; dv < DH; dv += 2) {
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+            a0 = fmaf(qv[d], kv[d * DH + dv], a0);
+            a1 = fmaf(qv[d], kv[d * DH + dv + 1], a1);
+        }
+        *reinterpret_cast<uint32_t*>(o + dv) = pack_bf16x2(a0 * zi * (float)L, a1 * zi * (float)L);
+    }
+}
+
+// ------------------------------------------------------------- LayerNorm ----
+// one wave per row of D (128 or 256) f32: torch's two-pass mean / variance (biased), eps
+// 1e-5.  mode 0: y -> bf16 out[row * ldo + col0 ..]; mode 1: x[row] += y, bf16(x) ->
+// out[row * ldo ..] (the residual update and the next layer's bf16 operand).
+template <int D>
+__global__ __launch_bounds__(256) void k_lf_ln(const float* __restrict__ in, const float* __restrict__ g,
+                                               const float* __restrict__ b, long rows, int mode, float* __restrict__ x,
+                                               bf16_t* __restrict__ out, int ldo) {
+    const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    constexpr int PER = D / 64;
+    float v[PER];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        v[i] = in[row * D + lane * PER + i];
+        s += v[i];
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const float d = v[i] - mean;
+        q = fmaf(d, d, q);
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)D + 1e-5f);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = lane * PER + i;
+        float y = (v[i] - mean) * rstd * g[c] + b[c];
+        if (mode == 1) {
+            y = x[row * D + c] + y;
+            x[row * D + c] = y;
+        }
+        out[row * ldo + c] = f32_to_bf16(y);
+    }
+}
+
+// ------------------------------------------------------- dual softmax -------
+// sim = (S / 256) / 0.1 (the reference divides each side by 16 and the product by the
+// temperature); per row i: max_j sim, sum_j exp(sim - max); per column likewise.
+__device__ __forceinline__ float lf_sim(float s) { return (s * (1.0f / 256.0f)) / 0.1f; }
+
+__global__ __launch_bounds__(256) void k_lf_rowstats(const float* __restrict__ S, int L, float* __restrict__ rmax,
+                                                     float* __restrict__ rsum) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= L) return;
+    const float* s = S + (size_t)row * L;
+    float m = -INFINITY;
+    for (int j = lane; j < L; j += 64) m = fmaxf(m, lf_sim(s[j]));
+    m = wave_max(m);
+    float z = 0.f;
+    for (int j = lane; j < L; j += 64) z += expf(lf_sim(s[j]) - m);
+    z = wave_sum(z);
+    if (lane == 0) {
+        rmax[row] = m;
+        rsum[row] = z;
+    }
+}
+
+// 64 columns per workgroup, 4 waves split the rows, partials combined through LDS
+__global__ __launch_bounds__(256) void k_lf_colstats(const float* __restrict__ S, int L, float* __restrict__ cmax,
+                                                     float* __restrict__ csum) {
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = blockIdx.x * 64 + lane;
+    const bool ok = col < L;
+    float m = -INFINITY;
+    if (ok)
+        for (int i = wave; i < L; i += 4) m = fmaxf(m, lf_sim(S[(size_t)i * L + col]));
+    red[wave][lane] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0][lane], red[1][lane]), fmaxf(red[2][lane], red[3][lane]));
+    __syncthreads();
+    float z = 0.f;
+    if (ok)
+        for (int i = wave; i < L; i += 4) z += expf(lf_sim(S[(size_t)i * L + col]) - m);
+    red[wave][lane] = z;
+    __syncthreads();
+    if (wave == 0 && ok) {
+        cmax[col] = m;
+        csum[col] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    }
+}
+
+// conf = softmax over dim 1 (column-wise) * softmax over dim 2 (row-wise), as torch
+__device__ __forceinline__ float lf_conf(float s, float rm, float rz, float cm, float cz) {
+    const float x = lf_sim(s);
+    return (expf(x - cm) / cz) * (expf(x - rm) / rz);
+}
+
+__global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S, int L, const float* __restrict__ rmax,
+                                                    const float* __restrict__ rsum, const float* __restrict__ cmax,
+                                                    const float* __restrict__ csum, float* __restrict__ bval,
+                                                    int32_t* __restrict__ bidx) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= L) return;
+    const float* s = S + (size_t)row * L;
+    const float rm = rmax[row], rz = rsum[row];
+    float bv = -1.f;
+    int bi = 0x7fffffff;
+    for (int j = lane; j < L; j += 64) {
+        const float c = lf_conf(s[j], rm, rz, cmax[j], csum[j]);
+        if (c > bv) { bv = c; bi = j; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {  // max value, first index on ties
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) {
+        bval[row] = bv;
+        bidx[row] = bi;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_lf_colmax(const float* __restrict__ S, int L, const float* __restrict__ rmax,
+                                                   const float* __restrict__ rsum, const float* __restrict__ cmax,
+                                                   const float* __restrict__ csum, float* __restrict__ cbest) {
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = blockIdx.x * 64 + lane;
+    const bool ok = col < L;
+    float m = -1.f;
+    if (ok) {
+        const float cm = cmax[col], cz = csum[col];
+        for (int i = wave; i < L; i += 4) m = fmaxf(m, lf_conf(S[(size_t)i * L + col], rmax[i], rsum[i], cm, cz));
+    }
+    red[wave][lane] = m;
+    __syncthreads();
+    if (wave == 0 && ok) cbest[col] = fmaxf(fmaxf(red[0][lane], red[1][lane]), fmaxf(red[2][lane], red[3][lane]));
+}
+
+// Mutual-nearest selection with threshold and border, compacted in row order (one
+// workgroup per pair): match (i, j = best_i) iff conf > thr, neither cell within
+// `border` cells of its map's edge, conf == column max of j.
+__global__ __launch_bounds__(1024) void k_lf_select(const float* __restrict__ bval, const int32_t* __restrict__ bidx,
+                                                    const float* __restrict__ cbest, int L, int hc, int wc, float thr,
+                                                    int border, int32_t* __restrict__ mi, int32_t* __restrict__ mj,
+                                                    float* __restrict__ mconf, int32_t* __restrict__ count) {
+    __shared__ int warp_tot[16];
+    __shared__ int base;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) base = 0;
+    __syncthreads();
+    auto inner = [&](int id) {
+        const int r = id / wc, c = id % wc;
+        return r >= border && r < hc - border && c >= border && c < wc - border;
+    };
+    for (int i0 = 0; i0 < L; i0 += 1024) {
+        const int i = i0 + tid;
+        bool ok = false;
+        float v = 0.f;
+        int j = 0;
+        if (i < L) {
+            v = bval[i];
+            j = bidx[i];
+            ok = v > thr && j >= 0 && j < L && inner(i) && inner(j) && v == cbest[j];
+        }
+        const unsigned long long bal = __ballot(ok);
+        const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) warp_tot[wave] = __popcll(bal);
+        __syncthreads();
+        int off = base;
+        for (int w = 0; w < wave; ++w) off += warp_tot[w];
+        if (ok) {
+            mi[off + pre] = i;
+            mj[off + pre] = j;
+            mconf[off + pre] = v;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int t = 0;
+            for (int w = 0; w < 16; ++w) t += warp_tot[w];
+            base += t;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) *count = base;
+}
+
+// ---------------------------------------------------------------- fine ------
+// Match m of a chunk = (pair mp[m], slot ms[m]): cell i = mi[pair * L + slot] of frame
+// frm[pair] (side 0), cell j = mj[..] of frame frm[P + pair] (side 1).  Window token t =
+// (dy, dx) of side s reads fine pixel (stride r - 2 + dy, stride c - 2 + dx) (zero
+// outside, F.unfold padding 2) -> bf16 win[((s * M + m) * 25 + t)][128]; the matched
+// coarse rows (side-major coarse residual stream xc) -> bf16 crow[s * M + m][256].
+__global__ void k_lf_windows(const float* __restrict__ fine, int Hf, int Wf, int wc, int stride,
+                             const int32_t* __restrict__ frm, int P, const int32_t* __restrict__ mi,
+                             const int32_t* __restrict__ mj, int L, const int32_t* __restrict__ mp,
+                             const int32_t* __restrict__ ms, int M, const float* __restrict__ xc,
+                             bf16_t* __restrict__ win, bf16_t* __restrict__ crow) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long nwin = (long)2 * M * 25 * 32;  // (side, m, t, c4) over 32 c4
+    if (e < nwin) {
+        const int c4 = (int)(e % 32);
+        long r = e / 32;
+        const int t = (int)(r % 25);
+        const long sm = r / 25;
+        const int m = (int)(sm % M), side = (int)(sm / M);
+        const int p = mp[m];
+        const size_t o = (size_t)p * L + ms[m];
+        const int cell = side ? mj[o] : mi[o], frame = frm[side * P + p];
+        const int y = (cell / wc) * stride - 2 + t / 5, x = (cell % wc) * stride - 2 + t % 5;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (y >= 0 && y < Hf && x >= 0 && x < Wf)
+            v = reinterpret_cast<const float4*>(fine + (((size_t)frame * Hf + y) * Wf + x) * 128)[c4];
+        reinterpret_cast<uint2*>(win + (size_t)r * 128)[c4] = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+        return;
+    }
+    const long e2 = e - nwin;  // coarse rows: (side, m, c4) over 64 c4
+    if (e2 >= (long)2 * M * 64) return;
+    const int c4 = (int)(e2 % 64);
+    const long r = e2 / 64;
+    const int m = (int)(r % M), side = (int)(r / M);
+    const int p = mp[m];
+    const size_t o = (size_t)p * L + ms[m];
+    const size_t src = ((size_t)side * P + p) * L + (side ? mj[o] : mi[o]);
+    const float4 v = reinterpret_cast<const float4*>(xc + src * 256)[c4];
+    reinterpret_cast<uint2*>(crow + (size_t)r * 256)[c4] = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+}
+
+// x[(s, m, t)][c] = A[(s, m, t)][c] + Cm[(s, m)][c] (f32) and its bf16 copy into cat
+__global__ void k_lf_fine_tokens(const float* __restrict__ A, const float* __restrict__ Cm, long rows,
+                                 float* __restrict__ x, bf16_t* __restrict__ cat) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (row, c4) over 32
+    if (e >= rows * 32) return;
+    const long row = e / 32;
+    const int c4 = (int)(e % 32);
+    const float4 a = reinterpret_cast<const float4*>(A + row * 128)[c4];
+    const float4 c = reinterpret_cast<const float4*>(Cm + (row / 25) * 128)[c4];
+    const float4 y = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w + c.w);
+    reinterpret_cast<float4*>(x + row * 128)[c4] = y;
+    reinterpret_cast<uint2*>(cat + row * 256)[c4] = make_uint2(pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w));
+}
+
+// per match: heatmap = softmax(x0[m][12] . x1[m][r] * 128^-1/2); expectation on the
+// normalised grid (x = linspace(-1, 1, 5)[r % 5], y = [r / 5]); keypoints in pixels:
+// kpts0 = 8 (i % wc, i / wc), kpts1 = 8 (j % wc, j / wc) + 2 * 2 * (x, y)
+__global__ __launch_bounds__(64) void k_lf_fine_match(const float* __restrict__ xf, int M,
+                                                      const int32_t* __restrict__ mp, const int32_t* __restrict__ ms,
+                                                      const int32_t* __restrict__ mi, const int32_t* __restrict__ mj,
+                                                      const float* __restrict__ mconf, int L, int wc, float scale_c,
+                                                      float scale_f, float* __restrict__ kp0, float* __restrict__ kp1,
+                                                      float* __restrict__ conf) {
+    const int m = blockIdx.x, lane = threadIdx.x;
+    if (m >= M) return;
+    const float* c0 = xf + ((size_t)m * 25 + 12) * 128;
+    float sim = -INFINITY;
+    if (lane < 25) {
+        const float* w = xf + (((size_t)M + m) * 25 + lane) * 128;
+        float a = 0.f;
+        for (int c = 0; c < 128; ++c) a = fmaf(c0[c], w[c], a);
+        sim = 0.08838834764831845f * a;
+    }
+    const float mx = wave_max(sim);
+    const float ex = lane < 25 ? expf(sim - mx) : 0.f;
+    const float z = wave_sum(ex);
+    const float h = ex / z;
+    const float g = lane < 25 ? -1.f + 0.5f * (float)(lane % 5) : 0.f;
+    const float gy = lane < 25 ? -1.f + 0.5f * (float)(lane / 5) : 0.f;
+    const float cx = wave_sum(h * g), cy = wave_sum(h * gy);
+    if (lane == 0) {
+        const size_t o = (size_t)mp[m] * L + ms[m];
+        const int i = mi[o], j = mj[o];
+        kp0[2 * o] = (float)(i % wc) * scale_c;
+        kp0[2 * o + 1] = (float)(i / wc) * scale_c;
+        kp1[2 * o] = (float)(j % wc) * scale_c + cx * 2.0f * scale_f;
+        kp1[2 * o + 1] = (float)(j / wc) * scale_c + cy * 2.0f * scale_f;
+        conf[o] = mconf[o];
+    }
+}
+
+inline size_t a256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+struct ConvSpec {
+    int cin, cout, k, s;
+};
+// mlg_loftr_weights.conv_w order (include/mlgate.h); 196-channel stages padded to 256
+constexpr ConvSpec CONVS[MLG_LOFTR_NCONV] = {
+    {128, 128, 3, 1}, {128, 128, 3, 1}, {128, 128, 3, 1}, {128, 128, 3, 1},                    // layer1
+    {128, 256, 3, 2}, {256, 256, 3, 1}, {128, 256, 1, 2}, {256, 256, 3, 1}, {256, 256, 3, 1},  // layer2
+    {256, 256, 3, 2}, {256, 256, 3, 1}, {256, 256, 1, 2}, {256, 256, 3, 1}, {256, 256, 3, 1},  // layer3
+    {256, 256, 1, 1}, {256, 256, 1, 1}, {256, 256, 3, 1}, {256, 256, 3, 1},                    // FPN 1/4
+    {128, 256, 1, 1}, {256, 256, 3, 1}, {256, 128, 3, 1}};                                     // FPN 1/2
+
+struct FeatLayout {
+    size_t xf, xb, yb, rf, tf, col, c3, c2, total;
+};
+
+FeatLayout feat_layout(int B, int H, int W) {
+    const size_t P2 = (size_t)B * (H / 2) * (W / 2);  // 1/2-resolution pixels
+    FeatLayout L{};
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        size_t r = o;
+        o += a256(bytes);
+        return r;
+    };
+    L.xf = take(P2 * 256 * 4);   // residual stream f32 (up to 256 channels)
+    L.xb = take(P2 * 256 * 2);   // its bf16 copy
+    L.yb = take(P2 * 256 * 2);   // block-internal bf16 activation
+    L.rf = take(P2 * 256 * 4);   // shortcut / lateral f32
+    L.tf = take(P2 * 256 * 4);   // FPN f32 temporaries
+    L.col = take(P2 * 9 * 256 * 2);  // im2col rows
+    L.c3 = take(P2 / 16 * 256 * 4 + 256);  // layer3 output f32 (1/8)
+    L.c2 = take(P2 / 4 * 256 * 4 + 256);   // layer2 output f32 (1/4) kept for the FPN
+    L.total = o;
+    return L;
+}
+
+int conv(const mlg_loftr_weights& w, int idx, const bf16_t* in, int B, int H, int W, bf16_t* col, const float* R,
+         float* X, bf16_t* C, int act, hipStream_t s) {
+    const ConvSpec sp = CONVS[idx];
+    const int Ho = (H + sp.s - 1) / sp.s, Wo = (W + sp.s - 1) / sp.s;
+    const long M = (long)B * Ho * Wo;
+    const bf16_t* A = in;
+    if (sp.k != 1 || sp.s != 1) {
+        const long items = M * sp.k * sp.k * (sp.cin / 8);
+        hipLaunchKernelGGL(k_lf_im2col, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, in, B, H, W, sp.cin,
+                           sp.k, sp.s, col);
+        MLG_LAUNCH_CHECK();
+        A = col;
+    }
+    const int K = sp.k * sp.k * sp.cin;
+    return mlg_gemm_conv(A, K, (const bf16_t*)w.conv_w[idx], w.conv_b[idx], R, sp.cout, X, sp.cout, C, sp.cout, act,
+                         sp.cout, (int)M, sp.cout, K, s);
+}
+
+#define LF_TRY(x)                    \
+    do {                             \
+        int rc_ = (x);               \
+        if (rc_ != MLG_OK) return rc_; \
+    } while (0)
+
+// one BasicBlock: in (f32 x + bf16 xb) -> out (same buffers), stride 1 or 2
+int basic_block(const mlg_loftr_weights& w, int c1, int c2, int cds, int B, int H, int W, float* x, bf16_t* xb,
+                bf16_t* yb, float* rf, bf16_t* col, hipStream_t s) {
+    const int st = CONVS[c1].s, Ho = (H + st - 1) / st, Wo = (W + st - 1) / st;
+    LF_TRY(conv(w, c1, xb, B, H, W, col, nullptr, nullptr, yb, 1, s));  // relu(bn1(conv1 x))
+    const float* R = x;
+    if (cds >= 0) {  // bn(downsample x) -> rf
+        LF_TRY(conv(w, cds, xb, B, H, W, col, nullptr, rf, nullptr, 0, s));
+        R = rf;
+    }
+    // relu(R + bn2(conv2 y)) -> x (f32) + xb; R may alias x (stride 1: same shape)
+    return conv(w, c2, yb, B, Ho, Wo, col, R, x, xb, 1, s);
+}
+
+}  // namespace
+
+size_t mlg_loftr_features_ws_bytes(int B, int H, int W) {
+    if (B <= 0 || H < 32 || W < 32 || (H % 8) || (W % 8)) return 0;
+    return feat_layout(B, H, W).total;
+}
+
+int mlg_loftr_features(const mlg_loftr_weights* wp, const uint8_t* frames, int B, int H, int W, int C,
+                       long frame_stride, void* ws, size_t ws_bytes, float* coarse, float* fine, void* stream) {
+    if (!wp || !frames || !ws || !coarse || !fine || B <= 0 || H < 32 || W < 32 || (H % 8) || (W % 8) ||
+        (C != 1 && C != 3 && C != 4))
+        return MLG_EINVAL;
+    const FeatLayout L = feat_layout(B, H, W);
+    if (ws_bytes < L.total) return MLG_ENOMEM;
+    const mlg_loftr_weights& w = *wp;
+    hipStream_t s = (hipStream_t)stream;
+    char* base = (char*)ws;
+    float* xf = (float*)(base + L.xf);
+    bf16_t* xb = (bf16_t*)(base + L.xb);
+    bf16_t* yb = (bf16_t*)(base + L.yb);
+    float* rf = (float*)(base + L.rf);
+    float* tf = (float*)(base + L.tf);
+    bf16_t* col = (bf16_t*)(base + L.col);
+    float* c3 = (float*)(base + L.c3);
+    float* c2 = (float*)(base + L.c2);
+    const int H2 = H / 2, W2 = W / 2, H4 = H / 4, W4 = W / 4, H8 = H / 8, W8 = W / 8;
+    hipLaunchKernelGGL(k_lf_stem, dim3((W2 + 15) / 16, (H2 + 7) / 8, B), dim3(256), 0, s, frames, frame_stride, H, W,
+                       C, w.stem_w, w.stem_b, xf, xb);
+    MLG_LAUNCH_CHECK();
+    // layer1 (1/2, 128)
+    LF_TRY(basic_block(w, 0, 1, -1, B, H2, W2, xf, xb, yb, rf, col, s));
+    LF_TRY(basic_block(w, 2, 3, -1, B, H2, W2, xf, xb, yb, rf, col, s));
+    // x1 (bf16) is needed by the FPN: keep it in tf's bf16 view? -- store x1 bf16 in fine
+    // (scratch until the end: fine is written last)
+    bf16_t* x1b = (bf16_t*)fine;
+    hipMemcpyAsync(x1b, xb, (size_t)B * H2 * W2 * 128 * 2, hipMemcpyDeviceToDevice, s);
+    // layer2 (1/4, 256p)
+    LF_TRY(basic_block(w, 4, 5, 6, B, H2, W2, xf, xb, yb, rf, col, s));
+    LF_TRY(basic_block(w, 7, 8, -1, B, H4, W4, xf, xb, yb, rf, col, s));
+    bf16_t* x2b = (bf16_t*)c2;  // bf16 copy of x2 (c2 is free until the FPN needs its f32 slot)
+    hipMemcpyAsync(x2b, xb, (size_t)B * H4 * W4 * 256 * 2, hipMemcpyDeviceToDevice, s);
+    // layer3 (1/8, 256)
+    LF_TRY(basic_block(w, 9, 10, 11, B, H4, W4, xf, xb, yb, rf, col, s));
+    LF_TRY(basic_block(w, 12, 13, -1, B, H8, W8, xf, xb, yb, rf, col, s));
+    // FPN: x3_out = outconv3(x3) -> coarse output (f32)
+    LF_TRY(conv(w, 14, xb, B, H8, W8, col, nullptr, coarse, nullptr, 0, s));
+    // x2_out = outconv2(x2) + up(x3_out) -> bf16 -> conv + BN + leaky -> conv
+    LF_TRY(conv(w, 15, x2b, B, H4, W4, col, nullptr, tf, nullptr, 0, s));
+    {
+        const long n = (long)B * H4 * W4 * 256;
+        hipLaunchKernelGGL(k_lf_up_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tf, coarse, B, H8, W8, 256,
+                           yb);
+        MLG_LAUNCH_CHECK();
+    }
+    LF_TRY(conv(w, 16, yb, B, H4, W4, col, nullptr, nullptr, xb, 2, s));
+    LF_TRY(conv(w, 17, xb, B, H4, W4, col, nullptr, c2, nullptr, 0, s));  // x2_out f32 (1/4, 256p)
+    // x1_out = outconv1(x1) + up(x2_out) -> conv + BN + leaky -> conv -> fine
+    LF_TRY(conv(w, 18, x1b, B, H2, W2, col, nullptr, tf, nullptr, 0, s));
+    {
+        const long n = (long)B * H2 * W2 * 256;
+        hipLaunchKernelGGL(k_lf_up_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tf, c2, B, H4, W4, 256,
+                           yb);
+        MLG_LAUNCH_CHECK();
+    }
+    LF_TRY(conv(w, 19, yb, B, H2, W2, col, nullptr, nullptr, xb, 2, s));
+    LF_TRY(conv(w, 20, xb, B, H2, W2, col, nullptr, fine, nullptr, 0, s));
+    (void)c3;
+    return MLG_OK;
+}
+
+// ------------------------------------------------------------- matching -----
+namespace {
+
+struct LayerBufs {
+    float* x;     // [rows][d] residual stream
+    bf16_t* cat;  // [rows][2d]: bf16(x) | norm1(msg)
+    float* qkv;   // [rows][3d]
+    bf16_t* msg;  // [rows][d]
+    float* t;     // [rows][d]
+    bf16_t* h;    // [rows][2d]
+    float* kv;    // [segs][8][dh][dh]
+    float* ks;    // [segs][8][dh]
+};
+
+// One LoFTREncoderLayer over `nseg` segments of L tokens (rows x0 .. of the buffers);
+// source rows src0 (== x0 for self).  d = 256 (coarse) or 128 (fine).
+int encoder_layer(const mlg_loftr_layer& lw, const LayerBufs& b, int d, long x0, long src0, int nseg, int L,
+                  hipStream_t s) {
+    const long rows = (long)nseg * L;
+    const int dh = d / 8;
+    float* qkv = b.qkv + x0 * 3 * d;
+    if (x0 == src0) {  // q | k | v in one GEMM, elu + 1 on q and k
+        LF_TRY(mlg_gemm_conv(b.cat + x0 * 2 * d, 2 * d, (const bf16_t*)lw.w, nullptr, nullptr, 0, qkv, 3 * d, nullptr,
+                             0, 3, 2 * d, (int)rows, 3 * d, d, s));
+    } else {
+        LF_TRY(mlg_gemm_conv(b.cat + x0 * 2 * d, 2 * d, (const bf16_t*)lw.w, nullptr, nullptr, 0, qkv, 3 * d, nullptr,
+                             0, 3, d, (int)rows, d, d, s));
+        LF_TRY(mlg_gemm_conv(b.cat + src0 * 2 * d, 2 * d, (const bf16_t*)lw.w + (size_t)d * d, nullptr, nullptr, 0,
+                             qkv + d, 3 * d, nullptr, 0, 3, d, (int)rows, 2 * d, d, s));
+    }
+    float* kv = b.kv + (size_t)(x0 / L) * 8 * dh * dh;
+    float* ks = b.ks + (size_t)(x0 / L) * 8 * dh;
+    if (d == 256) {
+        hipLaunchKernelGGL(k_lf_kv<32>, dim3(nseg * 8), dim3(256), 0, s, qkv + d, qkv + 2 * d, 3 * d, 3 * d, L, 8,
+                           (const int32_t*)nullptr, kv, ks);
+        MLG_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_lf_apply<32>, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, qkv, 3 * d, kv,
+                           ks, L, 8, rows, b.msg + x0 * d);
+    } else {
+        hipLaunchKernelGGL(k_lf_kv<16>, dim3(nseg * 8), dim3(256), 0, s, qkv + d, qkv + 2 * d, 3 * d, 3 * d, L, 8,
+                           (const int32_t*)nullptr, kv, ks);
+        MLG_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_lf_apply<16>, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, qkv, 3 * d, kv,
+                           ks, L, 8, rows, b.msg + x0 * d);
+    }
+    MLG_LAUNCH_CHECK();
+    // merge -> norm1 -> bf16 into cat[:, d:]
+    LF_TRY(mlg_gemm_conv(b.msg + x0 * d, d, (const bf16_t*)lw.wmerge, nullptr, nullptr, 0, b.t + x0 * d, d, nullptr,
+                         0, 0, 0, (int)rows, d, d, s));
+    const unsigned lnb = (unsigned)((rows + 3) / 4);
+    if (d == 256)
+        hipLaunchKernelGGL(k_lf_ln<256>, dim3(lnb), dim3(256), 0, s, b.t + x0 * d, lw.ln1_g, lw.ln1_b, rows, 0,
+                           (float*)nullptr, b.cat + x0 * 2 * d + d, 2 * d);
+    else
+        hipLaunchKernelGGL(k_lf_ln<128>, dim3(lnb), dim3(256), 0, s, b.t + x0 * d, lw.ln1_g, lw.ln1_b, rows, 0,
+                           (float*)nullptr, b.cat + x0 * 2 * d + d, 2 * d);
+    MLG_LAUNCH_CHECK();
+    // MLP: relu([x | msg] W1^T) W2^T -> norm2 -> residual
+    LF_TRY(mlg_gemm_conv(b.cat + x0 * 2 * d, 2 * d, (const bf16_t*)lw.w1, nullptr, nullptr, 0, nullptr, 0,
+                         b.h + x0 * 2 * d, 2 * d, 1, 2 * d, (int)rows, 2 * d, 2 * d, s));
+    LF_TRY(mlg_gemm_conv(b.h + x0 * 2 * d, 2 * d, (const bf16_t*)lw.w2, nullptr, nullptr, 0, b.t + x0 * d, d, nullptr,
+                         0, 0, 0, (int)rows, d, 2 * d, s));
+    if (d == 256)
+        hipLaunchKernelGGL(k_lf_ln<256>, dim3(lnb), dim3(256), 0, s, b.t + x0 * d, lw.ln2_g, lw.ln2_b, rows, 1,
+                           b.x + x0 * d, b.cat + x0 * 2 * d, 2 * d);
+    else
+        hipLaunchKernelGGL(k_lf_ln<128>, dim3(lnb), dim3(256), 0, s, b.t + x0 * d, lw.ln2_g, lw.ln2_b, rows, 1,
+                           b.x + x0 * d, b.cat + x0 * 2 * d, 2 * d);
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}
+
+// the reference's layer order: self on both sides; cross updates side 0 from side 1,
+// then side 1 from the updated side 0.  Side-major rows: side s, segment g at
+// (s * nseg + g) * L.
+int transformer(const mlg_loftr_layer* layers, int nl, const LayerBufs& b, int d, int nseg, int L, hipStream_t s) {
+    const long half = (long)nseg * L;
+    for (int i = 0; i < nl; ++i) {
+        if (i % 2 == 0) {
+            LF_TRY(encoder_layer(layers[i], b, d, 0, 0, 2 * nseg, L, s));
+        } else {
+            LF_TRY(encoder_layer(layers[i], b, d, 0, half, nseg, L, s));
+            LF_TRY(encoder_layer(layers[i], b, d, half, 0, nseg, L, s));
+        }
+    }
+    return MLG_OK;
+}
+
+struct MatchLayout {
+    size_t cx, ccat, cqkv, cmsg, ct, ch, ckv, cks;  // coarse transformer (rows 2 P L, d 256)
+    size_t fx, fcat, fqkv, fmsg, ft, fh, fkv, fks;  // fine transformer (rows 2 C 25, d 128)
+    size_t win, crow, cd, cm, S, rmax, rsum, cmax, csum, bval, bidx, cbest, mi, mj, mconf, cnt, frm, mp, ms, total;
+};
+
+constexpr int FINE_CHUNK = 4096;  // matches per fine-stage pass
+
+MatchLayout match_layout(int P, int L) {
+    MatchLayout M{};
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        size_t r = o;
+        o += a256(bytes);
+        return r;
+    };
+    const size_t rc = (size_t)2 * P * L, rf = (size_t)2 * FINE_CHUNK * 25;
+    M.cx = take(rc * 256 * 4);
+    M.ccat = take(rc * 512 * 2);
+    M.cqkv = take(rc * 768 * 4);
+    M.cmsg = take(rc * 256 * 2);
+    M.ct = take(rc * 256 * 4);
+    M.ch = take(rc * 512 * 2);
+    M.ckv = take((size_t)2 * P * 8 * 32 * 32 * 4);
+    M.cks = take((size_t)2 * P * 8 * 32 * 4);
+    M.fx = take(rf * 128 * 4);
+    M.fcat = take(rf * 256 * 2);
+    M.fqkv = take(rf * 384 * 4);
+    M.fmsg = take(rf * 128 * 2);
+    M.ft = take(rf * 128 * 4);
+    M.fh = take(rf * 256 * 2);
+    M.fkv = take((size_t)2 * FINE_CHUNK * 8 * 16 * 16 * 4);
+    M.fks = take((size_t)2 * FINE_CHUNK * 8 * 16 * 4);
+    M.win = take(rf * 128 * 2);
+    M.crow = take((size_t)2 * FINE_CHUNK * 256 * 2);
+    M.cd = take((size_t)2 * FINE_CHUNK * 128 * 2);
+    M.cm = take((size_t)2 * FINE_CHUNK * 128 * 4);
+    M.S = take((size_t)L * L * 4);
+    M.rmax = take((size_t)L * 4);
+    M.rsum = take((size_t)L * 4);
+    M.cmax = take((size_t)L * 4);
+    M.csum = take((size_t)L * 4);
+    M.bval = take((size_t)L * 4);
+    M.bidx = take((size_t)L * 4);
+    M.cbest = take((size_t)L * 4);
+    M.mi = take((size_t)P * L * 4);
+    M.mj = take((size_t)P * L * 4);
+    M.mconf = take((size_t)P * L * 4);
+    M.cnt = take((size_t)P * 4);
+    M.frm = take((size_t)2 * P * 4);
+    M.mp = take((size_t)FINE_CHUNK * 4);
+    M.ms = take((size_t)FINE_CHUNK * 4);
+    M.total = o;
+    return M;
+}
+
+}  // namespace
+
+size_t mlg_loftr_match_ws_bytes(int P, int H, int W) {
+    if (P <= 0 || H < 32 || W < 32 || (H % 8) || (W % 8)) return 0;
+    return match_layout(P, (H / 8) * (W / 8)).total;
+}
+
+int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const float* fine, int H, int W,
+                    const int32_t* pa, const int32_t* pb, int P, const float* pe, void* ws, size_t ws_bytes,
+                    int32_t* counts, float* kpts0, float* kpts1, float* conf, void* stream) {
+    if (!wp || !coarse || !fine || !pa || !pb || !pe || !ws || !counts || !kpts0 || !kpts1 || !conf || P <= 0 ||
+        H < 32 || W < 32 || (H % 8) || (W % 8))
+        return MLG_EINVAL;
+    const int hc = H / 8, wc = W / 8, L = hc * wc, Hf = H / 2, Wf = W / 2;
+    const MatchLayout ML = match_layout(P, L);
+    if (ws_bytes < ML.total) return MLG_ENOMEM;
+    const mlg_loftr_weights& w = *wp;
+    hipStream_t s = (hipStream_t)stream;
+    char* base = (char*)ws;
+    auto at = [&](size_t off) { return (void*)(base + off); };
+    const LayerBufs bc{(float*)at(ML.cx), (bf16_t*)at(ML.ccat), (float*)at(ML.cqkv), (bf16_t*)at(ML.cmsg),
+                       (float*)at(ML.ct), (bf16_t*)at(ML.ch), (float*)at(ML.ckv), (float*)at(ML.cks)};
+    const LayerBufs bf{(float*)at(ML.fx), (bf16_t*)at(ML.fcat), (float*)at(ML.fqkv), (bf16_t*)at(ML.fmsg),
+                       (float*)at(ML.ft), (bf16_t*)at(ML.fh), (float*)at(ML.fkv), (float*)at(ML.fks)};
+    bf16_t* win = (bf16_t*)at(ML.win);
+    bf16_t* crow = (bf16_t*)at(ML.crow);
+    bf16_t* cd = (bf16_t*)at(ML.cd);
+    float* cm = (float*)at(ML.cm);
+    float* S = (float*)at(ML.S);
+    float* rmax = (float*)at(ML.rmax);
+    float* rsum = (float*)at(ML.rsum);
+    float* cmax = (float*)at(ML.cmax);
+    float* csum = (float*)at(ML.csum);
+    float* bval = (float*)at(ML.bval);
+    int32_t* bidx = (int32_t*)at(ML.bidx);
+    float* cbest = (float*)at(ML.cbest);
+    int32_t* mi = (int32_t*)at(ML.mi);
+    int32_t* mj = (int32_t*)at(ML.mj);
+    float* mconf = (float*)at(ML.mconf);
+    int32_t* cnt = (int32_t*)at(ML.cnt);
+    int32_t* frm = (int32_t*)at(ML.frm);
+    int32_t* dmp = (int32_t*)at(ML.mp);
+    int32_t* dms = (int32_t*)at(ML.ms);
+
+    // coarse tokens, side-major: side 0 = frames pa, side 1 = frames pb
+    std::vector<int32_t> h_frames(2 * P);
+    for (int p = 0; p < P; ++p) {
+        h_frames[p] = pa[p];
+        h_frames[P + p] = pb[p];
+    }
+    if (hipMemcpyAsync(frm, h_frames.data(), h_frames.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+        return MLG_EHIP;
+    const long crows = (long)2 * P * L;
+    hipLaunchKernelGGL(k_lf_tokens, dim3((unsigned)((crows * 64 + 255) / 256)), dim3(256), 0, s, coarse, frm, L, pe,
+                       bc.x, bc.cat, (int)crows);
+    MLG_LAUNCH_CHECK();
+    LF_TRY(transformer(w.coarse, 8, bc, 256, P, L, s));
+    // dual softmax + mutual nearest, pair by pair over one [L, L] similarity buffer
+    for (int p = 0; p < P; ++p) {
+        const float* f0 = bc.x + (size_t)p * L * 256;
+        const float* f1 = bc.x + ((size_t)P + p) * L * 256;
+        LF_TRY(mlg_similarity_f32(f0, L, f1, L, 256, S, L, s));
+        hipLaunchKernelGGL(k_lf_rowstats, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum);
+        hipLaunchKernelGGL(k_lf_colstats, dim3((L + 63) / 64), dim3(256), 0, s, S, L, cmax, csum);
+        hipLaunchKernelGGL(k_lf_rowbest, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, cmax, csum, bval, bidx);
+        hipLaunchKernelGGL(k_lf_colmax, dim3((L + 63) / 64), dim3(256), 0, s, S, L, rmax, rsum, cmax, csum, cbest);
+        hipLaunchKernelGGL(k_lf_select, dim3(1), dim3(1024), 0, s, bval, bidx, cbest, L, hc, wc, 0.2f, 2,
+                           mi + (size_t)p * L, mj + (size_t)p * L, mconf + (size_t)p * L, cnt + p);
+        MLG_LAUNCH_CHECK();
+    }
+    std::vector<int32_t> h_cnt(P);
+    if (hipMemcpyAsync(h_cnt.data(), cnt, (size_t)P * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(counts, cnt, (size_t)P * 4, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return MLG_EHIP;
+    std::vector<int32_t> mp, ms;
+    for (int p = 0; p < P; ++p)
+        for (int k = 0; k < h_cnt[p]; ++k) {
+            mp.push_back(p);
+            ms.push_back(k);
+        }
+    const long Mtot = (long)mp.size();
+    for (long m0 = 0; m0 < Mtot; m0 += FINE_CHUNK) {
+        const int M = (int)std::min<long>(FINE_CHUNK, Mtot - m0);
+        if (hipMemcpyAsync(dmp, mp.data() + m0, (size_t)M * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(dms, ms.data() + m0, (size_t)M * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+            return MLG_EHIP;
+        const long items = (long)2 * M * 25 * 32 + (long)2 * M * 64;
+        hipLaunchKernelGGL(k_lf_windows, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, fine, Hf, Wf, wc,
+                           Hf / hc, frm, P, mi, mj, L, dmp, dms, M, bc.x, win, crow);
+        MLG_LAUNCH_CHECK();
+        const long frows = (long)2 * M * 25;
+        // merge_feat on [window | down_proj(coarse)]: the window half per token, the
+        // coarse half once per (side, match)
+        LF_TRY(mlg_gemm_conv(win, 128, (const bf16_t*)w.merge_wf, nullptr, nullptr, 0, bf.t, 128, nullptr, 0, 0, 0,
+                             (int)frows, 128, 128, s));
+        LF_TRY(mlg_gemm_conv(crow, 256, (const bf16_t*)w.down_w, w.down_b, nullptr, 0, nullptr, 0, cd, 128, 0, 0,
+                             2 * M, 128, 256, s));
+        LF_TRY(mlg_gemm_conv(cd, 128, (const bf16_t*)w.merge_wc, w.merge_b, nullptr, 0, cm, 128, nullptr, 0, 0, 0,
+                             2 * M, 128, 128, s));
+        hipLaunchKernelGGL(k_lf_fine_tokens, dim3((unsigned)((frows * 32 + 255) / 256)), dim3(256), 0, s, bf.t, cm,
+                           frows, bf.x, bf.cat);
+        MLG_LAUNCH_CHECK();
+        LF_TRY(transformer(w.fine, 2, bf, 128, M, 25, s));
+        hipLaunchKernelGGL(k_lf_fine_match, dim3(M), dim3(64), 0, s, bf.x, M, dmp, dms, mi, mj, mconf, L, wc,
+                           (float)H / (float)hc, (float)H / (float)Hf, kpts0, kpts1, conf);
+        MLG_LAUNCH_CHECK();
+        if (m0 + M < Mtot && hipStreamSynchronize(s) != hipSuccess) return MLG_EHIP;  // mp / ms reused
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) return MLG_EHIP;  // pageable uploads complete
+    return MLG_OK;
+}

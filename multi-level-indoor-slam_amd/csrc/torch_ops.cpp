@@ -230,6 +230,91 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> superpoint(const Tensor& fram
     return {kp, sc, ds, db, cnt};
 }
 
+// ------------------------------------------------------------------ LoFTR
+// weights: stem_w, stem_b, conv_w[21], conv_b[21] (empty = none), 8 coarse + 2 fine
+// layers x (w, wmerge, w1, w2, ln1_g, ln1_b, ln2_g, ln2_b), down_w, down_b, merge_wf,
+// merge_wc, merge_b (mlgate/loftr.py builds the list)
+constexpr int kLoftrTensors = 2 + 2 * MLG_LOFTR_NCONV + 10 * 8 + 5;
+
+mlg_loftr_weights loftr_weights(at::TensorList w) {
+    TORCH_CHECK((int)w.size() == kLoftrTensors, "loftr weights: expected ", kLoftrTensors, " tensors, got ", w.size());
+    mlg_loftr_weights s;
+    std::memset(&s, 0, sizeof(s));
+    int i = 0;
+    s.stem_w = cp<float>(w[i++]);
+    s.stem_b = cp<float>(w[i++]);
+    for (int c = 0; c < MLG_LOFTR_NCONV; ++c) s.conv_w[c] = cp<uint16_t>(w[i++]);
+    for (int c = 0; c < MLG_LOFTR_NCONV; ++c) s.conv_b[c] = cp<float>(w[i++]);
+    for (int l = 0; l < 10; ++l) {
+        mlg_loftr_layer& L = l < 8 ? s.coarse[l] : s.fine[l - 8];
+        L.w = cp<uint16_t>(w[i++]);
+        L.wmerge = cp<uint16_t>(w[i++]);
+        L.w1 = cp<uint16_t>(w[i++]);
+        L.w2 = cp<uint16_t>(w[i++]);
+        L.ln1_g = cp<float>(w[i++]);
+        L.ln1_b = cp<float>(w[i++]);
+        L.ln2_g = cp<float>(w[i++]);
+        L.ln2_b = cp<float>(w[i++]);
+    }
+    s.down_w = cp<uint16_t>(w[i++]);
+    s.down_b = cp<float>(w[i++]);
+    s.merge_wf = cp<uint16_t>(w[i++]);
+    s.merge_wc = cp<uint16_t>(w[i++]);
+    s.merge_b = cp<float>(w[i++]);
+    return s;
+}
+
+std::tuple<Tensor, Tensor> loftr_features(const Tensor& frames, at::TensorList w) {
+    want(frames, at::kByte, "frames");
+    TORCH_CHECK(frames.dim() == 4, "frames must be [B, H, W, C]");
+    const mlg_loftr_weights s = loftr_weights(w);
+    const int64_t B = frames.size(0), H = frames.size(1), W = frames.size(2), C = frames.size(3);
+    const size_t nbytes = mlg_loftr_features_ws_bytes((int)B, (int)H, (int)W);
+    TORCH_CHECK(nbytes > 0, "LoFTR needs H, W >= 32 and multiples of 8 (got ", H, "x", W, ")");
+    c10::DeviceGuard g(frames.device());
+    auto o = frames.options().dtype(at::kFloat);
+    Tensor coarse = at::empty({B, (H / 8) * (W / 8), 256}, o), fine = at::empty({B, (H / 2) * (W / 2), 128}, o);
+    Tensor ws = workspace(nbytes, frames);
+    check_rc(mlg_loftr_features(&s, cp<uint8_t>(frames), (int)B, (int)H, (int)W, (int)C, (long)(H * W * C),
+                                ws.data_ptr(), (size_t)ws.numel(), mp<float>(coarse), mp<float>(fine),
+                                stream_of(frames)),
+             "mlg_loftr_features");
+    return {coarse, fine};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> loftr_match(const Tensor& coarse, const Tensor& fine, const Tensor& pa,
+                                                       const Tensor& pb, const Tensor& pe, at::TensorList w, int64_t H,
+                                                       int64_t W) {
+    want(coarse, at::kFloat, "coarse");
+    want(fine, at::kFloat, "fine");
+    want(pe, at::kFloat, "pe");
+    want(pa, at::kInt, "pair_a", false);
+    want(pb, at::kInt, "pair_b", false);
+    const int64_t P = pa.numel(), F = coarse.size(0), L = (H / 8) * (W / 8);
+    TORCH_CHECK(pb.numel() == P && P > 0, "pair lists must be non-empty and of equal length");
+    TORCH_CHECK(coarse.dim() == 3 && coarse.size(1) == L && coarse.size(2) == 256, "coarse must be [F, H/8*W/8, 256]");
+    TORCH_CHECK(fine.dim() == 3 && fine.size(0) == F && fine.size(1) == (H / 2) * (W / 2) && fine.size(2) == 128,
+                "fine must be [F, H/2*W/2, 128]");
+    TORCH_CHECK(pe.numel() == L * 256, "pe must be [H/8*W/8, 256]");
+    const int32_t* a = pa.data_ptr<int32_t>();
+    const int32_t* b = pb.data_ptr<int32_t>();
+    for (int64_t p = 0; p < P; ++p)
+        TORCH_CHECK(a[p] >= 0 && a[p] < F && b[p] >= 0 && b[p] < F, "pair ", p, " indexes a missing frame");
+    const mlg_loftr_weights s = loftr_weights(w);
+    const size_t nbytes = mlg_loftr_match_ws_bytes((int)P, (int)H, (int)W);
+    TORCH_CHECK(nbytes > 0, "LoFTR needs H, W >= 32 and multiples of 8");
+    c10::DeviceGuard g(coarse.device());
+    auto o = coarse.options();
+    Tensor counts = at::empty({P}, o.dtype(at::kInt));
+    Tensor k0 = at::zeros({P, L, 2}, o), k1 = at::zeros({P, L, 2}, o), cf = at::zeros({P, L}, o);
+    Tensor ws = workspace(nbytes, coarse);
+    check_rc(mlg_loftr_match(&s, cp<float>(coarse), cp<float>(fine), (int)H, (int)W, a, b, (int)P, cp<float>(pe),
+                             ws.data_ptr(), (size_t)ws.numel(), mp<int32_t>(counts), mp<float>(k0), mp<float>(k1),
+                             mp<float>(cf), stream_of(coarse)),
+             "mlg_loftr_match");
+    return {counts, k0, k1, cf};
+}
+
 // --------------------------------------------------------------- LightGlue
 constexpr int kLgTensors = 1 + 9 * 10 * 2 + 9 * 4 + 8 * 2 + 1;
 
@@ -460,6 +545,9 @@ TORCH_LIBRARY(mlgate, m) {
           "int hypotheses, int seed, bool with_pose) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
     m.def("recover_pose(Tensor k1, Tensor k2, Tensor offsets, Tensor K, int k_stride, Tensor E, Tensor mask) -> Tensor");
     m.def("resnet50(Tensor frames, Tensor[] weights, int descriptor_dim) -> Tensor");
+    m.def("loftr_features(Tensor frames, Tensor[] weights) -> (Tensor, Tensor)");
+    m.def("loftr_match(Tensor coarse, Tensor fine, Tensor pair_a, Tensor pair_b, Tensor pe, Tensor[] weights, int H, "
+          "int W) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("pillow_resize_224(Tensor frames) -> Tensor");
     m.def("plane_ransac(Tensor pts, Tensor offsets, int iterations, int seed, float threshold) "
           "-> (Tensor, Tensor, Tensor)");
@@ -482,6 +570,8 @@ TORCH_LIBRARY_IMPL(mlgate, CUDA, m) {
     m.impl("ransac_epipolar", &ransac_epipolar);
     m.impl("recover_pose", &recover_pose);
     m.impl("resnet50", &resnet50);
+    m.impl("loftr_features", &loftr_features);
+    m.impl("loftr_match", &loftr_match);
     m.impl("pillow_resize_224", &pillow_resize_224);
     m.impl("plane_ransac", &plane_ransac);
     m.impl("proximity", &proximity);

@@ -2,10 +2,10 @@
 
 The dataclasses, the verifier decision rule (geometric_verification.py:586-634),
 the semantic cross-floor skip and its statistics (:688-744), SuperPoint + LightGlue
-matching (:196-312; mlgate.superpoint / mlgate.lightglue) and the RANSAC stage --
-essential / fundamental matrix + recoverPose (:104-188; mlgate.geometry) -- all run on
-the GPU.  SuperGlue and LoFTR resolve to the LightGlue path exactly as the reference
-does when their packages are missing.
+matching (:196-312; mlgate.superpoint / mlgate.lightglue), detector-free LoFTR
+(:424-526; mlgate.loftr) and the RANSAC stage -- essential / fundamental matrix +
+recoverPose (:104-188; mlgate.geometry) -- all run on the GPU.  SuperGlue resolves to
+the LightGlue path exactly as the reference does (its native branch defers to it).
 """
 import warnings
 from dataclasses import dataclass
@@ -171,9 +171,11 @@ class SuperGlue(BaseFeatureMatcher):
 
 
 class LoFTR(BaseFeatureMatcher):
-    """geometric_verification.py:424-526.  Without kornia the reference falls back to
-    LightGlue (with this warning); the detector-free LoFTR transformer itself is not
-    built yet, so this matcher runs the GPU LightGlue path."""
+    """Detector-free LoFTR on the GPU (geometric_verification.py:424-526): the reference's
+    native branch -- kornia.feature.LoFTR(pretrained='indoor') on cv2 BGR2GRAY / 255 frames
+    (mlgate.loftr, csrc/loftr.hip).  Frames must have H and W multiples of 8 (the
+    reference resizes other sizes down to multiples of 8 with cv2.resize; that resize is
+    not built: such frames raise)."""
 
     def __init__(self, device: str = 'cuda', weights: str = 'indoor'):
         super().__init__(device)
@@ -183,18 +185,38 @@ class LoFTR(BaseFeatureMatcher):
     def _load_model(self):
         if self._model_loaded:
             return
-        warnings.warn("LoFTR (kornia) not installed. Using LightGlue fallback. Install with: pip install kornia")
-        self._fallback = LightGlue(device=self.device)
+        from .loftr import LoFTRGPU
+        self._matcher = LoFTRGPU(device=self.device)
+        if self._matcher.weights_source.startswith("synthetic"):
+            warnings.warn("LoFTR weights not configured (MLGATE_LOFTR_WEIGHTS); using seeded synthetic weights")
         self._model_loaded = True
-        self._is_native = False
+        self._is_native = True
 
-    def detect_and_match(self, image1, image2):
+    @staticmethod
+    def _check(shape):
+        h, w = shape[:2]
+        if h % 8 or w % 8:
+            raise ValueError(f"LoFTR: frame {w}x{h} is not a multiple of 8 (the reference's cv2.resize to "
+                             f"{w // 8 * 8}x{h // 8 * 8} is not built)")
+
+    def detect_and_match(self, image1: np.ndarray, image2: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         self._load_model()
-        return self._fallback.detect_and_match(image1, image2)
+        im1, im2 = np.asarray(image1, np.uint8), np.asarray(image2, np.uint8)
+        self._check(im1.shape)
+        self._check(im2.shape)
+        dev = torch.device(self.device)
+        as4 = lambda im: torch.from_numpy(np.ascontiguousarray(im if im.ndim == 3 else im[..., None]))  # noqa: E731
+        if im1.shape == im2.shape:
+            k0, k1, c = self._matcher.match_frames(torch.stack([as4(im1), as4(im2)]).to(dev), [(0, 1)])[0]
+            return k0.astype(np.float32), k1.astype(np.float32), c.astype(np.float32)
+        raise ValueError("LoFTR: the two frames must share a shape (the reference resizes each to its own "
+                         "multiple of 8; mixed shapes are not built)")
 
     def detect_and_match_batch(self, frames, pairs):
+        """frames: device uint8 [F, H, W, C]; pairs [(a, b)] -> [(kpts_a, kpts_b, conf)]."""
         self._load_model()
-        return self._fallback.detect_and_match_batch(frames, pairs)
+        self._check(tuple(frames.shape[1:3]))
+        return self._matcher.match_frames(frames, pairs)
 
 
 _MATCHERS = {'lightglue': LightGlue, 'superglue': SuperGlue, 'loftr': LoFTR}

@@ -314,3 +314,164 @@ def resolve_resnet50_state_dict(path=None, seed=0):
     if path:
         return load_resnet50_state_dict(path), path
     return resnet50_state_dict(seed), f"synthetic(seed={seed})"
+
+
+# ----------------------------------------------------------------------------- LoFTR
+# kornia.feature.LoFTR(pretrained='indoor') (geometric_verification.py:446-449): the
+# ResNetFPN_8_2 backbone, the 8-layer coarse and 2-layer fine linear-attention
+# transformers and the fine preprocessing, with kornia's state-dict key names.
+LOFTR_DIMS = (128, 196, 256)
+
+
+def loftr_keys():
+    keys = ["backbone.conv1.weight"] + [f"backbone.bn1.{s}" for s in ("weight", "bias", "running_mean",
+                                                                       "running_var")]
+    bn = ("weight", "bias", "running_mean", "running_var")
+    for li in range(3):
+        for bi in range(2):
+            p = f"backbone.layer{li + 1}.{bi}."
+            keys += [p + "conv1.weight", p + "conv2.weight"] + [p + f"bn{j}.{s}" for j in (1, 2) for s in bn]
+            if li > 0 and bi == 0:
+                keys += [p + "downsample.0.weight"] + [p + f"downsample.1.{s}" for s in bn]
+    keys += ["backbone.layer3_outconv.weight", "backbone.layer2_outconv.weight", "backbone.layer1_outconv.weight"]
+    for n in (2, 1):
+        p = f"backbone.layer{n}_outconv2."
+        keys += [p + "0.weight", p + "3.weight"] + [p + f"1.{s}" for s in bn]
+    for pre, nl in (("loftr_coarse", 8), ("loftr_fine", 2)):
+        for i in range(nl):
+            p = f"{pre}.layers.{i}."
+            keys += [p + s for s in ("q_proj.weight", "k_proj.weight", "v_proj.weight", "merge.weight",
+                                     "mlp.0.weight", "mlp.2.weight", "norm1.weight", "norm1.bias", "norm2.weight",
+                                     "norm2.bias")]
+    keys += ["fine_preprocess.down_proj.weight", "fine_preprocess.down_proj.bias",
+             "fine_preprocess.merge_feat.weight", "fine_preprocess.merge_feat.bias"]
+    return keys
+
+
+def loftr_state_dict(seed=0, whiten=True):
+    """Seeded float32 weights with kornia's LoFTR key names and shapes (He-normal convs,
+    BatchNorm statistics near identity, 1 / sqrt(fan-in) linears; the transformers' norm2
+    gains small, so each layer refines rather than replaces the token).
+
+    With ``whiten`` the coarse lateral conv (layer3_outconv, 1x1 256 -> 256, no bias) is
+    the regularised whitening of layer3's responses on a few seeded synthetic scenes, with
+    their mean direction projected out: untrained ReLU features share one dominant
+    direction, which leaves the dual-softmax nothing to match; whitened ones make a
+    revisit produce confident coarse matches, as trained LoFTR features do."""
+    return {k: v.copy() for k, v in _loftr_sd(int(seed), bool(whiten)).items()}
+
+
+@functools.lru_cache(maxsize=2)
+def _loftr_sd(seed, whiten):
+    rng = np.random.default_rng(seed)
+    sd = {}
+
+    def normal(shape, std, mean=0.0):
+        return (rng.standard_normal(shape, dtype=np.float32) * np.float32(std) + np.float32(mean)).astype(np.float32)
+
+    def conv(name, cout, cin, k):
+        sd[name] = normal((cout, cin, k, k), np.sqrt(2.0 / (cin * k * k)))
+
+    def bn(p, c):
+        sd[p + ".weight"] = rng.uniform(0.8, 1.2, c).astype(np.float32)
+        sd[p + ".bias"] = normal((c,), 0.05)
+        sd[p + ".running_mean"] = normal((c,), 0.1)
+        sd[p + ".running_var"] = rng.uniform(0.6, 1.4, c).astype(np.float32)
+
+    d0, d1, d2 = LOFTR_DIMS
+    conv("backbone.conv1.weight", d0, 1, 7)
+    bn("backbone.bn1", d0)
+    cin = d0
+    for li, d in enumerate(LOFTR_DIMS):
+        for bi in range(2):
+            p = f"backbone.layer{li + 1}.{bi}."
+            conv(p + "conv1.weight", d, cin if bi == 0 else d, 3)
+            conv(p + "conv2.weight", d, d, 3)
+            bn(p + "bn1", d)
+            bn(p + "bn2", d)
+            if li > 0 and bi == 0:
+                conv(p + "downsample.0.weight", d, cin, 1)
+                bn(p + "downsample.1", d)
+        cin = d
+    conv("backbone.layer3_outconv.weight", d2, d2, 1)
+    conv("backbone.layer2_outconv.weight", d2, d1, 1)
+    conv("backbone.layer2_outconv2.0.weight", d2, d2, 3)
+    bn("backbone.layer2_outconv2.1", d2)
+    conv("backbone.layer2_outconv2.3.weight", d1, d2, 3)
+    conv("backbone.layer1_outconv.weight", d1, d0, 1)
+    conv("backbone.layer1_outconv2.0.weight", d1, d1, 3)
+    bn("backbone.layer1_outconv2.1", d1)
+    conv("backbone.layer1_outconv2.3.weight", d0, d1, 3)
+    for pre, nl, d in (("loftr_coarse", 8, 256), ("loftr_fine", 2, 128)):
+        for i in range(nl):
+            p = f"{pre}.layers.{i}."
+            for n in ("q_proj", "k_proj", "v_proj", "merge"):
+                sd[p + n + ".weight"] = normal((d, d), 1.0 / np.sqrt(d))
+            sd[p + "mlp.0.weight"] = normal((2 * d, 2 * d), np.sqrt(2.0 / (2 * d)))
+            sd[p + "mlp.2.weight"] = normal((d, 2 * d), 1.0 / np.sqrt(2 * d))
+            sd[p + "norm1.weight"] = normal((d,), 0.05, 1.0)
+            sd[p + "norm1.bias"] = normal((d,), 0.02)
+            sd[p + "norm2.weight"] = normal((d,), 0.02, 0.1)
+            sd[p + "norm2.bias"] = normal((d,), 0.01)
+    sd["fine_preprocess.down_proj.weight"] = normal((128, 256), 1.0 / 16)
+    sd["fine_preprocess.down_proj.bias"] = normal((128,), 0.02)
+    sd["fine_preprocess.merge_feat.weight"] = normal((128, 256), 1.0 / 16)
+    sd["fine_preprocess.merge_feat.bias"] = normal((128,), 0.02)
+    if whiten:
+        sd["backbone.layer3_outconv.weight"] = _loftr_whitening(sd, seed)
+    return sd
+
+
+def _loftr_whitening(sd, seed, n_scenes=3, reg=1e-2, h=240, w=320):
+    """Whitening of layer3's outputs (mean direction projected out) over the 1/8 grid of
+    `n_scenes` seeded synthetic frames.  One-time weight construction on the CPU."""
+    import torch
+    import torch.nn.functional as F
+    from . import synthetic
+    t = {k: torch.from_numpy(v) for k, v in sd.items()}
+
+    def bn(x, p):
+        return F.batch_norm(x, t[p + ".running_mean"], t[p + ".running_var"], t[p + ".weight"], t[p + ".bias"],
+                            False, 0.0, 1e-5)
+
+    def block(x, p, stride):
+        y = F.relu(bn(F.conv2d(x, t[p + ".conv1.weight"], stride=stride, padding=1), p + ".bn1"))
+        y = bn(F.conv2d(y, t[p + ".conv2.weight"], padding=1), p + ".bn2")
+        if stride != 1:
+            x = bn(F.conv2d(x, t[p + ".downsample.0.weight"], stride=stride), p + ".downsample.1")
+        return F.relu(x + y)
+
+    imgs = []
+    for i in range(n_scenes):
+        base = synthetic.scene(70_000 + 97 * seed + i, h, w).astype(np.int32)
+        imgs.append((base[..., 0] * 1868 + base[..., 1] * 9617 + base[..., 2] * 4899 + 8192) >> 14)
+    with torch.no_grad():
+        x = torch.from_numpy(np.stack(imgs).astype(np.float32) / 255.0)[:, None]
+        x = F.relu(bn(F.conv2d(x, t["backbone.conv1.weight"], stride=2, padding=3), "backbone.bn1"))
+        for li, stride in ((1, 1), (2, 2), (3, 2)):
+            x = block(block(x, f"backbone.layer{li}.0", stride), f"backbone.layer{li}.1", 1)
+    Z = x.permute(0, 2, 3, 1).reshape(-1, x.shape[1]).double().numpy()
+    mu = Z.mean(0)
+    P = np.eye(len(mu)) - np.outer(mu, mu) / (mu @ mu)
+    Zp = Z @ P
+    ev, V = np.linalg.eigh(np.cov(Zp.T))
+    Wh = (V / np.sqrt(np.maximum(ev, 0) + reg * ev.max())) @ V.T @ P
+    return Wh.astype(np.float32).reshape(len(mu), len(mu), 1, 1)
+
+
+def load_loftr_state_dict(path):
+    """kornia LoFTR checkpoint (loftr_indoor.ckpt: {'state_dict': ...} or a bare state dict)."""
+    import torch
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    sd = sd.get("state_dict", sd)
+    missing = [k for k in loftr_keys() if k not in sd]
+    if missing:
+        raise KeyError(f"checkpoint {path} lacks LoFTR keys, e.g. {missing[:3]}")
+    return {k: sd[k].float().cpu().numpy() for k in loftr_keys()}
+
+
+def resolve_loftr_state_dict(path=None, seed=0):
+    path = path or os.environ.get("MLGATE_LOFTR_WEIGHTS")
+    if path:
+        return load_loftr_state_dict(path), path
+    return loftr_state_dict(seed), f"synthetic(seed={seed})"

@@ -1,0 +1,105 @@
+"""LoFTR on the GPU (csrc/loftr.hip via torch.ops.mlgate.loftr_*) against the fp32 torch
+restatement of kornia's LoFTR (oracle/loftr.py; kornia and its 'indoor' weights are
+absent: seeded synthetic weights, parity unpinned against kornia itself).
+
+Bars (bf16 MFMA convs / GEMMs against an fp32 oracle):
+  * backbone (14 bf16 conv layers deep): per-cell cosine to the fp32 maps, mean >= 0.998
+    and min >= 0.97 (coarse 1/8 map), mean >= 0.995 and min >= 0.95 (fine 1/2 map);
+  * matching stage on the GPU's own features (stage-anchored, the oracle's f32 matching
+    on the same inputs): >= 95 % of the coarse matches (i, j) shared, confidences within
+    2e-2 relative, fine keypoints within 0.25 px on the shared matches;
+  * end to end: >= 90 % of the oracle's coarse matches found, keypoints within 0.5 px;
+  * the drop-in LoFTR.detect_and_match equals the batched path bit for bit.
+"""
+import numpy as np
+import pytest
+import torch
+
+from mlgate import synthetic
+from mlgate.loftr import LoFTRGPU
+from mlgate.weights import loftr_state_dict
+from oracle import loftr as ol
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def setup(dev):
+    sd = loftr_state_dict(0)
+    seq = synthetic.make_sequence(40, 8, 1)
+    po = seq.place_of
+    pairs = [(a, b) for a in range(40) for b in range(a + 1, 40) if po[a] == po[b]][:2]
+    pairs += [(a, b) for a in range(40) for b in range(a + 1, 40) if po[a] != po[b]][:1]
+    idx = sorted({i for p in pairs for i in p})
+    frames = synthetic.frames_host(seq, np.arange(40))
+    return sd, LoFTRGPU(device=str(dev), state_dict=sd), ol.Oracle(sd), frames, pairs, idx
+
+
+def _cos(a, b):
+    a, b = a.reshape(-1, a.shape[-1]).double(), b.reshape(-1, b.shape[-1]).double()
+    return torch.nn.functional.cosine_similarity(a, b, dim=1)
+
+
+@pytest.mark.parametrize("hw", [(480, 640), (136, 208)])
+def test_backbone_matches_oracle(dev, setup, hw):
+    sd, lf, orc, frames, _, _ = setup
+    H, W = hw
+    imgs = np.ascontiguousarray(frames[:2, :H, :W])
+    c, f = lf.features(torch.from_numpy(imgs).to(dev))
+    c, f = c.cpu(), f.cpu()
+    for b in range(2):
+        oc, of = orc.features(ol.to_gray(imgs[b]))
+        cc = _cos(c[b], oc[0].permute(1, 2, 0).reshape(-1, 256))
+        cf = _cos(f[b], of[0].permute(1, 2, 0).reshape(-1, 128))
+        stats = (float(cc.mean()), float(cc.min()), float(cf.mean()), float(cf.min()))
+        assert stats[0] >= 0.998 and stats[1] >= 0.97 and stats[2] >= 0.995 and stats[3] >= 0.95, stats
+
+
+def test_matching_stage_on_gpu_features(dev, setup):
+    sd, lf, orc, frames, pairs, idx = setup
+    H, W = 480, 640
+    fr = torch.from_numpy(frames[idx]).to(dev)
+    coarse, fine = lf.features(fr)
+    pos = {f: k for k, f in enumerate(idx)}
+    n, k0, k1, cf = lf.match_device(coarse, fine, H, W, [pos[a] for a, _ in pairs], [pos[b] for _, b in pairs])
+    n, k0, k1, cf = n.cpu().numpy(), k0.cpu().numpy(), k1.cpu().numpy(), cf.cpu().numpy()
+    wc = W // 8
+    for p, (a, b) in enumerate(pairs):
+        c0 = coarse[pos[a]].cpu().T.reshape(1, 256, H // 8, wc)
+        c1 = coarse[pos[b]].cpu().T.reshape(1, 256, H // 8, wc)
+        f0 = fine[pos[a]].cpu().T.reshape(1, 128, H // 2, W // 2)
+        f1 = fine[pos[b]].cpu().T.reshape(1, 128, H // 2, W // 2)
+        r = orc.match_features(c0, f0, c1, f1, H)
+        gi = (k0[p, :n[p], 1] / 8).astype(int) * wc + (k0[p, :n[p], 0] / 8).astype(int)  # coarse cell i
+        ref = {int(i): k for k, i in enumerate(r["i_ids"].numpy())}
+        shared = [k for k, i in enumerate(gi) if int(i) in ref]
+        if len(ref) == 0:
+            assert n[p] <= 2
+            continue
+        assert len(shared) >= 0.95 * len(ref), (p, len(shared), len(ref), n[p])
+        ok = 0
+        for k in shared:
+            rk = ref[int(gi[k])]
+            if np.allclose(k0[p, k], r["kpts0"][rk].numpy()) and np.abs(k1[p, k] - r["kpts1"][rk].numpy()).max() < 0.25:
+                ok += 1
+                assert abs(cf[p, k] - float(r["conf"][rk])) <= 2e-2 * float(r["conf"][rk])
+        assert ok >= 0.95 * len(shared), (p, ok, len(shared))
+
+
+def test_end_to_end_and_dropin(dev, setup):
+    from mlgate.verify import LoFTR
+    sd, lf, orc, frames, pairs, _ = setup
+    a, b = pairs[0]
+    got = lf.match_frames(torch.from_numpy(frames).to(dev), [(a, b)])[0]
+    ref = orc.detect_and_match(frames[a], frames[b])
+    assert len(ref[0]) > 100
+    rk = {tuple(np.rint(k).astype(int)): i for i, k in enumerate(ref[0])}
+    hit = [(i, rk[tuple(np.rint(k).astype(int))]) for i, k in enumerate(got[0]) if tuple(np.rint(k).astype(int)) in rk]
+    assert len(hit) >= 0.9 * len(ref[0]), (len(hit), len(ref[0]), len(got[0]))
+    close = sum(np.abs(got[1][i] - ref[1][j]).max() < 0.5 for i, j in hit)
+    assert close >= 0.9 * len(hit)
+    m = LoFTR(device=str(dev))
+    m._load_model()
+    m._matcher = lf
+    k0, k1, c = m.detect_and_match(frames[a], frames[b])
+    assert np.array_equal(k0, got[0]) and np.array_equal(k1, got[1]) and np.array_equal(c, got[2])

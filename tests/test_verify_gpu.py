@@ -4,8 +4,8 @@ against the fp32 oracle chain's per-pair verdicts (tests/golden/gate_chain.npz: 
 
 Covers the paths the batched gate does not call: LightGlue.detect_and_match on numpy
 images, GeometricVerifier.verify / verify_batch, the verify branch of
-SemanticGeometricVerifier.verify_with_semantics, and the SuperGlue / LoFTR matchers'
-fallback (the reference resolves both to LightGlue when their packages are missing).
+SemanticGeometricVerifier.verify_with_semantics, and the SuperGlue matcher's fallback
+(the reference resolves it to LightGlue; LoFTR is native: tests/test_loftr_gpu.py).
 
 Bar: is_valid identical to the fp32 chain on every pair; number of matches within 10 %
 and inliers within 15 % of the fp32 chain (bf16 GEMMs move a few percent of matches);
@@ -99,7 +99,7 @@ def test_verify_with_semantics_verify_branch(dev, chain):
     assert st["total_candidates"] == len(chain["sel"]) + 1
 
 
-@pytest.mark.parametrize("name,msg", [("superglue", "SuperGlue not installed"), ("loftr", "LoFTR (kornia)")])
+@pytest.mark.parametrize("name,msg", [("superglue", "SuperGlue not installed")])
 def test_fallback_matchers_equal_lightglue(dev, chain, name, msg):
     base = GeometricVerifier('lightglue', device=str(dev))
     v = GeometricVerifier(name, device=str(dev))

@@ -1,0 +1,55 @@
+"""LoFTR (configs[4]) timing on the GPU box: backbone per keyframe and matching per pair
+at 640x480 on synthetic revisit pairs, HIP-event timed (python tools/loftr_bench.py)."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "multi-level-indoor-slam_amd")]
+from mlgate import synthetic  # noqa: E402
+from mlgate.loftr import LoFTRGPU  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=32)
+    ap.add_argument("--pairs", type=int, default=32)
+    ap.add_argument("--iters", type=int, default=3)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    seq = synthetic.make_sequence(a.frames, max(2, a.frames // 4), 0)
+    fr = synthetic.frames_device(seq, np.arange(a.frames), dev)
+    lf = LoFTRGPU(device=dev)
+    po = seq.place_of
+    pairs = [(i, j) for i in range(a.frames) for j in range(i + 1, a.frames) if po[i] == po[j]][:a.pairs]
+    coarse, fine = lf.features(fr)
+    n, *_ = lf.match_device(coarse, fine, 480, 640, [p for p, _ in pairs], [q for _, q in pairs])
+    torch.cuda.synchronize()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    e[0].record()
+    for _ in range(a.iters):
+        coarse, fine = lf.features(fr)
+    e[1].record()
+    for _ in range(a.iters):
+        n, *_ = lf.match_device(coarse, fine, 480, 640, [p for p, _ in pairs], [q for _, q in pairs])
+    e[2].record()
+    torch.cuda.synchronize()
+    feat_ms = e[0].elapsed_time(e[1]) / a.iters
+    match_ms = e[1].elapsed_time(e[2]) / a.iters
+    gflop_feat = 2 * (240 * 320 * 49 * 128 + 240 * 320 * 9 * 128 * 128 * 4 + 120 * 160 * 9 * (128 * 196 + 3 * 196 * 196)
+                      + 120 * 160 * 196 * 128 + 60 * 80 * 9 * (196 * 256 + 3 * 256 * 256) + 60 * 80 * 196 * 256
+                      + 60 * 80 * 256 * 256 + 120 * 160 * (196 * 256 + 9 * 256 * 256 + 9 * 256 * 196)
+                      + 240 * 320 * (128 * 196 + 9 * 196 * 196 + 9 * 196 * 128)) / 1e9
+    print(json.dumps({"frames": a.frames, "pairs": len(pairs), "features_ms_per_frame": round(feat_ms / a.frames, 3),
+                      "backbone_gflop_per_frame": round(gflop_feat, 1),
+                      "backbone_tflops": round(gflop_feat * a.frames / feat_ms, 1),
+                      "match_ms_per_pair": round(match_ms / len(pairs), 3),
+                      "matches_mean": float(n.float().mean())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
