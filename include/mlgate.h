@@ -352,13 +352,16 @@ typedef struct {
     const float* merge_b;
 } mlg_loftr_weights;
 /* Backbone for B frames uint8 [B, H, W, C] (C = 3 BGR, 4 BGRA or 1 gray; frame_stride
- * bytes): coarse f32 [B, H/8 * W/8, 256] (1/8 map, row-major cells) and fine f32
- * [B, H/2 * W/2, 128].  H, W >= 32, multiples of 8. */
+ * bytes), H, W >= 32.  With H8 = H / 8 * 8, W8 = W / 8 * 8 (frames whose H or W is not a
+ * multiple of 8 are converted and resized as the reference does: cv2 BGR2GRAY, then
+ * cv2.resize INTER_LINEAR to W8 x H8): coarse f32 [B, H8/8 * W8/8, 256] (1/8 map,
+ * row-major cells) and fine f32 [B, H8/2 * W8/2, 128]. */
 size_t mlg_loftr_features_ws_bytes(int B, int H, int W);
 int mlg_loftr_features(const mlg_loftr_weights* w, const uint8_t* frames, int B, int H, int W, int C,
                        long frame_stride, void* workspace, size_t workspace_bytes, float* coarse, float* fine,
                        void* stream);
-/* Matching of P pairs (frames pa[p], pb[p]: HOST int32 arrays indexing coarse / fine):
+/* Matching of P pairs (frames pa[p], pb[p]: HOST int32 arrays indexing coarse / fine;
+ * H, W: the multiples of 8 the features were computed at; keypoints in that frame):
  * coarse transformer, dual-softmax coarse matches (conf > 0.2, 2-cell border, mutual
  * nearest), fine refinement.  pe: position encoding f32 [H/8 * W/8, 256] (device).
  * Outputs (device): counts int32 [P]; for pair p, match k < counts[p] (row order of the

@@ -97,6 +97,55 @@ __global__ __launch_bounds__(256) void k_lf_stem(const uint8_t* __restrict__ fra
     }
 }
 
+// ------------------------------------------------------- gray + resize ------
+// The reference's LoFTR input for frames whose H or W is not a multiple of 8:
+// cv2.cvtColor(BGR2GRAY) then cv2.resize(gray, (W8, H8)) with INTER_LINEAR
+// (geometric_verification.py:486-504): OpenCV's fixed-point generic path with 11-bit
+// coefficients -- horizontal sums in int, the vertical pass of its 128-bit vector loop
+// ((mulhi(S0 >> 4, b0) + mulhi(S1 >> 4, b1) + 2) >> 2) below byte `vend` of a row and
+// the scalar FixedPtCast<22> tail above it (oracle/csrc/oracle.c restates the same).
+__device__ __forceinline__ int lf_gray(const uint8_t* p, int C) {
+    return C >= 3 ? (p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + 8192) >> 14 : p[0];
+}
+__device__ __forceinline__ int lf_s16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+
+__global__ void k_lf_gray_resize(const uint8_t* __restrict__ frames, long frame_stride, int H, int W, int C, int DH,
+                                 int DW, int vend, uint8_t* __restrict__ out, int B) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (long)B * DH * DW) return;
+    const int dx = (int)(e % DW), dy = (int)((e / DW) % DH), b = (int)(e / ((long)DW * DH));
+    // x: clamped table (cv2 interpolation tables)
+    const double sx_scale = 1.0 / ((double)DW / W);
+    float fx = (float)((dx + 0.5) * sx_scale - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) { fx = 0.f; sx = 0; }
+    if (sx >= W - 1) { fx = 0.f; sx = W - 1; }
+    const int ax0 = lf_s16(__float2int_rn((1.f - fx) * 2048.f)), ax1 = lf_s16(__float2int_rn(fx * 2048.f));
+    // y: unclamped weights, clipped source rows
+    const double sy_scale = 1.0 / ((double)DH / H);
+    float fy = (float)((dy + 0.5) * sy_scale - 0.5);
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    const int by0 = lf_s16(__float2int_rn((1.f - fy) * 2048.f)), by1 = lf_s16(__float2int_rn(fy * 2048.f));
+    const int sy0 = min(max(sy, 0), H - 1), sy1 = min(max(sy + 1, 0), H - 1);
+    const int sx1 = sx + 1 < W ? sx + 1 : sx;
+    const uint8_t* img = frames + (size_t)b * frame_stride;
+    const uint8_t* r0 = img + (size_t)sy0 * W * C;
+    const uint8_t* r1 = img + (size_t)sy1 * W * C;
+    const int s0 = lf_gray(r0 + (size_t)sx * C, C) * ax0 + lf_gray(r0 + (size_t)sx1 * C, C) * ax1;
+    const int s1 = lf_gray(r1 + (size_t)sx * C, C) * ax0 + lf_gray(r1 + (size_t)sx1 * C, C) * ax1;
+    int v;
+    if (dx < vend) {
+        const int a0 = lf_s16(s0 >> 4), a1 = lf_s16(s1 >> 4);
+        v = (int)(int16_t)(((a0 * by0) >> 16) + ((a1 * by1) >> 16));
+        v = (v + 2) >> 2;
+    } else {
+        v = (s0 * by0 + s1 * by1 + (1 << 21)) >> 22;
+    }
+    out[e] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
 // ---------------------------------------------------------------- im2col ----
 // out[(b, oy, ox)][tap * C + c] for a k x k (k = 1 or 3) conv with padding k / 2 and
 // stride s over bf16 NHWC [B, H, W, C]; 8 channels (16 B) per thread.
@@ -536,7 +585,7 @@ constexpr ConvSpec CONVS[MLG_LOFTR_NCONV] = {
     {128, 256, 1, 1}, {256, 256, 3, 1}, {256, 128, 3, 1}};                                     // FPN 1/2
 
 struct FeatLayout {
-    size_t xf, xb, yb, rf, tf, col, c3, c2, total;
+    size_t xf, xb, yb, rf, tf, col, c3, c2, gray, total;
 };
 
 FeatLayout feat_layout(int B, int H, int W) {
@@ -556,6 +605,7 @@ FeatLayout feat_layout(int B, int H, int W) {
     L.col = take(P2 * 9 * 256 * 2);  // im2col rows
     L.c3 = take(P2 / 16 * 256 * 4 + 256);  // layer3 output f32 (1/8)
     L.c2 = take(P2 / 4 * 256 * 4 + 256);   // layer2 output f32 (1/4) kept for the FPN
+    L.gray = take(P2 * 4);                  // resized gray frames (H, W not multiples of 8)
     L.total = o;
     return L;
 }
@@ -601,17 +651,32 @@ int basic_block(const mlg_loftr_weights& w, int c1, int c2, int cds, int B, int 
 }  // namespace
 
 size_t mlg_loftr_features_ws_bytes(int B, int H, int W) {
-    if (B <= 0 || H < 32 || W < 32 || (H % 8) || (W % 8)) return 0;
-    return feat_layout(B, H, W).total;
+    if (B <= 0 || H < 32 || W < 32) return 0;
+    return feat_layout(B, H / 8 * 8, W / 8 * 8).total;
 }
 
-int mlg_loftr_features(const mlg_loftr_weights* wp, const uint8_t* frames, int B, int H, int W, int C,
+int mlg_loftr_features(const mlg_loftr_weights* wp, const uint8_t* frames_in, int B, int H_in, int W_in, int C,
                        long frame_stride, void* ws, size_t ws_bytes, float* coarse, float* fine, void* stream) {
-    if (!wp || !frames || !ws || !coarse || !fine || B <= 0 || H < 32 || W < 32 || (H % 8) || (W % 8) ||
+    if (!wp || !frames_in || !ws || !coarse || !fine || B <= 0 || H_in < 32 || W_in < 32 ||
         (C != 1 && C != 3 && C != 4))
         return MLG_EINVAL;
+    const int H = H_in / 8 * 8, W = W_in / 8 * 8;
     const FeatLayout L = feat_layout(B, H, W);
     if (ws_bytes < L.total) return MLG_ENOMEM;
+    const uint8_t* frames = frames_in;
+    if (H != H_in || W != W_in) {  // cv2 gray + INTER_LINEAR resize to multiples of 8
+        int vend = 0;  // first byte of a row in the vertical pass's scalar tail
+        for (; vend <= W - 16; vend += 16) {}
+        for (; vend < W - 8; vend += 8) {}
+        uint8_t* g = (uint8_t*)ws + L.gray;
+        const long n = (long)B * H * W;
+        hipLaunchKernelGGL(k_lf_gray_resize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           frames_in, frame_stride, H_in, W_in, C, H, W, vend, g, B);
+        MLG_LAUNCH_CHECK();
+        frames = g;
+        C = 1;
+        frame_stride = (long)H * W;
+    }
     const mlg_loftr_weights& w = *wp;
     hipStream_t s = (hipStream_t)stream;
     char* base = (char*)ws;

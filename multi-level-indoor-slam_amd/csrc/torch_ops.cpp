@@ -270,10 +270,11 @@ std::tuple<Tensor, Tensor> loftr_features(const Tensor& frames, at::TensorList w
     const mlg_loftr_weights s = loftr_weights(w);
     const int64_t B = frames.size(0), H = frames.size(1), W = frames.size(2), C = frames.size(3);
     const size_t nbytes = mlg_loftr_features_ws_bytes((int)B, (int)H, (int)W);
-    TORCH_CHECK(nbytes > 0, "LoFTR needs H, W >= 32 and multiples of 8 (got ", H, "x", W, ")");
+    TORCH_CHECK(nbytes > 0, "LoFTR needs H, W >= 32 (got ", H, "x", W, ")");
     c10::DeviceGuard g(frames.device());
     auto o = frames.options().dtype(at::kFloat);
-    Tensor coarse = at::empty({B, (H / 8) * (W / 8), 256}, o), fine = at::empty({B, (H / 2) * (W / 2), 128}, o);
+    const int64_t H8 = H / 8 * 8, W8 = W / 8 * 8;
+    Tensor coarse = at::empty({B, (H8 / 8) * (W8 / 8), 256}, o), fine = at::empty({B, (H8 / 2) * (W8 / 2), 128}, o);
     Tensor ws = workspace(nbytes, frames);
     check_rc(mlg_loftr_features(&s, cp<uint8_t>(frames), (int)B, (int)H, (int)W, (int)C, (long)(H * W * C),
                                 ws.data_ptr(), (size_t)ws.numel(), mp<float>(coarse), mp<float>(fine),

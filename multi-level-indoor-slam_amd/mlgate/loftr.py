@@ -128,8 +128,9 @@ class LoFTRGPU:
         self.ops = _native.ops()
 
     def features(self, frames):
-        """uint8 [F, H, W, C] device frames (H, W multiples of 8) -> (coarse [F, H/8 W/8, 256],
-        fine [F, H/2 W/2, 128]) f32 device tensors."""
+        """uint8 [F, H, W, C] device frames -> (coarse [F, H8/8 W8/8, 256], fine [F, H8/2 W8/2, 128])
+        f32 device tensors, H8 = H // 8 * 8 (other sizes go through cv2's gray + INTER_LINEAR
+        resize on the device, as the reference resizes)."""
         outs = [self.ops.loftr_features(frames[i:i + self.feature_batch].contiguous(), self.weights)
                 for i in range(0, frames.shape[0], self.feature_batch)]
         return torch.cat([c for c, _ in outs]), torch.cat([f for _, f in outs])
@@ -143,11 +144,12 @@ class LoFTRGPU:
         return self.ops.loftr_match(coarse, fine, pa, pb, pe, self.weights, int(H), int(W))
 
     def match_frames(self, frames, pairs):
-        """frames uint8 [F, H, W, C] (device), pairs [(a, b)] -> list of numpy (kpts0, kpts1, conf)."""
+        """frames uint8 [F, H, W, C] (device), pairs [(a, b)] -> list of numpy (kpts0, kpts1, conf)
+        in the pixel frame of the (H // 8 * 8, W // 8 * 8) resized gray image the model ran on."""
         pairs = list(pairs)
         if not pairs:
             return []
-        H, W = int(frames.shape[1]), int(frames.shape[2])
+        H, W = int(frames.shape[1]) // 8 * 8, int(frames.shape[2]) // 8 * 8
         used = sorted({i for p in pairs for i in p})
         pos = {f: j for j, f in enumerate(used)}
         sel = frames[torch.as_tensor(used, device=frames.device)] if len(used) < frames.shape[0] else frames

@@ -172,10 +172,10 @@ class SuperGlue(BaseFeatureMatcher):
 
 class LoFTR(BaseFeatureMatcher):
     """Detector-free LoFTR on the GPU (geometric_verification.py:424-526): the reference's
-    native branch -- kornia.feature.LoFTR(pretrained='indoor') on cv2 BGR2GRAY / 255 frames
-    (mlgate.loftr, csrc/loftr.hip).  Frames must have H and W multiples of 8 (the
-    reference resizes other sizes down to multiples of 8 with cv2.resize; that resize is
-    not built: such frames raise)."""
+    native branch -- kornia.feature.LoFTR(pretrained='indoor') on cv2 BGR2GRAY frames
+    resized down to multiples of 8 (cv2 INTER_LINEAR), /255, keypoints scaled back
+    (mlgate.loftr, csrc/loftr.hip).  Both frames must share a shape (mixed shapes are not
+    built)."""
 
     def __init__(self, device: str = 'cuda', weights: str = 'indoor'):
         super().__init__(device)
@@ -193,30 +193,26 @@ class LoFTR(BaseFeatureMatcher):
         self._is_native = True
 
     @staticmethod
-    def _check(shape):
+    def _scale(shape):
         h, w = shape[:2]
-        if h % 8 or w % 8:
-            raise ValueError(f"LoFTR: frame {w}x{h} is not a multiple of 8 (the reference's cv2.resize to "
-                             f"{w // 8 * 8}x{h // 8 * 8} is not built)")
+        return np.array([w / (w // 8 * 8), h / (h // 8 * 8)])  # float64, as :521-522
 
     def detect_and_match(self, image1: np.ndarray, image2: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         self._load_model()
         im1, im2 = np.asarray(image1, np.uint8), np.asarray(image2, np.uint8)
-        self._check(im1.shape)
-        self._check(im2.shape)
+        if im1.shape != im2.shape:
+            raise ValueError("LoFTR: the two frames must share a shape (mixed shapes are not built)")
         dev = torch.device(self.device)
         as4 = lambda im: torch.from_numpy(np.ascontiguousarray(im if im.ndim == 3 else im[..., None]))  # noqa: E731
-        if im1.shape == im2.shape:
-            k0, k1, c = self._matcher.match_frames(torch.stack([as4(im1), as4(im2)]).to(dev), [(0, 1)])[0]
-            return k0.astype(np.float32), k1.astype(np.float32), c.astype(np.float32)
-        raise ValueError("LoFTR: the two frames must share a shape (the reference resizes each to its own "
-                         "multiple of 8; mixed shapes are not built)")
+        k0, k1, c = self._matcher.match_frames(torch.stack([as4(im1), as4(im2)]).to(dev), [(0, 1)])[0]
+        sc = self._scale(im1.shape)
+        return k0 * sc, k1 * sc, c
 
     def detect_and_match_batch(self, frames, pairs):
         """frames: device uint8 [F, H, W, C]; pairs [(a, b)] -> [(kpts_a, kpts_b, conf)]."""
         self._load_model()
-        self._check(tuple(frames.shape[1:3]))
-        return self._matcher.match_frames(frames, pairs)
+        sc = self._scale(tuple(frames.shape[1:3]))
+        return [(a * sc, b * sc, c) for a, b, c in self._matcher.match_frames(frames, pairs)]
 
 
 _MATCHERS = {'lightglue': LightGlue, 'superglue': SuperGlue, 'loftr': LoFTR}

@@ -161,7 +161,7 @@ def fine_matching(f0, f1):
     M, WW, C = f0.shape
     W = int(math.sqrt(WW))
     sim = torch.einsum("mc,mrc->mr", f0[:, WW // 2, :], f1)
-    heat = torch.softmax(sim / C ** 0.5, dim=1).view(-1, W, W)
+    heat = torch.softmax((1.0 / C ** 0.5) * sim, dim=1).view(-1, W, W)
     g = torch.linspace(-1.0, 1.0, W)
     gx = g[None, None, :].expand(1, W, W)
     gy = g[None, :, None].expand(1, W, W)
@@ -213,11 +213,19 @@ class Oracle:
         return out
 
     def detect_and_match(self, img0, img1):
-        """geometric_verification.py:484-526 with the restated model (H, W multiples of 8)."""
+        """geometric_verification.py:484-526 with the restated model: gray, cv2.resize
+        INTER_LINEAR down to multiples of 8 (oracle/csrc/oracle.c restatement; a same-size
+        resize is cv2's copy), match, keypoints scaled back (float64, as :521-526)."""
+        from . import _lib
         g0, g1 = to_gray(img0), to_gray(img1)
-        if g0.shape[0] % 8 or g0.shape[1] % 8 or g0.shape != g1.shape:
-            raise ValueError("oracle: frames must share a shape that is a multiple of 8")
+        if g0.shape != g1.shape:
+            raise ValueError("oracle: frames must share a shape")
+        h, w = g0.shape
+        nh, nw = h // 8 * 8, w // 8 * 8
+        if (nh, nw) != (h, w):
+            g0, g1 = (_lib.resize_linear_u8(g[..., None], nh, nw)[..., 0] for g in (g0, g1))
         c0, f0 = self.features(g0)
         c1, f1 = self.features(g1)
-        r = self.match_features(c0, f0, c1, f1, g0.shape[0])
-        return r["kpts0"].numpy(), r["kpts1"].numpy(), r["conf"].numpy()
+        r = self.match_features(c0, f0, c1, f1, nh)
+        sc = np.array([w / nw, h / nh])
+        return r["kpts0"].numpy() * sc, r["kpts1"].numpy() * sc, r["conf"].numpy()

@@ -103,3 +103,23 @@ def test_end_to_end_and_dropin(dev, setup):
     m._matcher = lf
     k0, k1, c = m.detect_and_match(frames[a], frames[b])
     assert np.array_equal(k0, got[0]) and np.array_equal(k1, got[1]) and np.array_equal(c, got[2])
+
+
+def test_isec_frame_size_resize_path(dev, setup):
+    """720 x 540 (ISEC cam, not a multiple of 8 in height): the device gray + cv2
+    INTER_LINEAR resize to 720 x 536 (oracle: the C restatement of cv2.resize), matches
+    and keypoints scaled back as the reference does (float64)."""
+    from mlgate.verify import LoFTR
+    sd, lf, orc, _, pairs, _ = setup
+    seq = synthetic.make_sequence(40, 8, 1)
+    a, b = pairs[0]
+    fr = synthetic.frames_host(seq, np.array([a, b]), 540, 720)
+    m = LoFTR(device=str(dev))
+    m._load_model()
+    k0, k1, c = m.detect_and_match(fr[0], fr[1])
+    r0, r1, rc = orc.detect_and_match(fr[0], fr[1])
+    assert k0.dtype == np.float64 and len(r0) > 50
+    rk = {tuple(np.rint(k * 8).astype(int)): i for i, k in enumerate(r0)}
+    hit = [(i, rk[tuple(np.rint(k * 8).astype(int))]) for i, k in enumerate(k0) if tuple(np.rint(k * 8).astype(int)) in rk]
+    assert len(hit) >= 0.9 * len(r0), (len(hit), len(r0), len(k0))
+    assert sum(np.abs(k1[i] - r1[j]).max() < 0.5 for i, j in hit) >= 0.9 * len(hit)
