@@ -296,6 +296,34 @@ int mlg_lightglue(const mlg_lg_weights* w, const float* keypoints, const float* 
                   size_t workspace_bytes, int32_t* matches, float* scores, int32_t* num_matches, int32_t* stop_layer,
                   void* stream);
 
+/* --------------------------------------------------------- SuperGlue --
+ * The SuperGlue matcher of the reference's SuperGlue class configuration
+ * (geometric_verification.py:385-399: weights 'indoor', sinkhorn_iterations 20,
+ * match_threshold 0.2), whose native branch the reference never reaches (:419-421):
+ * keypoint encoder, 18-layer attentional GNN, final_proj, log-space optimal transport
+ * with the learned dustbin score, mutual-nearest matches above the threshold.
+ * Features as mlg_lightglue plus keypoint scores f32 [F, kmax]; W, H the frame size
+ * (keypoint normalisation).  layer[l] reuses the LightGlue block table: Wqkv = the three
+ * attention projections (rows permuted so each head's 64 channels are contiguous:
+ * SuperGlue's view(b, 64, 4, n) interleaves them), Wout = merge (input columns permuted
+ * the same way), Wf1 / bf1 = mlp.0 with mlp.1 BatchNorm folded, ln_g / ln_b unused,
+ * Wf2 / bf2 = mlp.3.  kenc_w[0..2] f32 [out][in] (BN folded), kenc_w4 / kenc_w5 and
+ * Wfinal bf16 [out][in] (not k-step-major).  Outputs as mlg_lightglue (matches
+ * ascending in the image0 index).  Synchronises `stream`. */
+typedef struct mlg_sg_weights {
+    const float* kenc_w[3]; const float* kenc_b[3];
+    const uint16_t* kenc_w4; const float* kenc_b4;
+    const uint16_t* kenc_w5; const float* kenc_b5;
+    mlg_lg_block layer[18];
+    const uint16_t* Wfinal; const float* bfinal;
+    float bin_score;
+} mlg_sg_weights;
+size_t mlg_superglue_workspace_bytes(int P, int kmax);
+int mlg_superglue(const mlg_sg_weights* w, const float* keypoints, const float* scores, const float* descriptors,
+                  const int32_t* counts, int F, int kmax, int W, int H, const int32_t* pair_a, const int32_t* pair_b,
+                  int P, int sinkhorn_iterations, float match_threshold, void* workspace, size_t workspace_bytes,
+                  int32_t* matches, float* match_scores, int32_t* num_matches, void* stream);
+
 /* ------------------------------------------------------------ RANSAC --
  * Batched replacement for BaseFeatureMatcher.verify_geometric_consistency and
  * estimate_relative_pose (scripts/semantic_gating/geometric_verification.py:104-188),

@@ -347,6 +347,25 @@ int mlg_lightglue(const mlg_lg_weights* w, const float* keypoints, const float* 
                              matches, scores, num_matches, stop_layer, (hipStream_t)stream);
 }
 
+static_assert(sizeof(mlg_sg_weights) == sizeof(mlg_sg_weights_i), "SuperGlue weight tables must match");
+
+size_t mlg_superglue_workspace_bytes(int P, int kmax) { return mlg_superglue_ws_bytes(P, kmax); }
+
+int mlg_superglue(const mlg_sg_weights* w, const float* keypoints, const float* scores, const float* descriptors,
+                  const int32_t* counts, int F, int kmax, int W, int H, const int32_t* pair_a, const int32_t* pair_b,
+                  int P, int sinkhorn_iterations, float match_threshold, void* workspace, size_t workspace_bytes,
+                  int32_t* matches, float* match_scores, int32_t* num_matches, void* stream) {
+    if (!w || !keypoints || !scores || !descriptors || !counts || !pair_a || !pair_b || !workspace || !matches ||
+        !match_scores || !num_matches || F <= 0 || P <= 0 || W <= 0 || H <= 0)
+        return MLG_EINVAL;
+    for (int p = 0; p < P; ++p)
+        if (pair_a[p] < 0 || pair_a[p] >= F || pair_b[p] < 0 || pair_b[p] >= F) return MLG_EINVAL;
+    const mlg_sg_weights_i& wi = *reinterpret_cast<const mlg_sg_weights_i*>(w);
+    return mlg_superglue_run(wi, keypoints, scores, descriptors, counts, kmax, W, H, pair_a, pair_b, P,
+                             sinkhorn_iterations, match_threshold, workspace, workspace_bytes, matches, match_scores,
+                             num_matches, (hipStream_t)stream);
+}
+
 size_t mlg_ransac_workspace_bytes(int P, long S_total, int hypotheses) {
     return mlg_ransac_ws_bytes(P, S_total, hypotheses);
 }

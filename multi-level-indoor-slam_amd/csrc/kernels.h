@@ -147,12 +147,27 @@ struct mlg_lg_conf_i {
     float thr, width;
     float* lz; uint8_t* flags;
 };
+// relu != 0: ReLU without LayerNorm (SuperGlue's MLP with BatchNorm folded into Wf1)
 int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s,
-               const mlg_lg_conf_i* conf = nullptr);
+               const mlg_lg_conf_i* conf = nullptr, int relu = 0);
 // lg_proj.hip -- LightGlue q/k/v projections (+ rotary for the self block) straight into
 // the attention operands; W packed k-step-major [16][768 | 512][16]; Npad % 64 == 0.
 int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,
                 const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s);
+// superglue.hip -- SuperGlue GNN + log-space optimal transport over a ragged batch of pairs
+struct mlg_sg_weights_i {
+    const float* kenc_w[3]; const float* kenc_b[3];
+    const bf16_t* kenc_w4; const float* kenc_b4;
+    const bf16_t* kenc_w5; const float* kenc_b5;
+    mlg_lg_block_i layer[18];
+    const bf16_t* Wfinal; const float* bfinal;
+    float bin_score;
+};
+size_t mlg_superglue_ws_bytes(int P, int kmax);
+int mlg_superglue_run(const mlg_sg_weights_i& w, const float* kpts, const float* kscores, const float* desc,
+                      const int32_t* counts, int kmax, int W, int H, const int32_t* pa, const int32_t* pb, int P,
+                      int iters, float thr, void* ws, size_t ws_bytes, int32_t* matches, float* mscores,
+                      int32_t* nmatch, hipStream_t s);
 size_t mlg_lightglue_ws_bytes(int P, int kmax);
 int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float* desc, const int32_t* counts, int kmax,
                       const int32_t* pa, const int32_t* pb, int P, float depth_conf, float width_conf,

@@ -126,9 +126,11 @@ __device__ __forceinline__ void zero(f32x16 (&acc)[NT][MT]) {
             for (int i = 0; i < 16; ++i) acc[t][mt][i] = 0.f;
 }
 
+// relu != 0: SuperGlue's MLP (BatchNorm folded into Wf1 / bf1 on the host, ReLU, no
+// LayerNorm) instead of LightGlue's LayerNorm + GELU (superglue.hip)
 __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ctx, float* __restrict__ X,
                                                   bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w,
-                                                  mlg_lg_conf_i cf) {
+                                                  mlg_lg_conf_i cf, int relu) {
     __shared__ __attribute__((aligned(16))) char lds[LDS_CAT];
     __shared__ float red[2][NW][R];
     // biases and LayerNorm affine, staged in LDS: epilogue reads never wait on VMEM
@@ -143,8 +145,8 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
     const int m0 = blockIdx.x * R;
     for (int i = tid; i < 512; i += 256) {
         s_bf1[i] = w.bf1[i];
-        s_lng[i] = w.ln_g[i];
-        s_lnb[i] = w.ln_b[i];
+        s_lng[i] = relu ? 1.f : w.ln_g[i];
+        s_lnb[i] = relu ? 0.f : w.ln_b[i];
         if (i < 256) {
             s_bout[i] = w.bout[i];
             s_bf2[i] = w.bf2[i];
@@ -213,9 +215,9 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
                     acc[t][mt][4 * g + 3] += b.w;
                 }
             }
-        float mean[MT], rstd[MT];
+        float mean[MT] = {0.f, 0.f}, rstd[MT] = {1.f, 1.f};
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
+        for (int mt = 0; mt < MT && !relu; ++mt) {
             float sum = 0.f;
 #pragma unroll
             for (int t = 0; t < 4; ++t)
@@ -226,7 +228,7 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
         }
         __syncthreads();  // also: every wave has finished reading [x | msg]
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
+        for (int mt = 0; mt < MT && !relu; ++mt) {
             float sum = 0.f;
 #pragma unroll
             for (int v = 0; v < NW; ++v) sum += red[0][v][32 * mt + col];
@@ -244,7 +246,7 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
         }
         __syncthreads();
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
+        for (int mt = 0; mt < MT && !relu; ++mt) {
             float q = 0.f;
 #pragma unroll
             for (int v = 0; v < NW; ++v) q += red[1][v][32 * mt + col];
@@ -260,10 +262,18 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
 #pragma unroll
                 for (int mt = 0; mt < MT; ++mt) {
                     const f32x16& a = acc[t][mt];
-                    const float y0 = gelu_erf_fast((a[4 * g] - mean[mt]) * rstd[mt] * lg.x + lb.x);
-                    const float y1 = gelu_erf_fast((a[4 * g + 1] - mean[mt]) * rstd[mt] * lg.y + lb.y);
-                    const float y2 = gelu_erf_fast((a[4 * g + 2] - mean[mt]) * rstd[mt] * lg.z + lb.z);
-                    const float y3 = gelu_erf_fast((a[4 * g + 3] - mean[mt]) * rstd[mt] * lg.w + lb.w);
+                    float y0, y1, y2, y3;
+                    if (relu) {
+                        y0 = fmaxf(a[4 * g], 0.f);
+                        y1 = fmaxf(a[4 * g + 1], 0.f);
+                        y2 = fmaxf(a[4 * g + 2], 0.f);
+                        y3 = fmaxf(a[4 * g + 3], 0.f);
+                    } else {
+                        y0 = gelu_erf_fast((a[4 * g] - mean[mt]) * rstd[mt] * lg.x + lb.x);
+                        y1 = gelu_erf_fast((a[4 * g + 1] - mean[mt]) * rstd[mt] * lg.y + lb.y);
+                        y2 = gelu_erf_fast((a[4 * g + 2] - mean[mt]) * rstd[mt] * lg.z + lb.z);
+                        y3 = gelu_erf_fast((a[4 * g + 3] - mean[mt]) * rstd[mt] * lg.w + lb.w);
+                    }
                     *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, n / 8) + 8 * hh) =
                         make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
                 }
@@ -373,12 +383,13 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
 }  // namespace
 
 int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s,
-               const mlg_lg_conf_i* conf) {
+               const mlg_lg_conf_i* conf, int relu) {
     if (M <= 0) return MLG_OK;
     if (ldc < 256 || (ldc % 8)) return MLG_EINVAL;
     mlg_lg_conf_i cf{};
     if (conf) cf = *conf;
-    hipLaunchKernelGGL(k_lg_ffn, dim3((unsigned)((M + R - 1) / R)), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf);
+    hipLaunchKernelGGL(k_lg_ffn, dim3((unsigned)((M + R - 1) / R)), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf,
+                       relu);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

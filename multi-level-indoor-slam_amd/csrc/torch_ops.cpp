@@ -316,6 +316,62 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> loftr_match(const Tensor& coarse, con
     return {counts, k0, k1, cf};
 }
 
+// --------------------------------------------------------------- SuperGlue
+// weights: kenc_w[0..2], kenc_b[0..2], kenc_w4, kenc_b4, kenc_w5, kenc_b5, 18 layers x
+// (Wqkv, bqkv, Wout, bout, Wf1, bf1, Wf2, bf2), Wfinal, bfinal; bin_score as a double
+constexpr int kSgTensors = 6 + 4 + 18 * 8 + 2;
+
+std::tuple<Tensor, Tensor, Tensor> superglue(const Tensor& kpts, const Tensor& scores, const Tensor& desc,
+                                             const Tensor& counts, const Tensor& pair_a, const Tensor& pair_b,
+                                             at::TensorList w, double bin_score, int64_t W, int64_t H, int64_t iters,
+                                             double thr) {
+    want(kpts, at::kFloat, "kpts");
+    want(scores, at::kFloat, "scores");
+    want(desc, at::kFloat, "desc");
+    want(counts, at::kInt, "counts", false);
+    want(pair_a, at::kInt, "pair_a", false);
+    want(pair_b, at::kInt, "pair_b", false);
+    TORCH_CHECK((int)w.size() == kSgTensors, "superglue weights: expected ", kSgTensors, " tensors");
+    const int64_t F = kpts.size(0), kmax = kpts.size(1), P = pair_a.numel();
+    TORCH_CHECK(kpts.dim() == 3 && kpts.size(2) == 2 && desc.dim() == 3 && desc.size(0) == F &&
+                    desc.size(1) == kmax && desc.size(2) == 256 && scores.numel() == F * kmax,
+                "kpts [F, kmax, 2] / scores [F, kmax] / desc [F, kmax, 256]");
+    TORCH_CHECK(counts.numel() == F && pair_b.numel() == P && P > 0, "counts [F], pair_a / pair_b [P]");
+    const int32_t* cn = cp<int32_t>(counts);
+    for (int64_t f = 0; f < F; ++f) TORCH_CHECK(cn[f] >= 0 && cn[f] <= kmax, "counts out of range");
+    mlg_sg_weights s;
+    std::memset(&s, 0, sizeof(s));
+    int i = 0;
+    for (int l = 0; l < 3; ++l) s.kenc_w[l] = cp<float>(w[i++]);
+    for (int l = 0; l < 3; ++l) s.kenc_b[l] = cp<float>(w[i++]);
+    s.kenc_w4 = cp<uint16_t>(w[i++]);
+    s.kenc_b4 = cp<float>(w[i++]);
+    s.kenc_w5 = cp<uint16_t>(w[i++]);
+    s.kenc_b5 = cp<float>(w[i++]);
+    for (int l = 0; l < 18; ++l) {
+        mlg_lg_block& b = s.layer[l];
+        b.Wqkv = cp<uint16_t>(w[i++]); b.bqkv = cp<float>(w[i++]);
+        b.Wout = cp<uint16_t>(w[i++]); b.bout = cp<float>(w[i++]);
+        b.Wf1 = cp<uint16_t>(w[i++]); b.bf1 = cp<float>(w[i++]);
+        b.Wf2 = cp<uint16_t>(w[i++]); b.bf2 = cp<float>(w[i++]);
+    }
+    s.Wfinal = cp<uint16_t>(w[i++]);
+    s.bfinal = cp<float>(w[i++]);
+    s.bin_score = (float)bin_score;
+    const size_t nbytes = mlg_superglue_workspace_bytes((int)P, (int)kmax);
+    c10::DeviceGuard g(kpts.device());
+    auto o = kpts.options();
+    Tensor m = at::empty({P, kmax, 2}, o.dtype(at::kInt)), sc = at::empty({P, kmax}, o.dtype(at::kFloat));
+    Tensor n = at::empty({P}, o.dtype(at::kInt));
+    Tensor ws = workspace(nbytes, kpts);
+    check_rc(mlg_superglue(&s, cp<float>(kpts), cp<float>(scores), cp<float>(desc), cn, (int)F, (int)kmax, (int)W,
+                           (int)H, cp<int32_t>(pair_a), cp<int32_t>(pair_b), (int)P, (int)iters, (float)thr,
+                           ws.data_ptr(), (size_t)ws.numel(), mp<int32_t>(m), mp<float>(sc), mp<int32_t>(n),
+                           stream_of(kpts)),
+             "mlg_superglue");
+    return {m, sc, n};
+}
+
 // --------------------------------------------------------------- LightGlue
 constexpr int kLgTensors = 1 + 9 * 10 * 2 + 9 * 4 + 8 * 2 + 1;
 
@@ -547,6 +603,8 @@ TORCH_LIBRARY(mlgate, m) {
     m.def("recover_pose(Tensor k1, Tensor k2, Tensor offsets, Tensor K, int k_stride, Tensor E, Tensor mask) -> Tensor");
     m.def("resnet50(Tensor frames, Tensor[] weights, int descriptor_dim) -> Tensor");
     m.def("loftr_features(Tensor frames, Tensor[] weights) -> (Tensor, Tensor)");
+    m.def("superglue(Tensor kpts, Tensor scores, Tensor desc, Tensor counts, Tensor pair_a, Tensor pair_b, "
+          "Tensor[] weights, float bin_score, int W, int H, int iters, float threshold) -> (Tensor, Tensor, Tensor)");
     m.def("loftr_match(Tensor coarse, Tensor fine, Tensor pair_a, Tensor pair_b, Tensor pe, Tensor[] weights, int H, "
           "int W) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("pillow_resize_224(Tensor frames) -> Tensor");
@@ -572,6 +630,7 @@ TORCH_LIBRARY_IMPL(mlgate, CUDA, m) {
     m.impl("recover_pose", &recover_pose);
     m.impl("resnet50", &resnet50);
     m.impl("loftr_features", &loftr_features);
+    m.impl("superglue", &superglue);
     m.impl("loftr_match", &loftr_match);
     m.impl("pillow_resize_224", &pillow_resize_224);
     m.impl("plane_ransac", &plane_ransac);

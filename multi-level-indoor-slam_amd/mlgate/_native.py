@@ -26,7 +26,7 @@ if _DIR_OVERRIDE:
     LIB_PATH = os.path.join(_DIR_OVERRIDE, "libmlgate.so")
     TORCH_LIB_PATH = os.path.join(_DIR_OVERRIDE, "libmlgate_torch.so")
 OPS = ("vit_forward_into", "knn_gate", "knn_query", "row_normalize", "similarity", "xcorr_score", "superpoint",
-       "lightglue", "ransac_epipolar", "recover_pose", "resnet50", "loftr_features", "loftr_match", "pillow_resize_224", "plane_ransac", "proximity",
+       "lightglue", "ransac_epipolar", "recover_pose", "resnet50", "loftr_features", "loftr_match", "superglue", "pillow_resize_224", "plane_ransac", "proximity",
        "prof_enable", "prof_reset", "prof_read")
 
 

@@ -5,8 +5,10 @@ the semantic cross-floor skip and its statistics (:688-744), SuperPoint + LightG
 matching (:196-312; mlgate.superpoint / mlgate.lightglue), detector-free LoFTR
 (:424-526; mlgate.loftr) and the RANSAC stage -- essential / fundamental matrix +
 recoverPose (:104-188; mlgate.geometry) -- all run on the GPU.  SuperGlue resolves to
-the LightGlue path exactly as the reference does (its native branch defers to it).
+the LightGlue path exactly as the reference does (its native branch defers to it), or,
+opted in, to the GPU SuperGlue + Sinkhorn matcher the class configures (mlgate.superglue).
 """
+import os
 import warnings
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
@@ -143,31 +145,73 @@ class LightGlue(BaseFeatureMatcher):
 
 
 class SuperGlue(BaseFeatureMatcher):
-    """geometric_verification.py:353-421: SuperGlue's native branch defers to its
-    LightGlue fallback in the reference (and the SuperGlue package is absent), so this
-    matcher IS the GPU LightGlue path, with the reference's warning."""
+    """geometric_verification.py:353-421.  The reference's native branch never runs
+    SuperGlue (:419-421 return the LightGlue fallback, and the magicleap package is
+    absent), so by default this matcher IS the GPU LightGlue path, with the reference's
+    warning.  ``MLGATE_SUPERGLUE_NATIVE=1`` (or ``.native = True``) selects the model the
+    class configures instead: magicleap SuperPoint settings (nms_radius 4,
+    keypoint_threshold 0.005, max_keypoints) + SuperGlue (sinkhorn_iterations 20,
+    match_threshold 0.2) on the GPU (mlgate.superglue, csrc/superglue.hip); weights from
+    MLGATE_SUPERGLUE_WEIGHTS, else seeded synthetic ones."""
 
     def __init__(self, device: str = 'cuda', max_keypoints: int = 2048, weights: str = 'indoor'):
         super().__init__(device)
         self.max_keypoints = max_keypoints
         self.weights = weights
+        self.native = None  # None: MLGATE_SUPERGLUE_NATIVE decides; True / False force it
         self._model_loaded = False
 
     def _load_model(self):
         if self._model_loaded:
             return
-        warnings.warn("SuperGlue not installed. Using LightGlue fallback.")
-        self._fallback = LightGlue(device=self.device, max_keypoints=self.max_keypoints)
+        native = self.native if self.native is not None else os.environ.get("MLGATE_SUPERGLUE_NATIVE") == "1"
+        if native:
+            from .superglue import SuperGlueGPU
+            from .superpoint import SuperPointGPU
+            self.extractor = SuperPointGPU(device=self.device, max_num_keypoints=self.max_keypoints,
+                                           detection_threshold=0.005, nms_radius=4)
+            self.matcher = SuperGlueGPU(device=self.device)
+            synth = [n for n, m in (("SuperPoint", self.extractor), ("SuperGlue", self.matcher))
+                     if m.weights_source.startswith("synthetic")]
+            if synth:
+                warnings.warn(f"{' and '.join(synth)} weights not configured (MLGATE_SUPERPOINT_WEIGHTS / "
+                              "MLGATE_SUPERGLUE_WEIGHTS); using seeded synthetic weights")
+            self._is_native = True
+        else:
+            warnings.warn("SuperGlue not installed. Using LightGlue fallback.")
+            self._fallback = LightGlue(device=self.device, max_keypoints=self.max_keypoints)
+            self._is_native = False
         self._model_loaded = True
-        self._is_native = False
 
     def detect_and_match(self, image1, image2):
         self._load_model()
-        return self._fallback.detect_and_match(image1, image2)
+        if not self._is_native:
+            return self._fallback.detect_and_match(image1, image2)
+        if np.shape(image1) != np.shape(image2):
+            raise ValueError("SuperGlue: the two frames must share a shape (one normalisation size per batch)")
+        h, w = np.shape(image1)[:2]
+        f1, f2 = self.extractor.extract([image1, image2])
+        m, sc = self.matcher.match(f1, f2, w, h)
+        return (f1["keypoints"][m[:, 0]].astype(np.float32), f2["keypoints"][m[:, 1]].astype(np.float32),
+                sc.astype(np.float32))
 
     def detect_and_match_batch(self, frames, pairs):
+        """frames: device uint8 [F, H, W, C]; pairs: [(a, b), ...] -> list of
+        (kpts_a [S, 2], kpts_b [S, 2], scores [S]) numpy arrays per pair."""
         self._load_model()
-        return self._fallback.detect_and_match_batch(frames, pairs)
+        if not self._is_native:
+            return self._fallback.detect_and_match_batch(frames, pairs)
+        pairs = list(pairs)
+        if not pairs:
+            return []
+        used = sorted({i for p in pairs for i in p})
+        pos = {f: j for j, f in enumerate(used)}
+        sel = frames[torch.as_tensor(used, device=frames.device)] if len(used) < frames.shape[0] else frames
+        kp, sc, ds, _, cnt = self.extractor.extract_device(sel)
+        m, s, n = self.matcher.match_device(kp, sc, ds, cnt.cpu().numpy(), [pos[a] for a, _ in pairs],
+                                            [pos[b] for _, b in pairs], int(frames.shape[2]), int(frames.shape[1]))
+        kp, m, s, n = kp.cpu().numpy(), m.cpu().numpy(), s.cpu().numpy(), n.cpu().numpy()
+        return [(kp[pos[a]][m[p, :n[p], 0]], kp[pos[b]][m[p, :n[p], 1]], s[p, :n[p]]) for p, (a, b) in enumerate(pairs)]
 
 
 class LoFTR(BaseFeatureMatcher):

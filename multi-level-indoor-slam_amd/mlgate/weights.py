@@ -475,3 +475,88 @@ def resolve_loftr_state_dict(path=None, seed=0):
     if path:
         return load_loftr_state_dict(path), path
     return loftr_state_dict(seed), f"synthetic(seed={seed})"
+
+
+# ----------------------------------------------------------------- SuperGlue (magicleap)
+SG_DIM, SG_LAYERS = 256, 18
+SG_KENC = (3, 32, 64, 128, 256, 256)  # KeypointEncoder MLP channels (layers [32, 64, 128, 256])
+
+
+def superglue_keys():
+    """magicleap superglue_{indoor,outdoor}.pth key names (eval: BatchNorm running stats)."""
+    bn = ("weight", "bias", "running_mean", "running_var")
+    keys = ["bin_score"]
+    for i in range(len(SG_KENC) - 1):
+        keys += [f"kenc.encoder.{3 * i}.weight", f"kenc.encoder.{3 * i}.bias"]
+        if i < len(SG_KENC) - 2:
+            keys += [f"kenc.encoder.{3 * i + 1}.{s}" for s in bn]
+    for i in range(SG_LAYERS):
+        p = f"gnn.layers.{i}."
+        for n in ("attn.proj.0", "attn.proj.1", "attn.proj.2", "attn.merge", "mlp.0", "mlp.3"):
+            keys += [p + n + ".weight", p + n + ".bias"]
+        keys += [p + "mlp.1." + s for s in bn]
+    return keys + ["final_proj.weight", "final_proj.bias"]
+
+
+@functools.lru_cache(maxsize=2)
+def superglue_state_dict(seed=0, res_gain=0.05, kenc_gain=0.05, final_scale=12.0, bin_score=1.0):
+    """Seeded float32 SuperGlue weights with magicleap's key names and Conv1d shapes.
+
+    Untrained but matcher-like on SuperPoint descriptors: small residual GNN updates
+    (``res_gain``) and a small keypoint encoding (``kenc_gain``) keep the states near the
+    unit descriptors, final_proj ~ ``final_scale`` * I turns the Sinkhorn input into a
+    sharpened descriptor similarity (scores / 16 ~ 9 cos), and eval BatchNorms with
+    non-trivial running statistics exercise the folding.
+    """
+    rng = np.random.default_rng(seed + 7000)
+    f = np.float32
+
+    def conv(o, i, gain=1.0):
+        return (rng.standard_normal((o, i, 1), dtype=f) * f(gain / np.sqrt(i)),
+                rng.standard_normal((o,), dtype=f) * f(0.02 * gain))
+
+    def bn(p, c):
+        return {p + "weight": f(1.0) + rng.standard_normal(c, dtype=f) * f(0.1),
+                p + "bias": rng.standard_normal(c, dtype=f) * f(0.05),
+                p + "running_mean": rng.standard_normal(c, dtype=f) * f(0.05),
+                p + "running_var": rng.uniform(0.5, 1.5, c).astype(f)}
+
+    sd = {"bin_score": np.array(bin_score, f)}
+    n = len(SG_KENC) - 1
+    for i in range(n):
+        last = i == n - 1
+        w, b = conv(SG_KENC[i + 1], SG_KENC[i], kenc_gain if last else 1.0)
+        sd[f"kenc.encoder.{3 * i}.weight"], sd[f"kenc.encoder.{3 * i}.bias"] = w, b
+        if not last:
+            sd.update(bn(f"kenc.encoder.{3 * i + 1}.", SG_KENC[i + 1]))
+    d = SG_DIM
+    for i in range(SG_LAYERS):
+        p = f"gnn.layers.{i}."
+        for k in range(3):
+            sd[p + f"attn.proj.{k}.weight"], sd[p + f"attn.proj.{k}.bias"] = conv(d, d)
+        sd[p + "attn.merge.weight"], sd[p + "attn.merge.bias"] = conv(d, d)
+        sd[p + "mlp.0.weight"], sd[p + "mlp.0.bias"] = conv(2 * d, 2 * d)
+        sd.update(bn(p + "mlp.1.", 2 * d))
+        w, _ = conv(d, 2 * d, res_gain)
+        sd[p + "mlp.3.weight"], sd[p + "mlp.3.bias"] = w, np.zeros(d, f)  # constant_(bias, 0.0) as upstream
+    w, b = conv(d, d, 0.05)
+    sd["final_proj.weight"] = w + (np.eye(d, dtype=f) * f(final_scale))[:, :, None]
+    sd["final_proj.bias"] = b
+    return sd
+
+
+def load_superglue_state_dict(path):
+    """magicleap superglue_*.pth from a local file (weights only)."""
+    import torch
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    missing = [k for k in superglue_keys() if k not in sd]
+    if missing:
+        raise KeyError(f"checkpoint {path} lacks SuperGlue keys, e.g. {missing[:3]}")
+    return {k: sd[k].float().cpu().numpy() for k in superglue_keys()}
+
+
+def resolve_superglue_state_dict(path=None, seed=0):
+    path = path or os.environ.get("MLGATE_SUPERGLUE_WEIGHTS")
+    if path:
+        return load_superglue_state_dict(path), path
+    return superglue_state_dict(seed), f"synthetic(seed={seed})"
