@@ -72,28 +72,18 @@ struct EpiBiasBF16 {  // y = acc + b  -> bf16
     }
 };
 
-// nn.GELU() (exact, erf form).  erf via Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7,
-// far below the bf16 rounding of the output): one v_rcp, one v_exp, five FMAs instead
-// of the ~30-instruction libm erff that made the fc1 epilogue VALU-bound.
-__device__ __forceinline__ float erf_fast(float x) {
-    const float ax = fabsf(x);
-    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
-    float p = fmaf(1.061405429f, t, -1.453152027f);
-    p = fmaf(p, t, 1.421413741f);
-    p = fmaf(p, t, -0.284496736f);
-    p = fmaf(p, t, 0.254829592f);
-    const float y = 1.0f - p * t * __expf(-ax * ax);
-    return copysignf(y, x);
-}
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
-
-struct EpiBiasGeluBF16 {  // y = gelu(acc + b) -> bf16   (mlp.fc1 + nn.GELU())
+// y = gelu(acc + b) -> bf16   (mlp.fc1 + nn.GELU(); the erf form as common.h gelu_poly2,
+// no transcendental: the A & S 7.1.26 form's v_rcp + v_exp per element made this epilogue
+// the VALU bound of fc1)
+struct EpiBiasGeluBF16 {
     bf16_t* C; int ldc; const float* bias;
     __device__ void operator()(int m, int n, const f32x4& v) const {
         const float4 b = *reinterpret_cast<const float4*>(bias + n);
+        const f32x2 g01 = gelu_poly2(f32x2{v[0] + b.x, v[1] + b.y});
+        const f32x2 g23 = gelu_poly2(f32x2{v[2] + b.z, v[3] + b.w});
         uint2 o;
-        o.x = pack_bf16x2(gelu_erf(v[0] + b.x), gelu_erf(v[1] + b.y));
-        o.y = pack_bf16x2(gelu_erf(v[2] + b.z), gelu_erf(v[3] + b.w));
+        o.x = pack_bf16x2(g01.x, g01.y);
+        o.y = pack_bf16x2(g23.x, g23.y);
         *reinterpret_cast<uint2*>(C + (size_t)m * ldc + n) = o;
     }
 };

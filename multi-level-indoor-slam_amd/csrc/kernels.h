@@ -73,6 +73,8 @@ size_t mlg_gem_partial_bytes(int B);
 // knn.hip
 int mlg_row_normalize(const float* X, float* Xn, int N, int D, float* norms, hipStream_t s);
 int mlg_similarity_f32(const float* A, int Q, const float* B, int N, int D, float* S, int lds, hipStream_t s);
+int mlg_similarity_f32_t(const float* A, int Q, const float* B, int N, int D, float* S, int lds, float* St, int ldt,
+                         hipStream_t s);
 int mlg_topk_gate(const float* S, int lds, int N, int Q, const double* tq, const double* tdb, const int64_t* fq,
                   const uint8_t* hfq, const int64_t* fdb, const uint8_t* hfdb, double min_gap, float thr, int k,
                   int gating, int32_t* idx, float* sim, uint8_t* valid, int32_t* count, unsigned long long* totals,

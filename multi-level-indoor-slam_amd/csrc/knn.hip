@@ -110,8 +110,10 @@ __global__ void k_row_normalize(const float* __restrict__ X, float* __restrict__
 // 128 x 128 tile, BK = 16, 256 threads = 2 x 2 waves of 64 x 64 (2 x 2 MFMA 32x32).
 constexpr int SBM = 128, SBN = 128, SBK = 16;
 
+// St (optional): the transpose, St[j][i] = S[i][j] (SuperGlue's column passes)
 __global__ __launch_bounds__(256, 2) void k_sim_f32(const float* __restrict__ A, int Q, const float* __restrict__ B,
-                                                    int N, int D, float* __restrict__ S, int lds) {
+                                                    int N, int D, float* __restrict__ S, int lds,
+                                                    float* __restrict__ St, int ldt) {
     __shared__ float As[SBK][SBM + 4];
     __shared__ float Bs[SBK][SBN + 4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -176,6 +178,21 @@ __global__ __launch_bounds__(256, 2) void k_sim_f32(const float* __restrict__ A,
             for (int r = 0; r < 16; ++r) {
                 const int i = m0 + wm * 64 + ta * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
                 if (i < Q) S[(size_t)i * lds + j] = acc[ta][tb][r];
+            }
+            if (St) {  // 4 consecutive rows i per lane and r-group: one 16-B store into row j of St
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int i0 = m0 + wm * 64 + ta * 32 + 8 * g + 4 * (lane >> 5);
+                    const f32x16& a = acc[ta][tb];
+                    float* t = St + (size_t)j * ldt + i0;
+                    if (i0 + 3 < Q) {
+                        *reinterpret_cast<float4*>(t) = make_float4(a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]);
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (i0 + e < Q) t[e] = a[4 * g + e];
+                    }
+                }
             }
         }
 }
@@ -576,10 +593,16 @@ int mlg_row_normalize(const float* X, float* Xn, int N, int D, float* norms, hip
 }
 
 int mlg_similarity_f32(const float* A, int Q, const float* B, int N, int D, float* S, int lds, hipStream_t s) {
+    return mlg_similarity_f32_t(A, Q, B, N, D, S, lds, nullptr, 0, s);
+}
+
+int mlg_similarity_f32_t(const float* A, int Q, const float* B, int N, int D, float* S, int lds, float* St, int ldt,
+                         hipStream_t s) {
     if (N <= 0 || D <= 0 || Q <= 0 || (D % 4) || lds < N) return MLG_EINVAL;
     if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return MLG_EINVAL;
+    if (St && (ldt < Q || (ldt % 4) || (reinterpret_cast<uintptr_t>(St) & 15))) return MLG_EINVAL;
     dim3 grid((N + SBN - 1) / SBN, (Q + SBM - 1) / SBM);
-    hipLaunchKernelGGL(k_sim_f32, grid, dim3(256), 0, s, A, Q, B, N, D, S, lds);
+    hipLaunchKernelGGL(k_sim_f32, grid, dim3(256), 0, s, A, Q, B, N, D, S, lds, St, ldt);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

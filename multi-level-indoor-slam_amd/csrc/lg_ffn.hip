@@ -22,13 +22,18 @@
 //             msg + bias, bf16, overwrites the ctx half in LDS
 //   2. ffn1 : wave w -> cols [128w, 128w+128) of 512 (K = 512 over [x | msg]);
 //             + bias, LayerNorm(512, eps 1e-5) statistics reduced lane -> half-wave ->
-//             4 waves through LDS (two passes: mean, then centred variance), GELU (erf),
+//             4 waves through LDS (two passes: mean, then centred variance), GELU (erf
+//             form, common.h gelu_poly2),
 //             bf16, overwrites [x | msg] in LDS
 //   3. ffn2 : wave w -> cols [64w, 64w+64) of 256   (K = 512);
 //             x += acc + bias (f32), bf16 copy of x written for the next projections.
 // The accumulator of the transposed product gives each lane 4 consecutive output
 // columns of one token: LayerNorm sums are lane-local up to one cross-half exchange,
 // and every epilogue store is a 4-wide vector.
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -45,20 +50,6 @@ constexpr int LDS_CAT = R * ROWB;
 __device__ __forceinline__ int cat_off(int row, int chunk) { return row * ROWB + ((chunk ^ (row & 15)) << 4); }
 
 __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
-
-// erf via Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, below the bf16 rounding of the
-// output); the same form as the ViT fc1 epilogue (gemm_bf16.hip).
-__device__ __forceinline__ float gelu_erf_fast(float x) {
-    const float z = x * 0.70710678118654752f;
-    const float az = fabsf(z);
-    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.0f));
-    float p = fmaf(1.061405429f, t, -1.453152027f);
-    p = fmaf(p, t, 1.421413741f);
-    p = fmaf(p, t, -0.284496736f);
-    p = fmaf(p, t, 0.254829592f);
-    const float e = copysignf(1.0f - p * t * __expf(-az * az), z);
-    return 0.5f * x * (1.0f + e);
-}
 
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 // log(sigmoid(x)) = min(x, 0) - log1p(exp(-|x|))  (torch's stable form)
@@ -128,6 +119,11 @@ __device__ __forceinline__ void zero(f32x16 (&acc)[NT][MT]) {
 
 // relu != 0: SuperGlue's MLP (BatchNorm folded into Wf1 / bf1 on the host, ReLU, no
 // LayerNorm) instead of LightGlue's LayerNorm + GELU (superglue.hip)
+//
+// Persistent form: gridDim.x workgroups (two per CU) walk the 64-row tiles with stride
+// gridDim.x: 10 % less time than one workgroup per tile (tools/ffn_ab.sh, same box).  A
+// half-tile start offset for half of the grid (so that co-resident workgroups would run
+// epilogue beside GEMM) measured no change and was dropped.
 __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ctx, float* __restrict__ X,
                                                   bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w,
                                                   mlg_lg_conf_i cf, int relu) {
@@ -142,7 +138,6 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
     float* s_lnb = prm + 1280;
     float* s_bf2 = prm + 1792;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
-    const int m0 = blockIdx.x * R;
     for (int i = tid; i < 512; i += 256) {
         s_bf1[i] = w.bf1[i];
         s_lng[i] = relu ? 1.f : w.ln_g[i];
@@ -152,232 +147,257 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
             s_bf2[i] = w.bf2[i];
         }
     }
-    // 0. tile -> LDS: the bf16 copy of x (written by the previous block) into chunks
-    //    0..31, ctx into chunks 32..63; 32 lanes x 16 B = one 512-B row per half-wave,
-    //    rows clamped to M - 1 (never stored)
-    {
-        uint4 rx[8], rc[8];
-        const int c = lane & 31;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int row = 8 * i + 2 * wave + hh;
-            const size_t gr = (size_t)min(m0 + row, M - 1);
-            rx[i] = *reinterpret_cast<const uint4*>(xcopy + gr * ldc + c * 8);
-            rc[i] = *reinterpret_cast<const uint4*>(ctx + gr * 256 + c * 8);
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int row = 8 * i + 2 * wave + hh;
-            *reinterpret_cast<uint4*>(lds + cat_off(row, c)) = rx[i];
-            *reinterpret_cast<uint4*>(lds + cat_off(row, 32 + c)) = rc[i];
-        }
-    }
-    __syncthreads();
-
-    // 1. msg = ctx . Wout^T + bout  -> bf16 over the ctx half
-    {
-        f32x16 acc[2][MT];
-        zero(acc);
-        gemm_phase<2>(w.Wout, 256, 64 * wave, 4, 32, lds, acc);
-        __syncthreads();  // every wave has read the ctx half
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int n = 64 * wave + 32 * t + 8 * g + 4 * hh;
-                const float4 b = *reinterpret_cast<const float4*>(s_bout + n);
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    const f32x16& a = acc[t][mt];
-                    *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, 32 + n / 8) + 8 * hh) =
-                        make_uint2(pack_bf16x2(a[4 * g] + b.x, a[4 * g + 1] + b.y),
-                                   pack_bf16x2(a[4 * g + 2] + b.z, a[4 * g + 3] + b.w));
-                }
+    const int ntiles = (M + R - 1) / R;
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int m0 = tile * R;
+        // 0. tile -> LDS: the bf16 copy of x (written by the previous block) into chunks
+        //    0..31, ctx into chunks 32..63; 32 lanes x 16 B = one 512-B row per half-wave,
+        //    rows clamped to M - 1 (never stored)
+        {
+            uint4 rx[8], rc[8];
+            const int c = lane & 31;
+    #pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = 8 * i + 2 * wave + hh;
+                const size_t gr = (size_t)min(m0 + row, M - 1);
+                rx[i] = *reinterpret_cast<const uint4*>(xcopy + gr * ldc + c * 8);
+                rc[i] = *reinterpret_cast<const uint4*>(ctx + gr * 256 + c * 8);
             }
-    }
-    __syncthreads();
-
-    // 2. h = [x | msg] . W1^T + b1; LayerNorm; GELU -> bf16 over [x | msg]
-    {
-        f32x16 acc[4][MT];
-        zero(acc);
-        gemm_phase<4>(w.Wf1, 512, 128 * wave, 8, 0, lds, acc);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float4 b = *reinterpret_cast<const float4*>(s_bf1 + 128 * wave + 32 * t + 8 * g + 4 * hh);
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    acc[t][mt][4 * g] += b.x;
-                    acc[t][mt][4 * g + 1] += b.y;
-                    acc[t][mt][4 * g + 2] += b.z;
-                    acc[t][mt][4 * g + 3] += b.w;
-                }
+    #pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = 8 * i + 2 * wave + hh;
+                *reinterpret_cast<uint4*>(lds + cat_off(row, c)) = rx[i];
+                *reinterpret_cast<uint4*>(lds + cat_off(row, 32 + c)) = rc[i];
             }
-        float mean[MT] = {0.f, 0.f}, rstd[MT] = {1.f, 1.f};
-#pragma unroll
-        for (int mt = 0; mt < MT && !relu; ++mt) {
-            float sum = 0.f;
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) sum += acc[t][mt][i];
-            sum += __shfl_xor(sum, 32, 64);
-            if (hh == 0) red[0][wave][32 * mt + col] = sum;
-        }
-        __syncthreads();  // also: every wave has finished reading [x | msg]
-#pragma unroll
-        for (int mt = 0; mt < MT && !relu; ++mt) {
-            float sum = 0.f;
-#pragma unroll
-            for (int v = 0; v < NW; ++v) sum += red[0][v][32 * mt + col];
-            mean[mt] = sum * (1.0f / 512.0f);
-            float q = 0.f;
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const float d = acc[t][mt][i] - mean[mt];
-                    q += d * d;
-                }
-            q += __shfl_xor(q, 32, 64);
-            if (hh == 0) red[1][wave][32 * mt + col] = q;
         }
         __syncthreads();
-#pragma unroll
-        for (int mt = 0; mt < MT && !relu; ++mt) {
-            float q = 0.f;
-#pragma unroll
-            for (int v = 0; v < NW; ++v) q += red[1][v][32 * mt + col];
-            rstd[mt] = rsqrtf(q * (1.0f / 512.0f) + 1e-5f);
+
+        // 1. msg = ctx . Wout^T + bout  -> bf16 over the ctx half
+        {
+            f32x16 acc[2][MT];
+            zero(acc);
+            gemm_phase<2>(w.Wout, 256, 64 * wave, 4, 32, lds, acc);
+            __syncthreads();  // every wave has read the ctx half
+    #pragma unroll
+            for (int t = 0; t < 2; ++t)
+    #pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int n = 64 * wave + 32 * t + 8 * g + 4 * hh;
+                    const float4 b = *reinterpret_cast<const float4*>(s_bout + n);
+    #pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) {
+                        const f32x16& a = acc[t][mt];
+                        *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, 32 + n / 8) + 8 * hh) =
+                            make_uint2(pack_bf16x2(a[4 * g] + b.x, a[4 * g + 1] + b.y),
+                                       pack_bf16x2(a[4 * g + 2] + b.z, a[4 * g + 3] + b.w));
+                    }
+                }
         }
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int n = 128 * wave + 32 * t + 8 * g + 4 * hh;
-                const float4 lg = *reinterpret_cast<const float4*>(s_lng + n);
-                const float4 lb = *reinterpret_cast<const float4*>(s_lnb + n);
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    const f32x16& a = acc[t][mt];
-                    float y0, y1, y2, y3;
-                    if (relu) {
-                        y0 = fmaxf(a[4 * g], 0.f);
-                        y1 = fmaxf(a[4 * g + 1], 0.f);
-                        y2 = fmaxf(a[4 * g + 2], 0.f);
-                        y3 = fmaxf(a[4 * g + 3], 0.f);
+        __syncthreads();
+
+        // 2. h = [x | msg] . W1^T + b1; LayerNorm; GELU -> bf16 over [x | msg]
+        {
+            f32x16 acc[4][MT];
+            zero(acc);
+            gemm_phase<4>(w.Wf1, 512, 128 * wave, 8, 0, lds, acc);
+    #pragma unroll
+            for (int t = 0; t < 4; ++t)
+    #pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float4 b = *reinterpret_cast<const float4*>(s_bf1 + 128 * wave + 32 * t + 8 * g + 4 * hh);
+    #pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) {
+                        acc[t][mt][4 * g] += b.x;
+                        acc[t][mt][4 * g + 1] += b.y;
+                        acc[t][mt][4 * g + 2] += b.z;
+                        acc[t][mt][4 * g + 3] += b.w;
+                    }
+                }
+            float mean[MT] = {0.f, 0.f}, rstd[MT] = {1.f, 1.f};
+    #pragma unroll
+            for (int mt = 0; mt < MT && !relu; ++mt) {
+                float sum = 0.f;
+    #pragma unroll
+                for (int t = 0; t < 4; ++t)
+    #pragma unroll
+                    for (int i = 0; i < 16; ++i) sum += acc[t][mt][i];
+                sum += __shfl_xor(sum, 32, 64);
+                if (hh == 0) red[0][wave][32 * mt + col] = sum;
+            }
+            __syncthreads();  // also: every wave has finished reading [x | msg]
+    #pragma unroll
+            for (int mt = 0; mt < MT && !relu; ++mt) {
+                float sum = 0.f;
+    #pragma unroll
+                for (int v = 0; v < NW; ++v) sum += red[0][v][32 * mt + col];
+                mean[mt] = sum * (1.0f / 512.0f);
+                float q = 0.f;
+    #pragma unroll
+                for (int t = 0; t < 4; ++t)
+    #pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const float d = acc[t][mt][i] - mean[mt];
+                        q += d * d;
+                    }
+                q += __shfl_xor(q, 32, 64);
+                if (hh == 0) red[1][wave][32 * mt + col] = q;
+            }
+            __syncthreads();
+    #pragma unroll
+            for (int mt = 0; mt < MT && !relu; ++mt) {
+                float q = 0.f;
+    #pragma unroll
+                for (int v = 0; v < NW; ++v) q += red[1][v][32 * mt + col];
+                rstd[mt] = rsqrtf(q * (1.0f / 512.0f) + 1e-5f);
+            }
+    #pragma unroll
+            for (int t = 0; t < 4; ++t)
+    #pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int n = 128 * wave + 32 * t + 8 * g + 4 * hh;
+                    const float4 lg = *reinterpret_cast<const float4*>(s_lng + n);
+                    const float4 lb = *reinterpret_cast<const float4*>(s_lnb + n);
+    #pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) {
+                        const f32x16& a = acc[t][mt];
+                        float y0, y1, y2, y3;
+                        if (relu) {
+                            y0 = fmaxf(a[4 * g], 0.f);
+                            y1 = fmaxf(a[4 * g + 1], 0.f);
+                            y2 = fmaxf(a[4 * g + 2], 0.f);
+                            y3 = fmaxf(a[4 * g + 3], 0.f);
+                        } else {
+                            const f32x2 u01 = gelu_poly2(f32x2{(a[4 * g] - mean[mt]) * rstd[mt] * lg.x + lb.x,
+                                                               (a[4 * g + 1] - mean[mt]) * rstd[mt] * lg.y + lb.y});
+                            const f32x2 u23 = gelu_poly2(f32x2{(a[4 * g + 2] - mean[mt]) * rstd[mt] * lg.z + lb.z,
+                                                               (a[4 * g + 3] - mean[mt]) * rstd[mt] * lg.w + lb.w});
+                            y0 = u01.x;
+                            y1 = u01.y;
+                            y2 = u23.x;
+                            y3 = u23.y;
+                        }
+                        *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, n / 8) + 8 * hh) =
+                            make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
+                    }
+                }
+        }
+        __syncthreads();
+
+        // 3. x += GELU(..) . W2^T + b2 (f32); bf16 copy of x for the next projections.
+        //    y = acc + b2 is staged in LDS ([64][256] f32 over the dead GELU tile, 16-B chunk
+        //    c of row r at c ^ (r & 15)), then each wave streams whole rows: 64 lanes x 16 B =
+        //    one 1-KiB f32 row of x read, updated and written, its 512-B bf16 copy written --
+        //    full-line HBM traffic instead of 16-B pieces of 32 rows per instruction.
+        {
+            // the residual rows this wave updates below, fetched now so their HBM latency
+            // hides under the ffn2 GEMM (rows past M clamped, never stored)
+            float4 xr[R / NW];
+    #pragma unroll
+            for (int i = 0; i < R / NW; ++i)
+                xr[i] = reinterpret_cast<const float4*>(X + (size_t)min(m0 + wave * (R / NW) + i, M - 1) * 256)[lane];
+            __builtin_amdgcn_sched_barrier(0);
+            f32x16 acc[2][MT];
+            zero(acc);
+            gemm_phase<2>(w.Wf2, 256, 64 * wave, 8, 0, lds, acc);
+            __syncthreads();  // every wave has read the GELU output
+    #pragma unroll
+            for (int t = 0; t < 2; ++t)
+    #pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int n = 64 * wave + 32 * t + 8 * g + 4 * hh;
+                    const float4 b = *reinterpret_cast<const float4*>(s_bf2 + n);
+    #pragma unroll
+                    for (int mt = 0; mt < MT; ++mt) {
+                        const int r = 32 * mt + col;
+                        const f32x16& a = acc[t][mt];
+                        *reinterpret_cast<float4*>(lds + r * 1024 + (((n >> 2) ^ (r & 15)) << 4)) =
+                            make_float4(a[4 * g] + b.x, a[4 * g + 1] + b.y, a[4 * g + 2] + b.z, a[4 * g + 3] + b.w);
+                    }
+                }
+            __syncthreads();
+            // Heads (cf.wm != nullptr): each lane keeps its 4-column partial dot of each of
+            // the wave's 16 rows; one reduce-scatter over the 64 lanes (8 + 4 + 2 + 1 + 1 + 1
+            // shuffles per head instead of 16 x 6) leaves every 4-lane group with one row's sum.
+            const bool heads = cf.wm != nullptr, conf = cf.wc != nullptr;
+            float4 wm4 = make_float4(0.f, 0.f, 0.f, 0.f), wc4 = wm4;
+            if (heads) wm4 = *reinterpret_cast<const float4*>(cf.wm + 4 * lane);
+            if (conf) wc4 = *reinterpret_cast<const float4*>(cf.wc + 4 * lane);
+            float pz[R / NW], pa[R / NW];
+    #pragma unroll
+            for (int i = 0; i < R / NW; ++i) {
+                const int r = wave * (R / NW) + i, m = m0 + r;
+                pz[i] = pa[i] = 0.f;
+                if (m >= M) continue;  // wave-uniform
+                const float4 y = *reinterpret_cast<const float4*>(lds + r * 1024 + ((lane ^ (r & 15)) << 4));
+                float4* px = reinterpret_cast<float4*>(X + (size_t)m * 256) + lane;
+                float4 x = xr[i];
+                x.x += y.x;
+                x.y += y.y;
+                x.z += y.z;
+                x.w += y.w;
+                *px = x;
+                *reinterpret_cast<uint2*>(xcopy + (size_t)m * ldc + 4 * lane) =
+                    make_uint2(pack_bf16x2(x.x, x.y), pack_bf16x2(x.z, x.w));
+                if (heads) pz[i] = x.x * wm4.x + x.y * wm4.y + x.z * wm4.z + x.w * wm4.w;
+                if (conf) pa[i] = x.x * wc4.x + x.y * wc4.y + x.z * wc4.z + x.w * wc4.w;
+            }
+            if (heads) {
+                // reduce-scatter: after the step over lane bit b the lane keeps the half of its
+                // rows selected by that bit; rows end up as row = 8 b5 + 4 b4 + 2 b3 + b2
+    #pragma unroll
+                for (int half = 8, bit = 32; half >= 1; half >>= 1, bit >>= 1) {
+                    const bool up = (lane & bit) != 0;
+    #pragma unroll
+                    for (int j = 0; j < half; ++j) {
+                        const float kz = up ? pz[half + j] : pz[j], sz = up ? pz[j] : pz[half + j];
+                        pz[j] = kz + __shfl_xor(sz, bit, 64);
+                        if (conf) {
+                            const float ka = up ? pa[half + j] : pa[j], sa = up ? pa[j] : pa[half + j];
+                            pa[j] = ka + __shfl_xor(sa, bit, 64);
+                        }
+                    }
+                }
+                float z = pz[0], a = pa[0];
+                z += __shfl_xor(z, 2, 64);
+                z += __shfl_xor(z, 1, 64);
+                if (conf) {
+                    a += __shfl_xor(a, 2, 64);
+                    a += __shfl_xor(a, 1, 64);
+                }
+                const int r = wave * (R / NW) + (lane >> 2), m = m0 + r;
+                if ((lane & 3) == 0 && m < M) {  // one writer per row (k_lg_conf semantics)
+                    z += cf.bm[0];
+                    if (cf.rowseg[m] < 0) {
+                        if (conf) cf.flags[m] = 0;
                     } else {
-                        y0 = gelu_erf_fast((a[4 * g] - mean[mt]) * rstd[mt] * lg.x + lb.x);
-                        y1 = gelu_erf_fast((a[4 * g + 1] - mean[mt]) * rstd[mt] * lg.y + lb.y);
-                        y2 = gelu_erf_fast((a[4 * g + 2] - mean[mt]) * rstd[mt] * lg.z + lb.z);
-                        y3 = gelu_erf_fast((a[4 * g + 3] - mean[mt]) * rstd[mt] * lg.w + lb.w);
+                        cf.lz[m] = logsigmoid_f(z);
+                        if (conf) {
+                            const float c = sigmoid_f(a + cf.bc[0]);
+                            const bool keep = sigmoid_f(z) > 1.f - cf.width || c <= cf.thr;
+                            cf.flags[m] = (uint8_t)((c < cf.thr) | (keep << 1));
+                        }
                     }
-                    *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, n / 8) + 8 * hh) =
-                        make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
                 }
             }
+        }
+        __syncthreads();  // the next tile overwrites the LDS image
     }
-    __syncthreads();
+}
 
-    // 3. x += GELU(..) . W2^T + b2 (f32); bf16 copy of x for the next projections.
-    //    y = acc + b2 is staged in LDS ([64][256] f32 over the dead GELU tile, 16-B chunk
-    //    c of row r at c ^ (r & 15)), then each wave streams whole rows: 64 lanes x 16 B =
-    //    one 1-KiB f32 row of x read, updated and written, its 512-B bf16 copy written --
-    //    full-line HBM traffic instead of 16-B pieces of 32 rows per instruction.
-    {
-        // the residual rows this wave updates below, fetched now so their HBM latency
-        // hides under the ffn2 GEMM (rows past M clamped, never stored)
-        float4 xr[R / NW];
-#pragma unroll
-        for (int i = 0; i < R / NW; ++i)
-            xr[i] = reinterpret_cast<const float4*>(X + (size_t)min(m0 + wave * (R / NW) + i, M - 1) * 256)[lane];
-        __builtin_amdgcn_sched_barrier(0);
-        f32x16 acc[2][MT];
-        zero(acc);
-        gemm_phase<2>(w.Wf2, 256, 64 * wave, 8, 0, lds, acc);
-        __syncthreads();  // every wave has read the GELU output
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int n = 64 * wave + 32 * t + 8 * g + 4 * hh;
-                const float4 b = *reinterpret_cast<const float4*>(s_bf2 + n);
-#pragma unroll
-                for (int mt = 0; mt < MT; ++mt) {
-                    const int r = 32 * mt + col;
-                    const f32x16& a = acc[t][mt];
-                    *reinterpret_cast<float4*>(lds + r * 1024 + (((n >> 2) ^ (r & 15)) << 4)) =
-                        make_float4(a[4 * g] + b.x, a[4 * g + 1] + b.y, a[4 * g + 2] + b.z, a[4 * g + 3] + b.w);
-                }
-            }
-        __syncthreads();
-        // Heads (cf.wm != nullptr): each lane keeps its 4-column partial dot of each of
-        // the wave's 16 rows; one reduce-scatter over the 64 lanes (8 + 4 + 2 + 1 + 1 + 1
-        // shuffles per head instead of 16 x 6) leaves every 4-lane group with one row's sum.
-        const bool heads = cf.wm != nullptr, conf = cf.wc != nullptr;
-        float4 wm4 = make_float4(0.f, 0.f, 0.f, 0.f), wc4 = wm4;
-        if (heads) wm4 = *reinterpret_cast<const float4*>(cf.wm + 4 * lane);
-        if (conf) wc4 = *reinterpret_cast<const float4*>(cf.wc + 4 * lane);
-        float pz[R / NW], pa[R / NW];
-#pragma unroll
-        for (int i = 0; i < R / NW; ++i) {
-            const int r = wave * (R / NW) + i, m = m0 + r;
-            pz[i] = pa[i] = 0.f;
-            if (m >= M) continue;  // wave-uniform
-            const float4 y = *reinterpret_cast<const float4*>(lds + r * 1024 + ((lane ^ (r & 15)) << 4));
-            float4* px = reinterpret_cast<float4*>(X + (size_t)m * 256) + lane;
-            float4 x = xr[i];
-            x.x += y.x;
-            x.y += y.y;
-            x.z += y.z;
-            x.w += y.w;
-            *px = x;
-            *reinterpret_cast<uint2*>(xcopy + (size_t)m * ldc + 4 * lane) =
-                make_uint2(pack_bf16x2(x.x, x.y), pack_bf16x2(x.z, x.w));
-            if (heads) pz[i] = x.x * wm4.x + x.y * wm4.y + x.z * wm4.z + x.w * wm4.w;
-            if (conf) pa[i] = x.x * wc4.x + x.y * wc4.y + x.z * wc4.z + x.w * wc4.w;
-        }
-        if (heads) {
-            // reduce-scatter: after the step over lane bit b the lane keeps the half of its
-            // rows selected by that bit; rows end up as row = 8 b5 + 4 b4 + 2 b3 + b2
-#pragma unroll
-            for (int half = 8, bit = 32; half >= 1; half >>= 1, bit >>= 1) {
-                const bool up = (lane & bit) != 0;
-#pragma unroll
-                for (int j = 0; j < half; ++j) {
-                    const float kz = up ? pz[half + j] : pz[j], sz = up ? pz[j] : pz[half + j];
-                    pz[j] = kz + __shfl_xor(sz, bit, 64);
-                    if (conf) {
-                        const float ka = up ? pa[half + j] : pa[j], sa = up ? pa[j] : pa[half + j];
-                        pa[j] = ka + __shfl_xor(sa, bit, 64);
-                    }
-                }
-            }
-            float z = pz[0], a = pa[0];
-            z += __shfl_xor(z, 2, 64);
-            z += __shfl_xor(z, 1, 64);
-            if (conf) {
-                a += __shfl_xor(a, 2, 64);
-                a += __shfl_xor(a, 1, 64);
-            }
-            const int r = wave * (R / NW) + (lane >> 2), m = m0 + r;
-            if ((lane & 3) == 0 && m < M) {  // one writer per row (k_lg_conf semantics)
-                z += cf.bm[0];
-                if (cf.rowseg[m] < 0) {
-                    if (conf) cf.flags[m] = 0;
-                } else {
-                    cf.lz[m] = logsigmoid_f(z);
-                    if (conf) {
-                        const float c = sigmoid_f(a + cf.bc[0]);
-                        const bool keep = sigmoid_f(z) > 1.f - cf.width || c <= cf.thr;
-                        cf.flags[m] = (uint8_t)((c < cf.thr) | (keep << 1));
-                    }
-                }
-            }
-        }
-    }
+int ffn_env(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+
+int ffn_num_cus() {
+    static const int n = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1)
+            return 256;
+        return c;
+    }();
+    return n;
 }
 
 }  // namespace
@@ -388,8 +408,12 @@ int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const
     if (ldc < 256 || (ldc % 8)) return MLG_EINVAL;
     mlg_lg_conf_i cf{};
     if (conf) cf = *conf;
-    hipLaunchKernelGGL(k_lg_ffn, dim3((unsigned)((M + R - 1) / R)), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf,
-                       relu);
+    // A/B knob (tools/ffn_ab.sh): MLG_FFN_GRID = workgroups per CU of the persistent grid
+    // (0: one workgroup per tile)
+    static const int per_cu = ffn_env("MLG_FFN_GRID", 2);
+    const long ntiles = (M + R - 1) / R;
+    const long grid = per_cu > 0 ? std::min<long>(ntiles, (long)per_cu * ffn_num_cus()) : ntiles;
+    hipLaunchKernelGGL(k_lg_ffn, dim3((unsigned)grid), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf, relu);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

@@ -695,15 +695,17 @@ int mlg_loftr_features(const mlg_loftr_weights* wp, const uint8_t* frames_in, in
     // layer1 (1/2, 128)
     LF_TRY(basic_block(w, 0, 1, -1, B, H2, W2, xf, xb, yb, rf, col, s));
     LF_TRY(basic_block(w, 2, 3, -1, B, H2, W2, xf, xb, yb, rf, col, s));
-    // x1 (bf16) is needed by the FPN: keep it in tf's bf16 view? -- store x1 bf16 in fine
-    // (scratch until the end: fine is written last)
+    // x1 (bf16) is needed by the FPN: kept in `fine` (scratch until the end: fine is
+    // written last)
     bf16_t* x1b = (bf16_t*)fine;
-    hipMemcpyAsync(x1b, xb, (size_t)B * H2 * W2 * 128 * 2, hipMemcpyDeviceToDevice, s);
+    if (hipMemcpyAsync(x1b, xb, (size_t)B * H2 * W2 * 128 * 2, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return MLG_EHIP;
     // layer2 (1/4, 256p)
     LF_TRY(basic_block(w, 4, 5, 6, B, H2, W2, xf, xb, yb, rf, col, s));
     LF_TRY(basic_block(w, 7, 8, -1, B, H4, W4, xf, xb, yb, rf, col, s));
     bf16_t* x2b = (bf16_t*)c2;  // bf16 copy of x2 (c2 is free until the FPN needs its f32 slot)
-    hipMemcpyAsync(x2b, xb, (size_t)B * H4 * W4 * 256 * 2, hipMemcpyDeviceToDevice, s);
+    if (hipMemcpyAsync(x2b, xb, (size_t)B * H4 * W4 * 256 * 2, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return MLG_EHIP;
     // layer3 (1/8, 256)
     LF_TRY(basic_block(w, 9, 10, 11, B, H4, W4, xf, xb, yb, rf, col, s));
     LF_TRY(basic_block(w, 12, 13, -1, B, H8, W8, xf, xb, yb, rf, col, s));

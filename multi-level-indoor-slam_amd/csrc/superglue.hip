@@ -19,11 +19,13 @@
 //                  the pre-layer states, as AttentionalGNN), mlg_lg_ffn in ReLU mode
 //                  (merge + MLP [x | msg] 512 -> 512 (BN folded) -> ReLU -> 256 + residual);
 //   final_proj     GEMM -> f32 matching descriptors;
-//   per pair       S = m0 . m1^T on the exact-f32 MFMA; Z = S / 16 with the learned
-//                  dustbin score on the extra row / column; 20 log-Sinkhorn iterations
-//                  (k_sg_rows: u = log_mu - logsumexp_j(Z + v); k_sg_cols: v = log_nu -
-//                  logsumexp_i(Z + u)); k_sg_rowmax / k_sg_colmax on Z + u + v - norm;
-//                  k_sg_select: mutual nearest, exp(score) > threshold, compacted.
+//   per pair       S = m0 . m1^T and T = S^T on the exact-f32 MFMA (one kernel, chunks
+//                  of pairs); Z =
+//                  S / 16 with the learned dustbin score on the extra row / column; 20
+//                  log-Sinkhorn iterations (k_sg_lse<false>: u = log_mu - logsumexp_j(Z + v)
+//                  over rows of S; k_sg_lse<true>: v = log_nu - logsumexp_i(Z + u) over rows
+//                  of T); k_sg_argmax<false / true> on Z + u + v - norm; k_sg_select:
+//                  mutual nearest, exp(score) > threshold, compacted.
 #include <math.h>
 
 #include <algorithm>
@@ -104,25 +106,15 @@ __global__ void k_sg_fill(float* __restrict__ a, long n, float v) {
 }
 
 // ------------------------------------------------------------- Sinkhorn -----
-// Pair c of a chunk: S_c [m][n] (row stride ld) -> Z_ij = S_ij / 16 (i < m, j < n), the
-// dustbin row / column and corner = alpha.  u [m + 1], v [n + 1] per pair.
+// Pair c of a chunk: S_c [m][n] and its transpose T_c [n][m] (row stride ld each) ->
+// Z_ij = S_ij / 16 (i < m, j < n), the dustbin row / column and corner = alpha.  u [m + 1]
+// and v [n + 1] of every pair live in two flat vectors (offsets uo, vo).  With the
+// transpose stored, the u update (logsumexp over a row of Z + v) and the v update (over a
+// column of Z + u) are the same row-wise pass: coalesced 16-B loads, one wave per row.
 struct SgPair {
-    int m, n, uo, vo;  // rows, cols, offsets of u and v in the chunk's vectors
+    int m, n, uo, vo, pid, pad0, pad1, pad2;
 };
 
-__device__ __forceinline__ float sg_z(const float* S, int ld, int i, int j, int m, int n, float alpha) {
-    return (i < m && j < n) ? S[(size_t)i * ld + j] * 0.0625f : alpha;
-}
-
-// online logsumexp of (a, b) pairs: (max, sum) merge
-__device__ __forceinline__ void lse_push(float x, float& mx, float& sm) {
-    if (x > mx) {
-        sm = sm * expf(mx - x) + 1.f;
-        mx = x;
-    } else {
-        sm += expf(x - mx);
-    }
-}
 __device__ __forceinline__ void lse_merge(float omx, float osm, float& mx, float& sm) {
     if (omx > mx) {
         sm = sm * expf(mx - omx) + osm;
@@ -132,18 +124,55 @@ __device__ __forceinline__ void lse_merge(float omx, float osm, float& mx, float
     }
 }
 
-// u_i = log_mu_i - logsumexp_j (Z_ij + v_j), one wave per row i in [0, m]
-__global__ __launch_bounds__(256) void k_sg_rows(const float* __restrict__ S, long sstride, int ld,
-                                                 const SgPair* __restrict__ pairs, float alpha,
-                                                 float* __restrict__ u, const float* __restrict__ v) {
+// TR = false: u_i = log_mu_i - logsumexp_j (Z_ij + v_j), rows i in [0, m] of S;
+// TR = true : v_j = log_nu_j - logsumexp_i (Z_ij + u_i), rows j in [0, n] of T.
+template <bool TR>
+__global__ __launch_bounds__(256) void k_sg_lse(const float* __restrict__ S, long sstride, int ld,
+                                                const SgPair* __restrict__ pairs, float alpha, float* __restrict__ out,
+                                                const float* __restrict__ in) {
     const int c = blockIdx.y, lane = threadIdx.x & 63;
     const SgPair p = pairs[c];
+    const int R = TR ? p.n : p.m, C = TR ? p.m : p.n;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i > p.m) return;
-    const float* Sc = S + (size_t)c * sstride;
-    const float* vc = v + p.vo;
+    if (i > R) return;
+    const float* inv = in + (TR ? p.uo : p.vo);
     float mx = -INFINITY, sm = 0.f;
-    for (int j = lane; j <= p.n; j += 64) lse_push(sg_z(Sc, ld, i, j, p.m, p.n, alpha) + vc[j], mx, sm);
+    if (i < R) {
+        // blocks of 2048 columns held in registers (8 float4 per lane): block max, one
+        // rescale, one exp per element
+        const float* row = S + (size_t)c * sstride + (size_t)i * ld;
+        for (int base = 0; base < C; base += 2048) {
+            float x[8][4];
+            float bm = -INFINITY;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int j0 = base + 256 * t + 4 * lane;
+                float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f), v4 = s4;
+                if (j0 < C) {
+                    s4 = *reinterpret_cast<const float4*>(row + j0);
+                    v4 = *reinterpret_cast<const float4*>(inv + j0);
+                }
+                x[t][0] = j0 < C ? s4.x * 0.0625f + v4.x : -INFINITY;
+                x[t][1] = j0 + 1 < C ? s4.y * 0.0625f + v4.y : -INFINITY;
+                x[t][2] = j0 + 2 < C ? s4.z * 0.0625f + v4.z : -INFINITY;
+                x[t][3] = j0 + 3 < C ? s4.w * 0.0625f + v4.w : -INFINITY;
+                bm = fmaxf(bm, fmaxf(fmaxf(x[t][0], x[t][1]), fmaxf(x[t][2], x[t][3])));
+            }
+            if (bm > mx) {
+                sm *= expf(mx - bm);
+                mx = bm;
+            }
+            if (mx > -INFINITY) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) sm += expf(x[t][k] - mx);
+            }
+        }
+        if (lane == 0) lse_merge(alpha + inv[C], 1.f, mx, sm);  // dustbin column
+    } else {  // dustbin row: alpha everywhere
+        for (int j = lane; j <= C; j += 64) lse_merge(alpha + inv[j], 1.f, mx, sm);
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const float omx = __shfl_xor(mx, o, 64), osm = __shfl_xor(sm, o, 64);
@@ -151,96 +180,49 @@ __global__ __launch_bounds__(256) void k_sg_rows(const float* __restrict__ S, lo
     }
     if (lane == 0) {
         const float norm = -logf((float)(p.m + p.n));
-        const float lmu = i < p.m ? norm : logf((float)p.n) + norm;
-        u[p.uo + i] = lmu - (mx + logf(sm));
+        const float lm = i < R ? norm : logf((float)C) + norm;
+        out[(TR ? p.vo : p.uo) + i] = lm - (mx + logf(sm));
     }
 }
 
-// v_j = log_nu_j - logsumexp_i (Z_ij + u_i); 64 columns per workgroup, 4 waves over rows
-__global__ __launch_bounds__(256) void k_sg_cols(const float* __restrict__ S, long sstride, int ld,
-                                                 const SgPair* __restrict__ pairs, float alpha,
-                                                 const float* __restrict__ u, float* __restrict__ v) {
-    __shared__ float rm[4][64], rs[4][64];
-    const int c = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const SgPair p = pairs[c];
-    const int j = blockIdx.x * 64 + lane;
-    const float* Sc = S + (size_t)c * sstride;
-    const float* uc = u + p.uo;
-    float mx = -INFINITY, sm = 0.f;
-    if (j <= p.n)
-        for (int i = wave; i <= p.m; i += 4) lse_push(sg_z(Sc, ld, i, j, p.m, p.n, alpha) + uc[i], mx, sm);
-    rm[wave][lane] = mx;
-    rs[wave][lane] = sm;
-    __syncthreads();
-    if (wave == 0 && j <= p.n) {
-        for (int w = 1; w < 4; ++w) lse_merge(rm[w][lane], rs[w][lane], mx, sm);
-        const float norm = -logf((float)(p.m + p.n));
-        const float lnu = j < p.n ? norm : logf((float)p.m) + norm;
-        v[p.vo + j] = lnu - (mx + logf(sm));
-    }
-}
-
-// final scores Z + u + v - norm restricted to i < m, j < n: row max (first argmax)
-__device__ __forceinline__ float sg_final(const float* S, int ld, int i, int j, const float* u, const float* v,
-                                          float norm) {
-    return ((S[(size_t)i * ld + j] * 0.0625f + u[i]) + v[j]) - norm;
-}
-
-__global__ __launch_bounds__(256) void k_sg_rowmax(const float* __restrict__ S, long sstride, int ld,
+// argmax over the inner block of Z + u + v - norm (first index on ties), one wave per
+// row: TR = false rows i of S (-> value and column index), TR = true rows j of T (-> row
+// index).  Both evaluate ((S_ij / 16 + u_i) + v_j) - norm, as torch does.
+template <bool TR>
+__global__ __launch_bounds__(256) void k_sg_argmax(const float* __restrict__ S, long sstride, int ld,
                                                    const SgPair* __restrict__ pairs, const float* __restrict__ u,
-                                                   const float* __restrict__ v, float* __restrict__ rmax,
-                                                   int32_t* __restrict__ ridx, int kmax) {
+                                                   const float* __restrict__ v, float* __restrict__ vmax,
+                                                   int32_t* __restrict__ idx, int kmax) {
     const int c = blockIdx.y, lane = threadIdx.x & 63;
     const SgPair p = pairs[c];
+    const int R = TR ? p.n : p.m, C = TR ? p.m : p.n;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (i >= p.m) return;
-    const float* Sc = S + (size_t)c * sstride;
+    if (i >= R) return;
+    const float* row = S + (size_t)c * sstride + (size_t)i * ld;
+    const float* uc = u + p.uo;
+    const float* vc = v + p.vo;
     const float norm = -logf((float)(p.m + p.n));
     float bv = -INFINITY;
     int bi = 0x7fffffff;
-    for (int j = lane; j < p.n; j += 64) {
-        const float z = sg_final(Sc, ld, i, j, u + p.uo, v + p.vo, norm);
-        if (z > bv) { bv = z; bi = j; }
+    for (int j = lane; j < C; j += 64) {
+        const float z = TR ? ((row[j] * 0.0625f + uc[j]) + vc[i]) - norm : ((row[j] * 0.0625f + uc[i]) + vc[j]) - norm;
+        if (z > bv) {
+            bv = z;
+            bi = j;
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const float ov = __shfl_xor(bv, o, 64);
         const int oi = __shfl_xor(bi, o, 64);
-        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        if (ov > bv || (ov == bv && oi < bi)) {
+            bv = ov;
+            bi = oi;
+        }
     }
     if (lane == 0) {
-        rmax[(size_t)c * kmax + i] = bv;
-        ridx[(size_t)c * kmax + i] = bi;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_sg_colmax(const float* __restrict__ S, long sstride, int ld,
-                                                   const SgPair* __restrict__ pairs, const float* __restrict__ u,
-                                                   const float* __restrict__ v, int32_t* __restrict__ cidx, int kmax) {
-    __shared__ float rv[4][64];
-    __shared__ int ri[4][64];
-    const int c = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const SgPair p = pairs[c];
-    const int j = blockIdx.x * 64 + lane;
-    const float* Sc = S + (size_t)c * sstride;
-    const float norm = -logf((float)(p.m + p.n));
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    if (j < p.n)
-        for (int i = wave; i < p.m; i += 4) {
-            const float z = sg_final(Sc, ld, i, j, u + p.uo, v + p.vo, norm);
-            if (z > bv) { bv = z; bi = i; }  // rows visited in increasing order per wave
-        }
-    rv[wave][lane] = bv;
-    ri[wave][lane] = bi;
-    __syncthreads();
-    if (wave == 0 && j < p.n) {
-        for (int w = 1; w < 4; ++w)
-            if (rv[w][lane] > bv || (rv[w][lane] == bv && ri[w][lane] < bi)) {
-                bv = rv[w][lane];
-                bi = ri[w][lane];
-            }
-        cidx[(size_t)c * kmax + j] = bi;
+        if (!TR) vmax[(size_t)c * kmax + i] = bv;
+        idx[(size_t)c * kmax + i] = bi;
     }
 }
 
@@ -248,13 +230,13 @@ __global__ __launch_bounds__(256) void k_sg_colmax(const float* __restrict__ S, 
 __global__ __launch_bounds__(1024) void k_sg_select(const SgPair* __restrict__ pairs, const float* __restrict__ rmax,
                                                     const int32_t* __restrict__ ridx,
                                                     const int32_t* __restrict__ cidx, int kmax, float thr,
-                                                    const int32_t* __restrict__ pair_id, int32_t* __restrict__ matches,
+                                                    int32_t* __restrict__ matches,
                                                     float* __restrict__ mscores, int32_t* __restrict__ nmatch) {
     __shared__ int warp_tot[16];
     __shared__ int base;
     const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const SgPair p = pairs[c];
-    const int pid = pair_id[c];
+    const int pid = p.pid;
     if (tid == 0) base = 0;
     __syncthreads();
     for (int i0 = 0; i0 < p.m; i0 += 1024) {
@@ -294,16 +276,25 @@ __global__ __launch_bounds__(1024) void k_sg_select(const SgPair* __restrict__ p
 
 inline size_t a256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-constexpr int SG_CHUNK = 16;  // pairs per Sinkhorn chunk ([16][kmax][kmax] f32 scores)
+// pairs per Sinkhorn chunk: S and T of a chunk within SG_CHUNK_MB (larger launches
+// amortise the ramp; 128 MB would keep them in the 256 MB last-level cache), at most 64
+#ifndef SG_CHUNK_MB
+#define SG_CHUNK_MB 512
+#endif
+inline int sg_chunk(int kmax) {
+    const size_t per = (size_t)2 * kmax * (((size_t)kmax + 3) & ~(size_t)3) * 4;
+    return (int)std::max<size_t>(1, std::min<size_t>(64, ((size_t)SG_CHUNK_MB << 20) / per));
+}
 
 struct SgLayout {
-    size_t x, cat, Q, K, Vt, ctx, h3, h4, live, ec, es, md, segs, tasks, outoff, S, u, v, pairs, rmax, ridx, cidx, pid,
+    size_t x, cat, Q, K, Vt, ctx, h3, h4, live, ec, es, md, segs, tasks, outoff, S, T, u, v, pairs, rmax, ridx, cidx,
         total;
 };
 
 SgLayout sg_layout(int P, int kmax) {
     const size_t N = (size_t)2 * P * (((size_t)kmax + 63) & ~(size_t)63);
     const size_t ldS = ((size_t)kmax + 3) & ~(size_t)3;
+    const size_t ch = (size_t)sg_chunk(kmax);
     SgLayout L{};
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -326,14 +317,14 @@ SgLayout sg_layout(int P, int kmax) {
     L.segs = take((size_t)2 * P * sizeof(SgSeg));
     L.tasks = take((size_t)4 * P * sizeof(int4));
     L.outoff = take((size_t)4 * P * 4);
-    L.S = take((size_t)SG_CHUNK * kmax * ldS * 4);
-    L.u = take((size_t)SG_CHUNK * (kmax + 1) * 4);
-    L.v = take((size_t)SG_CHUNK * (kmax + 1) * 4);
-    L.pairs = take((size_t)SG_CHUNK * sizeof(SgPair));
-    L.rmax = take((size_t)SG_CHUNK * kmax * 4);
-    L.ridx = take((size_t)SG_CHUNK * kmax * 4);
-    L.cidx = take((size_t)SG_CHUNK * kmax * 4);
-    L.pid = take((size_t)SG_CHUNK * 4);
+    L.S = take(ch * kmax * ldS * 4);
+    L.T = take(ch * kmax * ldS * 4);
+    L.u = take((size_t)P * (kmax + 4) * 4);
+    L.v = take((size_t)P * (kmax + 4) * 4);
+    L.pairs = take((size_t)P * sizeof(SgPair));
+    L.rmax = take(ch * kmax * 4);
+    L.ridx = take(ch * kmax * 4);
+    L.cidx = take(ch * kmax * 4);
     L.total = o;
     return L;
 }
@@ -394,13 +385,13 @@ int mlg_superglue_run(const mlg_sg_weights_i& w, const float* kpts, const float*
     int4* TASKS = (int4*)at(L.tasks);
     int* OUTOFF = (int*)at(L.outoff);
     float* S = (float*)at(L.S);
+    float* T = (float*)at(L.T);
     float* U = (float*)at(L.u);
     float* V = (float*)at(L.v);
     SgPair* PAIRS = (SgPair*)at(L.pairs);
     float* RMAX = (float*)at(L.rmax);
     int32_t* RIDX = (int32_t*)at(L.ridx);
     int32_t* CIDX = (int32_t*)at(L.cidx);
-    int32_t* PID = (int32_t*)at(L.pid);
 
     if (hipMemsetAsync(nmatch, 0, sizeof(int32_t) * P, s) != hipSuccess) return MLG_EHIP;
     // segments: pair p -> [a | b], empty sides skipped (no matches, as the reference's early exit)
@@ -459,43 +450,45 @@ int mlg_superglue_run(const mlg_sg_weights_i& w, const float* kpts, const float*
     }
     // matching descriptors
     SG_TRY(mlg_gemm_conv(CAT, 512, w.Wfinal, w.bfinal, nullptr, 0, MD, 256, nullptr, 0, 0, 0, Npad, 256, 256, s));
-    // per chunk of pairs: scores, Sinkhorn, mutual matches
+    // per chunk of pairs: scores and their transpose, Sinkhorn, mutual matches
     const int ldS = (kmax + 3) & ~3;
     const long sstride = (long)kmax * ldS;
-    for (int c0 = 0; c0 < np; c0 += SG_CHUNK) {
-        const int nc = std::min(SG_CHUNK, np - c0);
-        std::vector<SgPair> hp(nc);
-        std::vector<int32_t> hpid(nc);
-        int mm = 0, nn = 0, uo = 0, vo = 0;
+    const int chunk = sg_chunk(kmax);
+    std::vector<SgPair> hp(np);
+    int uo = 0, vo = 0;
+    for (int c = 0; c < np; ++c) {
+        const SgSeg a = segs[2 * c], b = segs[2 * c + 1];
+        hp[c] = SgPair{a.len, b.len, uo, vo, pair_of[c], 0, 0, 0};
+        uo += (a.len + 4) & ~3;  // 16-B aligned vectors
+        vo += (b.len + 4) & ~3;
+    }
+    if (hipMemcpyAsync(PAIRS, hp.data(), np * sizeof(SgPair), hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(U, 0, (size_t)uo * 4, s) != hipSuccess || hipMemsetAsync(V, 0, (size_t)vo * 4, s) != hipSuccess)
+        return MLG_EHIP;
+    for (int c0 = 0; c0 < np; c0 += chunk) {
+        const int nc = std::min(chunk, np - c0);
+        int mm = 0, nn = 0;
         for (int c = 0; c < nc; ++c) {
             const SgSeg a = segs[2 * (c0 + c)], b = segs[2 * (c0 + c) + 1];
-            hp[c] = SgPair{a.len, b.len, uo, vo};
-            uo += a.len + 1;
-            vo += b.len + 1;
             mm = std::max(mm, a.len);
             nn = std::max(nn, b.len);
-            hpid[c] = pair_of[c0 + c];
-            SG_TRY(mlg_similarity_f32(MD + (size_t)a.off * 256, a.len, MD + (size_t)b.off * 256, b.len, 256,
-                                      S + (size_t)c * sstride, ldS, s));
+            SG_TRY(mlg_similarity_f32_t(MD + (size_t)a.off * 256, a.len, MD + (size_t)b.off * 256, b.len, 256,
+                                        S + (size_t)c * sstride, ldS, T + (size_t)c * sstride, ldS, s));
         }
-        if (hipMemcpyAsync(PAIRS, hp.data(), nc * sizeof(SgPair), hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemcpyAsync(PID, hpid.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, s) != hipSuccess ||
-            hipMemsetAsync(U, 0, (size_t)uo * 4, s) != hipSuccess || hipMemsetAsync(V, 0, (size_t)vo * 4, s) != hipSuccess)
-            return MLG_EHIP;
-        const dim3 rows((mm + 1 + 3) / 4, nc), cols((nn + 1 + 63) / 64, nc);
+        const SgPair* pc = PAIRS + c0;
+        const dim3 rows((mm + 1 + 3) / 4, nc), cols((nn + 1 + 3) / 4, nc);
         for (int it = 0; it < iters; ++it) {
-            hipLaunchKernelGGL(k_sg_rows, rows, dim3(256), 0, s, S, sstride, ldS, PAIRS, w.bin_score, U, V);
-            hipLaunchKernelGGL(k_sg_cols, cols, dim3(256), 0, s, S, sstride, ldS, PAIRS, w.bin_score, U, V);
+            hipLaunchKernelGGL(k_sg_lse<false>, rows, dim3(256), 0, s, S, sstride, ldS, pc, w.bin_score, U, V);
+            hipLaunchKernelGGL(k_sg_lse<true>, cols, dim3(256), 0, s, T, sstride, ldS, pc, w.bin_score, V, U);
         }
-        hipLaunchKernelGGL(k_sg_rowmax, dim3((mm + 3) / 4, nc), dim3(256), 0, s, S, sstride, ldS, PAIRS, U, V, RMAX,
-                           RIDX, kmax);
-        hipLaunchKernelGGL(k_sg_colmax, dim3((nn + 63) / 64, nc), dim3(256), 0, s, S, sstride, ldS, PAIRS, U, V, CIDX,
-                           kmax);
-        hipLaunchKernelGGL(k_sg_select, dim3(nc), dim3(1024), 0, s, PAIRS, RMAX, RIDX, CIDX, kmax, thr, PID, matches,
-                           mscores, nmatch);
+        hipLaunchKernelGGL(k_sg_argmax<false>, dim3((mm + 3) / 4, nc), dim3(256), 0, s, S, sstride, ldS, pc, U, V,
+                           RMAX, RIDX, kmax);
+        hipLaunchKernelGGL(k_sg_argmax<true>, dim3((nn + 3) / 4, nc), dim3(256), 0, s, T, sstride, ldS, pc, U, V,
+                           (float*)nullptr, CIDX, kmax);
+        hipLaunchKernelGGL(k_sg_select, dim3(nc), dim3(1024), 0, s, pc, RMAX, RIDX, CIDX, kmax, thr, matches, mscores,
+                           nmatch);
         MLG_LAUNCH_CHECK();
-        // the pair tables are pageable host vectors reused per chunk
-        if (hipStreamSynchronize(s) != hipSuccess) return MLG_EHIP;
     }
+    // the segment / task / pair tables are pageable host vectors
     return hipStreamSynchronize(s) == hipSuccess ? MLG_OK : MLG_EHIP;
 }
