@@ -415,6 +415,24 @@ int mlg_prof_reset(void);
 int mlg_prof_read(int slot, double* total_ms, long* launches);
 int mlg_prof_read_work(int slot, double* flops);
 
+
+/* ---------------------------------------------------------- keyframe ingestion --
+ * HOST pointers (not device): PNG keyframes -> BGR uint8 [n, H, W, 3], replacing the
+ * cv2.imread(path) of process_image_sequence (place_recognition.py:965-968) on the
+ * '{timestamp:.6f}.png' files scripts/utils/bag_utils.py:222-271 writes.  IMREAD_COLOR
+ * semantics: palette -> RGB, gray -> 3 equal channels (1/2/4-bit samples scaled to
+ * 0..255), alpha stripped, 16-bit samples -> high byte, Adam7 undone, stored as BGR.
+ * A pool of `threads` host threads decodes image i into out + i*H*W*3 (pass a pinned
+ * buffer and copy it to HBM on a side stream); status[i] = 0, MLG_EINVAL (unreadable,
+ * corrupt or not a PNG: imread's None) or MLG_ESIZE (a valid PNG that is not H x W).
+ */
+#define MLG_ESIZE (-4)
+int mlg_png_info(const uint8_t* data, size_t len, int32_t* width, int32_t* height, int32_t* color_type,
+                 int32_t* bit_depth);
+int mlg_png_decode_bgr(const uint8_t* const* data, const size_t* lens, int n, uint8_t* out, int H, int W,
+                       int threads, int32_t* status);
+int mlg_png_load_bgr(const char* const* paths, int n, uint8_t* out, int H, int W, int threads, int32_t* status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -116,6 +116,7 @@ const char* mlg_strerror(int status) {
         case MLG_EINVAL: return "invalid argument (shape, alignment or size)";
         case MLG_EHIP: return "HIP launch error";
         case MLG_ENOMEM: return "workspace too small";
+        case MLG_ESIZE: return "image size differs from the batch size";
         default: return "unknown mlgate status";
     }
 }

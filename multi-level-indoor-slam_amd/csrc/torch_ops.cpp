@@ -15,6 +15,8 @@
 #include <torch/library.h>
 
 #include <cstring>
+#include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/mlgate.h"
@@ -582,6 +584,38 @@ std::tuple<double, int64_t, double> prof_read(int64_t slot) {
     return {ms, (int64_t)n, work};
 }
 
+
+// ------------------------------------------------------------ keyframe ingestion
+// Host ops (CPU key): the decoders write a caller-owned host tensor, normally a pinned
+// staging buffer that mlgate.ingest uploads on a side stream.
+Tensor png_load_into(std::vector<std::string> paths, Tensor out, int64_t H, int64_t W, int64_t threads) {
+    want(out, at::kByte, "out", false);
+    const int64_t n = (int64_t)paths.size();
+    TORCH_CHECK(out.numel() >= n * H * W * 3, "out: needs ", n * H * W * 3, " bytes, has ", out.numel());
+    std::vector<const char*> cps(paths.size());
+    for (size_t i = 0; i < paths.size(); ++i) cps[i] = paths[i].c_str();
+    Tensor status = at::zeros({n}, at::TensorOptions().dtype(at::kInt));
+    check_rc(mlg_png_load_bgr(cps.data(), (int)n, mp<uint8_t>(out), (int)H, (int)W, (int)threads,
+                              mp<int32_t>(status)), "mlg_png_load_bgr");
+    return status;
+}
+
+std::tuple<Tensor, Tensor> png_decode(std::vector<Tensor> blobs, int64_t H, int64_t W, int64_t threads) {
+    const int64_t n = (int64_t)blobs.size();
+    std::vector<const uint8_t*> ptrs(n);
+    std::vector<size_t> lens(n);
+    for (int64_t i = 0; i < n; ++i) {
+        want(blobs[i], at::kByte, "blob", false);
+        ptrs[i] = cp<uint8_t>(blobs[i]);
+        lens[i] = (size_t)blobs[i].numel();
+    }
+    Tensor out = at::zeros({n, H, W, 3}, at::TensorOptions().dtype(at::kByte));
+    Tensor status = at::zeros({n}, at::TensorOptions().dtype(at::kInt));
+    check_rc(mlg_png_decode_bgr(ptrs.data(), lens.data(), (int)n, mp<uint8_t>(out), (int)H, (int)W, (int)threads,
+                                mp<int32_t>(status)), "mlg_png_decode_bgr");
+    return {out, status};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(mlgate, m) {
@@ -612,6 +646,8 @@ TORCH_LIBRARY(mlgate, m) {
           "-> (Tensor, Tensor, Tensor)");
     m.def("proximity(Tensor pos, Tensor? floor, int row0, int nrows, float radius, int min_gap, bool strict) "
           "-> (Tensor, Tensor, Tensor, Tensor)");
+    m.def("png_load_into(str[] paths, Tensor(a!) out, int H, int W, int threads) -> Tensor");
+    m.def("png_decode(Tensor[] blobs, int H, int W, int threads) -> (Tensor, Tensor)");
     m.def("prof_enable(int mask) -> int");
     m.def("prof_reset() -> int");
     m.def("prof_read(int slot) -> (float, int, float)");
@@ -635,6 +671,11 @@ TORCH_LIBRARY_IMPL(mlgate, CUDA, m) {
     m.impl("pillow_resize_224", &pillow_resize_224);
     m.impl("plane_ransac", &plane_ransac);
     m.impl("proximity", &proximity);
+}
+
+TORCH_LIBRARY_IMPL(mlgate, CPU, m) {
+    m.impl("png_load_into", &png_load_into);
+    m.impl("png_decode", &png_decode);
 }
 
 TORCH_LIBRARY_IMPL(mlgate, CompositeExplicitAutograd, m) {

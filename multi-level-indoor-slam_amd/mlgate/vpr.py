@@ -441,19 +441,37 @@ class SemanticPlaceRecognition:
 def process_image_sequence(image_dir: Union[str, Path], timestamps: np.ndarray, floor_labels: np.ndarray,
                            vpr_method: str = 'mixvpr',
                            device: str = 'cuda') -> Tuple[SemanticPlaceRecognition, List[PlaceMatch]]:
-    """Sorted *.png then *.jpg of a directory -> database -> floor-gated loop closures."""
-    try:
-        import cv2
-    except ImportError as e:
-        raise ImportError("OpenCV is required for image loading. Install with: pip install opencv-python") from e
+    """Sorted *.png then *.jpg of a directory -> database -> floor-gated loop closures
+    (place_recognition.py:936-991).
+
+    PNG keyframes (what bag_utils.extract_images writes) are decoded by the native
+    loader (mlgate.ingest: host thread pool -> pinned buffer -> HBM on a side stream)
+    and added in device batches; the database, warnings and matches are those of the
+    reference's one-image-at-a-time loop.  *.jpg files still need OpenCV's decoder."""
+    from . import ingest
     image_dir = Path(image_dir)
     spr = SemanticPlaceRecognition(vpr_method=vpr_method, device=device)
     files = sorted(image_dir.glob('*.png')) + sorted(image_dir.glob('*.jpg'))
     if len(files) != len(timestamps):
         warnings.warn(f"Number of images ({len(files)}) != timestamps ({len(timestamps)}). Using minimum of both.")
     n = min(len(files), len(timestamps), len(floor_labels))
+    files = files[:n]
+    cv2 = None
+    if any(f.suffix == '.jpg' for f in files):
+        try:
+            import cv2
+        except ImportError as e:
+            raise ImportError("OpenCV is required for image loading. Install with: pip install opencv-python") from e
     print(f"Processing {n} images with {vpr_method}...")
-    for i in range(n):
+    pngs = [i for i, f in enumerate(files) if f.suffix == '.png']
+    for idx, frames in ingest.KeyframeStream([files[i] for i in pngs], device=device):
+        rows = [pngs[j] for j in idx]
+        spr.add_images(frames, [timestamps[i] for i in rows], [int(floor_labels[i]) for i in rows],
+                       [str(files[i]) for i in rows])
+        for i in rows:
+            if (i + 1) % 100 == 0:
+                print(f"  Processed {i + 1}/{n} images")
+    for i in range(len(pngs), n):  # *.jpg files sort after every *.png file
         img = cv2.imread(str(files[i]))
         if img is None:
             warnings.warn(f"Failed to load image: {files[i]}")
