@@ -120,10 +120,12 @@ __device__ __forceinline__ void zero(f32x16 (&acc)[NT][MT]) {
 // relu != 0: SuperGlue's MLP (BatchNorm folded into Wf1 / bf1 on the host, ReLU, no
 // LayerNorm) instead of LightGlue's LayerNorm + GELU (superglue.hip)
 //
-// Persistent form: gridDim.x workgroups (two per CU) walk the 64-row tiles with stride
-// gridDim.x: 10 % less time than one workgroup per tile (tools/ffn_ab.sh, same box).  A
-// half-tile start offset for half of the grid (so that co-resident workgroups would run
-// epilogue beside GEMM) measured no change and was dropped.
+// PERSIST = false (default): one workgroup per 64-row tile, 228 VGPRs, no scratch.
+// PERSIST = true (MLG_FFN_GRID = workgroups per CU): the grid walks the tiles with stride
+// gridDim.x; the compiler hoists lane addresses out of the tile loop and spills 436 B
+// per lane around it: 3.66 vs 2.94 ms per 2 M-token launch and 4.29 vs 3.20 s of FFN per
+// bench step on one box (tools/gpu_ab_ffn_proj.sh), so it is off.
+template <bool PERSIST>
 __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ctx, float* __restrict__ X,
                                                   bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w,
                                                   mlg_lg_conf_i cf, int relu) {
@@ -380,6 +382,7 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
                 }
             }
         }
+        if (!PERSIST) break;  // one tile per workgroup: no loop, no state carried across tiles
         __syncthreads();  // the next tile overwrites the LDS image
     }
 }
@@ -410,10 +413,15 @@ int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const
     if (conf) cf = *conf;
     // A/B knob (tools/ffn_ab.sh): MLG_FFN_GRID = workgroups per CU of the persistent grid
     // (0: one workgroup per tile)
-    static const int per_cu = ffn_env("MLG_FFN_GRID", 2);
+    static const int per_cu = ffn_env("MLG_FFN_GRID", 0);
     const long ntiles = (M + R - 1) / R;
-    const long grid = per_cu > 0 ? std::min<long>(ntiles, (long)per_cu * ffn_num_cus()) : ntiles;
-    hipLaunchKernelGGL(k_lg_ffn, dim3((unsigned)grid), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf, relu);
+    if (per_cu > 0) {
+        const long grid = std::min<long>(ntiles, (long)per_cu * ffn_num_cus());
+        hipLaunchKernelGGL(k_lg_ffn<true>, dim3((unsigned)grid), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf, relu);
+    } else {
+        hipLaunchKernelGGL(k_lg_ffn<false>, dim3((unsigned)ntiles), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf,
+                           relu);
+    }
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

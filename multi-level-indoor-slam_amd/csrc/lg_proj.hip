@@ -16,12 +16,13 @@
 // C = X . W^T, which hands a lane 4 consecutive tokens of one dim: one 8-B store into
 // the transposed V^T row, where the transposed product would need 4 scattered 2-B
 // stores.  Same fragments, operand order only.
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace {
 
-constexpr int R = 64;      // tokens per workgroup
 constexpr int ROWB = 512;  // LDS bytes per token row: 256 bf16
 
 // chunk c (0..31) of row r at slot c ^ (r & 15): the 16 lanes of a ds_read_b128 lane
@@ -34,35 +35,36 @@ __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_ca
 // row r at slot c ^ (r & 7).  Rows are tokens for q / k and head dims for V^T; either way
 // a head's 64 rows are ONE contiguous 8 KiB block of the destination, written as whole
 // 1 KiB pieces (per-lane 8-B stores at a 128-B row stride touched 32 lines each).
+template <int R>
 __device__ __forceinline__ int stage_off(int h, int row, int e) {
-    return (h * 64 + row) * 128 + ((((e >> 3) ^ (row & 7))) << 4) + (e & 7) * 2;
+    return (h * R + row) * 128 + ((((e >> 3) ^ (row & 7))) << 4) + (e & 7) * 2;
 }
 
 // acc[mt] over K = 256 (16 k-steps; step ks: LDS chunk 2 ks + hh, W slab ks).
 // SWAP: acc = X . W^T (lane col = output column), else acc = W . X^T (lane col = token).
-template <bool SWAP>
+template <bool SWAP, int MT>
 __device__ __forceinline__ void proj_gemm(const bf16_t* __restrict__ wrow, size_t step, const char* lds,
-                                          f32x16 (&acc)[2]) {
+                                          f32x16 (&acc)[MT]) {
     const int lane = threadIdx.x & 63, col = lane & 31, hh = lane >> 5;
     const char* xrow = lds + col * ROWB;
     const int sw = col & 15;
-    bf16x8 wf[4], xa[2], xb[2];
+    bf16x8 wf[4], xa[MT], xb[MT];
 #pragma unroll
     for (int s = 0; s < 4; ++s) wf[s] = ld16(wrow + s * step);
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) xa[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + ((hh ^ sw) << 4));
+    for (int mt = 0; mt < MT; ++mt) xa[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + ((hh ^ sw) << 4));
 #pragma unroll 1
     for (int kb = 0; kb < 4; ++kb) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int ks = 4 * kb + s;
             const int cn = ((2 * min(ks + 1, 15) + hh) ^ sw) << 4;
-            bf16x8(&cur)[2] = (s & 1) ? xb : xa;
-            bf16x8(&nxt)[2] = (s & 1) ? xa : xb;
+            bf16x8(&cur)[MT] = (s & 1) ? xb : xa;
+            bf16x8(&nxt)[MT] = (s & 1) ? xa : xb;
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt) nxt[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + cn);
+            for (int mt = 0; mt < MT; ++mt) nxt[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + cn);
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+            for (int mt = 0; mt < MT; ++mt)
                 acc[mt] = SWAP ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[mt], wf[s], acc[mt], 0, 0, 0)
                                : __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s], cur[mt], acc[mt], 0, 0, 0);
             wf[s] = ld16(wrow + min(ks + 4, 15) * step);
@@ -71,13 +73,15 @@ __device__ __forceinline__ void proj_gemm(const bf16_t* __restrict__ wrow, size_
     }
 }
 
-template <bool SELF>
+// MT 32-token m-tiles per workgroup (R = 32 MT tokens; default 2, see mlg_lg_proj).
+template <bool SELF, int MT>
 __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcopy, int ldx,
                                                 const bf16_t* __restrict__ W, const float* __restrict__ bias,
                                                 const float* __restrict__ ecos, const float* __restrict__ esin,
                                                 const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
                                                 bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad) {
     constexpr int N = SELF ? 768 : 512;
+    constexpr int R = 32 * MT;
     __shared__ __attribute__((aligned(16))) char lds[R * ROWB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
     // 1-D grid, dealt so the parts (q, k, v / qk, v) of one token tile are consecutive
@@ -87,27 +91,29 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
     constexpr int NPART = SELF ? 3 : 2;
     const int per_xcd = (int)gridDim.x >> 3;
     const int logical = ((int)blockIdx.x & 7) * per_xcd + ((int)blockIdx.x >> 3);
-    if (logical >= (Npad / R) * NPART) return;
+    if (logical >= ((Npad + R - 1) / R) * NPART) return;
     const int m0 = (logical / NPART) * R, part = logical % NPART;
     const bool is_v = part == (SELF ? 2 : 1);
+    const int nrow = min(R, Npad - m0);  // a multiple of 64
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < R / 16; ++i) {
         const int f = i * 512 + tid, row = f >> 5, c = f & 31;
-        *reinterpret_cast<uint4*>(lds + xoff(row, c)) =
-            *reinterpret_cast<const uint4*>(xcopy + (size_t)(m0 + row) * ldx + c * 8);
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (row < nrow) v = *reinterpret_cast<const uint4*>(xcopy + (size_t)(m0 + row) * ldx + c * 8);
+        *reinterpret_cast<uint4*>(lds + xoff(row, c)) = v;
     }
     __syncthreads();
 
     const int nb = 256 * part + 32 * wave;  // first output column (row of W) of this wave
     const bf16_t* wrow = W + (size_t)(nb + col) * 16 + 8 * hh;
-    f32x16 acc[2];
+    f32x16 acc[MT];
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
 
     if (!is_v) {
-        proj_gemm<false>(wrow, (size_t)N * 16, lds, acc);
+        proj_gemm<false, MT>(wrow, (size_t)N * 16, lds, acc);
         __syncthreads();  // every wave has read the x tile
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -115,8 +121,8 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
             const int h = n >> 6, d = n & 63;
             const float4 b = *reinterpret_cast<const float4*>(bias + 256 * part + n);
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                const int r = 32 * mt + col, m = m0 + r;
+            for (int mt = 0; mt < MT; ++mt) {
+                const int r = 32 * mt + col, m = min(m0 + r, Npad - 1);  // rows >= Npad: never stored
                 const f32x16& a = acc[mt];
                 float x0 = a[4 * g] + b.x, x1 = a[4 * g + 1] + b.y, x2 = a[4 * g + 2] + b.z, x3 = a[4 * g + 3] + b.w;
                 if (SELF) {  // t * cos + rotate_half(t) * sin, uncontracted as torch
@@ -137,37 +143,40 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
                 }
                 uint2 o = make_uint2(0u, 0u);
                 if (live[m]) o = make_uint2(pack_bf16x2(x0, x1), pack_bf16x2(x2, x3));
-                *reinterpret_cast<uint2*>(lds + stage_off(h, r, d)) = o;
+                *reinterpret_cast<uint2*>(lds + stage_off<R>(h, r, d)) = o;
             }
         }
     } else {
-        proj_gemm<true>(wrow, (size_t)N * 16, lds, acc);
+        proj_gemm<true, MT>(wrow, (size_t)N * 16, lds, acc);
         __syncthreads();  // every wave has read the x tile
         const int n = 32 * wave + col, h = n >> 6, d = n & 63;
         const float b = bias[256 * part + n];
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                const int m = m0 + 32 * mt + 8 * g + 4 * hh;  // 4 consecutive tokens
+            for (int mt = 0; mt < MT; ++mt) {
+                const int r = 32 * mt + 8 * g + 4 * hh, m = m0 + r;  // 4 consecutive tokens
                 const f32x16& a = acc[mt];
-                const uint32_t lv = *reinterpret_cast<const uint32_t*>(live + m);
+                const uint32_t lv = r < nrow ? *reinterpret_cast<const uint32_t*>(live + m) : 0u;
                 const float v0 = (lv & 0xff) ? a[4 * g] + b : 0.f;
                 const float v1 = (lv & 0xff00) ? a[4 * g + 1] + b : 0.f;
                 const float v2 = (lv & 0xff0000) ? a[4 * g + 2] + b : 0.f;
                 const float v3 = (lv >> 24) ? a[4 * g + 3] + b : 0.f;
-                *reinterpret_cast<uint2*>(lds + stage_off(h, d, m & 63)) =
+                // V^T staging rows: (64-key block of the tile) * 64 + d
+                *reinterpret_cast<uint2*>(lds + stage_off<R>(h, (r >> 6) * 64 + d, r & 63)) =
                     make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
             }
     }
     __syncthreads();
-    // copy-out: per head one contiguous [64 rows][64] block at (h * Npad + m0) * 64
+    // copy-out: per head one contiguous [R rows][64] block at (h * Npad + m0) * 64 (for
+    // V^T the R / 64 tiled [64 d][64 keys] blocks of the tile's keys, also contiguous)
     bf16_t* dst = is_v ? Vt : (part == 0 ? Q : K);
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const int L = p * 512 + tid, h = L >> 9, row = (L >> 3) & 63, c = L & 7;
-        *reinterpret_cast<uint4*>(dst + ((size_t)h * Npad + m0 + row) * 64 + c * 8) =
-            *reinterpret_cast<const uint4*>(lds + stage_off(h, row, 8 * c));
+    for (int p = 0; p < R / 16; ++p) {
+        const int L = p * 512 + tid, h = L / (8 * R), row = (L >> 3) % R, c = L & 7;
+        if (row < nrow)
+            *reinterpret_cast<uint4*>(dst + ((size_t)h * Npad + m0 + row) * 64 + c * 8) =
+                *reinterpret_cast<const uint4*>(lds + stage_off<R>(h, row, 8 * c));
     }
 }
 
@@ -175,14 +184,31 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
 
 int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,
                 const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s) {
-    if (Npad <= 0 || (Npad % R) || ldx < 256 || (ldx % 8)) return MLG_EINVAL;
-    const unsigned grid = (unsigned)((((long)(Npad / R) * (self_block ? 3 : 2)) + 7) & ~7L);
+    if (Npad <= 0 || (Npad % 64) || ldx < 256 || (ldx % 8)) return MLG_EINVAL;
+    // A/B knob: MLG_PROJ_MT = 32-token m-tiles per workgroup (2: 64 tokens, 4: 128).
+    // 128-token tiles halve the weight bytes per FLOP but measured 2-7 % slower on one
+    // box (tools/gpu_ab_ffn_proj.sh: self 2.39 vs 2.35 ms, cross 1.27 vs 1.19 ms at 2 M
+    // tokens): the weight stream is not what bounds this kernel.
+    static const int mt = [] {
+        const char* v = getenv("MLG_PROJ_MT");
+        return v && atoi(v) == 4 ? 4 : 2;
+    }();
+    const int R = 32 * mt;
+    const unsigned grid = (unsigned)((((long)((Npad + R - 1) / R) * (self_block ? 3 : 2)) + 7) & ~7L);
     if (self_block) {
-        hipLaunchKernelGGL(k_lg_proj<true>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin, live, Q, K,
-                           Vt, Npad);
+        if (mt == 4)
+            hipLaunchKernelGGL((k_lg_proj<true, 4>), dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin,
+                               live, Q, K, Vt, Npad);
+        else
+            hipLaunchKernelGGL((k_lg_proj<true, 2>), dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin,
+                               live, Q, K, Vt, Npad);
     } else {
-        hipLaunchKernelGGL(k_lg_proj<false>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, (const float*)nullptr,
-                           (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad);
+        if (mt == 4)
+            hipLaunchKernelGGL((k_lg_proj<false, 4>), dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias,
+                               (const float*)nullptr, (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad);
+        else
+            hipLaunchKernelGGL((k_lg_proj<false, 2>), dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias,
+                               (const float*)nullptr, (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad);
     }
     MLG_LAUNCH_CHECK();
     return MLG_OK;

@@ -17,14 +17,16 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_SO) or os.path.getmtime(_SO) < os.path.getmtime(
-                os.path.join(_HERE, "csrc", "oracle.c")):
+        if not os.path.exists(_SO) or os.path.getmtime(_SO) < max(
+                os.path.getmtime(os.path.join(_HERE, "csrc", f)) for f in ("oracle.c", "orb.c")):
             build()
         _lib = ctypes.CDLL(_SO)
         _lib.orc_resize_linear_u8.restype = ctypes.c_int
         _lib.orc_resize_vec_end.restype = ctypes.c_int
         _lib.orc_row_norms_f32.restype = ctypes.c_int
         _lib.orc_knn_rows.restype = ctypes.c_int
+        _lib.orc_orb_detect.restype = ctypes.c_int
+        _lib.orc_bf_match.restype = ctypes.c_int
     return _lib
 
 
