@@ -416,6 +416,41 @@ int mlg_prof_read(int slot, double* total_ms, long* launches);
 int mlg_prof_read_work(int slot, double* flops);
 
 
+/* ------------------------------------------------------ ORB + BFMatcher fallback --
+ * LightGlue._load_fallback / _detect_and_match_fallback (geometric_verification.py:
+ * 244-248, 314-350): cv2.ORB_create(nfeatures).detectAndCompute on BGR2GRAY frames and
+ * cv2.BFMatcher(NORM_HAMMING, crossCheck=True).match sorted by distance, for a batch of
+ * frames / pairs.  The ORB geometry (OpenCV ORB_Impl defaults: 8 levels x 1.2, edge 31,
+ * FAST threshold 20, patch 31) is computed by the caller (mlgate/orb.py) into a HOST
+ * mlg_orb_params; `pattern` is a device int16 [256 pairs][2 points][x, y] point table
+ * (OpenCV's bit_pattern_31_ or, by default, its makeRandomPattern(31) stream).
+ * Outputs per frame f, slots [f * max_kp, f * max_kp + counts[f]): keypoints (x, y) in
+ * level-0 pixels, Harris responses, angles (degrees), levels, 32-byte descriptors, in
+ * level order and within a level by (response desc, y, x).  counts[f] < 0: a per-level
+ * candidate list overflowed (not expected below 16 M-pixel frames).
+ */
+#define MLG_ORB_LEVELS 8
+typedef struct mlg_orb_params {
+    int level_w[MLG_ORB_LEVELS], level_h[MLG_ORB_LEVELS];
+    int level_features[MLG_ORB_LEVELS]; /* nfeaturesPerLevel */
+    int level_vec_end[MLG_ORB_LEVELS];  /* cv2.resize SIMD/scalar split of each level row */
+    float level_scale[MLG_ORB_LEVELS];
+    int umax[16];
+    int gauss[7]; /* 7-tap Gaussian, 8 fractional bits, sum 256 */
+    int fast_threshold, edge_threshold;
+} mlg_orb_params;
+size_t mlg_orb_workspace_bytes(const mlg_orb_params* p, int F, int H, int W, int max_kp);
+int mlg_orb_detect(const mlg_orb_params* p, const int16_t* pattern, const uint8_t* frames, long frame_stride, int F,
+                   int H, int W, int C, int max_kp, void* ws, size_t ws_bytes, float* keypoints, float* responses,
+                   float* angles, int32_t* levels, uint8_t* descriptors, int32_t* counts, void* stream);
+/* Cross-checked nearest neighbours of frames pair_a[p] -> pair_b[p] (descriptors /
+ * counts as mlg_orb_detect wrote them), sorted by distance, ties by query index:
+ * slots [p * max_kp, p * max_kp + nmatch[p]) of query_idx / train_idx / distance. */
+size_t mlg_orb_match_workspace_bytes(int P, int max_kp);
+int mlg_orb_match(const uint8_t* descriptors, const int32_t* counts, int max_kp, const int32_t* pair_a,
+                  const int32_t* pair_b, int P, void* ws, size_t ws_bytes, int32_t* query_idx, int32_t* train_idx,
+                  int32_t* distance, int32_t* nmatch, void* stream);
+
 /* ---------------------------------------------------------- keyframe ingestion --
  * HOST pointers (not device): PNG keyframes -> BGR uint8 [n, H, W, 3], replacing the
  * cv2.imread(path) of process_image_sequence (place_recognition.py:965-968) on the

@@ -585,6 +585,74 @@ std::tuple<double, int64_t, double> prof_read(int64_t slot) {
 }
 
 
+// ------------------------------------------------------------------ ORB fallback
+// iparams: int32 [57] = level_w[8], level_h[8], level_features[8], level_vec_end[8],
+// umax[16], gauss[7], fast_threshold, edge_threshold; scales: float32 [8] (host tensors)
+mlg_orb_params orb_params(const Tensor& ip, const Tensor& sc) {
+    want(ip, at::kInt, "orb iparams", false);
+    want(sc, at::kFloat, "orb scales", false);
+    TORCH_CHECK(ip.numel() == 57 && sc.numel() == MLG_ORB_LEVELS, "orb params: expected 57 ints and 8 scales");
+    const int32_t* v = ip.data_ptr<int32_t>();
+    mlg_orb_params p;
+    std::memset(&p, 0, sizeof(p));
+    for (int l = 0; l < MLG_ORB_LEVELS; ++l) {
+        p.level_w[l] = v[l];
+        p.level_h[l] = v[8 + l];
+        p.level_features[l] = v[16 + l];
+        p.level_vec_end[l] = v[24 + l];
+        p.level_scale[l] = sc.data_ptr<float>()[l];
+    }
+    for (int i = 0; i < 16; ++i) p.umax[i] = v[32 + i];
+    for (int i = 0; i < 7; ++i) p.gauss[i] = v[48 + i];
+    p.fast_threshold = v[55];
+    p.edge_threshold = v[56];
+    return p;
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> orb_detect(Tensor frames, Tensor pattern, Tensor iparams,
+                                                                      Tensor scales, int64_t max_kp) {
+    want(frames, at::kByte, "frames");
+    want(pattern, at::kShort, "pattern");
+    TORCH_CHECK(frames.dim() == 4, "frames: [F, H, W, C] uint8");
+    TORCH_CHECK(pattern.numel() == 1024, "pattern: 256 pairs x 2 points x (x, y)");
+    const c10::DeviceGuard guard(frames.device());
+    const mlg_orb_params p = orb_params(iparams, scales);
+    const int F = (int)frames.size(0), H = (int)frames.size(1), W = (int)frames.size(2), C = (int)frames.size(3);
+    const size_t wsb = mlg_orb_workspace_bytes(&p, F, H, W, (int)max_kp);
+    TORCH_CHECK(wsb > 0, "orb_detect: invalid geometry");
+    Tensor ws = workspace(wsb, frames);
+    auto o = frames.options();
+    Tensor kp = at::empty({F, max_kp, 2}, o.dtype(at::kFloat)), resp = at::empty({F, max_kp}, o.dtype(at::kFloat));
+    Tensor ang = at::empty({F, max_kp}, o.dtype(at::kFloat)), lev = at::empty({F, max_kp}, o.dtype(at::kInt));
+    Tensor desc = at::zeros({F, max_kp, 32}, o), cnt = at::empty({F}, o.dtype(at::kInt));
+    check_rc(mlg_orb_detect(&p, cp<int16_t>(pattern), cp<uint8_t>(frames), (long)H * W * C, F, H, W, C, (int)max_kp,
+                            mp<void>(ws), wsb, mp<float>(kp), mp<float>(resp), mp<float>(ang), mp<int32_t>(lev),
+                            mp<uint8_t>(desc), mp<int32_t>(cnt), stream_of(frames)),
+             "mlg_orb_detect");
+    return {kp, resp, ang, lev, desc, cnt};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> orb_match(Tensor desc, Tensor counts, Tensor pair_a, Tensor pair_b) {
+    want(desc, at::kByte, "descriptors");
+    want(counts, at::kInt, "counts");
+    want(pair_a, at::kInt, "pair_a");
+    want(pair_b, at::kInt, "pair_b");
+    TORCH_CHECK(desc.dim() == 3 && desc.size(2) == 32, "descriptors: [F, max_kp, 32]");
+    const c10::DeviceGuard guard(desc.device());
+    const int P = (int)pair_a.numel(), K = (int)desc.size(1);
+    TORCH_CHECK(pair_b.numel() == P, "pair_a / pair_b sizes differ");
+    auto o = desc.options().dtype(at::kInt);
+    Tensor q = at::empty({P, K}, o), t = at::empty({P, K}, o), d = at::empty({P, K}, o), n = at::zeros({P}, o);
+    if (P == 0) return {q, t, d, n};
+    const size_t wsb = mlg_orb_match_workspace_bytes(P, K);
+    Tensor ws = workspace(wsb, desc);
+    check_rc(mlg_orb_match(cp<uint8_t>(desc), cp<int32_t>(counts), K, cp<int32_t>(pair_a), cp<int32_t>(pair_b), P,
+                           mp<void>(ws), wsb, mp<int32_t>(q), mp<int32_t>(t), mp<int32_t>(d), mp<int32_t>(n),
+                           stream_of(desc)),
+             "mlg_orb_match");
+    return {q, t, d, n};
+}
+
 // ------------------------------------------------------------ keyframe ingestion
 // Host ops (CPU key): the decoders write a caller-owned host tensor, normally a pinned
 // staging buffer that mlgate.ingest uploads on a side stream.
@@ -646,6 +714,9 @@ TORCH_LIBRARY(mlgate, m) {
           "-> (Tensor, Tensor, Tensor)");
     m.def("proximity(Tensor pos, Tensor? floor, int row0, int nrows, float radius, int min_gap, bool strict) "
           "-> (Tensor, Tensor, Tensor, Tensor)");
+    m.def("orb_detect(Tensor frames, Tensor pattern, Tensor iparams, Tensor scales, int max_kp) "
+          "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
+    m.def("orb_match(Tensor desc, Tensor counts, Tensor pair_a, Tensor pair_b) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("png_load_into(str[] paths, Tensor(a!) out, int H, int W, int threads) -> Tensor");
     m.def("png_decode(Tensor[] blobs, int H, int W, int threads) -> (Tensor, Tensor)");
     m.def("prof_enable(int mask) -> int");
@@ -671,6 +742,8 @@ TORCH_LIBRARY_IMPL(mlgate, CUDA, m) {
     m.impl("pillow_resize_224", &pillow_resize_224);
     m.impl("plane_ransac", &plane_ransac);
     m.impl("proximity", &proximity);
+    m.impl("orb_detect", &orb_detect);
+    m.impl("orb_match", &orb_match);
 }
 
 TORCH_LIBRARY_IMPL(mlgate, CPU, m) {

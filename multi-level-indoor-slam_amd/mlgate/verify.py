@@ -98,6 +98,13 @@ class LightGlue(BaseFeatureMatcher):
     def _load_model(self):
         if self._model_loaded:
             return
+        if os.environ.get("MLGATE_LIGHTGLUE_FALLBACK", "").lower() in ("1", "orb"):
+            # the reference's ImportError branch (:237-242), selected explicitly: the
+            # GPU SuperPoint + LightGlue are always available here
+            warnings.warn("LightGlue not installed. Using ORB+BFMatcher fallback. "
+                          "Install with: pip install git+https://github.com/cvg/LightGlue.git")
+            self._load_fallback()
+            return
         from .lightglue import LightGlueGPU
         from .superpoint import SuperPointGPU
         self.extractor = SuperPointGPU(device=self.device, max_num_keypoints=self.max_keypoints,
@@ -111,8 +118,62 @@ class LightGlue(BaseFeatureMatcher):
         self._model_loaded = True
         self._is_native = True
 
+    def _load_fallback(self):
+        """cv2.ORB_create(nfeatures=max_keypoints) + BFMatcher(NORM_HAMMING, crossCheck)
+        (:244-248) as the GPU ORB (mlgate.orb, csrc/orb.hip)."""
+        from .orb import OrbGPU
+        self.orb = OrbGPU(device=self.device, nfeatures=self.max_keypoints)
+        self.bf = self.orb
+        self._model_loaded = True
+        self._is_native = False
+
+    def _detect_and_match_fallback(self, image1: np.ndarray, image2: np.ndarray):
+        """:314-350 -- ORB on both frames, cross-checked Hamming matches sorted by distance,
+        confidence 1 - distance / max distance."""
+        return self._fallback_pairs([image1, image2], [(0, 1)])[0]
+
+    def _fallback_pairs(self, images, pairs):
+        if not hasattr(self, "orb"):
+            self._load_fallback()
+        frames = [np.asarray(im) for im in images]
+        groups = {}
+        for i, f in enumerate(frames):
+            groups.setdefault(f.shape, []).append(i)
+        feats = {}
+        for shape, idx in groups.items():  # one launch sequence per frame size
+            batch = torch.from_numpy(np.ascontiguousarray(np.stack([frames[i] for i in idx]))).to(self.orb.device)
+            if batch.dim() == 3:
+                batch = batch.unsqueeze(-1)
+            kp, _, _, _, ds, cnt = self.orb.detect_device(batch)
+            for j, i in enumerate(idx):
+                feats[i] = (kp[j], ds[j], cnt[j])
+        return self._match_feats(feats, pairs)
+
+    def _match_feats(self, feats, pairs):
+        out = []
+        for a, b in pairs:
+            ka, da, na = feats[a]
+            kb, db, nb = feats[b]
+            n1, n2 = int(na), int(nb)
+            if n1 == 0 or n2 == 0 or n1 < 5 or n2 < 5:
+                out.append((np.array([]), np.array([]), np.array([])))
+                continue
+            desc = torch.stack([da, db])
+            cnt = torch.tensor([n1, n2], dtype=torch.int32, device=desc.device)
+            q, t, d, n = self.orb.match_device(desc, cnt, [0], [1])
+            m = int(n[0])
+            q, t, d = q[0, :m].cpu().numpy(), t[0, :m].cpu().numpy(), d[0, :m].cpu().numpy()
+            k1, k2 = ka.cpu().numpy(), kb.cpu().numpy()
+            m1 = np.array([k1[i].tolist() for i in q])
+            m2 = np.array([k2[j].tolist() for j in t])
+            max_dist = max(float(x) for x in d) if m else 1
+            out.append((m1, m2, np.array([1 - float(x) / max_dist for x in d])))
+        return out
+
     def detect_and_match(self, image1: np.ndarray, image2: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         self._load_model()
+        if not getattr(self, "_is_native", False):
+            return self._detect_and_match_fallback(image1, image2)
         if np.shape(image1) == np.shape(image2):
             f1, f2 = self.extractor.extract([image1, image2])
         else:
@@ -129,6 +190,12 @@ class LightGlue(BaseFeatureMatcher):
         pairs = list(pairs)
         if not pairs:
             return []
+        if not getattr(self, "_is_native", False):  # ORB fallback: one detect over the used frames
+            used = sorted({i for p in pairs for i in p})
+            sel = frames[torch.as_tensor(used, device=frames.device)]
+            kp, _, _, _, ds, cnt = self.orb.detect_device(sel)
+            feats = {f: (kp[j], ds[j], cnt[j]) for j, f in enumerate(used)}
+            return self._match_feats(feats, pairs)
         used = sorted({i for p in pairs for i in p})
         pos = {f: j for j, f in enumerate(used)}
         sel = frames[torch.as_tensor(used, device=frames.device)] if len(used) < frames.shape[0] else frames
