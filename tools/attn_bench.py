@@ -9,6 +9,7 @@ error of two sampled tasks against a float32 torch restatement.
 """
 import argparse
 import json
+import math
 import os
 import sys
 
@@ -34,6 +35,8 @@ def main():
     ap.add_argument("--len", type=int, default=2048)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--ragged", action="store_true")
+    ap.add_argument("--exp2", action="store_true",
+                    help="q in exp2 units (x log2(e) / 8, as lg_proj writes it for the current kernel)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     L = _native.lib()
@@ -45,7 +48,8 @@ def main():
     Qf = torch.randn(H, Npad, 64, device=dev, generator=g)
     Kf = torch.randn(H, Npad, 64, device=dev, generator=g)
     Vf = torch.randn(H, Npad, 64, device=dev, generator=g)
-    Q, K, Vt = Qf.to(torch.bfloat16), Kf.to(torch.bfloat16), tile_vt(Vf, Npad)
+    qs = math.log2(math.e) / 8.0 if args.exp2 else 1.0
+    Q, K, Vt = (Qf * qs).to(torch.bfloat16), Kf.to(torch.bfloat16), tile_vt(Vf, Npad)
     O = torch.zeros(Npad, H * 64, dtype=torch.bfloat16, device=dev)
     res = {"pairs": args.pairs, "len": args.len, "ragged": args.ragged}
     for kind in ("self", "cross"):
@@ -80,7 +84,8 @@ def main():
             q = Q[:, qo:qo + ql].float()
             k = K[:, ko:ko + kl].float()
             v = Vt.float().transpose(2, 3).reshape(H, Npad, 64)[:, ko:ko + kl]
-            ref = torch.softmax(q @ k.transpose(1, 2) / 8.0, -1) @ v
+            sc = q @ k.transpose(1, 2) * (math.log(2.0) if args.exp2 else 0.125)
+            ref = torch.softmax(sc, -1) @ v
             got = O[int(outs[ti]):int(outs[ti]) + ql].float().view(ql, H, 64).transpose(0, 1)
             err = max(err, float((got - ref).abs().max()))
         res[kind] = {"ms": round(ms, 3), "tflops": round(flops / ms / 1e9, 1), "max_abs_err": err}
