@@ -18,6 +18,8 @@
 // stores.  Same fragments, operand order only.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -73,6 +75,83 @@ __device__ __forceinline__ void proj_gemm(const bf16_t* __restrict__ wrow, size_
     }
 }
 
+// Bias (+ rotary), live-row mask, staging through the dead x tile `lds` and the
+// coalesced copy-out of one R-token tile of part `part` (the caller has barriered after
+// the GEMM's last LDS read).
+// FAC_LDS: the tile's rotary factors sit in LDS at `ecos` / `esin` as [R tokens][32]
+// (resident form) instead of the global [Npad][32] tables.
+template <bool SELF, int MT, bool FAC_LDS = false>
+__device__ __forceinline__ void proj_epilogue(const f32x16 (&acc)[MT], bool is_v, int part, int m0, int nrow,
+                                              char* lds, const float* __restrict__ bias,
+                                              const float* __restrict__ ecos, const float* __restrict__ esin,
+                                              const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
+                                              bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad) {
+    constexpr int R = 32 * MT;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
+    if (!is_v) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = 32 * wave + 8 * g + 4 * hh;  // column within the part
+            const int h = n >> 6, d = n & 63;
+            const float4 b = *reinterpret_cast<const float4*>(bias + 256 * part + n);
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                const int r = 32 * mt + col, m = min(m0 + r, Npad - 1);  // rows >= Npad: never stored
+                const f32x16& a = acc[mt];
+                float x0 = a[4 * g] + b.x, x1 = a[4 * g + 1] + b.y, x2 = a[4 * g + 2] + b.z, x3 = a[4 * g + 3] + b.w;
+                if (SELF) {  // t * cos + rotate_half(t) * sin, uncontracted as torch
+                    // (cos, sin) of frequencies d/2, d/2 + 1, read after the GEMM (held
+                    // across it they cost 32 VGPRs = one workgroup per CU less) straight
+                    // from global: an LDS-staged copy of the tile's factors gave run-to-run
+                    // different q / k on gfx950 (unexplained; tests/test_kernels_gpu.py::
+                    // test_lightglue_kernels_deterministic)
+                    const size_t eo = (size_t)(FAC_LDS ? r : m) * 32 + (n & 63) / 2;
+                    const float2 rc = *reinterpret_cast<const float2*>(ecos + eo);
+                    const float2 rs = *reinterpret_cast<const float2*>(esin + eo);
+                    const float2 e0 = make_float2(rc.x, rs.x), e1 = make_float2(rc.y, rs.y);
+                    const float r0 = __fadd_rn(__fmul_rn(x0, e0.x), __fmul_rn(-x1, e0.y));
+                    const float r1 = __fadd_rn(__fmul_rn(x1, e0.x), __fmul_rn(x0, e0.y));
+                    const float r2 = __fadd_rn(__fmul_rn(x2, e1.x), __fmul_rn(-x3, e1.y));
+                    const float r3 = __fadd_rn(__fmul_rn(x3, e1.x), __fmul_rn(x2, e1.y));
+                    x0 = r0; x1 = r1; x2 = r2; x3 = r3;
+                }
+                uint2 o = make_uint2(0u, 0u);
+                if (live[m]) o = make_uint2(pack_bf16x2(x0, x1), pack_bf16x2(x2, x3));
+                *reinterpret_cast<uint2*>(lds + stage_off<R>(h, r, d)) = o;
+            }
+        }
+    } else {
+        const int n = 32 * wave + col, h = n >> 6, d = n & 63;
+        const float b = bias[256 * part + n];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+                const int r = 32 * mt + 8 * g + 4 * hh, m = m0 + r;  // 4 consecutive tokens
+                const f32x16& a = acc[mt];
+                const uint32_t lv = r < nrow ? *reinterpret_cast<const uint32_t*>(live + m) : 0u;
+                const float v0 = (lv & 0xff) ? a[4 * g] + b : 0.f;
+                const float v1 = (lv & 0xff00) ? a[4 * g + 1] + b : 0.f;
+                const float v2 = (lv & 0xff0000) ? a[4 * g + 2] + b : 0.f;
+                const float v3 = (lv >> 24) ? a[4 * g + 3] + b : 0.f;
+                // V^T staging rows: (64-key block of the tile) * 64 + d
+                *reinterpret_cast<uint2*>(lds + stage_off<R>(h, (r >> 6) * 64 + d, r & 63)) =
+                    make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+            }
+    }
+    __syncthreads();
+    // copy-out: per head one contiguous [R rows][64] block at (h * Npad + m0) * 64 (for
+    // V^T the R / 64 tiled [64 d][64 keys] blocks of the tile's keys, also contiguous)
+    bf16_t* dst = is_v ? Vt : (part == 0 ? Q : K);
+#pragma unroll
+    for (int p = 0; p < R / 16; ++p) {
+        const int L = p * 512 + tid, h = L / (8 * R), row = (L >> 3) % R, c = L & 7;
+        if (row < nrow)
+            *reinterpret_cast<uint4*>(dst + ((size_t)h * Npad + m0 + row) * 64 + c * 8) =
+                *reinterpret_cast<const uint4*>(lds + stage_off<R>(h, row, 8 * c));
+    }
+}
+
 // MT 32-token m-tiles per workgroup (R = 32 MT tokens; default 2, see mlg_lg_proj).
 template <bool SELF, int MT>
 __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcopy, int ldx,
@@ -114,69 +193,119 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
 
     if (!is_v) {
         proj_gemm<false, MT>(wrow, (size_t)N * 16, lds, acc);
-        __syncthreads();  // every wave has read the x tile
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int n = 32 * wave + 8 * g + 4 * hh;  // column within the part
-            const int h = n >> 6, d = n & 63;
-            const float4 b = *reinterpret_cast<const float4*>(bias + 256 * part + n);
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                const int r = 32 * mt + col, m = min(m0 + r, Npad - 1);  // rows >= Npad: never stored
-                const f32x16& a = acc[mt];
-                float x0 = a[4 * g] + b.x, x1 = a[4 * g + 1] + b.y, x2 = a[4 * g + 2] + b.z, x3 = a[4 * g + 3] + b.w;
-                if (SELF) {  // t * cos + rotate_half(t) * sin, uncontracted as torch
-                    // (cos, sin) of frequencies d/2, d/2 + 1, read after the GEMM (held
-                    // across it they cost 32 VGPRs = one workgroup per CU less) straight
-                    // from global: an LDS-staged copy of the tile's factors gave run-to-run
-                    // different q / k on gfx950 (unexplained; tests/test_kernels_gpu.py::
-                    // test_lightglue_kernels_deterministic)
-                    const size_t eo = (size_t)m * 32 + (n & 63) / 2;
-                    const float2 rc = *reinterpret_cast<const float2*>(ecos + eo);
-                    const float2 rs = *reinterpret_cast<const float2*>(esin + eo);
-                    const float2 e0 = make_float2(rc.x, rs.x), e1 = make_float2(rc.y, rs.y);
-                    const float r0 = __fadd_rn(__fmul_rn(x0, e0.x), __fmul_rn(-x1, e0.y));
-                    const float r1 = __fadd_rn(__fmul_rn(x1, e0.x), __fmul_rn(x0, e0.y));
-                    const float r2 = __fadd_rn(__fmul_rn(x2, e1.x), __fmul_rn(-x3, e1.y));
-                    const float r3 = __fadd_rn(__fmul_rn(x3, e1.x), __fmul_rn(x2, e1.y));
-                    x0 = r0; x1 = r1; x2 = r2; x3 = r3;
-                }
-                uint2 o = make_uint2(0u, 0u);
-                if (live[m]) o = make_uint2(pack_bf16x2(x0, x1), pack_bf16x2(x2, x3));
-                *reinterpret_cast<uint2*>(lds + stage_off<R>(h, r, d)) = o;
-            }
-        }
     } else {
         proj_gemm<true, MT>(wrow, (size_t)N * 16, lds, acc);
-        __syncthreads();  // every wave has read the x tile
-        const int n = 32 * wave + col, h = n >> 6, d = n & 63;
-        const float b = bias[256 * part + n];
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) {
-                const int r = 32 * mt + 8 * g + 4 * hh, m = m0 + r;  // 4 consecutive tokens
-                const f32x16& a = acc[mt];
-                const uint32_t lv = r < nrow ? *reinterpret_cast<const uint32_t*>(live + m) : 0u;
-                const float v0 = (lv & 0xff) ? a[4 * g] + b : 0.f;
-                const float v1 = (lv & 0xff00) ? a[4 * g + 1] + b : 0.f;
-                const float v2 = (lv & 0xff0000) ? a[4 * g + 2] + b : 0.f;
-                const float v3 = (lv >> 24) ? a[4 * g + 3] + b : 0.f;
-                // V^T staging rows: (64-key block of the tile) * 64 + d
-                *reinterpret_cast<uint2*>(lds + stage_off<R>(h, (r >> 6) * 64 + d, r & 63)) =
-                    make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
-            }
     }
-    __syncthreads();
-    // copy-out: per head one contiguous [R rows][64] block at (h * Npad + m0) * 64 (for
-    // V^T the R / 64 tiled [64 d][64 keys] blocks of the tile's keys, also contiguous)
-    bf16_t* dst = is_v ? Vt : (part == 0 ? Q : K);
+    __syncthreads();  // every wave has read the x tile
+    proj_epilogue<SELF, MT>(acc, is_v, part, m0, nrow, lds, bias, ecos, esin, live, Q, K, Vt, Npad);
+}
+
+// ---------------------------------------------------------------- resident form
+// One workgroup (8 waves) per (part, slot) walks token tiles; wave w keeps its 32
+// output columns' weights for all 16 k-steps in registers (64 VGPRs, loaded once), so
+// the GEMM reads only the x tile from LDS and nothing from L2.  The next tile's x rows
+// arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction, XOR swizzle
+// applied to the source addresses) into the other of two buffers while this tile is
+// computed and written.  Grid: per XCD `slots` x NPART workgroups; the parts of one
+// token tile run on one XCD at the same time (tile t -> XCD t % 8), so x is read from
+// HBM once and from that XCD's L2 by the other parts.
+typedef __attribute__((address_space(3))) char lds_char;
+__device__ __forceinline__ unsigned lds_addr(char* p) { return (unsigned)(uintptr_t)(lds_char*)p; }
+__device__ __forceinline__ void dma16(const void* g, unsigned m0) {
+    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
+}
+
+template <bool SWAP>
+__device__ __forceinline__ void res_gemm(const bf16x8 (&wf)[16], const char* lds, f32x16 (&acc)[2]) {
+    const int lane = threadIdx.x & 63, col = lane & 31, hh = lane >> 5;
+    const char* xrow = lds + col * ROWB;
+    const int sw = col & 15;
+    bf16x8 xa[2], xb[2];
 #pragma unroll
-    for (int p = 0; p < R / 16; ++p) {
-        const int L = p * 512 + tid, h = L / (8 * R), row = (L >> 3) % R, c = L & 7;
-        if (row < nrow)
-            *reinterpret_cast<uint4*>(dst + ((size_t)h * Npad + m0 + row) * 64 + c * 8) =
-                *reinterpret_cast<const uint4*>(lds + stage_off<R>(h, row, 8 * c));
+    for (int mt = 0; mt < 2; ++mt) xa[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + ((hh ^ sw) << 4));
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+        bf16x8(&cur)[2] = (ks & 1) ? xb : xa;
+        bf16x8(&nxt)[2] = (ks & 1) ? xa : xb;
+        if (ks < 15) {
+            const int cn = ((2 * (ks + 1) + hh) ^ sw) << 4;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) nxt[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + cn);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+            acc[mt] = SWAP ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[mt], wf[ks], acc[mt], 0, 0, 0)
+                           : __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], cur[mt], acc[mt], 0, 0, 0);
+    }
+}
+
+template <bool SELF>
+__global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ xcopy, int ldx,
+                                                       const bf16_t* __restrict__ W, const float* __restrict__ bias,
+                                                       const float* __restrict__ ecos,
+                                                       const float* __restrict__ esin,
+                                                       const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
+                                                       bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad,
+                                                       int slots) {
+    constexpr int N = SELF ? 768 : 512, NPART = SELF ? 3 : 2, R = 64;
+    // per buffer: x tile (32 KiB; the output staging image overlays it), then for the
+    // self block the tile's rotary factors cos / sin [64][32] f32 (8 KiB each)
+    constexpr int XB = R * ROWB, BUF = XB + (SELF ? 2 * R * 32 * 4 : 0);
+    __shared__ __attribute__((aligned(16))) char buf0[BUF];
+    __shared__ __attribute__((aligned(16))) char buf1[BUF];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 31, hh = lane >> 5;
+    const int xcd = (int)blockIdx.x & 7, j = (int)blockIdx.x >> 3;
+    const int part = j % NPART, slot = j / NPART;
+    const int ntiles = Npad / R, stride = 8 * slots;
+    int t = xcd + 8 * slot;
+    if (slot >= slots || t >= ntiles) return;
+    const bool is_v = part == NPART - 1;
+    bf16x8 wf[16];
+    {
+        const bf16_t* wrow = W + (size_t)(256 * part + 32 * wave + col) * 16 + 8 * hh;
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) wf[ks] = ld16(wrow + (size_t)ks * N * 16);
+    }
+    // this wave's four 1 KiB DMA pieces of a tile: rows 8 w + 2 i + (lane >> 5), slot lane & 31
+    const int drow = 8 * wave + (lane >> 5), dslot = lane & 31;
+    auto issue = [&](int tile, char* buf) {
+        const unsigned base = lds_addr(buf) + 4096 * wave;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = drow + 2 * i;
+            dma16(xcopy + (size_t)(tile * R + row) * ldx + ((dslot ^ (row & 15)) * 8), base + 1024 * i);
+        }
+        if (SELF) {  // 8 KiB of cos and of sin: one 1 KiB piece of each per wave
+            const unsigned fb = lds_addr(buf) + XB + 1024 * wave;
+            const size_t fo = (size_t)tile * R * 32 + 256 * wave + 4 * lane;
+            dma16(ecos + fo, fb);
+            dma16(esin + fo, fb + R * 32 * 4);
+        }
+    };
+    issue(t, buf0);
+    for (int it = 0;; ++it) {
+        char* cur = (it & 1) ? buf1 : buf0;
+        char* nxt = (it & 1) ? buf0 : buf1;
+        // this wave's DMA of tile t has landed: vector-memory operations retire in issue
+        // order, and the only ones issued after that DMA are the previous tile's four
+        // copy-out stores per lane, which may stay in flight (vmcnt counts stores too)
+        if (it == 0) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        else __builtin_amdgcn_s_waitcnt(0x0F74);          // vmcnt(4)
+        __syncthreads();  // ... and every other wave's
+        const int tn = t + stride;
+        if (tn < ntiles) issue(tn, nxt);
+        f32x16 acc[2];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
+        if (is_v) res_gemm<true>(wf, cur, acc);
+        else res_gemm<false>(wf, cur, acc);
+        __syncthreads();  // every wave has read the x tile
+        const float* fc = reinterpret_cast<const float*>(cur + XB);
+        proj_epilogue<SELF, 2, true>(acc, is_v, part, t * R, R, cur, bias, fc, fc + R * 32, live, Q, K, Vt, Npad);
+        if (tn >= ntiles) break;
+        t = tn;
     }
 }
 
@@ -193,6 +322,33 @@ int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, 
         const char* v = getenv("MLG_PROJ_MT");
         return v && atoi(v) == 4 ? 4 : 2;
     }();
+    // default: the weights-resident persistent form; MLG_PROJ_RES=0 selects the tiled form
+    static const int res = [] {
+        const char* v = getenv("MLG_PROJ_RES");
+        return v ? atoi(v) : 1;
+    }();
+    if (res) {
+        static const int cus = [] {
+            int dev = 0, c = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 8)
+                return 256;
+            return c;
+        }();
+        const int npart = self_block ? 3 : 2, ntiles = Npad / 64;
+        // one workgroup per CU (256 VGPRs, 64-96 KiB LDS), `slots` part-groups per XCD
+        const int slots = std::max(1, std::min((cus / 8) / npart, (ntiles + 7) / 8));
+        const unsigned grid = (unsigned)(8 * slots * npart);
+        if (self_block)
+            hipLaunchKernelGGL(k_lg_proj_res<true>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin, live,
+                               Q, K, Vt, Npad, slots);
+        else
+            hipLaunchKernelGGL(k_lg_proj_res<false>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias,
+                               (const float*)nullptr, (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad,
+                               slots);
+        MLG_LAUNCH_CHECK();
+        return MLG_OK;
+    }
     const int R = 32 * mt;
     const unsigned grid = (unsigned)((((long)((Npad + R - 1) / R) * (self_block ? 3 : 2)) + 7) & ~7L);
     if (self_block) {

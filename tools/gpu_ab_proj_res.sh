@@ -1,0 +1,19 @@
+#!/bin/bash
+# Same-box A/B of the LightGlue projections: weights-resident persistent form
+# (MLG_PROJ_RES=1, default) vs the tiled form (MLG_PROJ_RES=0); parity tests first.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_lightglue_gpu.py tests/test_superglue_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/projres_pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/projres_pytest.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+for r in 1 0 1 0; do
+  MLG_PROJ_RES=$r timeout -k 10 120 python3 tools/proj_ab.py --iters 10 > gpurun_out/projres_$r.log 2>&1
+  rc=$?; echo "res=$r rc=$rc $(tail -1 gpurun_out/projres_$r.log | cut -c1-200)"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
+for r in 1 0; do
+  MLG_PROJ_RES=$r timeout -k 10 400 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/projres_bench_$r.log 2>&1
+  rc=$?; echo "bench res=$r rc=$rc"; tail -1 gpurun_out/projres_bench_$r.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['stage_ms_per_step'], d['config']['false_loop_closure_rejections'])"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
