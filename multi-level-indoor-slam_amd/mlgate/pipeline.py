@@ -210,6 +210,15 @@ class DeviceGate:
             self.K = torch.from_numpy(Kc.reshape(9).copy()).to(self.dev) if K is not None else None
         self.last = {}
 
+    def _side_stream(self):
+        """The RANSAC stream (MLGATE_RANSAC_SIDE=0: the main stream, for A/B runs)."""
+        if getattr(self, "_side", None) is None:
+            import os
+            same = os.environ.get("MLGATE_RANSAC_SIDE", "1") == "0"
+            self._side = (self.torch.cuda.current_stream(self.dev) if same
+                          else self.torch.cuda.Stream(device=self.dev))
+        return self._side
+
     def step(self):
         """Gate the sequence once.  Returns this rank's counts (dict of ints): matches,
         the four rejection terms, pairs verified, pairs geometrically valid, accepted."""
@@ -256,26 +265,40 @@ class DeviceGate:
         # can verify any pair; the union of the slices is the global pair list)
         pa_t, pb_t = self.mdist.balanced_pairs(pa_t, pb_t, self.world, self.rank)
         pa, pb = pa_t.cpu().numpy(), pb_t.cpu().numpy()
-        n_valid = gate_rej = 0
+        # RANSAC of chunk c runs on a side stream while LightGlue matches chunk c + 1 on
+        # this one (mlg_lightglue waits on its stream once per layer; the side stream
+        # fills those gaps and the CUs the small RANSAC / assignment grids leave idle)
+        main = torch.cuda.current_stream(self.dev)
+        side = self._side_stream()
+        n_valid_t = torch.zeros((), dtype=torch.int64, device=self.dev)
+        gate_rej_t = torch.zeros((), dtype=torch.int64, device=self.dev)
         for c0 in range(0, len(pa), self.lg_chunk):
             ca, cb = pa[c0:c0 + self.lg_chunk], pb[c0:c0 + self.lg_chunk]
             m, _, n, _ = self.lg.match_device(kp_all, ds_all, counts, ca, cb)
-            # matched keypoints -> one batched RANSAC (+ recoverPose when K is given)
-            P = len(ca)
-            lv = torch.arange(self.kp, device=self.dev)[None, :] < n[:, None]
-            pi, si = torch.nonzero(lv, as_tuple=True)
-            ta = torch.from_numpy(ca).to(self.dev).long()
-            tb = torch.from_numpy(cb).to(self.dev).long()
-            k1 = kp_all[ta[pi], m[pi, si, 0].long()].contiguous()
-            k2 = kp_all[tb[pi], m[pi, si, 1].long()].contiguous()
-            offs = torch.zeros(P + 1, dtype=torch.int32, device=self.dev)
-            offs[1:] = torch.cumsum(n, 0)
-            _, _, inl, _, _ = geometry.epipolar_ransac_device(k1, k2, offs, self.K, 0, 3.0)
-            ratio = inl.double() / n.clamp(min=1).double()
-            ok = (n >= 5) & (inl >= self.min_inliers) & (ratio >= self.min_inlier_ratio)
-            n_valid += int(ok.sum())
-            # the floor gate on the geometrically valid pairs
-            gate_rej += int((ok & ((self.f_all[ta] - self.f_all[tb]).abs() > self.limit)).sum())
+            ready = torch.cuda.Event()
+            ready.record(main)
+            with torch.cuda.stream(side):
+                side.wait_event(ready)
+                m.record_stream(side)
+                n.record_stream(side)
+                # matched keypoints -> one batched RANSAC (+ recoverPose when K is given)
+                P = len(ca)
+                lv = torch.arange(self.kp, device=self.dev)[None, :] < n[:, None]
+                pi, si = torch.nonzero(lv, as_tuple=True)
+                ta = torch.from_numpy(ca).to(self.dev).long()
+                tb = torch.from_numpy(cb).to(self.dev).long()
+                k1 = kp_all[ta[pi], m[pi, si, 0].long()].contiguous()
+                k2 = kp_all[tb[pi], m[pi, si, 1].long()].contiguous()
+                offs = torch.zeros(P + 1, dtype=torch.int32, device=self.dev)
+                offs[1:] = torch.cumsum(n, 0)
+                _, _, inl, _, _ = geometry.epipolar_ransac_device(k1, k2, offs, self.K, 0, 3.0)
+                ratio = inl.double() / n.clamp(min=1).double()
+                ok = (n >= 5) & (inl >= self.min_inliers) & (ratio >= self.min_inlier_ratio)
+                n_valid_t += ok.sum()
+                # the floor gate on the geometrically valid pairs
+                gate_rej_t += (ok & ((self.f_all[ta] - self.f_all[tb]).abs() > self.limit)).sum()
+        main.wait_stream(side)
+        n_valid, gate_rej = int(n_valid_t), int(gate_rej_t)
         out["pairs_verified"] = len(pa)
         out["verified_valid"] = n_valid
         out["verifier_invalid"] = len(pa) - n_valid
