@@ -69,6 +69,30 @@ def imread(path) -> Optional[np.ndarray]:
     return out[0].numpy() if st[0] == 0 else None
 
 
+def jpeg_reader():
+    """A ``path -> BGR uint8 [H, W, 3] or None`` JPEG reader: cv2.imread when OpenCV is
+    installed (the reference's call), else Pillow (the same libjpeg-turbo decoder with
+    OpenCV's defaults: islow IDCT, fancy upsampling), converted to RGB and channel-swapped.
+    Raises the reference's ImportError when neither is available."""
+    try:
+        import cv2
+        return lambda p: cv2.imread(str(p))
+    except ImportError:
+        pass
+    try:
+        from PIL import Image
+    except ImportError as e:
+        raise ImportError("OpenCV is required for image loading. Install with: pip install opencv-python") from e
+
+    def read(p):
+        try:
+            with Image.open(p) as im:
+                return np.ascontiguousarray(np.asarray(im.convert("RGB"))[..., ::-1])
+        except (OSError, ValueError):
+            return None
+    return read
+
+
 class KeyframeStream:
     """Iterate over PNG keyframes in device batches: yields ``(indices, frames)`` with
     ``frames`` a uint8 [b, H, W, 3] BGR tensor on ``device`` and ``indices`` the positions

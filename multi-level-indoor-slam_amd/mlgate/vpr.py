@@ -447,7 +447,8 @@ def process_image_sequence(image_dir: Union[str, Path], timestamps: np.ndarray, 
     PNG keyframes (what bag_utils.extract_images writes) are decoded by the native
     loader (mlgate.ingest: host thread pool -> pinned buffer -> HBM on a side stream)
     and added in device batches; the database, warnings and matches are those of the
-    reference's one-image-at-a-time loop.  *.jpg files still need OpenCV's decoder."""
+    reference's one-image-at-a-time loop.  *.jpg files go through cv2.imread when OpenCV is
+    installed, else through Pillow's libjpeg(-turbo) decode (mlgate.ingest.jpeg_reader)."""
     from . import ingest
     image_dir = Path(image_dir)
     spr = SemanticPlaceRecognition(vpr_method=vpr_method, device=device)
@@ -456,12 +457,9 @@ def process_image_sequence(image_dir: Union[str, Path], timestamps: np.ndarray, 
         warnings.warn(f"Number of images ({len(files)}) != timestamps ({len(timestamps)}). Using minimum of both.")
     n = min(len(files), len(timestamps), len(floor_labels))
     files = files[:n]
-    cv2 = None
+    jpeg_read = None
     if any(f.suffix == '.jpg' for f in files):
-        try:
-            import cv2
-        except ImportError as e:
-            raise ImportError("OpenCV is required for image loading. Install with: pip install opencv-python") from e
+        jpeg_read = ingest.jpeg_reader()  # cv2.imread, else Pillow's libjpeg decode; ImportError if neither
     print(f"Processing {n} images with {vpr_method}...")
     pngs = [i for i, f in enumerate(files) if f.suffix == '.png']
     for idx, frames in ingest.KeyframeStream([files[i] for i in pngs], device=device):
@@ -472,7 +470,7 @@ def process_image_sequence(image_dir: Union[str, Path], timestamps: np.ndarray, 
             if (i + 1) % 100 == 0:
                 print(f"  Processed {i + 1}/{n} images")
     for i in range(len(pngs), n):  # *.jpg files sort after every *.png file
-        img = cv2.imread(str(files[i]))
+        img = jpeg_read(files[i])
         if img is None:
             warnings.warn(f"Failed to load image: {files[i]}")
             continue

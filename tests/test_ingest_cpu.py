@@ -204,3 +204,18 @@ def test_file_loader(tmp_path):
     assert (st == 0).all()
     for i, f in enumerate(frames):
         assert np.array_equal(out[i], f[..., ::-1])
+
+
+def test_jpeg_reader_without_opencv(tmp_path):
+    """*.jpg keyframes: cv2.imread when OpenCV exists, else Pillow's libjpeg decode (BGR)."""
+    yy, xx = np.mgrid[0:40, 0:56]
+    rgb = np.stack([xx * 4, yy * 6, (xx + yy) * 2], -1).astype(np.uint8)  # smooth: JPEG-friendly
+    p = tmp_path / "2.000000.jpg"
+    PIL.fromarray(rgb).save(p, quality=95)
+    read = ingest.jpeg_reader()
+    got = read(p)
+    assert got.shape == (40, 56, 3) and got.dtype == np.uint8
+    assert np.array_equal(got, np.asarray(PIL.open(p).convert("RGB"))[..., ::-1])
+    assert np.abs(got.astype(int) - rgb[..., ::-1]).mean() < 8  # lossy, but the same image
+    (tmp_path / "bad.jpg").write_bytes(b"\xff\xd8 nope")
+    assert read(tmp_path / "bad.jpg") is None
