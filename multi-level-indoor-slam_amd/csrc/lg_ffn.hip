@@ -39,11 +39,7 @@
 
 namespace {
 
-constexpr int R = 64;       // token rows per workgroup
-constexpr int NW = 4;       // waves per workgroup
-constexpr int MT = R / 32;  // 32-row m-tiles
 constexpr int ROWB = 1024;  // LDS bytes per token row: 512 bf16
-constexpr int LDS_CAT = R * ROWB;
 
 // 16-B chunk c of row r at slot c ^ (r & 15): the 16 lanes of each ds_read_b128 lane
 // group (rows {0-3,12-15,20-27} + 32 k, one chunk) then hit 16 distinct bank quads.
@@ -64,7 +60,7 @@ __device__ __forceinline__ float logsigmoid_f(float x) { return fminf(x, 0.f) - 
 // fragments are read one k-step ahead into the other half of a double buffer.  Loads
 // past the last step re-read the last step (no branches, so the waitcnt pass counts
 // the in-flight loads exactly); addresses are recomputed per call, not hoisted.
-template <int NT>
+template <int NT, int MT>
 __device__ __forceinline__ void gemm_phase(const bf16_t* __restrict__ W, int N, int n0, int nkb, int chunk0,
                                            const char* lds, f32x16 (&acc)[NT][MT]) {
     const int lane = threadIdx.x & 63, col = lane & 31, hh = lane >> 5;
@@ -107,7 +103,7 @@ __device__ __forceinline__ void gemm_phase(const bf16_t* __restrict__ W, int N, 
     }
 }
 
-template <int NT>
+template <int NT, int MT>
 __device__ __forceinline__ void zero(f32x16 (&acc)[NT][MT]) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -125,11 +121,14 @@ __device__ __forceinline__ void zero(f32x16 (&acc)[NT][MT]) {
 // gridDim.x; the compiler hoists lane addresses out of the tile loop and spills 436 B
 // per lane around it: 3.66 vs 2.94 ms per 2 M-token launch and 4.29 vs 3.20 s of FFN per
 // bench step on one box (tools/gpu_ab_ffn_proj.sh), so it is off.
-template <bool PERSIST>
-__global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ctx, float* __restrict__ X,
+// R token rows per workgroup of NW waves: <64, 4> (two workgroups per CU) or <128, 8>
+// (one per CU: every weight fragment fetched from L2 feeds twice the MFMAs).
+template <bool PERSIST, int R, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_t* __restrict__ ctx, float* __restrict__ X,
                                                   bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w,
                                                   mlg_lg_conf_i cf, int relu) {
-    __shared__ __attribute__((aligned(16))) char lds[LDS_CAT];
+    constexpr int MT = R / 32, NT1 = 256 / NW / 32, NT2 = 512 / NW / 32, NTH = 64 * NW;
+    __shared__ __attribute__((aligned(16))) char lds[R * ROWB];
     __shared__ float red[2][NW][R];
     // biases and LayerNorm affine, staged in LDS: epilogue reads never wait on VMEM
     // behind the in-flight weight loads
@@ -140,7 +139,7 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
     float* s_lnb = prm + 1280;
     float* s_bf2 = prm + 1792;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
-    for (int i = tid; i < 512; i += 256) {
+    for (int i = tid; i < 512; i += NTH) {
         s_bf1[i] = w.bf1[i];
         s_lng[i] = relu ? 1.f : w.ln_g[i];
         s_lnb[i] = relu ? 0.f : w.ln_b[i];
@@ -156,18 +155,19 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
         //    0..31, ctx into chunks 32..63; 32 lanes x 16 B = one 512-B row per half-wave,
         //    rows clamped to M - 1 (never stored)
         {
-            uint4 rx[8], rc[8];
+            constexpr int PASSES = R / (2 * NW);
+            uint4 rx[PASSES], rc[PASSES];
             const int c = lane & 31;
     #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int row = 8 * i + 2 * wave + hh;
+            for (int i = 0; i < PASSES; ++i) {
+                const int row = 2 * NW * i + 2 * wave + hh;
                 const size_t gr = (size_t)min(m0 + row, M - 1);
                 rx[i] = *reinterpret_cast<const uint4*>(xcopy + gr * ldc + c * 8);
                 rc[i] = *reinterpret_cast<const uint4*>(ctx + gr * 256 + c * 8);
             }
     #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int row = 8 * i + 2 * wave + hh;
+            for (int i = 0; i < PASSES; ++i) {
+                const int row = 2 * NW * i + 2 * wave + hh;
                 *reinterpret_cast<uint4*>(lds + cat_off(row, c)) = rx[i];
                 *reinterpret_cast<uint4*>(lds + cat_off(row, 32 + c)) = rc[i];
             }
@@ -176,15 +176,15 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
 
         // 1. msg = ctx . Wout^T + bout  -> bf16 over the ctx half
         {
-            f32x16 acc[2][MT];
+            f32x16 acc[NT1][MT];
             zero(acc);
-            gemm_phase<2>(w.Wout, 256, 64 * wave, 4, 32, lds, acc);
+            gemm_phase<NT1, MT>(w.Wout, 256, 32 * NT1 * wave, 4, 32, lds, acc);
             __syncthreads();  // every wave has read the ctx half
     #pragma unroll
-            for (int t = 0; t < 2; ++t)
+            for (int t = 0; t < NT1; ++t)
     #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const int n = 64 * wave + 32 * t + 8 * g + 4 * hh;
+                    const int n = 32 * NT1 * wave + 32 * t + 8 * g + 4 * hh;
                     const float4 b = *reinterpret_cast<const float4*>(s_bout + n);
     #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) {
@@ -199,14 +199,14 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
 
         // 2. h = [x | msg] . W1^T + b1; LayerNorm; GELU -> bf16 over [x | msg]
         {
-            f32x16 acc[4][MT];
+            f32x16 acc[NT2][MT];
             zero(acc);
-            gemm_phase<4>(w.Wf1, 512, 128 * wave, 8, 0, lds, acc);
+            gemm_phase<NT2, MT>(w.Wf1, 512, 32 * NT2 * wave, 8, 0, lds, acc);
     #pragma unroll
-            for (int t = 0; t < 4; ++t)
+            for (int t = 0; t < NT2; ++t)
     #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const float4 b = *reinterpret_cast<const float4*>(s_bf1 + 128 * wave + 32 * t + 8 * g + 4 * hh);
+                    const float4 b = *reinterpret_cast<const float4*>(s_bf1 + 32 * NT2 * wave + 32 * t + 8 * g + 4 * hh);
     #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) {
                         acc[t][mt][4 * g] += b.x;
@@ -215,12 +215,14 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
                         acc[t][mt][4 * g + 3] += b.w;
                     }
                 }
-            float mean[MT] = {0.f, 0.f}, rstd[MT] = {1.f, 1.f};
+            float mean[MT], rstd[MT];
+    #pragma unroll
+            for (int mt = 0; mt < MT; ++mt) { mean[mt] = 0.f; rstd[mt] = 1.f; }
     #pragma unroll
             for (int mt = 0; mt < MT && !relu; ++mt) {
                 float sum = 0.f;
     #pragma unroll
-                for (int t = 0; t < 4; ++t)
+                for (int t = 0; t < NT2; ++t)
     #pragma unroll
                     for (int i = 0; i < 16; ++i) sum += acc[t][mt][i];
                 sum += __shfl_xor(sum, 32, 64);
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
                 mean[mt] = sum * (1.0f / 512.0f);
                 float q = 0.f;
     #pragma unroll
-                for (int t = 0; t < 4; ++t)
+                for (int t = 0; t < NT2; ++t)
     #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         const float d = acc[t][mt][i] - mean[mt];
@@ -253,10 +255,10 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
                 rstd[mt] = rsqrtf(q * (1.0f / 512.0f) + 1e-5f);
             }
     #pragma unroll
-            for (int t = 0; t < 4; ++t)
+            for (int t = 0; t < NT2; ++t)
     #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const int n = 128 * wave + 32 * t + 8 * g + 4 * hh;
+                    const int n = 32 * NT2 * wave + 32 * t + 8 * g + 4 * hh;
                     const float4 lg = *reinterpret_cast<const float4*>(s_lng + n);
                     const float4 lb = *reinterpret_cast<const float4*>(s_lnb + n);
     #pragma unroll
@@ -298,15 +300,15 @@ __global__ __launch_bounds__(256, 2) void k_lg_ffn(const bf16_t* __restrict__ ct
             for (int i = 0; i < R / NW; ++i)
                 xr[i] = reinterpret_cast<const float4*>(X + (size_t)min(m0 + wave * (R / NW) + i, M - 1) * 256)[lane];
             __builtin_amdgcn_sched_barrier(0);
-            f32x16 acc[2][MT];
+            f32x16 acc[NT1][MT];
             zero(acc);
-            gemm_phase<2>(w.Wf2, 256, 64 * wave, 8, 0, lds, acc);
+            gemm_phase<NT1, MT>(w.Wf2, 256, 32 * NT1 * wave, 8, 0, lds, acc);
             __syncthreads();  // every wave has read the GELU output
     #pragma unroll
-            for (int t = 0; t < 2; ++t)
+            for (int t = 0; t < NT1; ++t)
     #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const int n = 64 * wave + 32 * t + 8 * g + 4 * hh;
+                    const int n = 32 * NT1 * wave + 32 * t + 8 * g + 4 * hh;
                     const float4 b = *reinterpret_cast<const float4*>(s_bf2 + n);
     #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) {
@@ -414,13 +416,22 @@ int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const
     // A/B knob (tools/ffn_ab.sh): MLG_FFN_GRID = workgroups per CU of the persistent grid
     // (0: one workgroup per tile)
     static const int per_cu = ffn_env("MLG_FFN_GRID", 0);
-    const long ntiles = (M + R - 1) / R;
+    // A/B knob: MLG_FFN_ROWS = token rows per workgroup (64: 4 waves, 128: 8 waves)
+    static const int rows = ffn_env("MLG_FFN_ROWS", 64) == 128 ? 128 : 64;
+    if (rows == 128) {
+        hipLaunchKernelGGL((k_lg_ffn<false, 128, 8>), dim3((unsigned)((M + 127) / 128)), dim3(512), 0, s, ctx, X, xcopy,
+                           ldc, M, w, cf, relu);
+        MLG_LAUNCH_CHECK();
+        return MLG_OK;
+    }
+    const long ntiles = (M + 63) / 64;
     if (per_cu > 0) {
         const long grid = std::min<long>(ntiles, (long)per_cu * ffn_num_cus());
-        hipLaunchKernelGGL(k_lg_ffn<true>, dim3((unsigned)grid), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf, relu);
-    } else {
-        hipLaunchKernelGGL(k_lg_ffn<false>, dim3((unsigned)ntiles), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf,
+        hipLaunchKernelGGL((k_lg_ffn<true, 64, 4>), dim3((unsigned)grid), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf,
                            relu);
+    } else {
+        hipLaunchKernelGGL((k_lg_ffn<false, 64, 4>), dim3((unsigned)ntiles), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w,
+                           cf, relu);
     }
     MLG_LAUNCH_CHECK();
     return MLG_OK;

@@ -10,7 +10,7 @@ rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/attn_pytest.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 for arm in new old new old; do
   if [ $arm = old ]; then export MLGATE_LIB_DIR=$PWD/ab_old; else unset MLGATE_LIB_DIR; fi
-  X=""; if [ $arm = new ]; then X="--exp2"; fi
+  X="${ATTN_NEW_ARGS:-}"; if [ $arm = old ]; then X=""; fi
   timeout -k 10 120 python3 tools/attn_bench.py --pairs 1024 --iters 5 $X > gpurun_out/attn_$arm.log 2>&1
   rc=$?; echo "attn $arm rc=$rc $(tail -1 gpurun_out/attn_$arm.log)"
   if [ $rc -ne 0 ]; then exit $rc; fi

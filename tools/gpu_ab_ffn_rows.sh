@@ -1,0 +1,19 @@
+#!/bin/bash
+# Same-box A/B of the fused FFN tile: MLG_FFN_ROWS=128 (8 waves, one workgroup per CU)
+# vs 64 (4 waves, two per CU); the FFN / LightGlue / SuperGlue parity tests under 128 first.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+MLG_FFN_ROWS=128 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_lightglue_gpu.py tests/test_superglue_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ffnrows_pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/ffnrows_pytest.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+for r in 128 64 128 64; do
+  MLG_FFN_ROWS=$r timeout -k 10 120 python3 tools/proj_ab.py --iters 10 > gpurun_out/ffnrows_$r.log 2>&1
+  rc=$?; echo "rows=$r rc=$rc $(grep -o '"lg_ffn_ms": [0-9.]*' gpurun_out/ffnrows_$r.log)"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
+for r in 128 64; do
+  MLG_FFN_ROWS=$r timeout -k 10 400 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/ffnrows_bench_$r.log 2>&1
+  rc=$?; echo "bench rows=$r rc=$rc"; tail -1 gpurun_out/ffnrows_bench_$r.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['stage_ms_per_step']['lightglue_ffn_fused'], d['config']['false_loop_closure_rejections'])"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
