@@ -60,7 +60,7 @@ __device__ __forceinline__ float logsigmoid_f(float x) { return fminf(x, 0.f) - 
 // fragments are read one k-step ahead into the other half of a double buffer.  Loads
 // past the last step re-read the last step (no branches, so the waitcnt pass counts
 // the in-flight loads exactly); addresses are recomputed per call, not hoisted.
-template <int NT, int MT>
+template <int NT, int MT, int RING = 4>
 __device__ __forceinline__ void gemm_phase(const bf16_t* __restrict__ W, int N, int n0, int nkb, int chunk0,
                                            const char* lds, f32x16 (&acc)[NT][MT]) {
     const int lane = threadIdx.x & 63, col = lane & 31, hh = lane >> 5;
@@ -71,19 +71,19 @@ __device__ __forceinline__ void gemm_phase(const bf16_t* __restrict__ W, int N, 
     for (int t = 0; t < NT; ++t) wrow[t] = W + (size_t)(n0 + 32 * t + col) * 16 + 8 * hh;
     const char* xrow = lds + col * ROWB;  // + 32 mt rows per m-tile
     const int sw = col & 15;             // = row & 15 for every m-tile
-    bf16x8 wf[NT][4], xa[MT], xb[MT];
+    bf16x8 wf[NT][RING], xa[MT], xb[MT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) wf[t][s] = ld16(wrow[t] + s * step);
+        for (int s = 0; s < RING; ++s) wf[t][s] = ld16(wrow[t] + s * step);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
         xa[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + (((chunk0 + hh) ^ sw) << 4));
 #pragma unroll 1
-    for (int kb = 0; kb < nkb; ++kb) {
+    for (int kb = 0; kb < 4 * nkb / RING; ++kb) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int ks = 4 * kb + s;
+        for (int s = 0; s < RING; ++s) {
+            const int ks = RING * kb + s;
             const int cn = ((chunk0 + 2 * min(ks + 1, last) + hh) ^ sw) << 4;
             bf16x8(&cur)[MT] = (s & 1) ? xb : xa;
             bf16x8(&nxt)[MT] = (s & 1) ? xa : xb;
@@ -95,7 +95,7 @@ __device__ __forceinline__ void gemm_phase(const bf16_t* __restrict__ W, int N, 
                 for (int t = 0; t < NT; ++t)
                     acc[t][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[t][s], cur[mt], acc[t][mt], 0, 0, 0);
 #pragma unroll
-            for (int t = 0; t < NT; ++t) wf[t][s] = ld16(wrow[t] + min(ks + 4, last) * step);
+            for (int t = 0; t < NT; ++t) wf[t][s] = ld16(wrow[t] + min(ks + RING, last) * step);
             // pin the refill here: left alone, the scheduler sinks it next to its use
             // (minimising live ranges) and every step waits on a fresh L2 round trip
             __builtin_amdgcn_sched_barrier(0);
@@ -128,6 +128,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                                                   bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w,
                                                   mlg_lg_conf_i cf, int relu) {
     constexpr int MT = R / 32, NT1 = 256 / NW / 32, NT2 = 512 / NW / 32, NTH = 64 * NW;
+    constexpr int RING = NW == 8 ? 8 : 4;  // weight k-steps in flight per wave
     __shared__ __attribute__((aligned(16))) char lds[R * ROWB];
     __shared__ float red[2][NW][R];
     // biases and LayerNorm affine, staged in LDS: epilogue reads never wait on VMEM
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
         {
             f32x16 acc[NT1][MT];
             zero(acc);
-            gemm_phase<NT1, MT>(w.Wout, 256, 32 * NT1 * wave, 4, 32, lds, acc);
+            gemm_phase<NT1, MT, RING>(w.Wout, 256, 32 * NT1 * wave, 4, 32, lds, acc);
             __syncthreads();  // every wave has read the ctx half
     #pragma unroll
             for (int t = 0; t < NT1; ++t)
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
         {
             f32x16 acc[NT2][MT];
             zero(acc);
-            gemm_phase<NT2, MT>(w.Wf1, 512, 32 * NT2 * wave, 8, 0, lds, acc);
+            gemm_phase<NT2, MT, RING>(w.Wf1, 512, 32 * NT2 * wave, 8, 0, lds, acc);
     #pragma unroll
             for (int t = 0; t < NT2; ++t)
     #pragma unroll
@@ -302,7 +303,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             __builtin_amdgcn_sched_barrier(0);
             f32x16 acc[NT1][MT];
             zero(acc);
-            gemm_phase<NT1, MT>(w.Wf2, 256, 32 * NT1 * wave, 8, 0, lds, acc);
+            gemm_phase<NT1, MT, RING>(w.Wf2, 256, 32 * NT1 * wave, 8, 0, lds, acc);
             __syncthreads();  // every wave has read the GELU output
     #pragma unroll
             for (int t = 0; t < NT1; ++t)
@@ -416,6 +417,10 @@ int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const
     // A/B knob (tools/ffn_ab.sh): MLG_FFN_GRID = workgroups per CU of the persistent grid
     // (0: one workgroup per tile)
     static const int per_cu = ffn_env("MLG_FFN_GRID", 0);
+    // timing probe only (tools/gpu_ab_ffn_epi.sh): ReLU instead of LayerNorm + GELU, to
+    // price the LightGlue epilogue; results are then NOT LightGlue's
+    static const int probe_relu = ffn_env("MLG_FFN_PROBE_RELU", 0);
+    if (probe_relu) relu = 1;
     // A/B knob: MLG_FFN_ROWS = token rows per workgroup (64: 4 waves, 128: 8 waves)
     static const int rows = ffn_env("MLG_FFN_ROWS", 64) == 128 ? 128 : 64;
     if (rows == 128) {

@@ -15,7 +15,8 @@ import json
 import sys
 
 SLOT_KERNELS = {"lightglue_attention": "k_attention_varlen", "lightglue_ffn_fused": "k_lg_ffn",
-                "vit_attention": "k_attention(", "superpoint_conv3x3": "k_conv3x3"}
+                "lightglue_qkv_gemms": "k_lg_proj", "vit_attention": "k_attention(",
+                "superpoint_conv3x3": "k_conv3x3"}
 
 
 def main():
