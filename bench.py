@@ -213,10 +213,12 @@ def main():
                                    "(k=%d, gap 10 s, thr 0.5) + floor-gated retrieval" % args.k
                                    + ("; configs[2] verify_with_semantics on every floor-valid candidate: "
                                       "SuperPoint(2048) + LightGlue + OpenCV-sequenced E-RANSAC (K = ISEC cam1) + "
-                                      "decision rule; floor gate on the geometrically valid pairs"
+                                      "decision rule (LightGlue once per unordered pair, RANSAC + decision per ordered pair); "
+                                      "floor gate on the geometrically valid pairs"
                                       if gate.verify else ""),
                        "keyframes": N, "k": args.k, "vit_batch": args.batch, "parallelism": f"frame-sharded x{world}",
                        "matches": counts["matches"], "pairs_verified": counts["pairs_verified"],
+                       "pairs_matched_lightglue": counts.get("pairs_matched_lightglue", 0),
                        "pairs_geometrically_valid": counts["verified_valid"],
                        "loop_closures_accepted": counts["accepted"],
                        "false_loop_closure_rejections": rej},

@@ -296,6 +296,17 @@ int mlg_lightglue(const mlg_lg_weights* w, const float* keypoints, const float* 
                   size_t workspace_bytes, int32_t* matches, float* scores, int32_t* num_matches, int32_t* stop_layer,
                   void* stream);
 
+/* LightGlue is symmetric in its two images (shared weights; self / cross blocks, the
+ * dual-softmax assignment, early stopping and pruning all treat image0 and image1 alike),
+ * so the full gate matches each unordered pair once.  This gathers, per ordered pair p,
+ * the matches of unordered row rows[p] of a mlg_lightglue output; with swap[p] != 0 the
+ * image roles are exchanged and the matches re-sorted ascending in the new image0 index
+ * -- the order the swapped call returns.  matches_out int32 [P, kmax, 2], scores_out
+ * f32 [P, kmax], num_out int32 [P]; rows / swap device arrays. */
+int mlg_lg_orient_matches(const int32_t* matches, const float* scores, const int32_t* num_matches,
+                          const int32_t* rows, const uint8_t* swap, int P, int kmax, int32_t* matches_out,
+                          float* scores_out, int32_t* num_out, void* stream);
+
 /* --------------------------------------------------------- SuperGlue --
  * The SuperGlue matcher of the reference's SuperGlue class configuration
  * (geometric_verification.py:385-399: weights 'indoor', sinkhorn_iterations 20,

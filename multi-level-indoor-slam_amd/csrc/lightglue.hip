@@ -17,6 +17,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "../../include/mlgate.h"
 
 namespace {
 
@@ -558,6 +559,61 @@ __global__ __launch_bounds__(256) void k_lg_filter(const Asg* __restrict__ tab, 
     if (tid == 0) count[a.pair] = base_sh;
 }
 
+
+// ---------------------------------------------------------- pair orientation
+// Ordered pair p takes the matches of unordered-pair row rows[p]; with swap[p] the
+// image roles are exchanged: (i0, i1) -> (i1, i0), re-sorted ascending in the new image0
+// index, which is the order LightGlue itself returns for the swapped call (its matches
+// are mutual nearest neighbours, so each index appears at most once: a scatter into
+// kmax slots plus an ordered compaction sorts them exactly).  Scores follow their match.
+__global__ __launch_bounds__(256) void k_lg_orient(const int32_t* __restrict__ m_in, const float* __restrict__ s_in,
+                                                   const int32_t* __restrict__ n_in, const int32_t* __restrict__ rows,
+                                                   const uint8_t* __restrict__ swap, int kmax,
+                                                   int32_t* __restrict__ m_out, float* __restrict__ s_out,
+                                                   int32_t* __restrict__ n_out) {
+    __shared__ int slot[2048];
+    __shared__ int wsum[256];
+    const int p = blockIdx.x, tid = threadIdx.x, r = rows[p];
+    const int n = n_in[r];
+    const int32_t* mi = m_in + (size_t)r * kmax * 2;
+    const float* si = s_in + (size_t)r * kmax;
+    int32_t* mo = m_out + (size_t)p * kmax * 2;
+    float* so = s_out + (size_t)p * kmax;
+    if (!swap[p]) {
+        for (int i = tid; i < n; i += 256) {
+            mo[2 * i] = mi[2 * i];
+            mo[2 * i + 1] = mi[2 * i + 1];
+            so[i] = si[i];
+        }
+        if (tid == 0) n_out[p] = n;
+        return;
+    }
+    for (int i = tid; i < kmax; i += 256) slot[i] = -1;
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) slot[mi[2 * i + 1]] = i;  // image1 index -> match
+    __syncthreads();
+    const int per = (kmax + 255) / 256, b0 = tid * per;  // ordered compaction of the slots
+    int c = 0;
+    for (int j = b0; j < min(b0 + per, kmax); ++j) c += slot[j] >= 0;
+    wsum[tid] = c;
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int t = 0; t < 256; ++t) { const int v = wsum[t]; wsum[t] = acc; acc += v; }
+    }
+    __syncthreads();
+    int o = wsum[tid];
+    for (int j = b0; j < min(b0 + per, kmax); ++j) {
+        const int i = slot[j];
+        if (i < 0) continue;
+        mo[2 * o] = j;
+        mo[2 * o + 1] = mi[2 * i];
+        so[o] = si[i];
+        ++o;
+    }
+    if (tid == 0) n_out[p] = n;
+}
+
 size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct LgLayout {
@@ -912,5 +968,18 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     // the last assignment's table (h_asg) and possibly a final layout upload are pageable
     // copies still queued on s: they must complete before the vectors go out of scope
     if (hipStreamSynchronize(s) != hipSuccess) return MLG_EHIP;
+    return MLG_OK;
+}
+
+int mlg_lg_orient_matches(const int32_t* matches, const float* scores, const int32_t* num_matches,
+                          const int32_t* rows, const uint8_t* swap, int P, int kmax, int32_t* matches_out,
+                          float* scores_out, int32_t* num_out, void* stream) {
+    if (P <= 0) return MLG_OK;
+    if (kmax <= 0 || kmax > 2048 || !matches || !scores || !num_matches || !rows || !swap || !matches_out ||
+        !scores_out || !num_out)
+        return MLG_EINVAL;
+    hipLaunchKernelGGL(k_lg_orient, dim3((unsigned)P), dim3(256), 0, (hipStream_t)stream, matches, scores,
+                       num_matches, rows, swap, kmax, matches_out, scores_out, num_out);
+    MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

@@ -434,6 +434,27 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lightglue(const Tensor& kpts, const T
     return {m, sc, n, stop};
 }
 
+std::tuple<Tensor, Tensor, Tensor> lg_orient(const Tensor& m, const Tensor& sc, const Tensor& n, const Tensor& rows,
+                                             const Tensor& swap) {
+    want(m, at::kInt, "matches");
+    want(sc, at::kFloat, "scores");
+    want(n, at::kInt, "num_matches");
+    want(rows, at::kInt, "rows");
+    want(swap, at::kByte, "swap");
+    TORCH_CHECK(m.dim() == 3 && m.size(2) == 2 && sc.size(0) == m.size(0) && n.numel() == m.size(0),
+                "matches [R, kmax, 2], scores [R, kmax], num [R]");
+    TORCH_CHECK(rows.numel() == swap.numel(), "rows / swap sizes differ");
+    const int64_t P = rows.numel(), kmax = m.size(1);
+    c10::DeviceGuard g(m.device());
+    Tensor mo = at::empty({P, kmax, 2}, m.options()), so = at::empty({P, kmax}, sc.options());
+    Tensor no = at::empty({P}, n.options());
+    check_rc(mlg_lg_orient_matches(cp<int32_t>(m), cp<float>(sc), cp<int32_t>(n), cp<int32_t>(rows),
+                                   cp<uint8_t>(swap), (int)P, (int)kmax, mp<int32_t>(mo), mp<float>(so),
+                                   mp<int32_t>(no), stream_of(m)),
+             "mlg_lg_orient_matches");
+    return {mo, so, no};
+}
+
 // ------------------------------------------------------------------ RANSAC
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> ransac_epipolar(const Tensor& k1, const Tensor& k2,
                                                                    const Tensor& offs, const c10::optional<Tensor>& K,
@@ -714,6 +735,7 @@ TORCH_LIBRARY(mlgate, m) {
           "-> (Tensor, Tensor, Tensor)");
     m.def("proximity(Tensor pos, Tensor? floor, int row0, int nrows, float radius, int min_gap, bool strict) "
           "-> (Tensor, Tensor, Tensor, Tensor)");
+    m.def("lg_orient(Tensor m, Tensor sc, Tensor n, Tensor rows, Tensor swap) -> (Tensor, Tensor, Tensor)");
     m.def("orb_detect(Tensor frames, Tensor pattern, Tensor iparams, Tensor scales, int max_kp) "
           "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
     m.def("orb_match(Tensor desc, Tensor counts, Tensor pair_a, Tensor pair_b) -> (Tensor, Tensor, Tensor, Tensor)");
@@ -742,6 +764,7 @@ TORCH_LIBRARY_IMPL(mlgate, CUDA, m) {
     m.impl("pillow_resize_224", &pillow_resize_224);
     m.impl("plane_ransac", &plane_ransac);
     m.impl("proximity", &proximity);
+    m.impl("lg_orient", &lg_orient);
     m.impl("orb_detect", &orb_detect);
     m.impl("orb_match", &orb_match);
 }

@@ -95,6 +95,7 @@ EXPORTS = {
     "mlg_prof_reset": (c_int, []),
     "mlg_prof_read": (c_int, [c_int, ctypes.POINTER(c_double), ctypes.POINTER(c_long)]),
     "mlg_prof_read_work": (c_int, [c_int, ctypes.POINTER(c_double)]),
+    "mlg_lg_orient_matches": (c_int, [c_void_p] * 5 + [c_int, c_int] + [c_void_p] * 4),
     "mlg_png_info": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mlg_png_decode_bgr": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_png_load_bgr": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),

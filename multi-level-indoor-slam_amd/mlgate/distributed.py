@@ -42,7 +42,7 @@ class RowGather:
         return self.out
 
 
-def balanced_pairs(pa, pb, world, rank, group=None):
+def balanced_pairs(pa, pb, world, rank, group=None, group_reverse=False):
     """Pair-level load balance for the verification stage.  Each rank holds the
     gate-accepted (query, match) pairs of its own query rows (int32 tensors, row-major
     order); their number varies with the floor layout and the revisit pattern, so
@@ -50,7 +50,11 @@ def balanced_pairs(pa, pb, world, rank, group=None):
     lists (8 B per pair) and take the rank-th contiguous slice of the global,
     rank-ordered list: the union of the slices is exactly the global list and slice
     sizes differ by at most one.  Every keyframe's features are all-gathered before this
-    step, so any rank can verify any pair."""
+    step, so any rank can verify any pair.
+    With ``group_reverse`` the slices are cut over the UNORDERED pairs instead: (a, b) and
+    (b, a) land on the same rank, which matches them once (LightGlue is symmetric in its
+    two images; mlg_lg_orient_matches); the unordered pairs are split evenly, in
+    ascending (min, max) order."""
     if world == 1:
         return pa, pb
     dev = pa.device
@@ -65,6 +69,15 @@ def balanced_pairs(pa, pb, world, rank, group=None):
     bufs = [torch.empty_like(send) for _ in range(world)]
     dist.all_gather(bufs, send, group=group)
     allp = torch.cat([b[:, :s] for b, s in zip(bufs, sizes)], dim=1)
+    if group_reverse:
+        lo_ = torch.minimum(allp[0], allp[1]).long()
+        hi_ = torch.maximum(allp[0], allp[1]).long()
+        span = int(hi_.max().item()) + 1 if hi_.numel() else 1
+        ukey, inv = torch.unique(lo_ * span + hi_, sorted=True, return_inverse=True)
+        nu = ukey.numel()
+        ulo, uhi = rank * nu // world, (rank + 1) * nu // world
+        sel = torch.nonzero((inv >= ulo) & (inv < uhi), as_tuple=True)[0]
+        return allp[0, sel].contiguous(), allp[1, sel].contiguous()
     total = allp.shape[1]
     lo, hi = rank * total // world, (rank + 1) * total // world
     return allp[0, lo:hi].contiguous(), allp[1, lo:hi].contiguous()

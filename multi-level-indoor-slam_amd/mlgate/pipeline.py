@@ -31,6 +31,8 @@ from typing import Dict, List, Optional
 
 import numpy as np
 
+from . import _native
+
 from .floors import IMUFloorDetector
 from .gate import LoopClosureCandidate, SemanticLoopClosureGate
 from .verify import MatchResult, SemanticGeometricVerifier
@@ -210,6 +212,11 @@ class DeviceGate:
             self.K = torch.from_numpy(Kc.reshape(9).copy()).to(self.dev) if K is not None else None
         self.last = {}
 
+    def _dedup(self):
+        """Match each unordered pair once (MLGATE_LG_DEDUP=0: every ordered pair, for A/B)."""
+        import os
+        return os.environ.get("MLGATE_LG_DEDUP", "1") != "0"
+
     def _side_stream(self):
         """The RANSAC stream (MLGATE_RANSAC_SIDE=0: the main stream, for A/B runs)."""
         if getattr(self, "_side", None) is None:
@@ -263,8 +270,26 @@ class DeviceGate:
             pa_t, pb_t = pa_t[same], pb_t[same]
         # pair-level load balance across ranks (features are all-gathered, so any rank
         # can verify any pair; the union of the slices is the global pair list)
-        pa_t, pb_t = self.mdist.balanced_pairs(pa_t, pb_t, self.world, self.rank)
+        dedup = self._dedup()
+        pa_t, pb_t = self.mdist.balanced_pairs(pa_t, pb_t, self.world, self.rank, group_reverse=dedup)
         pa, pb = pa_t.cpu().numpy(), pb_t.cpu().numpy()
+        self.last_pairs = (pa, pb)
+        # LightGlue once per UNORDERED pair: it is symmetric in its two images (shared
+        # weights; self / cross blocks, dual-softmax assignment, early stopping and pruning
+        # treat both alike), so (b, a) is (a, b) with the image roles exchanged and the
+        # matches re-sorted by the new image0 index (mlg_lg_orient_matches).  Every ORDERED
+        # pair still gets its own RANSAC on its own match order and its own decision, as
+        # verify_with_semantics gives each (query, match) (geometric_verification.py:688-744).
+        if dedup:
+            key = np.minimum(pa, pb).astype(np.int64) * self.N + np.maximum(pa, pb)
+            ukey, inv = np.unique(key, return_inverse=True)
+            ua, ub = (ukey // self.N).astype(np.int32), (ukey % self.N).astype(np.int32)
+            swap_all = (pa > pb).astype(np.uint8)
+        else:
+            ua, ub, inv, swap_all = pa, pb, np.arange(len(pa)), np.zeros(len(pa), np.uint8)
+        order = np.argsort(inv, kind="stable")
+        bounds = np.searchsorted(inv[order], np.arange(0, len(ua) + self.lg_chunk, self.lg_chunk))
+        out["pairs_matched_lightglue"] = len(ua)
         # RANSAC of chunk c runs on a side stream while LightGlue matches chunk c + 1 on
         # this one (mlg_lightglue waits on its stream once per layer; the side stream
         # fills those gaps and the CUs the small RANSAC / assignment grids leave idle)
@@ -272,9 +297,17 @@ class DeviceGate:
         side = self._side_stream()
         n_valid_t = torch.zeros((), dtype=torch.int64, device=self.dev)
         gate_rej_t = torch.zeros((), dtype=torch.int64, device=self.dev)
-        for c0 in range(0, len(pa), self.lg_chunk):
-            ca, cb = pa[c0:c0 + self.lg_chunk], pb[c0:c0 + self.lg_chunk]
-            m, _, n, _ = self.lg.match_device(kp_all, ds_all, counts, ca, cb)
+        for ci, c0 in enumerate(range(0, len(ua), self.lg_chunk)):
+            mu, su, nu, _ = self.lg.match_device(kp_all, ds_all, counts, ua[c0:c0 + self.lg_chunk],
+                                                 ub[c0:c0 + self.lg_chunk])
+            sel = order[bounds[ci]:bounds[ci + 1]]  # the ordered pairs of these unordered ones
+            ca, cb = pa[sel], pb[sel]
+            if dedup:
+                rows = torch.from_numpy((inv[sel] - c0).astype(np.int32)).to(self.dev)
+                sw = torch.from_numpy(swap_all[sel]).to(self.dev)
+                m, _, n = _native.ops().lg_orient(mu, su, nu, rows, sw)
+            else:
+                m, n = mu, nu
             ready = torch.cuda.Event()
             ready.record(main)
             with torch.cuda.stream(side):

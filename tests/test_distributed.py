@@ -93,3 +93,41 @@ def test_balanced_pairs_partition_the_global_list(tmp_path):
     out = str(tmp_path / "pairs.txt")
     mp.spawn(_pairs_worker, args=(3, _free_port(), out), nprocs=3, join=True)
     assert open(out).read() == "ok"
+
+
+def _pairs_rev_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(10 + rank)
+    n = [40, 0, 57][rank]
+    pa = rng.integers(0, 30, n).astype(np.int32)
+    pb = rng.integers(0, 30, n).astype(np.int32)
+    if rank == 2:  # reverses of rank 0's pairs, found by another rank's queries
+        r0 = np.random.default_rng(10)
+        a0, b0 = r0.integers(0, 30, 40).astype(np.int32), r0.integers(0, 30, 40).astype(np.int32)
+        pa[:20], pb[:20] = b0[:20], a0[:20]
+    sa, sb = mdist.balanced_pairs(torch.from_numpy(pa), torch.from_numpy(pb), world, rank, group_reverse=True)
+    got = mdist.gather_objects_to_rank0((sa.numpy(), sb.numpy()), world, rank)
+    full = mdist.gather_objects_to_rank0((pa, pb), world, rank)
+    if rank == 0:
+        allp = sorted(zip(np.concatenate([f[0] for f in full]).tolist(), np.concatenate([f[1] for f in full]).tolist()))
+        gotp = sorted(p for g in got for p in zip(g[0].tolist(), g[1].tolist()))
+        owner = {}
+        clash = False
+        for r, g in enumerate(got):
+            for a, b in zip(g[0].tolist(), g[1].tolist()):
+                k = (min(a, b), max(a, b))
+                clash |= owner.setdefault(k, r) != r
+        per_rank = [len({(min(a, b), max(a, b)) for a, b in zip(g[0].tolist(), g[1].tolist())}) for g in got]
+        ok = gotp == allp and not clash and max(per_rank) - min(per_rank) <= 1
+        with open(out_path, "w") as f:
+            f.write("ok" if ok else f"mismatch clash={clash} {per_rank}")
+    dist.destroy_process_group()
+
+
+def test_balanced_pairs_group_reverse(tmp_path):
+    """group_reverse: the union is still the global pair multiset, (a, b) and (b, a) land
+    on one rank (matched once there), unordered pairs split within one of each other."""
+    out = str(tmp_path / "pairs_rev.txt")
+    mp.spawn(_pairs_rev_worker, args=(3, _free_port(), out), nprocs=3, join=True)
+    assert open(out).read() == "ok"

@@ -141,6 +141,54 @@ def test_device_gate_counts_equal_full_gate(dev, chain, reports, cfg):
     assert out["matches"] == len(rep.matches) and out["accepted"] == len(rep.accepted)
 
 
+@pytest.mark.parametrize("cfg", list(CFG))
+def test_device_gate_unordered_matching_changes_nothing(dev, chain, cfg, monkeypatch):
+    """LightGlue once per unordered pair (the default) vs once per ordered pair: the same
+    counts, the same per-pair decisions in every configuration."""
+    frames = torch.from_numpy(chain["frames"]).to(dev)
+    rg, vg = CFG[cfg]
+    outs = {}
+    for dd in ("1", "0"):
+        monkeypatch.setenv("MLGATE_LG_DEDUP", dd)
+        g = DeviceGate(frames, chain["seq"].t, chain["labels"], device=str(dev), k=chain["k"],
+                       similarity_threshold=chain["thr"], min_time_gap=chain["gap"], retrieval_floor_gating=rg,
+                       verifier_floor_gating=vg, K=ogeo.ISEC_K, vit_batch=64, lg_chunk=64)
+        outs[dd] = g.step()
+    a, b = dict(outs["1"]), dict(outs["0"])
+    assert a.pop("pairs_matched_lightglue") <= b.pop("pairs_matched_lightglue")
+    assert a == b
+
+
+def test_orient_matches_is_the_swapped_call(dev):
+    """mlg_lg_orient_matches: (i0, i1) -> (i1, i0) sorted by the new image0 index, scores
+    carried along; unswapped rows copied."""
+    from mlgate import _native
+    rng = np.random.default_rng(3)
+    R, K = 5, 300
+    m = np.full((R, K, 2), -7, np.int32)
+    sc = np.zeros((R, K), np.float32)
+    n = rng.integers(0, K, R).astype(np.int32)
+    for r in range(R):
+        i0 = np.sort(rng.choice(K, n[r], replace=False))
+        i1 = rng.choice(K, n[r], replace=False)
+        m[r, :n[r], 0], m[r, :n[r], 1] = i0, i1
+        sc[r, :n[r]] = rng.random(n[r])
+    rows = np.array([0, 1, 1, 4, 2, 3], np.int32)
+    swap = np.array([1, 0, 1, 1, 0, 1], np.uint8)
+    T = lambda x: torch.from_numpy(x).to(dev)  # noqa: E731
+    mo, so, no = _native.ops().lg_orient(T(m), T(sc), T(n), T(rows), T(swap))
+    mo, so, no = mo.cpu().numpy(), so.cpu().numpy(), no.cpu().numpy()
+    for p, (r, s_) in enumerate(zip(rows, swap)):
+        k = n[r]
+        assert no[p] == k
+        if s_:
+            o = np.argsort(m[r, :k, 1])
+            assert np.array_equal(mo[p, :k, 0], m[r, :k, 1][o]) and np.array_equal(mo[p, :k, 1], m[r, :k, 0][o])
+            assert np.array_equal(so[p, :k], sc[r, :k][o])
+        else:
+            assert np.array_equal(mo[p, :k], m[r, :k]) and np.array_equal(so[p, :k], sc[r, :k])
+
+
 def test_ransac_inliers_equal_opencv_loop_on_gpu_matches(dev, chain, reports):
     """Stage-anchored RANSAC: on the GPU's own matches, the GPU inlier count equals that
     of OpenCV's sequential RANSAC loop restated in numpy (same cv::RNG sample stream)."""
