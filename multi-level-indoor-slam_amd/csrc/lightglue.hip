@@ -13,6 +13,7 @@
 // (one small D2H copy per layer), stops pairs whose confident ratio exceeds
 // depth_confidence (their assignment runs at that layer), prunes segments above the
 // pruning threshold, and compacts the layout with one gather.
+#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -614,6 +615,30 @@ __global__ __launch_bounds__(256) void k_lg_orient(const int32_t* __restrict__ m
     if (tid == 0) n_out[p] = n;
 }
 
+
+// Layer 0's self block on the frame layout -> the pair layout: pair segment k copies the
+// rows of its frame's segment (x f32 and the bf16 x copy in CAT's first 256 columns).
+// mv[k] = (pair offset, live rows, frame offset, -).
+__global__ __launch_bounds__(256) void k_lg_gather_rows(const int4* __restrict__ mv, const float* __restrict__ xf,
+                                                        const bf16_t* __restrict__ catf, float* __restrict__ x,
+                                                        bf16_t* __restrict__ cat) {
+    const int4 m = mv[blockIdx.y];
+    const int r0 = blockIdx.x * 16;
+    if (r0 >= m.y) return;
+    for (int e = threadIdx.x; e < 16 * 64; e += 256) {  // 16 rows x 64 float4 of x
+        const int i = r0 + e / 64, c = e % 64;
+        if (i >= m.y) continue;
+        reinterpret_cast<float4*>(x + (size_t)(m.x + i) * LG_D)[c] =
+            reinterpret_cast<const float4*>(xf + (size_t)(m.z + i) * LG_D)[c];
+    }
+    for (int e = threadIdx.x; e < 16 * 32; e += 256) {  // 16 rows x 32 x 16 B of the bf16 copy
+        const int i = r0 + e / 32, c = e % 32;
+        if (i >= m.y) continue;
+        reinterpret_cast<uint4*>(cat + (size_t)(m.x + i) * 512)[c] =
+            reinterpret_cast<const uint4*>(catf + (size_t)(m.z + i) * 512)[c];
+    }
+}
+
 size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct LgLayout {
@@ -786,11 +811,80 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         MLG_LAUNCH_CHECK();
         return MLG_OK;
     };
+    // Layer 0's self block reads one image only (its tokens, its positional encoding), so
+    // it runs once per distinct frame of the call -- a frame layout in the secondary
+    // buffers -- and its output rows are copied into every pair segment of that frame:
+    // the same kernels on the same rows, so the same bits as running it per pair.
+    std::vector<Seg> fsegs;
+    std::vector<int4> f_tasks, f_moves;
+    std::vector<int> f_out;
+    bool self0_done = false;
+    {
+        std::unordered_map<int, int> fidx;
+        std::vector<int> fmap(segs.size());
+        int foff = 0;
+        for (size_t k = 0; k < segs.size(); ++k) {
+            auto it = fidx.find(segs[k].frame);
+            if (it == fidx.end()) {
+                it = fidx.emplace(segs[k].frame, (int)fsegs.size()).first;
+                fsegs.push_back(Seg{foff, segs[k].len, segs[k].frame, 0});
+                foff += (segs[k].len + 63) & ~63;
+            }
+            fmap[k] = it->second;
+        }
+        if (fsegs.size() < segs.size()) {
+            const int NpadF = std::max(foff, 64);
+            int maxqf = 0;
+            double tok = 0, work = 0;
+            for (const Seg& f : fsegs) {
+                f_tasks.push_back(make_int4(f.off, f.len, f.off, f.len));
+                f_out.push_back(f.off);
+                maxqf = std::max(maxqf, f.len);
+                tok += f.len;
+                work += 4.0 * LG_H * 64 * (double)f.len * f.len;
+            }
+            for (size_t k = 0; k < segs.size(); ++k)
+                f_moves.push_back(make_int4(segs[k].off, segs[k].len, fsegs[fmap[k]].off, 0));
+            const int nf = (int)fsegs.size();
+            if (hipMemcpyAsync(SEGS, fsegs.data(), fsegs.size() * sizeof(Seg), hipMemcpyHostToDevice, s) != hipSuccess ||
+                hipMemcpyAsync(TASKS, f_tasks.data(), f_tasks.size() * sizeof(int4), hipMemcpyHostToDevice, s) !=
+                    hipSuccess ||
+                hipMemcpyAsync(OUTOFF, f_out.data(), f_out.size() * sizeof(int), hipMemcpyHostToDevice, s) !=
+                    hipSuccess ||
+                hipMemcpyAsync(MOVES, f_moves.data(), f_moves.size() * sizeof(int4), hipMemcpyHostToDevice, s) !=
+                    hipSuccess)
+                return MLG_EHIP;
+            hipLaunchKernelGGL(k_lg_live, dim3((NpadF + 255) / 256), dim3(256), 0, s, SEGS, nf, LIVE, ROWSEG, NpadF);
+            hipLaunchKernelGGL(k_lg_kpnorm, dim3((unsigned)nf), dim3(256), 0, s, SEGS, kpts, kmax,
+                               (float4*)(base + L.norm));
+            hipLaunchKernelGGL(k_lg_init, dim3((unsigned)((kmax + 63) / 64), (unsigned)nf), dim3(256), 0, s, SEGS,
+                               (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X2, CAT2, EC2, ES2, IND2);
+            MLG_LAUNCH_CHECK();
+            {
+                MlgProfScope prof(6, s, 2.0 * tok * 768 * 256);
+                LG_TRY(mlg_lg_proj(true, CAT2, 512, w.self[0].Wqkv, w.self[0].bqkv, EC2, ES2, LIVE, Q, K, VT, NpadF, s));
+            }
+            {
+                MlgProfScope prof(5, s, work);
+                LG_TRY(mlg_attention_varlen(Q, K, VT, CTX, LG_D, NpadF, LG_H, TASKS, OUTOFF, nf, maxqf, s));
+            }
+            {
+                MlgProfScope prof(8, s, 3584.0 * tok);
+                LG_TRY(mlg_lg_ffn(CTX, X2, CAT2, 512, NpadF, w.self[0], s, nullptr));
+            }
+            self0_done = true;
+        }
+    }
     LG_TRY(upload_layout());
     hipLaunchKernelGGL(k_lg_kpnorm, dim3((unsigned)segs.size()), dim3(256), 0, s, SEGS, kpts, kmax, (float4*)(base + L.norm));
     hipLaunchKernelGGL(k_lg_init, dim3((unsigned)((kmax + 63) / 64), (unsigned)segs.size()), dim3(256), 0, s, SEGS,
                        (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X, CAT, EC, ES, IND);
     MLG_LAUNCH_CHECK();
+    if (self0_done) {
+        hipLaunchKernelGGL(k_lg_gather_rows, dim3((unsigned)((kmax + 15) / 16), (unsigned)segs.size()), dim3(256), 0, s,
+                           MOVES, X2, CAT2, X, CAT);
+        MLG_LAUNCH_CHECK();
+    }
 
     auto live_tokens = [&]() {
         double t = 0;
@@ -865,13 +959,16 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
 
     std::vector<int> stats(segs.size() * 2);
     for (int i = 0; i < LG_L && !segs.empty(); ++i) {
-        // self block: projection + rotary + head split fused in the GEMM epilogue
-        {
-            MlgProfScope prof(6, s, 2.0 * live_tokens() * 768 * 256);
-            LG_TRY(mlg_lg_proj(true, CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, s));
+        // self block: projection + rotary + head split fused in the GEMM epilogue (layer 0's
+        // already ran per frame above when frames repeat)
+        if (!(i == 0 && self0_done)) {
+            {
+                MlgProfScope prof(6, s, 2.0 * live_tokens() * 768 * 256);
+                LG_TRY(mlg_lg_proj(true, CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, s));
+            }
+            LG_TRY(attention(false));
+            LG_TRY(ffn(w.self[i], nullptr));
         }
-        LG_TRY(attention(false));
-        LG_TRY(ffn(w.self[i], nullptr));
         // cross block
         {
             MlgProfScope prof(6, s, 2.0 * live_tokens() * 512 * 256);

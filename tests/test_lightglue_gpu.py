@@ -123,3 +123,38 @@ def test_lightglue_against_fp32_reference(dev, lg, sd):
     gi = np.array([g[c] for c in common])
     ri = np.array([r[c] for c in common])
     np.testing.assert_allclose(gs[gi], ref["scores"].numpy()[ri], atol=5e-2)
+
+
+def test_lightglue_repeated_frames_equal_single_pairs(lg):
+    """Frames shared by several pairs of one call run layer 0's self block once per frame
+    (csrc/lightglue.hip frame layout): every pair's matches, scores and stop layer must be
+    bit-identical to matching that pair alone."""
+    rng = np.random.default_rng(21)
+    sizes = [600, 1200, 450, 900]
+    frames = []
+    for m in sizes:
+        k = np.stack([rng.uniform(0, 640, m), rng.uniform(0, 480, m)], 1).astype(np.float32)
+        d = rng.standard_normal((m, 256)).astype(np.float32)
+        frames.append((k, d / np.linalg.norm(d, axis=1, keepdims=True)))
+    for i in (1, 3):  # overlapping views of frame 0
+        k0, d0 = frames[0]
+        no = min(len(k0), sizes[i]) // 2
+        k, d = frames[i]
+        k[:no] = k0[:no] + rng.normal(0, 2, (no, 2)).astype(np.float32)
+        d[:no] = d0[:no] + 0.02 * rng.standard_normal((no, 256)).astype(np.float32)
+        d[:no] /= np.linalg.norm(d[:no], axis=1, keepdims=True)
+    kmax = max(sizes)
+    kp = torch.zeros(len(frames), kmax, 2)
+    ds = torch.zeros(len(frames), kmax, 256)
+    for f, (k, d) in enumerate(frames):
+        kp[f, :len(k)], ds[f, :len(k)] = torch.from_numpy(k), torch.from_numpy(d)
+    kp, ds = kp.to(lg.device), ds.to(lg.device)
+    pa, pb = np.array([0, 0, 1, 3, 2, 0], np.int32), np.array([1, 3, 3, 0, 0, 2], np.int32)
+    m, s, n, stop = lg.match_device(kp, ds, sizes, pa, pb)
+    m, s, n = m.cpu().numpy(), s.cpu().numpy(), n.cpu().numpy()
+    for p in range(len(pa)):
+        m1, s1, n1, st1 = lg.match_device(kp, ds, sizes, pa[p:p + 1], pb[p:p + 1])
+        k1 = int(n1[0])
+        assert k1 == n[p] and st1[0] == stop[p]
+        assert np.array_equal(m1[0, :k1].cpu().numpy(), m[p, :k1]) and np.array_equal(s1[0, :k1].cpu().numpy(), s[p, :k1])
+    assert n[0] > 0 and n[3] > 0
