@@ -16,6 +16,8 @@
 // Requirements (checked by the host launcher): K % 64 == 0, N % 128 == 0,
 // 16-byte aligned A / W rows.  M is arbitrary (rows >= M are clamped on load and
 // masked on store).
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -562,6 +564,127 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A
 #undef D256_COMPUTE
 #undef D256_DMA
 }
+
+// Variant 5: the 256 x 256 persistent tile of k_gemm256 with K-tiles of 32 in a 4-deep
+// LDS ring (4 x 32 KiB): the DMA of K-tile t + 3 is issued when t is computed, so three
+// compute steps (not one) hide each tile's fetch; the ring runs on across output tiles
+// (the last three steps of a tile fetch the next tile's first three K-tiles).  Same MFMA
+// k order as k_gemm256, so the same bits.
+template <class Epi>
+__global__ __launch_bounds__(512, 2) void k_gemm256q(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                    int M, int N, int K, int lda, int ldw, Epi epi) {
+    constexpr int BK = 32, TM = 256, TN = 256;
+    constexpr int A_BYTES = TM * BK * 2, STAGE = (TM + TN) * BK * 2;  // 32 KiB
+    constexpr int NA = 2, NB = 2;                                      // DMAs per wave per K-tile
+    constexpr int WAIT2 = 0xF70 | (2 * (NA + NB));                     // two newer K-tiles may fly
+    __shared__ __attribute__((aligned(16))) char ringbuf[4 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nN = N / TN, nM = (M + TM - 1) / TM, ntiles = nN * nM;
+    const int xcd = blockIdx.x & 7, per_xcd = gridDim.x >> 3;
+    const int tx = (ntiles + 7) >> 3;
+    const int tile_end = min((xcd + 1) * tx, ntiles);
+    int tile = xcd * tx + (blockIdx.x >> 3);
+    if (tile >= tile_end) return;
+
+    const int lr = lane >> 2, lp = lane & 3;  // 16 rows x 4 chunks of 16 B per DMA wave-instruction
+    const int wm = wave & 1, wn = wave >> 1;
+    const int da = NA * wave * 1024, db = A_BYTES + NB * wave * 1024;
+    const int nk = K / BK;  // >= 3 (checked by the launcher)
+    unsigned ob[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int row = (NB * wave + i) * 16 + lr;
+        ob[i] = (unsigned)(row * ldw + ((lp ^ ((row >> 1) & 3)) * 8)) * 2u;
+    }
+    auto a_offsets = [&](int t, unsigned* oa) {
+        const int m0 = (t / nN) * TM;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int row = (NA * wave + i) * 16 + lr;
+            oa[i] = (unsigned)((min(m0 + row, M - 1) - m0) * lda + ((lp ^ ((row >> 1) & 3)) * 8)) * 2u;
+        }
+    };
+    auto a_base = [&](int t) { return A + (size_t)((t / nN) * TM) * lda; };
+    auto b_base = [&](int t) { return W + (size_t)((t % nN) * TN) * ldw; };
+#define Q256_DMA(ST, OA, SA, SB, k0)                                                                       \
+    {                                                                                                      \
+        const unsigned b_ = lds_addr(ST);                                                                  \
+        const bf16_t* sa_ = (SA) + (k0);                                                                   \
+        const bf16_t* sb_ = (SB) + (k0);                                                                   \
+        _Pragma("unroll") for (int i = 0; i < NA; ++i) dma16s((OA)[i], sa_, b_ + da + i * 1024);           \
+        _Pragma("unroll") for (int i = 0; i < NB; ++i) dma16s(ob[i], sb_, b_ + db + i * 1024);             \
+    }
+    // the K-tile stream: (tile, k) pairs in order, the fetch position runs 3 ahead
+    int ftile = tile, fk = 0;
+    unsigned foa[NA];
+    a_offsets(ftile, foa);
+    const bf16_t* fsa = a_base(ftile);
+    const bf16_t* fsb = b_base(ftile);
+    int fslot = 0;
+    auto fetch_next = [&]() {
+        Q256_DMA(ringbuf + fslot * STAGE, foa, fsa, fsb, fk * BK);
+        fslot = (fslot + 1) & 3;
+        if (++fk == nk) {  // continue with the next output tile of this workgroup (or re-read)
+            fk = 0;
+            if (ftile + per_xcd < tile_end) {
+                ftile += per_xcd;
+                a_offsets(ftile, foa);
+                fsa = a_base(ftile);
+                fsb = b_base(ftile);
+            } else {
+                fk = nk - 1;  // past the last tile: harmless re-reads of its last K-tile
+            }
+        }
+    };
+    fetch_next();
+    fetch_next();
+    fetch_next();
+    __builtin_amdgcn_s_waitcnt(WAIT2);
+    __builtin_amdgcn_s_barrier();
+    int cslot = 0;
+    for (; tile < tile_end; tile += per_xcd) {
+        f32x4 acc[4][8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < nk; ++t) {
+            fetch_next();  // K-tile t + 3 of the stream, into the slot computed last step
+            const char* ST = ringbuf + cslot * STAGE;
+            bf16x8 af[8], wf[4];
+            const int ch = lane >> 4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = wn * 64 + i * 16 + (lane & 15);
+                wf[i] = *reinterpret_cast<const bf16x8*>(ST + A_BYTES + soff<32>(row, ch));
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int row = wm * 128 + j * 16 + (lane & 15);
+                af[j] = *reinterpret_cast<const bf16x8*>(ST + soff<32>(row, ch));
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], af[j], acc[i][j], 0, 0, 0);
+            cslot = (cslot + 1) & 3;
+            __builtin_amdgcn_s_waitcnt(WAIT2);  // K-tile t + 1 has landed (t + 2, t + 3 may fly)
+            __builtin_amdgcn_s_barrier();
+        }
+        const int mt = tile / nN, m0 = mt * TM, n0 = (tile - mt * nN) * TN;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4;
+                const int m = m0 + wm * 128 + j * 16 + (lane & 15);
+                if (m < M) epi(m, n, acc[i][j]);
+            }
+    }
+    __builtin_amdgcn_s_waitcnt(0xF70);
+#undef Q256_DMA
+}
 }  // namespace dma
 
 // 1: 128x128 register-staged; 2: 128x256 DMA BK=64 (3 stages); 3: 128x256 DMA BK=32 (2 WG/CU);
@@ -583,13 +706,25 @@ int num_cus() {
 template <class Epi>
 int launch(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldw, Epi epi, hipStream_t s,
            int variant = -1) {
+    static const bool env_read = [] {  // A/B knob for whole runs (tools/gpu_ab_gemm.sh)
+        if (const char* v = getenv("MLG_GEMM_VARIANT")) {
+            const int x = atoi(v);
+            if (x >= 1 && x <= 5) g_variant = x;
+        }
+        return true;
+    }();
+    (void)env_read;
     if (variant < 0) variant = g_variant;
     g_num_cus = num_cus();
     if (M <= 0 || N <= 0 || K <= 0 || (K % BK) || (lda % 8) || (ldw % 8) || lda < K || ldw < K)
         return MLG_EINVAL;
     if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W)) & 15) return MLG_EINVAL;
     const long nwg_dma = (long)(N / dma::BN) * ((M + dma::BM - 1) / dma::BM);
-    if (variant == 4 && N % 256 == 0 && (K / 64) % 2 == 0) {
+    if (variant == 5 && N % 256 == 0 && K % 32 == 0 && K / 32 >= 3) {
+        const long ntiles = (long)(N / 256) * ((M + 255) / 256);
+        const long grid = std::min<long>(g_num_cus, (ntiles + 7) / 8 * 8);  // persistent: <= 1 per CU
+        hipLaunchKernelGGL(dma::k_gemm256q<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K, lda, ldw, epi);
+    } else if ((variant == 4 || variant == 5) && N % 256 == 0 && (K / 64) % 2 == 0) {
         const long ntiles = (long)(N / 256) * ((M + 255) / 256);
         const long grid = std::min<long>(g_num_cus, (ntiles + 7) / 8 * 8);  // persistent: <= 1 per CU
         hipLaunchKernelGGL(dma::k_gemm256<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K, lda, ldw, epi);
@@ -640,7 +775,7 @@ int mlg_gemm_conv(const bf16_t* A, int lda, const bf16_t* W, const float* bias, 
     return launch(A, W, M, N, K_, lda, K_, EpiConv{bias, R, ldr, X, ldx, C, ldc, act, act_cols}, s);
 }
 int mlg_gemm_set_variant(int variant) {
-    if (variant < 1 || variant > 4) return MLG_EINVAL;
+    if (variant < 1 || variant > 5) return MLG_EINVAL;
     g_variant = variant;
     return MLG_OK;
 }

@@ -29,7 +29,7 @@ def rel_err(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (1060, 256, 768), (530, 3072, 768), (777, 768, 3072),
                                    (33920 - 17, 2304, 768), (129, 256, 192)])
 def test_gemm_f32out(dev, M, N, K, variant):

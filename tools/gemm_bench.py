@@ -43,17 +43,17 @@ def main():
     A = torch.randn(33920 - 17, 768, device=dev, generator=g).to(torch.bfloat16)
     W = torch.randn(3072, 768, device=dev, generator=g).to(torch.bfloat16)
     outs = {}
-    for v in (1, 2, 3, 4):
+    for v in (1, 2, 3, 4, 5):
         C = torch.empty(A.shape[0], 3072, device=dev)
         _native.check(L.mlg_op_gemm_f32out_variant(v, _native.ptr(A), _native.ptr(W), _native.ptr(C), A.shape[0],
                                                    3072, 768, _native.stream_of(dev)), "gemm")
         outs[v] = C
     torch.cuda.synchronize()
-    print(json.dumps({"variants_bit_identical": bool(torch.equal(outs[1], outs[2]) and torch.equal(outs[1], outs[3]) and torch.equal(outs[1], outs[4]))}),
+    print(json.dumps({"variants_bit_identical": all(bool(torch.equal(outs[1], outs[v])) for v in (2, 3, 4, 5))}),
           flush=True)
 
     # loop throughput vs fixed per-tile cost: time C = A W^T (f32 out) at K = 768 .. 6144
-    for v in (2, 4):
+    for v in (4, 5):
         row = {"variant": v, "M": 33920, "N": 3072}
         for K in (768, 1536, 3072, 6144):
             A = torch.randn(33920, K, device=dev, generator=g).to(torch.bfloat16)
