@@ -269,6 +269,124 @@ __global__ __launch_bounds__(64) void k_topk_gate(const float* __restrict__ S, i
     }
 }
 
+
+// Large k (256 < k <= 4096; the reference's argsort()[:k] has no limit): one workgroup
+// per query row.  Each candidate is the 64-bit key (orderable similarity << 32 | index),
+// whose descending order is exactly (similarity desc, index desc); a radix select over
+// eight 8-bit digits (MSB first, 256-bin LDS histograms, one pass over the row each)
+// finds the k-th largest key, the keys at or above it are gathered into LDS and
+// bitonic-sorted, then emitted with the threshold / floor rule of k_topk_gate.
+constexpr int TOPK_LARGE = 4096;
+__device__ __forceinline__ uint64_t knn_key(float v, int j) {
+    uint32_t u = __float_as_uint(v);
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((uint64_t)u << 32) | (uint32_t)j;
+}
+__global__ __launch_bounds__(256) void k_topk_large(const float* __restrict__ S, int lds, int N, int Q,
+                                                    const double* __restrict__ tq, const double* __restrict__ tdb,
+                                                    const int64_t* __restrict__ fq, const uint8_t* __restrict__ hfq,
+                                                    const int64_t* __restrict__ fdb, const uint8_t* __restrict__ hfdb,
+                                                    double min_gap, float thr, int k, int gating,
+                                                    int32_t* __restrict__ idx_out, float* __restrict__ sim_out,
+                                                    uint8_t* __restrict__ valid_out, int32_t* __restrict__ count_out,
+                                                    unsigned long long* __restrict__ totals) {
+    __shared__ uint64_t keys[TOPK_LARGE];
+    __shared__ int hist[256];
+    __shared__ int s_total, s_n;
+    __shared__ uint64_t s_prefix;
+    __shared__ int s_need;
+    const int tid = threadIdx.x, r = blockIdx.x;
+    if (r >= Q) return;
+    const double ti = tq[r];
+    const float* row = S + (size_t)r * lds;
+    // candidates left after the time-gap mask
+    if (tid == 0) s_total = 0;
+    __syncthreads();
+    int c = 0;
+    for (int j = tid; j < N; j += 256) c += !(fabs(tdb[j] - ti) < min_gap);
+    atomicAdd(&s_total, c);
+    __syncthreads();
+    const int total = s_total;
+    const int kk = min(k, total);
+    // radix select: prefix of the kk-th largest key, digit by digit from the top
+    uint64_t prefix = 0;
+    int need = kk;  // rank (1-based, from the top) still to find below the fixed prefix
+    for (int d = 7; d >= 0 && kk > 0 && kk < total; --d) {
+        for (int b = tid; b < 256; b += 256) hist[b] = 0;
+        __syncthreads();
+        const uint64_t hmask = d == 7 ? 0ull : (~0ull << (8 * (d + 1)));
+        for (int j = tid; j < N; j += 256) {
+            if (fabs(tdb[j] - ti) < min_gap) continue;
+            const uint64_t key = knn_key(row[j], j);
+            if ((key & hmask) != prefix) continue;
+            atomicAdd(&hist[(int)((key >> (8 * d)) & 0xff)], 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0, b = 255;
+            for (; b > 0; --b) {
+                if (acc + hist[b] >= need) break;
+                acc += hist[b];
+            }
+            s_prefix = prefix | ((uint64_t)b << (8 * d));
+            s_need = need - acc;
+        }
+        __syncthreads();
+        prefix = s_prefix;
+        need = s_need;
+        __syncthreads();
+    }
+    // gather the kk largest keys (all candidates when kk == total)
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    for (int j = tid; j < N; j += 256) {
+        if (fabs(tdb[j] - ti) < min_gap) continue;
+        const uint64_t key = knn_key(row[j], j);
+        if (kk < total && key < prefix) continue;
+        const int slot = atomicAdd(&s_n, 1);
+        if (slot < TOPK_LARGE) keys[slot] = key;
+    }
+    __syncthreads();
+    const int n = min(s_n, kk);
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int i = n + tid; i < P; i += 256) keys[i] = 0ull;  // sort to the end (descending)
+    __syncthreads();
+    for (int kb = 2; kb <= P; kb <<= 1)
+        for (int jb = kb >> 1; jb > 0; jb >>= 1) {
+            for (int i = tid; i < P; i += 256) {
+                const int ixj = i ^ jb;
+                if (ixj > i) {
+                    const uint64_t a = keys[i], b = keys[ixj];
+                    if (((i & kb) == 0) == (a < b)) { keys[i] = b; keys[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    if (tid == 0) {
+        const bool hf_i = gating && hfq[r] != 0;
+        const int64_t fi = gating ? fq[r] : 0;
+        int emitted = 0, nvalid = 0;
+        for (int e = 0; e < n; ++e) {
+            const int j = (int)(uint32_t)keys[e];
+            const float v = row[j];
+            if (v < thr) break;
+            bool ok = true;
+            if (hf_i && hfdb[j]) ok = fi == fdb[j];
+            idx_out[(size_t)r * k + emitted] = j;
+            sim_out[(size_t)r * k + emitted] = v;
+            if (valid_out) valid_out[(size_t)r * k + emitted] = ok;
+            nvalid += ok;
+            ++emitted;
+        }
+        count_out[r] = emitted;
+        if (totals) {
+            atomicAdd(totals + 0, (unsigned long long)nvalid);
+            atomicAdd(totals + 1, (unsigned long long)(emitted - nvalid));
+        }
+    }
+}
+
 // ---------------------------------------------------------- fused path ----
 // numpy pairwise-sum tree of one 8192-element chunk: leaves (<= 128 elements) in order.
 // Each lane walks the same DFS; lane L sums leaves L, L + 64, ... (pairwise_leaf, the
@@ -611,9 +729,12 @@ int mlg_topk_gate(const float* S, int lds, int N, int Q, const double* tq, const
                   const uint8_t* hfq, const int64_t* fdb, const uint8_t* hfdb, double min_gap, float thr, int k,
                   int gating, int32_t* idx, float* sim, uint8_t* valid, int32_t* count, unsigned long long* totals,
                   hipStream_t s) {
-    if (N <= 0 || Q <= 0 || k <= 0 || k > 256 || lds < N) return MLG_EINVAL;
+    if (N <= 0 || Q <= 0 || k <= 0 || k > TOPK_LARGE || lds < N) return MLG_EINVAL;
     if (gating && (!fq || !hfq || !fdb || !hfdb)) return MLG_EINVAL;
-    if (k <= 32)
+    if (k > 256)
+        hipLaunchKernelGGL(k_topk_large, dim3(Q), dim3(256), 0, s, S, lds, N, Q, tq, tdb, fq, hfq, fdb, hfdb, min_gap,
+                           thr, k, gating, idx, sim, valid, count, totals);
+    else if (k <= 32)
         hipLaunchKernelGGL(k_topk_gate<32>, dim3(Q), dim3(64), 0, s, S, lds, N, Q, tq, tdb, fq, hfq, fdb, hfdb,
                            min_gap, thr, k, gating, idx, sim, valid, count, totals);
     else

@@ -123,7 +123,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> knn_gate(const Tensor& desc, const Te
     TORCH_CHECK(desc.dim() == 2, "desc must be [N, D]");
     const int64_t N = desc.size(0), D = desc.size(1);
     TORCH_CHECK(t.numel() == N && floor.numel() == N && has_floor.numel() == N, "t / floor / has_floor must be [N]");
-    TORCH_CHECK(k >= 1 && k <= 256, "k must be in [1, 256]");
+    TORCH_CHECK(k >= 1 && k <= 4096, "k must be in [1, 4096]");
     TORCH_CHECK(q0 >= 0 && Q >= 0 && q0 + Q <= N, "query rows out of range");
     if (totals.has_value() && totals->defined()) {
         want(*totals, at::kLong, "totals");
@@ -151,7 +151,7 @@ std::tuple<Tensor, Tensor, Tensor> knn_query(const Tensor& db, const Tensor& q, 
     want(t_q, at::kDouble, "t_q");
     const int64_t N = db.size(0), D = db.size(1), Q = q.size(0);
     TORCH_CHECK(q.dim() == 2 && q.size(1) == D && t_db.numel() == N && t_q.numel() == Q, "knn_query shapes");
-    TORCH_CHECK(k >= 1 && k <= 256, "k must be in [1, 256]");
+    TORCH_CHECK(k >= 1 && k <= 4096, "k must be in [1, 4096]");
     c10::DeviceGuard g(db.device());
     auto o = db.options();
     Tensor idx = at::empty({Q, k}, o.dtype(at::kInt)), sim = at::empty({Q, k}, o.dtype(at::kFloat));

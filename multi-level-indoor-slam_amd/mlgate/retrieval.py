@@ -8,7 +8,7 @@ import numpy as np
 
 from . import _native
 
-MAX_K = 256
+MAX_K = 4096  # k <= 32: fused scan; <= 256: per-lane lists; <= 4096: radix select (knn.hip)
 
 
 def knn_gate(desc, t, floor, has_floor, min_gap, thr, k, gating, q0=0, Q=None, totals=None):

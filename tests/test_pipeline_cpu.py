@@ -111,6 +111,6 @@ def test_gate_nan_label_accepted_like_reference():
 def test_k_above_device_limit_raises_before_device_work():
     spr = SemanticPlaceRecognition('cricavpr', device='cuda')
     spr.vpr.descriptors = [PlaceDescriptor(timestamp=float(i), descriptor=np.ones(4, np.float32), floor_label=1)
-                           for i in range(257)]
+                           for i in range(4097)]
     with pytest.raises(ValueError):
-        spr.find_loop_closures(k=300)
+        spr.find_loop_closures(k=5000)

@@ -158,3 +158,27 @@ def test_large_n_without_similarity_matrix(dev):
         c = count[r]
         assert c == oc[0] and np.array_equal(idx[r, :c], oi[0, :c]) and np.array_equal(sim[r, :c], osim[0, :c])
         assert np.array_equal(valid[r, :c].astype(bool), ov[0, :c].astype(bool))
+
+
+@pytest.mark.parametrize("k", [300, 1000, 4096])
+@pytest.mark.parametrize("gating", [True, False])
+def test_large_k_radix_select(dev, k, gating):
+    """256 < k <= 4096 (k_topk_large: radix select + LDS sort) against the oracle's
+    per-row loop on the same similarity matrix: indices, order, validity bit-exact."""
+    from oracle import retrieval as oret
+    rng = np.random.default_rng(k)
+    n, d = 1500, 64
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    t = np.arange(n, dtype=np.float64) * 0.7
+    fl = rng.integers(0, 4, n).astype(np.int64)
+    hf = (rng.random(n) > 0.1).astype(np.uint8)
+    thr = -0.05 if k != 1000 else 0.02
+    Xd = torch.from_numpy(X).to(dev)
+    S = retrieval.pairwise_similarities(Xd).cpu().numpy()
+    out = retrieval.knn_gate(Xd, torch.from_numpy(t).to(dev), torch.from_numpy(fl).to(dev),
+                             torch.from_numpy(hf).to(dev), 10.0, thr, k, gating)
+    q, m, sim, valid = retrieval.flatten_matches(*out)
+    rq, rm, rs, rv = oret.find_loop_closures(X, t, fl, hf, 10.0, thr, k, gating, S=S)
+    assert np.array_equal(q, rq) and np.array_equal(m, rm)
+    assert np.array_equal(valid, rv.astype(bool))
+    assert np.array_equal(sim, rs)
