@@ -33,10 +33,14 @@ __device__ __forceinline__ int xoff(int row, int chunk) { return row * ROWB + ((
 
 __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+__device__ __forceinline__ int fac_swz(int row) { return (row >> 1) & 7; }
+
 // Output staging image over the dead x tile: [4 heads][64 rows][64] bf16, 16-B chunk c of
 // row r at slot c ^ (r & 7).  Rows are tokens for q / k and head dims for V^T; either way
 // a head's 64 rows are ONE contiguous 8 KiB block of the destination, written as whole
 // 1 KiB pieces (per-lane 8-B stores at a 128-B row stride touched 32 lines each).
+// (A swizzle on r >> 1, 2-way instead of 4-way bank conflicts on the epilogue's writes,
+// measured no faster.)
 template <int R>
 __device__ __forceinline__ int stage_off(int h, int row, int e) {
     return (h * R + row) * 128 + ((((e >> 3) ^ (row & 7))) << 4) + (e & 7) * 2;
@@ -78,8 +82,9 @@ __device__ __forceinline__ void proj_gemm(const bf16_t* __restrict__ wrow, size_
 // Bias (+ rotary), live-row mask, staging through the dead x tile `lds` and the
 // coalesced copy-out of one R-token tile of part `part` (the caller has barriered after
 // the GEMM's last LDS read).
-// FAC_LDS: the tile's rotary factors sit in LDS at `ecos` / `esin` as [R tokens][32]
-// (resident form) instead of the global [Npad][32] tables.
+// FAC_LDS (resident form): the tile's rotary factors sit in LDS at `ecos` / `esin` as
+// [R tokens][32] instead of the global [Npad][32] tables, `bias` is this part's 256
+// biases in LDS and `live` the tile's R live bytes in LDS (no global load in the epilogue).
 template <bool SELF, int MT, bool FAC_LDS = false>
 __device__ __forceinline__ void proj_epilogue(const f32x16 (&acc)[MT], bool is_v, int part, int m0, int nrow,
                                               char* lds, const float* __restrict__ bias,
@@ -93,7 +98,7 @@ __device__ __forceinline__ void proj_epilogue(const f32x16 (&acc)[MT], bool is_v
         for (int g = 0; g < 4; ++g) {
             const int n = 32 * wave + 8 * g + 4 * hh;  // column within the part
             const int h = n >> 6, d = n & 63;
-            const float4 b = *reinterpret_cast<const float4*>(bias + 256 * part + n);
+            const float4 b = *reinterpret_cast<const float4*>(bias + (FAC_LDS ? 0 : 256 * part) + n);
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
                 const int r = 32 * mt + col, m = min(m0 + r, Npad - 1);  // rows >= Npad: never stored
@@ -105,7 +110,12 @@ __device__ __forceinline__ void proj_epilogue(const f32x16 (&acc)[MT], bool is_v
                     // from global: an LDS-staged copy of the tile's factors gave run-to-run
                     // different q / k on gfx950 (unexplained; tests/test_kernels_gpu.py::
                     // test_lightglue_kernels_deterministic)
-                    const size_t eo = (size_t)(FAC_LDS ? r : m) * 32 + (n & 63) / 2;
+                    // resident form: 16-B chunk c of factor row r sits at chunk c ^ ((r >> 1) & 7)
+                    // (fac_swz), so the 32 rows a wave-instruction reads spread over the banks
+                    // (unswizzled, rows 128 B apart: a 16-way bank conflict per read)
+                    const int j = (n & 63) / 2;
+                    const size_t eo = FAC_LDS ? (size_t)r * 32 + 4 * ((j >> 2) ^ fac_swz(r)) + (j & 3)
+                                              : (size_t)m * 32 + j;
                     const float2 rc = *reinterpret_cast<const float2*>(ecos + eo);
                     const float2 rs = *reinterpret_cast<const float2*>(esin + eo);
                     const float2 e0 = make_float2(rc.x, rs.x), e1 = make_float2(rc.y, rs.y);
@@ -116,20 +126,20 @@ __device__ __forceinline__ void proj_epilogue(const f32x16 (&acc)[MT], bool is_v
                     x0 = r0; x1 = r1; x2 = r2; x3 = r3;
                 }
                 uint2 o = make_uint2(0u, 0u);
-                if (live[m]) o = make_uint2(pack_bf16x2(x0, x1), pack_bf16x2(x2, x3));
+                if (live[FAC_LDS ? r : m]) o = make_uint2(pack_bf16x2(x0, x1), pack_bf16x2(x2, x3));
                 *reinterpret_cast<uint2*>(lds + stage_off<R>(h, r, d)) = o;
             }
         }
     } else {
         const int n = 32 * wave + col, h = n >> 6, d = n & 63;
-        const float b = bias[256 * part + n];
+        const float b = bias[(FAC_LDS ? 0 : 256 * part) + n];
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
                 const int r = 32 * mt + 8 * g + 4 * hh, m = m0 + r;  // 4 consecutive tokens
                 const f32x16& a = acc[mt];
-                const uint32_t lv = r < nrow ? *reinterpret_cast<const uint32_t*>(live + m) : 0u;
+                const uint32_t lv = r < nrow ? *reinterpret_cast<const uint32_t*>(live + (FAC_LDS ? r : m)) : 0u;
                 const float v0 = (lv & 0xff) ? a[4 * g] + b : 0.f;
                 const float v1 = (lv & 0xff00) ? a[4 * g + 1] + b : 0.f;
                 const float v2 = (lv & 0xff0000) ? a[4 * g + 2] + b : 0.f;
@@ -246,13 +256,15 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
                                                        const float* __restrict__ esin,
                                                        const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
                                                        bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad,
-                                                       int slots) {
+                                                       int slots, int probe) {
     constexpr int N = SELF ? 768 : 512, NPART = SELF ? 3 : 2, R = 64;
     // per buffer: x tile (32 KiB; the output staging image overlays it), then for the
     // self block the tile's rotary factors cos / sin [64][32] f32 (8 KiB each)
     constexpr int XB = R * ROWB, BUF = XB + (SELF ? 2 * R * 32 * 4 : 0);
-    __shared__ __attribute__((aligned(16))) char buf0[BUF];
-    __shared__ __attribute__((aligned(16))) char buf1[BUF];
+    // + the tile's R live bytes (LDS-DMA with the tile)
+    __shared__ __attribute__((aligned(16))) char buf0[BUF + R];
+    __shared__ __attribute__((aligned(16))) char buf1[BUF + R];
+    __shared__ __attribute__((aligned(16))) float bias_l[256];  // this part's biases
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 31, hh = lane >> 5;
     const int xcd = (int)blockIdx.x & 7, j = (int)blockIdx.x >> 3;
     const int part = j % NPART, slot = j / NPART;
@@ -260,6 +272,7 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
     int t = xcd + 8 * slot;
     if (slot >= slots || t >= ntiles) return;
     const bool is_v = part == NPART - 1;
+    if (threadIdx.x < 256) bias_l[threadIdx.x] = bias[256 * part + threadIdx.x];  // read after the loop-top barrier
     bf16x8 wf[16];
     {
         const bf16_t* wrow = W + (size_t)(256 * part + 32 * wave + col) * 16 + 8 * hh;
@@ -275,12 +288,19 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
             const int row = drow + 2 * i;
             dma16(xcopy + (size_t)(tile * R + row) * ldx + ((dslot ^ (row & 15)) * 8), base + 1024 * i);
         }
-        if (SELF) {  // 8 KiB of cos and of sin: one 1 KiB piece of each per wave
+        if (probe & 4) return;
+        // (the v part fetches them too: skipping that measured slower, 1.92 vs 1.71 ms at 2 M
+        // tokens; probably the three parts of a tile then drift apart and lose the L2 reuse)
+        if (SELF && !(probe & 8)) {  // 8 KiB of cos and of sin: one 1 KiB piece of each per wave
             const unsigned fb = lds_addr(buf) + XB + 1024 * wave;
-            const size_t fo = (size_t)tile * R * 32 + 256 * wave + 4 * lane;
+            // lane -> LDS row 8 w + (lane >> 3), chunk lane & 7, filled from chunk
+            // (lane & 7) ^ fac_swz(row) of the global row
+            const int frow = 8 * wave + (lane >> 3);
+            const size_t fo = (size_t)(tile * R + frow) * 32 + 4 * ((lane & 7) ^ fac_swz(frow));
             dma16(ecos + fo, fb);
             dma16(esin + fo, fb + R * 32 * 4);
         }
+        if (wave == 0 && lane < R / 16) dma16(live + (size_t)tile * R + 16 * lane, lds_addr(buf) + BUF);
     };
     issue(t, buf0);
     for (int it = 0;; ++it) {
@@ -288,7 +308,8 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
         char* nxt = (it & 1) ? buf0 : buf1;
         // this wave's DMA of tile t has landed: vector-memory operations retire in issue
         // order, and the only ones issued after that DMA are the previous tile's four
-        // copy-out stores per lane, which may stay in flight (vmcnt counts stores too)
+        // copy-out stores per lane, which may stay in flight (vmcnt counts stores too;
+        // the epilogue issues no global load)
         if (it == 0) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         else __builtin_amdgcn_s_waitcnt(0x0F74);          // vmcnt(4)
         __syncthreads();  // ... and every other wave's
@@ -299,11 +320,14 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
-        if (is_v) res_gemm<true>(wf, cur, acc);
-        else res_gemm<false>(wf, cur, acc);
+        if (!(probe & 1)) {
+            if (is_v) res_gemm<true>(wf, cur, acc);
+            else res_gemm<false>(wf, cur, acc);
+        }
         __syncthreads();  // every wave has read the x tile
         const float* fc = reinterpret_cast<const float*>(cur + XB);
-        proj_epilogue<SELF, 2, true>(acc, is_v, part, t * R, R, cur, bias, fc, fc + R * 32, live, Q, K, Vt, Npad);
+        if (!(probe & 2)) proj_epilogue<SELF, 2, true>(acc, is_v, part, t * R, R, cur, bias_l, fc, fc + R * 32,
+                                     reinterpret_cast<const uint8_t*>(cur + BUF), Q, K, Vt, Npad);
         if (tn >= ntiles) break;
         t = tn;
     }
@@ -335,17 +359,22 @@ int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, 
                 return 256;
             return c;
         }();
+        // timing probes only (results wrong): 1 no GEMM, 2 no epilogue, 4 no DMA, 8 no factor DMA
+        static const int probe = [] {
+            const char* v = getenv("MLG_PROJ_PROBE");
+            return v ? atoi(v) : 0;
+        }();
         const int npart = self_block ? 3 : 2, ntiles = Npad / 64;
         // one workgroup per CU (256 VGPRs, 64-96 KiB LDS), `slots` part-groups per XCD
         const int slots = std::max(1, std::min((cus / 8) / npart, (ntiles + 7) / 8));
         const unsigned grid = (unsigned)(8 * slots * npart);
         if (self_block)
             hipLaunchKernelGGL(k_lg_proj_res<true>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin, live,
-                               Q, K, Vt, Npad, slots);
+                               Q, K, Vt, Npad, slots, probe);
         else
             hipLaunchKernelGGL(k_lg_proj_res<false>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias,
                                (const float*)nullptr, (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad,
-                               slots);
+                               slots, probe);
         MLG_LAUNCH_CHECK();
         return MLG_OK;
     }
