@@ -86,13 +86,14 @@ __device__ __forceinline__ void proj_gemm(const bf16_t* __restrict__ wrow, size_
 // [R tokens][32] instead of the global [Npad][32] tables, `bias` is this part's 256
 // biases in LDS and `live` the tile's R live bytes in LDS (no global load in the epilogue).
 template <bool SELF, int MT, bool FAC_LDS = false>
-__device__ __forceinline__ void proj_epilogue(const f32x16 (&acc)[MT], bool is_v, int part, int m0, int nrow,
+__device__ __forceinline__ void proj_epilogue(const f32x16 (&acc)[MT], bool is_v, int part, int m0, int nrow_,
                                               char* lds, const float* __restrict__ bias,
                                               const float* __restrict__ ecos, const float* __restrict__ esin,
                                               const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
                                               bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad) {
     constexpr int R = 32 * MT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
+    const int nrow = nrow_ & 0xffff;  // bit 16: timing probe, no copy-out
     if (!is_v) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -156,7 +157,7 @@ __device__ __forceinline__ void proj_epilogue(const f32x16 (&acc)[MT], bool is_v
 #pragma unroll
     for (int p = 0; p < R / 16; ++p) {
         const int L = p * 512 + tid, h = L / (8 * R), row = (L >> 3) % R, c = L & 7;
-        if (row < nrow)
+        if (row < nrow && !(nrow_ >> 16))
             *reinterpret_cast<uint4*>(dst + ((size_t)h * Npad + m0 + row) * 64 + c * 8) =
                 *reinterpret_cast<const uint4*>(lds + stage_off<R>(h, row, 8 * c));
     }
@@ -326,7 +327,7 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
         }
         __syncthreads();  // every wave has read the x tile
         const float* fc = reinterpret_cast<const float*>(cur + XB);
-        if (!(probe & 2)) proj_epilogue<SELF, 2, true>(acc, is_v, part, t * R, R, cur, bias_l, fc, fc + R * 32,
+        if (!(probe & 2)) proj_epilogue<SELF, 2, true>(acc, is_v, part, t * R, R | ((probe & 16) << 12), cur, bias_l, fc, fc + R * 32,
                                      reinterpret_cast<const uint8_t*>(cur + BUF), Q, K, Vt, Npad);
         if (tn >= ntiles) break;
         t = tn;
@@ -359,7 +360,8 @@ int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, 
                 return 256;
             return c;
         }();
-        // timing probes only (results wrong): 1 no GEMM, 2 no epilogue, 4 no DMA, 8 no factor DMA
+        // timing probes only (results wrong): 1 no GEMM, 2 no epilogue, 4 no DMA, 8 no factor DMA,
+        // 16 no copy-out stores
         static const int probe = [] {
             const char* v = getenv("MLG_PROJ_PROBE");
             return v ? atoi(v) : 0;
