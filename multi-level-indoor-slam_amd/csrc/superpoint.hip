@@ -92,8 +92,14 @@ template <int CIN, int COUT_T, bool POOL>
 __global__ __launch_bounds__(512) void k_conv3x3(const bf16_t* __restrict__ in, const bf16_t* __restrict__ wt,
                                                  const float* __restrict__ bias, bf16_t* __restrict__ out, int H,
                                                  int W, int Cout, int tiles_x) {
-    constexpr int HS = CIN * 2 + 16;      // halo pixel stride (bytes), +16 breaks bank aliasing
-    constexpr int BS = KC * 2 + 16;       // weight row stride (bytes)
+    // Row strides padded by 32 B (an odd multiple of 32 B in all): a ds_read_b128 lane group
+    // ({0-3,12-15,20-27}, ... -- MI355X_MICROARCH.md LDS table) covers the 16 pixel columns
+    // once with k-chunk a for 8 of them and a + 1 for the other 8; at 16-B chunk stride s
+    // (mod 16) the slots (col * s + chunk) mod 16 are all distinct for s = 2 mod 4, while the
+    // former +16 B padding (s odd) left 2-way bank conflicts on every halo and weight read
+    // (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.44, profiles/r02p_pmc_lightglue.txt)
+    constexpr int HS = CIN * 2 + 32;      // halo pixel stride (bytes)
+    constexpr int BS = KC * 2 + 32;       // weight row stride (bytes)
     constexpr int NT = COUT_T / 16;       // N-tiles (output channels) per wave
     constexpr int STEPS = 9 * (CIN / KC);
     constexpr int HALO_BYTES = HALO * HALO * HS;
