@@ -42,7 +42,9 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md, no spa
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 SLOTS = {0: "vit_fc1_gemm", 1: "vit_fc2_gemm", 2: "vit_qkv_gemm", 3: "vit_proj_gemm", 4: "vit_attention",
          5: "lightglue_attention", 6: "lightglue_qkv_gemms", 7: "superpoint_conv3x3", 8: "lightglue_ffn_fused"}
-HBM_SLOTS = {8}  # slots whose recorded work is algorithmic HBM bytes (bound "hbm"), not FLOPs
+# slots whose recorded work is algorithmic HBM bytes (bound "hbm"), not FLOPs: none since
+# the fused FFN (slot 8, 256 FLOP per HBM byte, at the ridge) is priced in FLOPs
+HBM_SLOTS = set()
 ISEC_K = np.array([[893.63, 0.0, 376.95], [0.0, 893.97, 266.57], [0.0, 0.0, 1.0]])  # cam1, SURVEY §8
 
 

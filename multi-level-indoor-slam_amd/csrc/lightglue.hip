@@ -869,7 +869,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
                 LG_TRY(mlg_attention_varlen(Q, K, VT, CTX, LG_D, NpadF, LG_H, TASKS, OUTOFF, nf, maxqf, s));
             }
             {
-                MlgProfScope prof(8, s, 3584.0 * tok);
+                MlgProfScope prof(8, s, 917504.0 * tok);
                 LG_TRY(mlg_lg_ffn(CTX, X2, CAT2, 512, NpadF, w.self[0], s, nullptr));
             }
             self0_done = true;
@@ -905,9 +905,12 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     // out_proj / to_out + FFN + residual, fused (lg_ffn.hip)
     // (conf: the layer's token-confidence / matchability heads, fused into the tail)
     auto ffn = [&](const mlg_lg_block_i& bw, const mlg_lg_conf_i* conf) -> int {
-        // algorithmic HBM bytes per live token: ctx + bf16 x in (512 + 512), f32 x read +
-        // written (1024 + 1024), bf16 x copy written (512)
-        MlgProfScope prof(8, s, 3584.0 * live_tokens());
+        // algorithmic FLOPs per live token: 2 (256 x 256 + 512 x 512 + 256 x 512) = 917,504.
+        // Its HBM bytes per token (ctx + bf16 x in 512 + 512, f32 x read + written 1024 +
+        // 1024, bf16 x copy 512 = 3,584) give 256 FLOP/B, near the ridge (2.5 PF / 8 TB/s =
+        // 312): the three GEMM phases, not HBM, bound it, so the slot is
+        // priced against the MFMA peak
+        MlgProfScope prof(8, s, 917504.0 * live_tokens());
         return mlg_lg_ffn(CTX, X, CAT, 512, Npad, bw, s, conf);
     };
     // assignment + filter of the listed segment pairs (k = index of image a's segment)
