@@ -97,7 +97,8 @@ int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, 
  * desc: float32 [N, D]; t: float64 [N]; floor: int64 [N]; has_floor: uint8 [N]
  * (0 = floor_label None).  Outputs (device): idx int32 [Q, k], sim float32 [Q, k],
  * valid uint8 [Q, k], count int32 [Q] (entries per row, in emission order);
- * totals uint64[2] (+= valid, rejected) or NULL.  1 <= k <= 256.
+ * totals uint64[2] (+= valid, rejected) or NULL.  1 <= k <= 4096 (k > 256: a per-row
+ * radix select over (similarity, index) keys).
  */
 size_t mlg_knn_workspace_bytes(int N, int D, int Q);
 /* Workspace for a given k, for mlg_knn_gate (query = 0) or mlg_knn_query (query = 1):

@@ -182,3 +182,31 @@ def test_large_k_radix_select(dev, k, gating):
     assert np.array_equal(q, rq) and np.array_equal(m, rm)
     assert np.array_equal(valid, rv.astype(bool))
     assert np.array_equal(sim, rs)
+
+
+@pytest.mark.parametrize("k", [300, 1000])
+def test_query_large_k(dev, k):
+    """query() with k > 256 (k_topk_large): the first 256 entries equal the k = 256 path
+    bit for bit, the sorted similarities match the oracle's within SIM_TOL, the order is
+    (similarity desc, index desc), and the count is every unmasked entry up to k."""
+    from oracle import retrieval as oret
+    rng = np.random.default_rng(7 + k)
+    n = 1500
+    db = rng.standard_normal((n, 64)).astype(np.float32)
+    q = rng.standard_normal(64).astype(np.float32)
+    t = np.arange(n, dtype=np.float64) * 0.7
+    ts, gap = 300.0, 10.0
+    dbd = torch.from_numpy(db).to(dev)
+    tdb = torch.from_numpy(t).to(dev)
+    qd = torch.from_numpy(q[None]).to(dev)
+    tq = torch.tensor([ts], dtype=torch.float64, device=dev)
+    idx, sim, cnt = retrieval.knn_query(dbd, qd, tdb, tq, gap, k)
+    i2, s2, c2 = retrieval.knn_query(dbd, qd, tdb, tq, gap, 256)
+    c = int(cnt[0])
+    idx, sim = idx[0, :c].cpu().numpy(), sim[0, :c].cpu().numpy()
+    ro, rs = oret.query(db, q, t, ts, k, gap)
+    assert c == len(ro) == min(k, int((np.abs(t - ts) >= gap).sum()))
+    assert np.array_equal(idx[:256], i2[0, :256].cpu().numpy()) and np.array_equal(sim[:256], s2[0, :256].cpu().numpy())
+    assert np.max(np.abs(sim - rs)) <= SIM_TOL
+    assert np.all((sim[:-1] > sim[1:]) | ((sim[:-1] == sim[1:]) & (idx[:-1] > idx[1:])))
+    assert len(set(idx.tolist())) == c and np.all(np.abs(t[idx] - ts) >= gap)
