@@ -1,4 +1,5 @@
 #!/bin/bash
+# (The MLGATE_LG_THREADS branch this script exercised was removed after the A/B; see profiles/r02r_ab_lightglue_threads.txt.)
 # Same-box A/B: LightGlue chunks on 2 host threads / streams (MLGATE_LG_THREADS=2) vs 1;
 # the full-gate GPU tests under both settings first.
 set -u
