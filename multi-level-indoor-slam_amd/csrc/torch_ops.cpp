@@ -1,3 +1,4 @@
+#include <cstdlib>
 // PyTorch-ROCm custom operators over the mlgate C ABI (include/mlgate.h).
 //
 // TORCH_LIBRARY(mlgate, m) declares one operator per ABI entry point the Python
@@ -49,7 +50,15 @@ T* mp(const Tensor& t) {
 }
 
 Tensor workspace(size_t bytes, const Tensor& like) {
-    return at::empty({(int64_t)std::max<size_t>(bytes, 1)}, like.options().dtype(at::kByte));
+    Tensor t = at::empty({(int64_t)std::max<size_t>(bytes, 1)}, like.options().dtype(at::kByte));
+    // diagnostic (MLG_WS_POISON=1): every workspace starts as all-ones bytes (NaN in f32 /
+    // bf16), so a kernel that reads workspace it never wrote shows up as changed results
+    static const bool poison = [] {
+        const char* v = getenv("MLG_WS_POISON");
+        return v && atoi(v) != 0;
+    }();
+    if (poison) t.fill_(255);
+    return t;
 }
 
 // ------------------------------------------------------------------ ViT-B/14
