@@ -12,6 +12,7 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
 
 SLOT_KERNELS = {"lightglue_attention": "k_attention_varlen", "lightglue_ffn_fused": "k_lg_ffn",
@@ -35,13 +36,14 @@ def main():
                 write += d.get("WRITE_SIZE", [])
         if not fetch or not write:
             continue
+        pairs = int(os.environ.get("PAIRS", "4096"))
         fb = 2.0 * 1024 * sum(fetch) / len(fetch)
         wb = 1024.0 * sum(write) / len(write)
         res[slot] = {"kernel": pat.rstrip("("), "dispatches": len(fetch), "fetch_bytes_per_launch": round(fb),
                      "write_bytes_per_launch": round(wb), "bytes_per_launch": round(fb + wb),
                      "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of "
-                               "tools/lg_bench.py --iters 1 --pairs 1024 (one 1024-pair LightGlue call = bench.py's "
-                               "lg_chunk); FETCH_SIZE x2 (gfx950)"}
+                               f"tools/lg_bench.py --iters 1 --pairs {pairs} (one {pairs}-pair LightGlue call = "
+                               "bench.py's lg_chunk); FETCH_SIZE x2 (gfx950)"}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))

@@ -1,7 +1,7 @@
 #!/bin/bash
 # HBM traffic per launch of the LightGlue kernels: two PMC passes (FETCH_SIZE, WRITE_SIZE;
 # never combined with tracing), each its own rocprofv3 run of tools/lg_bench.py (one
-# 1024-pair LightGlue call = bench.py's lg_chunk; a --pmc pass over the whole bench
+# $PAIRS-pair LightGlue call = bench.py's lg_chunk; a --pmc pass over the whole bench
 # segfaulted inside the profiler), then tools/pmc_traffic.py writes
 # profiles/pmc_traffic.json (bench.py's roofline.traffic).
 set -u
@@ -13,7 +13,7 @@ i=0
 for pass in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
   timeout -s KILL 200 rocprofv3 --pmc $pass --output-format csv -d "$OUT/pass$i" -o run -- \
-      python3 "$REPO/tools/lg_bench.py" --iters 1 --pairs 1024 > "$OUT/pass$i.log" 2>&1
+      python3 "$REPO/tools/lg_bench.py" --iters 1 --pairs ${PAIRS:-4096} --frames ${FRAMES:-1024} > "$OUT/pass$i.log" 2>&1
   rc=$?; echo "pass $i ($pass) rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
