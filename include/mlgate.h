@@ -308,6 +308,21 @@ int mlg_lg_orient_matches(const int32_t* matches, const float* scores, const int
                           const int32_t* rows, const uint8_t* swap, int P, int kmax, int32_t* matches_out,
                           float* scores_out, int32_t* num_out, void* stream);
 
+/* Diagnostics (tools/lg_determinism.py; no reference counterpart): between _begin and
+ * _end, the CALLING THREAD's mlg_lightglue calls append, after every stage, one 64-bit
+ * hash per 64-row tile of the buffer the stage wrote into dev_buf (uint64 words, device
+ * memory).  _end returns the number of stages recorded (tags[i] = layer * 100 + stage,
+ * layer 99 = layer 0's per-frame self block; counts[i] = its hashes, in buffer order)
+ * or MLG_ENOMEM if dev_buf was too small. */
+int mlg_dbg_lg_trace_begin(void* dev_buf, size_t bytes);
+int mlg_dbg_lg_trace_end(int32_t* tags, int32_t* counts, int max_entries);
+/* Diagnostics (tools/ffn_interference.py): fill every CU's 160 KiB of LDS (sink: a device
+ * int32 [256] scratch that is never written for patterns other than 0x12345679), or every
+ * SIMD's 512 VGPRs + AGPRs, with `pattern` -- a kernel launched next on `stream` that
+ * reads LDS or registers it never wrote then shows pattern-dependent results. */
+int mlg_dbg_fill_lds(uint32_t pattern, void* sink, void* stream);
+int mlg_dbg_fill_regs(uint32_t pattern, void* stream);
+
 /* --------------------------------------------------------- SuperGlue --
  * The SuperGlue matcher of the reference's SuperGlue class configuration
  * (geometric_verification.py:385-399: weights 'indoor', sinkhorn_iterations 20,

@@ -329,12 +329,14 @@ __device__ __forceinline__ unsigned lds_addr(char* p) { return (unsigned)(uintpt
 // Issued through inline asm so hipcc's waitcnt pass does not conservatively drain
 // vmcnt(0) before every fragment read of the other stages; all waits on these DMAs
 // are the explicit counted s_waitcnt vmcnt of the pipeline.
+// `s_nop 0`: the SALU-write-M0 -> LDS-DMA-read-M0 wait state, which hipcc pads for the
+// builtin but not for an asm statement (it puts its s_mov_b32 m0 directly in front).
 __device__ __forceinline__ void dma16(const void* g, unsigned m0) {
-    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
 }
 // Same with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset.
 __device__ __forceinline__ void dma16s(unsigned voff, const void* sbase, unsigned m0) {
-    asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "{m0}"(m0) : "memory");
 }
 
 template <int BK>

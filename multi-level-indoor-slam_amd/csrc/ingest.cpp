@@ -18,6 +18,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <climits>
+#include <exception>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -204,6 +206,9 @@ int decode_into(const uint8_t* d, size_t n, uint8_t* out, int H, int W) {
         }
         if (pw[k] && ph[k]) raw_total += ph[k] * (row_bytes(p, pw[k]) + 1);
     }
+    // one inflate call: zlib's avail_in / avail_out are uInt, so neither side may pass 4 GiB
+    // (a 65536 x 65536 16-bit RGBA header would ask for 32 GiB)
+    if (raw_total > UINT_MAX || p.idat.size() > UINT_MAX) return MLG_ENOMEM;
     std::vector<uint8_t> raw(raw_total);
     z_stream zs{};
     if (inflateInit(&zs) != Z_OK) return MLG_ENOMEM;
@@ -254,6 +259,17 @@ bool read_file(const char* path, std::vector<uint8_t>& buf) {
     return ok;
 }
 
+// A failed allocation (std::bad_alloc / length_error from the vectors of one file)
+// becomes that file's status instead of std::terminate inside a pool thread.
+template <class F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::exception&) {
+        return MLG_ENOMEM;
+    }
+}
+
 template <class F>
 void pool(int n, int threads, F&& job) {
     threads = std::max(1, std::min(threads, n));
@@ -288,7 +304,7 @@ int mlg_png_decode_bgr(const uint8_t* const* data, const size_t* lens, int n, ui
                        int threads, int32_t* status) {
     if (n < 0 || H <= 0 || W <= 0 || (n && (!data || !lens || !out || !status))) return MLG_EINVAL;
     const size_t frame = (size_t)H * W * 3;
-    pool(n, threads, [&](int i) { status[i] = decode_into(data[i], lens[i], out + frame * i, H, W); });
+    pool(n, threads, [&](int i) { status[i] = guarded([&] { return decode_into(data[i], lens[i], out + frame * i, H, W); }); });
     return MLG_OK;
 }
 
@@ -296,9 +312,10 @@ int mlg_png_load_bgr(const char* const* paths, int n, uint8_t* out, int H, int W
     if (n < 0 || H <= 0 || W <= 0 || (n && (!paths || !out || !status))) return MLG_EINVAL;
     const size_t frame = (size_t)H * W * 3;
     pool(n, threads, [&](int i) {
-        std::vector<uint8_t> buf;
-        status[i] = read_file(paths[i], buf) ? decode_into(buf.data(), buf.size(), out + frame * i, H, W)
-                                             : MLG_EINVAL;
+        status[i] = guarded([&] {
+            std::vector<uint8_t> buf;
+            return read_file(paths[i], buf) ? decode_into(buf.data(), buf.size(), out + frame * i, H, W) : MLG_EINVAL;
+        });
     });
     return MLG_OK;
 }

@@ -222,8 +222,13 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
 // HBM once and from that XCD's L2 by the other parts.
 typedef __attribute__((address_space(3))) char lds_char;
 __device__ __forceinline__ unsigned lds_addr(char* p) { return (unsigned)(uintptr_t)(lds_char*)p; }
+// The `s_nop 0` is the SALU-write-M0 -> LDS-DMA-read-M0 wait state (gfx9 family): hipcc
+// sets M0 for the "{m0}" operand with an s_mov_b32 placed directly in front of the
+// statement and pads hazards only for instructions it models, not for asm.  Without it
+// the DMA could take the previous piece's M0 and land 1 KiB in the wrong slot, depending
+// on issue timing (run-to-run / co-scheduling dependent results: DESIGN.md §5, r03a).
 __device__ __forceinline__ void dma16(const void* g, unsigned m0) {
-    asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m0) : "memory");
 }
 
 template <bool SWAP>

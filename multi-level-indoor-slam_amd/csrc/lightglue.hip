@@ -238,6 +238,7 @@ struct Asg {
     int m, n, ra, rb;  // rows of image a / b, their first layout rows
     long soff;         // S offset (floats)
     int pair, ld;      // pair index, S row stride (n rounded up to 4: float4 rows)
+    int lo_first, pad; // image a's frame index > image b's: k_asg_sim's cross-term order
 };
 
 constexpr int SBM = 128;               // k_asg_sim tile (rows = columns)
@@ -310,8 +311,20 @@ __global__ __launch_bounds__(256, 2) void k_asg_sim(const Asg* __restrict__ tab,
         for (int x = 0; x < 2; ++x)
 #pragma unroll
             for (int y = 0; y < 2; ++y) {
-                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb][x], bl[cb][y], acc[x][y], 0, 0, 0);
-                acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cb][x], bh[cb][y], acc[x][y], 0, 0, 0);
+                // the two cross terms in a canonical order: hi of the lower frame's image x lo
+                // of the other first, whichever side it is on.  The swapped call (b, a) then
+                // adds the same products in the same order to every element, so S(b, a) is
+                // S(a, b)^T bit for bit and LightGlue(b, a) is exactly swap(LightGlue(a, b))
+                // -- what lets the full gate match each unordered pair once (pipeline.py).
+                // (A fixed ah.bl-then-al.bh order rounded the swapped call's cross terms the
+                // other way round: 1 of 1024 reverse pairs kept a different match, r02k.)
+                if (!a.lo_first) {
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb][x], bl[cb][y], acc[x][y], 0, 0, 0);
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cb][x], bh[cb][y], acc[x][y], 0, 0, 0);
+                } else {
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[cb][x], bh[cb][y], acc[x][y], 0, 0, 0);
+                    acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb][x], bl[cb][y], acc[x][y], 0, 0, 0);
+                }
                 acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[cb][x], bh[cb][y], acc[x][y], 0, 0, 0);
             }
     }
@@ -641,6 +654,65 @@ __global__ __launch_bounds__(256) void k_lg_gather_rows(const int4* __restrict__
 
 size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// ------------------------------------------------------------------ debug trace
+// mlg_dbg_lg_trace_begin / _end (include/mlgate.h): the calling thread's mlg_lightglue
+// calls append, after every stage, one 64-bit hash per 64-row tile of the buffer the
+// stage wrote (planes x tiles of tile_bytes), so two runs can be compared stage by stage.
+struct LgTrace {
+    uint64_t* buf = nullptr;
+    size_t cap = 0, used = 0;
+    bool overflow = false;
+    std::vector<int> tags, counts;
+};
+thread_local LgTrace* t_trace = nullptr;
+
+// tile t = rows [t * rpt, (t + 1) * rpt) of each plane; row r's first row_bytes bytes
+// (a multiple of 4) at base + plane * plane_stride + r * row_stride; rows with
+// live[r] == 0 skipped when `live` is given (padding rows hold stale workspace)
+__global__ __launch_bounds__(256) void k_dbg_hash(const uint8_t* __restrict__ base, int rpt, int row_bytes,
+                                                  size_t row_stride, int planes, size_t plane_stride,
+                                                  const uint8_t* __restrict__ live, uint64_t* __restrict__ out) {
+    const int wpr = row_bytes / 4, words = rpt * wpr;
+    uint64_t h = 0;
+    for (int p = 0; p < planes; ++p)
+        for (int i = threadIdx.x; i < words; i += 256) {
+            const size_t r = (size_t)blockIdx.x * rpt + i / wpr;
+            if (live && !live[r]) continue;
+            uint64_t w = *reinterpret_cast<const uint32_t*>(base + p * plane_stride + r * row_stride + (i % wpr) * 4);
+            w ^= (uint64_t)((size_t)p * words + i + 1) * 0x9E3779B97F4A7C15ull;
+            w ^= w >> 33;
+            w *= 0xff51afd7ed558ccdull;
+            w ^= w >> 33;
+            w *= 0xc4ceb9fe1a85ec53ull;
+            w ^= w >> 33;
+            h += w;
+        }
+    __shared__ uint64_t sh[256];
+    sh[threadIdx.x] = h;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = sh[0];
+}
+
+// tag = layer * 100 + stage (layer 99: layer 0's self block on the frame layout)
+void trace(int tag, const void* base, int rpt, int row_bytes, size_t row_stride, int planes, size_t plane_stride,
+           int ntiles, hipStream_t s, const uint8_t* live = nullptr) {
+    LgTrace* t = t_trace;
+    if (!t || ntiles <= 0 || row_bytes < 4) return;
+    if (t->used + (size_t)ntiles > t->cap) {
+        t->overflow = true;
+        return;
+    }
+    hipLaunchKernelGGL(k_dbg_hash, dim3((unsigned)ntiles), dim3(256), 0, s, (const uint8_t*)base, rpt, row_bytes & ~3,
+                       row_stride, planes, plane_stride, live, t->buf + t->used);
+    t->used += ntiles;
+    t->tags.push_back(tag);
+    t->counts.push_back(ntiles);
+}
+
 struct LgLayout {
     size_t x, cat, ecos, esin, ind, x2, cat2, ecos2, esin2, ind2, Q, K, Vt, ctx, hf, hb, live, rowseg, lz, keep,
         stats, segs, tasks, outoff, moves, mdesc, rmax, rlog, cmax, clog, arg, val, part, asg, norm, S, total;
@@ -754,6 +826,20 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     float2* PART = (float2*)(base + L.part);
     Asg* ASG = (Asg*)(base + L.asg);
     float* SS = (float*)(base + L.S);
+    // debug trace (mlg_dbg_lg_trace_begin): per-stage hashes of 64-row tiles
+    // live rows only (LIVE is the current layout's mask); byte-per-row buffers as 64-B tiles
+    auto tr_rows = [&](int tag, const void* p, size_t row_bytes, int np, size_t stride = 0) {
+        if (!t_trace) return;
+        if (row_bytes < 4) trace(tag, p, 1, 64, 64, 1, 0, np / 64, s);
+        else trace(tag, p, 64, (int)row_bytes, stride ? stride : row_bytes, 1, 0, np / 64, s, LIVE);
+    };
+    auto tr_heads = [&](int tag, const void* p, int np) {  // Q / K / V^T: [4 heads][np rows][64] bf16
+        if (t_trace) trace(tag, p, 64, 128, 128, 4, (size_t)np * 128, np / 64, s);
+    };
+    auto tr_tab = [&](int tag, const void* p, size_t bytes) {
+        if (t_trace && bytes >= 4) trace(tag, p, 1, (int)bytes, 0, 1, 0, 1, s);
+    };
+    int tl = 0;  // layer of the next table upload (trace tags)
 
     // Host tables below are uploaded with hipMemcpyAsync on `s` and only rewritten after
     // the stream has been synchronised (the per-layer statistics read-back, and one final
@@ -809,6 +895,10 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         hipLaunchKernelGGL(k_lg_live, dim3((Npad + 255) / 256), dim3(256), 0, s, SEGS, (int)segs.size(), LIVE, ROWSEG,
                            Npad);
         MLG_LAUNCH_CHECK();
+        tr_tab(tl * 100 + 3, SEGS, segs.size() * sizeof(Seg));
+        tr_tab(tl * 100 + 4, TASKS, h_tasks.size() * sizeof(int4));
+        tr_tab(tl * 100 + 5, OUTOFF, h_out.size() * sizeof(int));
+        tr_rows(tl * 100 + 6, LIVE, 1, Npad);
         return MLG_OK;
     };
     // Layer 0's self block reads one image only (its tokens, its positional encoding), so
@@ -860,18 +950,28 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
             hipLaunchKernelGGL(k_lg_init, dim3((unsigned)((kmax + 63) / 64), (unsigned)nf), dim3(256), 0, s, SEGS,
                                (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X2, CAT2, EC2, ES2, IND2);
             MLG_LAUNCH_CHECK();
+            tr_tab(9903, SEGS, fsegs.size() * sizeof(Seg));
+            tr_tab(9904, TASKS, f_tasks.size() * sizeof(int4));
+            tr_rows(9901, X2, LG_D * 4, NpadF);
+            tr_rows(9902, CAT2, 512, NpadF, 1024);
             {
                 MlgProfScope prof(6, s, 2.0 * tok * 768 * 256);
                 LG_TRY(mlg_lg_proj(true, CAT2, 512, w.self[0].Wqkv, w.self[0].bqkv, EC2, ES2, LIVE, Q, K, VT, NpadF, s));
             }
+            tr_heads(9910, Q, NpadF);
+            tr_heads(9911, K, NpadF);
+            tr_heads(9912, VT, NpadF);
             {
                 MlgProfScope prof(5, s, work);
                 LG_TRY(mlg_attention_varlen(Q, K, VT, CTX, LG_D, NpadF, LG_H, TASKS, OUTOFF, nf, maxqf, s));
             }
+            tr_rows(9913, CTX, 512, NpadF);
             {
                 MlgProfScope prof(8, s, 917504.0 * tok);
                 LG_TRY(mlg_lg_ffn(CTX, X2, CAT2, 512, NpadF, w.self[0], s, nullptr));
             }
+            tr_rows(9914, X2, LG_D * 4, NpadF);
+            tr_rows(9915, CAT2, 512, NpadF, 1024);
             self0_done = true;
         }
     }
@@ -885,6 +985,8 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
                            MOVES, X2, CAT2, X, CAT);
         MLG_LAUNCH_CHECK();
     }
+    tr_rows(1, X, LG_D * 4, Npad);
+    tr_rows(2, CAT, 512, Npad, 1024);
 
     auto live_tokens = [&]() {
         double t = 0;
@@ -918,6 +1020,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         // mdesc = final_proj(x) for every token, as bf16 hi + lo; the 1/4 per side folds into S / 16
         LG_TRY(mlg_gemm_bias_split_bf16(CAT, 512, w.Wfinal[i], w.bfinal[i], MDH, MDH + (size_t)Npad * LG_D, Npad, LG_D,
                                          LG_D, s));
+        if (t_trace) trace(i * 100 + 40, MDH, 64, 32, 32, 32, (size_t)Npad * 32, Npad / 64, s);
         // one table upload for all chunks (the per-layer statistics read-back orders its
         // reuse), so chunks follow each other without a host round trip
         h_asg.clear();
@@ -931,11 +1034,14 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
             a.soff = (long)(c % L.asg_cap) * kmax * ((kmax + 3) & ~3);
             a.pair = pair_of[ks[c] / 2];
             a.ld = (sb.len + 3) & ~3;
+            a.lo_first = sa.frame > sb.frame;
+            a.pad = 0;
             h_asg.push_back(a);
             if (stop_layer) stop_layer[a.pair] = i + 1;
         }
         if (hipMemcpyAsync(ASG, h_asg.data(), h_asg.size() * sizeof(Asg), hipMemcpyHostToDevice, s) != hipSuccess)
             return MLG_EHIP;
+        tr_tab(i * 100 + 41, ASG, h_asg.size() * sizeof(Asg));
         for (size_t c0 = 0; c0 < ks.size(); c0 += L.asg_cap) {
             const size_t c1 = std::min(ks.size(), c0 + L.asg_cap);
             int maxm = 0, maxn = 0;
@@ -969,8 +1075,14 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
                 MlgProfScope prof(6, s, 2.0 * live_tokens() * 768 * 256);
                 LG_TRY(mlg_lg_proj(true, CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, s));
             }
+            tr_heads(i * 100 + 10, Q, Npad);
+            tr_heads(i * 100 + 11, K, Npad);
+            tr_heads(i * 100 + 12, VT, Npad);
             LG_TRY(attention(false));
+            tr_rows(i * 100 + 13, CTX, 512, Npad);
             LG_TRY(ffn(w.self[i], nullptr));
+            tr_rows(i * 100 + 14, X, LG_D * 4, Npad);
+            tr_rows(i * 100 + 15, CAT, 512, Npad, 1024);
         }
         // cross block
         {
@@ -978,13 +1090,24 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
             LG_TRY(mlg_lg_proj(false, CAT, 512, w.cross[i].Wqkv, w.cross[i].bqkv, nullptr, nullptr, LIVE, Q, nullptr, VT,
                                Npad, s));
         }
+        tr_heads(i * 100 + 20, Q, Npad);
+        tr_heads(i * 100 + 21, VT, Npad);
         LG_TRY(attention(true));
+        tr_rows(i * 100 + 22, CTX, 512, Npad);
         // layer i's heads on the updated tokens: matchability log-sigmoid (the assignment's
         // certainty term) and, before the last layer, confidences + early-stop / prune flags
         const bool last = i == LG_L - 1;
         const mlg_lg_conf_i heads{ROWSEG, last ? nullptr : w.wconf[i], last ? nullptr : w.bconf[i], w.wmatch[i],
-                                  w.bmatch[i], last ? 0.f : conf_threshold(i), width_conf, LZ, KEEP};
+                                  w.bmatch[i], last ? 0.f : (depth_conf > 0.f ? conf_threshold(i) : -INFINITY),
+                                  width_conf, LZ, KEEP};
+        // (depth_confidence <= 0: upstream computes no token confidences, so its pruning
+        // mask is matchability alone -- a threshold of -inf drops the "low confidence is
+        // never pruned" term; the stop bit is unused then)
         LG_TRY(ffn(w.cross[i], &heads));
+        tr_rows(i * 100 + 23, X, LG_D * 4, Npad);
+        tr_rows(i * 100 + 24, CAT, 512, Npad, 1024);
+        tr_rows(i * 100 + 25, LZ, 4, Npad);
+        if (!last) tr_rows(i * 100 + 26, KEEP, 1, Npad);
 
         if (last) {
             std::vector<size_t> ks;
@@ -994,6 +1117,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         }
         hipLaunchKernelGGL(k_lg_segstats, dim3((unsigned)segs.size()), dim3(256), 0, s, SEGS, KEEP, STATS);
         MLG_LAUNCH_CHECK();
+        tr_tab(i * 100 + 27, STATS, segs.size() * 2 * sizeof(int));
         if (hipMemcpyAsync(stats.data(), STATS, segs.size() * 2 * sizeof(int), hipMemcpyDeviceToHost, s) !=
                 hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
@@ -1062,8 +1186,14 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
             pair_of.push_back(npair[k / 2]);
         }
         Npad = std::max(noff, 64);
+        tl = i + 1;
+        if (!h_moves.empty()) tr_tab(tl * 100 + 31, MOVES, h_moves.size() * sizeof(int4));
         if (!segs.empty()) LG_TRY(upload_layout());
+        if (!h_moves.empty() && !segs.empty()) tr_rows(tl * 100 + 30, X, LG_D * 4, Npad);
         stats.assign(segs.size() * 2, 0);
+    }
+    if (t_trace) {
+        trace(9990, nmatch, 1, P * 4, 0, 1, 0, 1, s);
     }
     // the last assignment's table (h_asg) and possibly a final layout upload are pageable
     // copies still queued on s: they must complete before the vectors go out of scope
@@ -1083,3 +1213,30 @@ int mlg_lg_orient_matches(const int32_t* matches, const float* scores, const int
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }
+
+// ---------------------------------------------------------------- debug trace ABI
+extern "C" {
+int mlg_dbg_lg_trace_begin(void* dev_buf, size_t bytes) {
+    if (!dev_buf || bytes < 8) return MLG_EINVAL;
+    delete t_trace;
+    t_trace = new LgTrace;
+    t_trace->buf = (uint64_t*)dev_buf;
+    t_trace->cap = bytes / 8;
+    return MLG_OK;
+}
+
+int mlg_dbg_lg_trace_end(int32_t* tags, int32_t* counts, int max_entries) {
+    LgTrace* t = t_trace;
+    if (!t) return MLG_EINVAL;
+    t_trace = nullptr;
+    const int n = (int)t->tags.size();
+    const bool overflow = t->overflow;
+    if (tags && counts)
+        for (int i = 0; i < n && i < max_entries; ++i) {
+            tags[i] = t->tags[i];
+            counts[i] = t->counts[i];
+        }
+    delete t;
+    return overflow ? MLG_ENOMEM : n;
+}
+}  // extern "C"

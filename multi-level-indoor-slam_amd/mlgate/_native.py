@@ -16,15 +16,6 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmlgate.so")
 TORCH_LIB_PATH = os.path.join(_HERE, "libmlgate_torch.so")
-# A/B tooling only (tools/*_bench.py): load another build of the same library
-_LIB_OVERRIDE = os.environ.get("MLGATE_LIB_AB")
-if _LIB_OVERRIDE:
-    LIB_PATH = _LIB_OVERRIDE
-# A/B tooling only: a directory holding another build of both libraries
-_DIR_OVERRIDE = os.environ.get("MLGATE_LIB_DIR")
-if _DIR_OVERRIDE:
-    LIB_PATH = os.path.join(_DIR_OVERRIDE, "libmlgate.so")
-    TORCH_LIB_PATH = os.path.join(_DIR_OVERRIDE, "libmlgate_torch.so")
 OPS = ("vit_forward_into", "knn_gate", "knn_query", "row_normalize", "similarity", "xcorr_score", "superpoint",
        "lightglue", "ransac_epipolar", "recover_pose", "resnet50", "loftr_features", "loftr_match", "superglue", "pillow_resize_224", "plane_ransac", "proximity",
        "prof_enable", "prof_reset", "prof_read")
@@ -96,6 +87,10 @@ EXPORTS = {
     "mlg_prof_read": (c_int, [c_int, ctypes.POINTER(c_double), ctypes.POINTER(c_long)]),
     "mlg_prof_read_work": (c_int, [c_int, ctypes.POINTER(c_double)]),
     "mlg_lg_orient_matches": (c_int, [c_void_p] * 5 + [c_int, c_int] + [c_void_p] * 4),
+    "mlg_dbg_lg_trace_begin": (c_int, [c_void_p, c_size_t]),
+    "mlg_dbg_lg_trace_end": (c_int, [c_void_p, c_void_p, c_int]),
+    "mlg_dbg_fill_lds": (c_int, [ctypes.c_uint32, c_void_p, c_void_p]),
+    "mlg_dbg_fill_regs": (c_int, [ctypes.c_uint32, c_void_p]),
     "mlg_png_info": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mlg_png_decode_bgr": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_png_load_bgr": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
@@ -118,8 +113,6 @@ def lib():
                               "g.build()'` (hipcc --offload-arch=gfx950)")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in EXPORTS.items():
-            if _LIB_OVERRIDE and not hasattr(L, name):
-                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -159,7 +159,7 @@ class DeviceGate:
     def __init__(self, frames, timestamps, floor_labels, world=1, rank=0, device='cuda', k=10,
                  similarity_threshold=0.5, min_time_gap=10.0, strict_mode=True, retrieval_floor_gating=True,
                  verifier_floor_gating=True, verify=True, K=None, min_inliers=20, min_inlier_ratio=0.25,
-                 vit_batch=123, sp_batch=64, lg_chunk=1024, max_keypoints=2048, vit_state_dict=None):
+                 vit_batch=123, sp_batch=64, lg_chunk=1024, max_keypoints=2048, vit_state_dict=None, record=False):
         import torch
         from . import distributed as mdist
         from .lightglue import LightGlueGPU
@@ -211,6 +211,10 @@ class DeviceGate:
             Kc = np.asarray(K if K is not None else np.eye(3), np.float64)
             self.K = torch.from_numpy(Kc.reshape(9).copy()).to(self.dev) if K is not None else None
         self.last = {}
+        # record=True: step() keeps every verified ordered pair's (a, b, matches, inliers,
+        # is_valid) in self.last_pair_results (host arrays in verification order)
+        self.record = record
+        self.last_pair_results = None
 
     def _dedup(self):
         """Match each unordered pair once (MLGATE_LG_DEDUP=0: every ordered pair, for A/B)."""
@@ -297,6 +301,7 @@ class DeviceGate:
         side = self._side_stream()
         n_valid_t = torch.zeros((), dtype=torch.int64, device=self.dev)
         gate_rej_t = torch.zeros((), dtype=torch.int64, device=self.dev)
+        rec = [] if self.record else None
         for ci, c0 in enumerate(range(0, len(ua), self.lg_chunk)):
             mu, su, nu, _ = self.lg.match_device(kp_all, ds_all, counts, ua[c0:c0 + self.lg_chunk],
                                                  ub[c0:c0 + self.lg_chunk])
@@ -328,10 +333,20 @@ class DeviceGate:
                 ratio = inl.double() / n.clamp(min=1).double()
                 ok = (n >= 5) & (inl >= self.min_inliers) & (ratio >= self.min_inlier_ratio)
                 n_valid_t += ok.sum()
+                if rec is not None:
+                    rec.append((sel, n, inl, ok))
                 # the floor gate on the geometrically valid pairs
                 gate_rej_t += (ok & ((self.f_all[ta] - self.f_all[tb]).abs() > self.limit)).sum()
         main.wait_stream(side)
         n_valid, gate_rej = int(n_valid_t), int(gate_rej_t)
+        if rec is not None:
+            r = {"a": pa, "b": pb, "matches": np.zeros(len(pa), np.int32), "inliers": np.zeros(len(pa), np.int32),
+                 "is_valid": np.zeros(len(pa), bool)}
+            for sel, n, inl, ok in rec:
+                r["matches"][sel] = n.cpu().numpy()
+                r["inliers"][sel] = inl.cpu().numpy()
+                r["is_valid"][sel] = ok.cpu().numpy()
+            self.last_pair_results = r
         out["pairs_verified"] = len(pa)
         out["verified_valid"] = n_valid
         out["verifier_invalid"] = len(pa) - n_valid

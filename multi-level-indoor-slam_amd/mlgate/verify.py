@@ -282,26 +282,48 @@ class SuperGlue(BaseFeatureMatcher):
 
 
 class LoFTR(BaseFeatureMatcher):
-    """Detector-free LoFTR on the GPU (geometric_verification.py:424-526): the reference's
-    native branch -- kornia.feature.LoFTR(pretrained='indoor') on cv2 BGR2GRAY frames
+    """geometric_verification.py:424-526.  The reference runs kornia's LoFTR when kornia
+    imports (pretrained `weights`) and otherwise warns and uses the LightGlue fallback
+    (:447-467).  kornia and its checkpoints are absent here, so by default this class
+    behaves like the reference in that environment: the warning, then the GPU LightGlue
+    path.  The native detector-free matcher -- kornia.feature.LoFTR on cv2 BGR2GRAY frames
     resized down to multiples of 8 (cv2 INTER_LINEAR), /255, keypoints scaled back
-    (mlgate.loftr, csrc/loftr.hip).  Both frames must share a shape (mixed shapes are not
-    built)."""
+    (mlgate.loftr, csrc/loftr.hip) -- is opt-in: ``MLGATE_LOFTR_NATIVE=1``, a checkpoint in
+    ``MLGATE_LOFTR_WEIGHTS``, or ``.native = True``.  It is the 'indoor' configuration;
+    'outdoor' needs its checkpoint in MLGATE_LOFTR_WEIGHTS (otherwise the fallback is
+    used).  The native kernels match frames of one shape; a pair of differently shaped
+    frames is matched by the LightGlue fallback, with a warning."""
 
     def __init__(self, device: str = 'cuda', weights: str = 'indoor'):
         super().__init__(device)
         self.weights = weights
+        self.native = None  # None: the environment decides (see the class docstring)
         self._model_loaded = False
+
+    def _want_native(self):
+        if self.native is not None:
+            return bool(self.native)
+        return os.environ.get("MLGATE_LOFTR_NATIVE") == "1" or bool(os.environ.get("MLGATE_LOFTR_WEIGHTS"))
 
     def _load_model(self):
         if self._model_loaded:
             return
-        from .loftr import LoFTRGPU
-        self._matcher = LoFTRGPU(device=self.device)
-        if self._matcher.weights_source.startswith("synthetic"):
-            warnings.warn("LoFTR weights not configured (MLGATE_LOFTR_WEIGHTS); using seeded synthetic weights")
+        native = self._want_native()
+        if native and self.weights != 'indoor' and not os.environ.get("MLGATE_LOFTR_WEIGHTS"):
+            warnings.warn(f"LoFTR weights {self.weights!r}: no checkpoint in MLGATE_LOFTR_WEIGHTS; "
+                          "using the LightGlue fallback")
+            native = False
+        if native:
+            from .loftr import LoFTRGPU
+            self._matcher = LoFTRGPU(device=self.device)
+            if self._matcher.weights_source.startswith("synthetic"):
+                warnings.warn("LoFTR weights not configured (MLGATE_LOFTR_WEIGHTS); using seeded synthetic weights")
+            self._is_native = True
+        else:
+            warnings.warn("LoFTR (kornia) not installed. Using LightGlue fallback. Install with: pip install kornia")
+            self._fallback = LightGlue(device=self.device)
+            self._is_native = False
         self._model_loaded = True
-        self._is_native = True
 
     @staticmethod
     def _scale(shape):
@@ -310,9 +332,14 @@ class LoFTR(BaseFeatureMatcher):
 
     def detect_and_match(self, image1: np.ndarray, image2: np.ndarray) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         self._load_model()
+        if not self._is_native:
+            return self._fallback.detect_and_match(image1, image2)
         im1, im2 = np.asarray(image1, np.uint8), np.asarray(image2, np.uint8)
         if im1.shape != im2.shape:
-            raise ValueError("LoFTR: the two frames must share a shape (mixed shapes are not built)")
+            warnings.warn("LoFTR: frames of different shapes are matched by the LightGlue fallback")
+            if not hasattr(self, "_fallback"):
+                self._fallback = LightGlue(device=self.device)
+            return self._fallback.detect_and_match(image1, image2)
         dev = torch.device(self.device)
         as4 = lambda im: torch.from_numpy(np.ascontiguousarray(im if im.ndim == 3 else im[..., None]))  # noqa: E731
         k0, k1, c = self._matcher.match_frames(torch.stack([as4(im1), as4(im2)]).to(dev), [(0, 1)])[0]
@@ -322,6 +349,8 @@ class LoFTR(BaseFeatureMatcher):
     def detect_and_match_batch(self, frames, pairs):
         """frames: device uint8 [F, H, W, C]; pairs [(a, b)] -> [(kpts_a, kpts_b, conf)]."""
         self._load_model()
+        if not self._is_native:
+            return self._fallback.detect_and_match_batch(frames, pairs)
         sc = self._scale(tuple(frames.shape[1:3]))
         return [(a * sc, b * sc, c) for a, b, c in self._matcher.match_frames(frames, pairs)]
 
@@ -393,9 +422,10 @@ class GeometricVerifier:
     def verify_batch(self, image_pairs: List[Tuple[np.ndarray, np.ndarray]], K: Optional[np.ndarray] = None,
                      indices: Optional[List[Tuple[int, int]]] = None) -> List[MatchResult]:
         """Same results as verifying each pair in turn (geometric_verification.py:636-662),
-        computed as one batched SuperPoint + LightGlue + RANSAC pass when the images
-        share a shape (every matcher has a batched path; SuperGlue / LoFTR through the
-        LightGlue fallback the reference resolves them to)."""
+        computed as one batched matching + RANSAC pass when the images share a shape
+        (every matcher has a batched path: SuperPoint + LightGlue; SuperGlue and LoFTR
+        through the LightGlue fallback the reference resolves them to without magicleap /
+        kornia, or their native kernels when opted in)."""
         if not image_pairs:
             return []
         if len({np.shape(im) for pair in image_pairs for im in pair}) == 1:

@@ -172,14 +172,16 @@ class Oracle:
                 if (ratio > depth_confidence) if force_stop is None else (i + 1 == force_stop):
                     break
             if width_confidence > 0 and len(x0) > pruning_min_kpts:
-                keep = (torch.sigmoid(self.matchability(x0, i)).squeeze(-1) > 1 - width_confidence) | \
-                    (t0 <= conf_threshold(i))
+                keep = torch.sigmoid(self.matchability(x0, i)).squeeze(-1) > 1 - width_confidence
+                if depth_confidence > 0:  # upstream: no token confidences without early stopping
+                    keep |= t0 <= conf_threshold(i)
                 keep = torch.where(keep)[0]
                 ind0, x0, e0 = ind0[keep], x0[keep], e0[:, keep]
                 prune0[ind0] += 1
             if width_confidence > 0 and len(x1) > pruning_min_kpts:
-                keep = (torch.sigmoid(self.matchability(x1, i)).squeeze(-1) > 1 - width_confidence) | \
-                    (t1 <= conf_threshold(i))
+                keep = torch.sigmoid(self.matchability(x1, i)).squeeze(-1) > 1 - width_confidence
+                if depth_confidence > 0:  # upstream: no token confidences without early stopping
+                    keep |= t1 <= conf_threshold(i)
                 keep = torch.where(keep)[0]
                 ind1, x1, e1 = ind1[keep], x1[keep], e1[:, keep]
                 prune1[ind1] += 1

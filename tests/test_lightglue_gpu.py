@@ -158,3 +158,54 @@ def test_lightglue_repeated_frames_equal_single_pairs(lg):
         assert k1 == n[p] and st1[0] == stop[p]
         assert np.array_equal(m1[0, :k1].cpu().numpy(), m[p, :k1]) and np.array_equal(s1[0, :k1].cpu().numpy(), s[p, :k1])
     assert n[0] > 0 and n[3] > 0
+
+
+def test_lightglue_swapped_pair_is_the_exact_swap(lg):
+    """LightGlue(b, a) == swap(LightGlue(a, b)) bit for bit -- matches (re-sorted by the new
+    image0 index), scores and stop layers -- so the full gate's once-per-unordered-pair
+    matching (pipeline.py) gives every ordered pair exactly its own call's result.  Cases
+    cover pruning (> 1536 keypoints), early stopping and ragged sizes; frame indices on
+    both sides of each other (the assignment's canonical cross-term order, lightglue.hip
+    k_asg_sim)."""
+    rng = np.random.default_rng(31)
+    cases = [feats(rng, 2048, 1900), feats(rng, 1700, 300), feats(rng, 700, 650), feats(rng, 64, 70),
+             feats(rng, 1200, 1250, overlap=0.9), feats(rng, 900, 880, overlap=0.1)]
+    kmax = 2048
+    F = 2 * len(cases)
+    kp = torch.zeros(F, kmax, 2)
+    ds = torch.zeros(F, kmax, 256)
+    counts = []
+    for i, (k0, d0, k1, d1) in enumerate(cases):
+        for j, (k, d) in enumerate(((k0, d0), (k1, d1))):
+            kp[2 * i + j, :len(k)] = torch.from_numpy(k)
+            ds[2 * i + j, :len(k)] = torch.from_numpy(d)
+            counts.append(len(k))
+    kp, ds = kp.to(lg.device), ds.to(lg.device)
+    a, b = np.arange(0, F, 2, dtype=np.int32), np.arange(1, F, 2, dtype=np.int32)
+    m1, s1, n1, st1 = (x.cpu().numpy() if torch.is_tensor(x) else x for x in lg.match_device(kp, ds, counts, a, b))
+    m2, s2, n2, st2 = (x.cpu().numpy() if torch.is_tensor(x) else x for x in lg.match_device(kp, ds, counts, b, a))
+    assert np.array_equal(st1, st2)
+    assert np.array_equal(n1, n2)
+    for p in range(len(cases)):
+        k = int(n1[p])
+        o = np.argsort(m1[p, :k, 1])
+        assert np.array_equal(m2[p, :k, 0], m1[p, :k, 1][o]) and np.array_equal(m2[p, :k, 1], m1[p, :k, 0][o]), p
+        assert np.array_equal(s2[p, :k].view(np.uint32), s1[p, :k][o].view(np.uint32)), p
+    assert n1.min() > 0
+
+
+def test_lightglue_no_early_stop_prunes_on_matchability_only(dev, sd):
+    """depth_confidence <= 0 (early stopping off): upstream computes no token confidences,
+    so a point is kept iff its matchability > 1 - width_confidence (get_pruning_mask with
+    confidences None); the kernel's keep bit must drop the confidence term too."""
+    lg = LightGlueGPU(sd, device=str(dev), depth_confidence=-1)
+    rng = np.random.default_rng(77)
+    case = feats(rng, 2048, 1900)
+    got_m, got_s, got_stop = _run_gpu(lg, [case])[0]
+    ref = Oracle(sd).match(*case, depth_confidence=-1)
+    assert got_stop == ref["stop"] == 9
+    rm, rs = ref["matches"].numpy(), ref["scores"].numpy()
+    g = {tuple(x): i for i, x in enumerate(got_m.tolist())}
+    r = {tuple(x): i for i, x in enumerate(rm.tolist())}
+    common = set(g) & set(r)
+    assert len(common) >= 0.95 * max(len(g), len(r)), (len(common), len(g), len(r))

@@ -99,6 +99,7 @@ def test_end_to_end_and_dropin(dev, setup):
     close = sum(np.abs(got[1][i] - ref[1][j]).max() < 0.5 for i, j in hit)
     assert close >= 0.9 * len(hit)
     m = LoFTR(device=str(dev))
+    m.native = True
     m._load_model()
     m._matcher = lf
     k0, k1, c = m.detect_and_match(frames[a], frames[b])
@@ -115,6 +116,7 @@ def test_isec_frame_size_resize_path(dev, setup):
     a, b = pairs[0]
     fr = synthetic.frames_host(seq, np.array([a, b]), 540, 720)
     m = LoFTR(device=str(dev))
+    m.native = True
     m._load_model()
     k0, k1, c = m.detect_and_match(fr[0], fr[1])
     r0, r1, rc = orc.detect_and_match(fr[0], fr[1])
@@ -123,3 +125,27 @@ def test_isec_frame_size_resize_path(dev, setup):
     hit = [(i, rk[tuple(np.rint(k * 8).astype(int))]) for i, k in enumerate(k0) if tuple(np.rint(k * 8).astype(int)) in rk]
     assert len(hit) >= 0.9 * len(r0), (len(hit), len(r0), len(k0))
     assert sum(np.abs(k1[i] - r1[j]).max() < 0.5 for i, j in hit) >= 0.9 * len(hit)
+
+
+def test_default_is_the_reference_lightglue_fallback(dev, monkeypatch):
+    """Without kornia the reference's LoFTR warns and matches with LightGlue
+    (geometric_verification.py:458-467); the drop-in does the same unless the native
+    matcher is opted in (MLGATE_LOFTR_NATIVE / MLGATE_LOFTR_WEIGHTS / .native)."""
+    from mlgate.verify import LightGlue, LoFTR
+    monkeypatch.delenv("MLGATE_LOFTR_NATIVE", raising=False)
+    monkeypatch.delenv("MLGATE_LOFTR_WEIGHTS", raising=False)
+    seq = synthetic.make_sequence(40, 4, 2)
+    same = [i for i in range(1, 40) if seq.place_of[i] == seq.place_of[0]]
+    fr = synthetic.frames_host(seq, [0, same[0]])
+    m = LoFTR(device=str(dev))
+    with pytest.warns(UserWarning, match="kornia"):
+        got = m.detect_and_match(fr[0], fr[1])
+    ref = LightGlue(device=str(dev)).detect_and_match(fr[0], fr[1])
+    assert not m._is_native
+    assert all(np.array_equal(x, y) for x, y in zip(got, ref)) and len(got[0]) > 0
+    # 'outdoor' without a checkpoint: the fallback too, even when native is requested
+    o = LoFTR(device=str(dev), weights='outdoor')
+    o.native = True
+    with pytest.warns(UserWarning, match="outdoor"):
+        o._load_model()
+    assert not o._is_native

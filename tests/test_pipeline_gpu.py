@@ -144,19 +144,26 @@ def test_device_gate_counts_equal_full_gate(dev, chain, reports, cfg):
 @pytest.mark.parametrize("cfg", list(CFG))
 def test_device_gate_unordered_matching_changes_nothing(dev, chain, cfg, monkeypatch):
     """LightGlue once per unordered pair (the default) vs once per ordered pair: the same
-    counts, the same per-pair decisions in every configuration."""
+    counts and, PER ORDERED PAIR, the same match count, inlier count and decision in every
+    configuration (LightGlue(b, a) is exactly swap(LightGlue(a, b)):
+    test_lightglue_gpu.py::test_lightglue_swapped_pair_is_the_exact_swap)."""
     frames = torch.from_numpy(chain["frames"]).to(dev)
     rg, vg = CFG[cfg]
-    outs = {}
+    outs, recs = {}, {}
     for dd in ("1", "0"):
         monkeypatch.setenv("MLGATE_LG_DEDUP", dd)
         g = DeviceGate(frames, chain["seq"].t, chain["labels"], device=str(dev), k=chain["k"],
                        similarity_threshold=chain["thr"], min_time_gap=chain["gap"], retrieval_floor_gating=rg,
-                       verifier_floor_gating=vg, K=ogeo.ISEC_K, vit_batch=64, lg_chunk=64)
+                       verifier_floor_gating=vg, K=ogeo.ISEC_K, vit_batch=64, lg_chunk=64, record=True)
         outs[dd] = g.step()
+        r = g.last_pair_results
+        recs[dd] = {(int(x), int(y)): (int(n), int(i), bool(v))
+                    for x, y, n, i, v in zip(r["a"], r["b"], r["matches"], r["inliers"], r["is_valid"])}
     a, b = dict(outs["1"]), dict(outs["0"])
     assert a.pop("pairs_matched_lightglue") <= b.pop("pairs_matched_lightglue")
     assert a == b
+    assert recs["1"] == recs["0"]
+    assert len(recs["1"]) == a["pairs_verified"] > 0
 
 
 def test_orient_matches_is_the_swapped_call(dev):
