@@ -13,8 +13,10 @@ essential-matrix RANSAC + recoverPose with K = ISEC cam1, the verifier's decisio
 (>= 20 inliers, ratio >= 0.25); the floor gate on the geometrically valid pairs.  The
 line reports the four-term false-loop-closure rejection count of the step.
 Multi-GPU: frames are sharded across ranks (strong scaling: fixed total); descriptors
-and SuperPoint features are all-gathered over RCCL; each rank gates its own query rows,
-then the gate-accepted pairs are all-gathered and re-split evenly for verification.
+are all-gathered over RCCL; each rank gates its own query rows, the gate-accepted pairs
+are all-gathered and re-split evenly (unordered pairs kept on one rank) for verification,
+and each rank receives the SuperPoint features of exactly the keyframes its pairs touch
+(all_to_all); the counts are all-reduced.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--verify all|none]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -225,6 +227,7 @@ def main():
                        "pairs_matched_lightglue": counts.get("pairs_matched_lightglue", 0),
                        "pairs_geometrically_valid": counts["verified_valid"],
                        "loop_closures_accepted": counts["accepted"],
+                       "superpoint_features_exchanged_gb": round(counts.get("features_exchanged_bytes", 0) / 1e9, 3),
                        "false_loop_closure_rejections": rej},
             "roofline": {"kernel": SLOTS[dom], "bound": "hbm" if hbm else "mfma",
                          "achieved": round(achieved, 2) if achieved else None,

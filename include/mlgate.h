@@ -97,8 +97,8 @@ int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, 
  * desc: float32 [N, D]; t: float64 [N]; floor: int64 [N]; has_floor: uint8 [N]
  * (0 = floor_label None).  Outputs (device): idx int32 [Q, k], sim float32 [Q, k],
  * valid uint8 [Q, k], count int32 [Q] (entries per row, in emission order);
- * totals uint64[2] (+= valid, rejected) or NULL.  1 <= k <= 4096 (k > 256: a per-row
- * radix select over (similarity, index) keys).
+ * totals uint64[2] (+= valid, rejected) or NULL.  k >= 1, unbounded (k > 256: a per-row
+ * radix select over (similarity, index) keys, in windows of 4096 ranks).
  */
 size_t mlg_knn_workspace_bytes(int N, int D, int Q);
 /* Workspace for a given k, for mlg_knn_gate (query = 0) or mlg_knn_query (query = 1):
@@ -130,6 +130,16 @@ int mlg_similarity(const float* A, int Q, const float* B, int N, int D, float* S
 size_t mlg_xcorr_workspace_bytes(int n1, int n2, int D);
 int mlg_xcorr_score(const float* q, int n1, const float* m, int n2, int D, void* workspace, size_t workspace_bytes,
                     float* score, void* stream);
+
+/* CricaVPR.rerank_candidates at scale (place_recognition.py:714-757): the
+ * compute_cross_correlation_score of P (query, candidate) pairs in one pass.  feats: f32
+ * [F, L, D] local features of F frames (not normalised); query / cand: device int32 [P]
+ * frame indices; scores: device f32 [P], each bit-identical to mlg_xcorr_score on that
+ * pair (same row normalisation, same exact-f32 MFMA tiles, same reduction order); no
+ * [L, L] matrix is written. */
+size_t mlg_xcorr_batch_workspace_bytes(int F, int L, int D, int P);
+int mlg_xcorr_batch(const float* feats, int F, int L, int D, const int32_t* query, const int32_t* cand, int P,
+                    void* workspace, size_t workspace_bytes, float* scores, void* stream);
 
 /* ----------------------------------------------------------- op-level access --
  * Individual kernels of the ViT path (parity tests against a float32 reference). */

@@ -409,6 +409,14 @@ int mlg_xcorr_score(const float* q, int n1, const float* m, int n2, int D, void*
     return MLG_OK;
 }
 
+size_t mlg_xcorr_batch_workspace_bytes(int F, int L, int D, int P) { return mlg_xcorr_batch_ws_bytes(F, L, D, P); }
+
+int mlg_xcorr_batch(const float* feats, int F, int L, int D, const int32_t* query, const int32_t* cand, int P,
+                    void* workspace, size_t workspace_bytes, float* scores, void* stream) {
+    return mlg_xcorr_batch_run(feats, F, L, D, query, cand, P, workspace, workspace_bytes, scores,
+                               (hipStream_t)stream);
+}
+
 int mlg_op_gemm_f32out(const uint16_t* A, const uint16_t* W, float* C, int M, int N, int K, void* stream) {
     return mlg_gemm_f32out(A, W, C, M, N, K, (hipStream_t)stream);
 }

@@ -80,6 +80,9 @@ int mlg_topk_gate(const float* S, int lds, int N, int Q, const double* tq, const
                   int gating, int32_t* idx, float* sim, uint8_t* valid, int32_t* count, unsigned long long* totals,
                   hipStream_t s);
 int mlg_xcorr_reduce(const float* C, int n1, int n2, float* out, hipStream_t s);
+size_t mlg_xcorr_batch_ws_bytes(int F, int L, int D, int P);
+int mlg_xcorr_batch_run(const float* feats, int F, int L, int D, const int32_t* qa, const int32_t* qb, int P,
+                        void* ws, size_t ws_bytes, float* score, hipStream_t s);
 // fused kNN (k <= 32): no [Q, N] matrix; workspace mlg_knn_fused_ws_bytes(Q, N, k)
 int mlg_row_normalize_wave(const float* X, float* Xn, int N, int D, float* norms, hipStream_t s);
 int mlg_knn_fused_splits(int Q, int N);

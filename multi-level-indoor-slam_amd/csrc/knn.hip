@@ -110,16 +110,14 @@ __global__ void k_row_normalize(const float* __restrict__ X, float* __restrict__
 // 128 x 128 tile, BK = 16, 256 threads = 2 x 2 waves of 64 x 64 (2 x 2 MFMA 32x32).
 constexpr int SBM = 128, SBN = 128, SBK = 16;
 
-// St (optional): the transpose, St[j][i] = S[i][j] (SuperGlue's column passes)
-__global__ __launch_bounds__(256, 2) void k_sim_f32(const float* __restrict__ A, int Q, const float* __restrict__ B,
-                                                    int N, int D, float* __restrict__ S, int lds,
-                                                    float* __restrict__ St, int ldt) {
-    __shared__ float As[SBK][SBM + 4];
-    __shared__ float Bs[SBK][SBN + 4];
+// The 128 x 128 tile (m0, n0) of A . B^T on the exact-f32 MFMA (rows of A past Q and of
+// B past N are clamped copies: the caller masks them).  One k order for every caller, so
+// k_sim_f32 and k_xcorr_tiles produce the same bits.
+__device__ __forceinline__ void sim_tile(const float* __restrict__ A, int Q, const float* __restrict__ B, int N,
+                                         int D, int m0, int n0, float (&As)[SBK][SBM + 4], float (&Bs)[SBK][SBN + 4],
+                                         f32x16 (&acc)[2][2]) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int m0 = blockIdx.y * SBM, n0 = blockIdx.x * SBN;
     const int wm = wave >> 1, wn = wave & 1;
-    f32x16 acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -167,6 +165,19 @@ __global__ __launch_bounds__(256, 2) void k_sim_f32(const float* __restrict__ A,
         }
         __syncthreads();
     }
+}
+
+// St (optional): the transpose, St[j][i] = S[i][j] (SuperGlue's column passes)
+__global__ __launch_bounds__(256, 2) void k_sim_f32(const float* __restrict__ A, int Q, const float* __restrict__ B,
+                                                    int N, int D, float* __restrict__ S, int lds,
+                                                    float* __restrict__ St, int ldt) {
+    __shared__ float As[SBK][SBM + 4];
+    __shared__ float Bs[SBK][SBN + 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m0 = blockIdx.y * SBM, n0 = blockIdx.x * SBN;
+    const int wm = wave >> 1, wn = wave & 1;
+    f32x16 acc[2][2];
+    sim_tile(A, Q, B, N, D, m0, n0, As, Bs, acc);
     // D[i][j]: col j = lane & 31, row i = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
 #pragma unroll
     for (int ta = 0; ta < 2; ++ta)
@@ -270,12 +281,15 @@ __global__ __launch_bounds__(64) void k_topk_gate(const float* __restrict__ S, i
 }
 
 
-// Large k (256 < k <= 4096; the reference's argsort()[:k] has no limit): one workgroup
-// per query row.  Each candidate is the 64-bit key (orderable similarity << 32 | index),
-// whose descending order is exactly (similarity desc, index desc); a radix select over
-// eight 8-bit digits (MSB first, 256-bin LDS histograms, one pass over the row each)
-// finds the k-th largest key, the keys at or above it are gathered into LDS and
-// bitonic-sorted, then emitted with the threshold / floor rule of k_topk_gate.
+// Large k (k > 256, no upper limit: the reference's argsort()[:k] has none): one
+// workgroup per query row.  Each candidate is the 64-bit key (orderable similarity << 32
+// | index), whose descending order is exactly (similarity desc, index desc).  The ranks
+// are emitted in windows of TOPK_LARGE: a radix select over eight 8-bit digits (MSB
+// first, 256-bin LDS histograms, one pass over the row each) finds the window's last key
+// among the keys below the previous window's, those keys are gathered into LDS and
+// bitonic-sorted, then emitted with the threshold / floor rule of k_topk_gate; the next
+// window starts below the last key emitted.  Emission stops at the first similarity
+// under the threshold, so a large k costs windows only while candidates pass it.
 constexpr int TOPK_LARGE = 4096;
 __device__ __forceinline__ uint64_t knn_key(float v, int j) {
     uint32_t u = __float_as_uint(v);
@@ -292,15 +306,21 @@ __global__ __launch_bounds__(256) void k_topk_large(const float* __restrict__ S,
                                                     unsigned long long* __restrict__ totals) {
     __shared__ uint64_t keys[TOPK_LARGE];
     __shared__ int hist[256];
-    __shared__ int s_total, s_n;
-    __shared__ uint64_t s_prefix;
+    __shared__ int s_total, s_n, s_emitted, s_nvalid, s_stop;
+    __shared__ uint64_t s_prefix, s_upper;
     __shared__ int s_need;
     const int tid = threadIdx.x, r = blockIdx.x;
     if (r >= Q) return;
     const double ti = tq[r];
     const float* row = S + (size_t)r * lds;
     // candidates left after the time-gap mask
-    if (tid == 0) s_total = 0;
+    if (tid == 0) {
+        s_total = 0;
+        s_emitted = 0;
+        s_nvalid = 0;
+        s_stop = 0;
+        s_upper = ~0ull;
+    }
     __syncthreads();
     int c = 0;
     for (int j = tid; j < N; j += 256) c += !(fabs(tdb[j] - ti) < min_gap);
@@ -308,81 +328,98 @@ __global__ __launch_bounds__(256) void k_topk_large(const float* __restrict__ S,
     __syncthreads();
     const int total = s_total;
     const int kk = min(k, total);
-    // radix select: prefix of the kk-th largest key, digit by digit from the top
-    uint64_t prefix = 0;
-    int need = kk;  // rank (1-based, from the top) still to find below the fixed prefix
-    for (int d = 7; d >= 0 && kk > 0 && kk < total; --d) {
-        for (int b = tid; b < 256; b += 256) hist[b] = 0;
+    const bool hf_i = gating && hfq[r] != 0;
+    const int64_t fi = gating ? fq[r] : 0;
+    for (int done = 0; done < kk && !s_stop; done += TOPK_LARGE) {
+        const uint64_t upper = s_upper;   // keys of this window are below it (all on window 0)
+        const bool first = done == 0;
+        const int left = total - done;    // candidates not yet emitted
+        const int want = min(kk - done, TOPK_LARGE);
+        // radix select: prefix of the want-th largest key below `upper`
+        uint64_t prefix = 0;
+        int need = want;
+        for (int d = 7; d >= 0 && want < left; --d) {
+            for (int b = tid; b < 256; b += 256) hist[b] = 0;
+            __syncthreads();
+            const uint64_t hmask = d == 7 ? 0ull : (~0ull << (8 * (d + 1)));
+            for (int j = tid; j < N; j += 256) {
+                if (fabs(tdb[j] - ti) < min_gap) continue;
+                const uint64_t key = knn_key(row[j], j);
+                if ((!first && key >= upper) || (key & hmask) != prefix) continue;
+                atomicAdd(&hist[(int)((key >> (8 * d)) & 0xff)], 1);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int acc = 0, b = 255;
+                for (; b > 0; --b) {
+                    if (acc + hist[b] >= need) break;
+                    acc += hist[b];
+                }
+                s_prefix = prefix | ((uint64_t)b << (8 * d));
+                s_need = need - acc;
+            }
+            __syncthreads();
+            prefix = s_prefix;
+            need = s_need;
+            __syncthreads();
+        }
+        // gather the window's keys (every key below `upper` when the window takes the rest)
+        if (tid == 0) s_n = 0;
         __syncthreads();
-        const uint64_t hmask = d == 7 ? 0ull : (~0ull << (8 * (d + 1)));
         for (int j = tid; j < N; j += 256) {
             if (fabs(tdb[j] - ti) < min_gap) continue;
             const uint64_t key = knn_key(row[j], j);
-            if ((key & hmask) != prefix) continue;
-            atomicAdd(&hist[(int)((key >> (8 * d)) & 0xff)], 1);
+            if (!first && key >= upper) continue;
+            if (want < left && key < prefix) continue;
+            const int slot = atomicAdd(&s_n, 1);
+            if (slot < TOPK_LARGE) keys[slot] = key;
         }
         __syncthreads();
-        if (tid == 0) {
-            int acc = 0, b = 255;
-            for (; b > 0; --b) {
-                if (acc + hist[b] >= need) break;
-                acc += hist[b];
-            }
-            s_prefix = prefix | ((uint64_t)b << (8 * d));
-            s_need = need - acc;
-        }
+        const int n = min(s_n, want);
+        int P = 1;
+        while (P < n) P <<= 1;
+        for (int i = n + tid; i < P; i += 256) keys[i] = 0ull;  // sort to the end (descending)
         __syncthreads();
-        prefix = s_prefix;
-        need = s_need;
-        __syncthreads();
-    }
-    // gather the kk largest keys (all candidates when kk == total)
-    if (tid == 0) s_n = 0;
-    __syncthreads();
-    for (int j = tid; j < N; j += 256) {
-        if (fabs(tdb[j] - ti) < min_gap) continue;
-        const uint64_t key = knn_key(row[j], j);
-        if (kk < total && key < prefix) continue;
-        const int slot = atomicAdd(&s_n, 1);
-        if (slot < TOPK_LARGE) keys[slot] = key;
-    }
-    __syncthreads();
-    const int n = min(s_n, kk);
-    int P = 1;
-    while (P < n) P <<= 1;
-    for (int i = n + tid; i < P; i += 256) keys[i] = 0ull;  // sort to the end (descending)
-    __syncthreads();
-    for (int kb = 2; kb <= P; kb <<= 1)
-        for (int jb = kb >> 1; jb > 0; jb >>= 1) {
-            for (int i = tid; i < P; i += 256) {
-                const int ixj = i ^ jb;
-                if (ixj > i) {
-                    const uint64_t a = keys[i], b = keys[ixj];
-                    if (((i & kb) == 0) == (a < b)) { keys[i] = b; keys[ixj] = a; }
+        for (int kb = 2; kb <= P; kb <<= 1)
+            for (int jb = kb >> 1; jb > 0; jb >>= 1) {
+                for (int i = tid; i < P; i += 256) {
+                    const int ixj = i ^ jb;
+                    if (ixj > i) {
+                        const uint64_t a = keys[i], b = keys[ixj];
+                        if (((i & kb) == 0) == (a < b)) { keys[i] = b; keys[ixj] = a; }
+                    }
                 }
+                __syncthreads();
             }
-            __syncthreads();
+        if (tid == 0) {
+            int emitted = s_emitted, nvalid = s_nvalid;
+            for (int e = 0; e < n; ++e) {
+                const int j = (int)(uint32_t)keys[e];
+                const float v = row[j];
+                if (v < thr) {
+                    s_stop = 1;
+                    break;
+                }
+                bool ok = true;
+                if (hf_i && hfdb[j]) ok = fi == fdb[j];
+                idx_out[(size_t)r * k + emitted] = j;
+                sim_out[(size_t)r * k + emitted] = v;
+                if (valid_out) valid_out[(size_t)r * k + emitted] = ok;
+                nvalid += ok;
+                ++emitted;
+            }
+            s_emitted = emitted;
+            s_nvalid = nvalid;
+            if (n > 0) s_upper = keys[n - 1];
+            if (n < want) s_stop = 1;
         }
+        __syncthreads();
+    }
     if (tid == 0) {
-        const bool hf_i = gating && hfq[r] != 0;
-        const int64_t fi = gating ? fq[r] : 0;
-        int emitted = 0, nvalid = 0;
-        for (int e = 0; e < n; ++e) {
-            const int j = (int)(uint32_t)keys[e];
-            const float v = row[j];
-            if (v < thr) break;
-            bool ok = true;
-            if (hf_i && hfdb[j]) ok = fi == fdb[j];
-            idx_out[(size_t)r * k + emitted] = j;
-            sim_out[(size_t)r * k + emitted] = v;
-            if (valid_out) valid_out[(size_t)r * k + emitted] = ok;
-            nvalid += ok;
-            ++emitted;
-        }
-        count_out[r] = emitted;
+        count_out[r] = s_emitted;
         if (totals) {
-            atomicAdd(totals + 0, (unsigned long long)nvalid);
-            atomicAdd(totals + 1, (unsigned long long)(emitted - nvalid));
+            atomicAdd(totals + 0, (unsigned long long)s_nvalid);
+            atomicAdd(totals + 1, (unsigned long long)(s_emitted - s_nvalid));
         }
     }
 }
@@ -701,7 +738,121 @@ __global__ __launch_bounds__(256) void k_xcorr_reduce(const float* __restrict__ 
     if (threadIdx.x == 0) out[0] = sqrtf((red[0][0] / (float)n1) * (red[1][0] / (float)n2));
 }
 
+// ------------------------------------------------------- batched rerank ------
+// CricaVPR.rerank_candidates at scale (place_recognition.py:714-757): the cross-
+// correlation score of many (query, candidate) local-feature pairs in one pass.  Grid
+// (column tile, row tile, pair): each workgroup computes one 128 x 128 tile of C = qn mn^T
+// (sim_tile: the same exact-f32 MFMA k order as the single-pair mlg_xcorr_score) and keeps
+// only its maxima -- every row's max over the tile's columns and every column's max over
+// the tile's rows -- so no [n1, n2] matrix is written; k_xcorr_finish takes the max over
+// the tiles and the means in k_xcorr_reduce's order (the same bits as the single pair).
+// feats: L2-normalised rows, frame f at feats + f * L * D; rowp [P][ct][L], colp [P][rt][L].
+__global__ __launch_bounds__(256, 2) void k_xcorr_tiles(const float* __restrict__ feats, int L, int D,
+                                                        const int32_t* __restrict__ qa,
+                                                        const int32_t* __restrict__ qb, float* __restrict__ rowp,
+                                                        float* __restrict__ colp) {
+    __shared__ float As[SBK][SBM + 4];
+    __shared__ float Bs[SBK][SBN + 4];
+    __shared__ float part[2][2][SBM];  // [row / col][wave half][index in tile]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int p = blockIdx.z, ct = blockIdx.x, rt = blockIdx.y;
+    const int m0 = rt * SBM, n0 = ct * SBN;
+    const int nct = gridDim.x, nrt = gridDim.y;
+    const float* A = feats + (size_t)qa[p] * L * D;
+    const float* B = feats + (size_t)qb[p] * L * D;
+    f32x16 acc[2][2];
+    sim_tile(A, L, B, L, D, m0, n0, As, Bs, acc);
+    // D[i][j]: col j = lane & 31, row i = (r & 3) + 8 (r >> 2) + 4 (lane >> 5); rows / columns
+    // past L are clamped copies and are masked out of both maxima
+    const int hh = lane >> 5, c = lane & 31;
+    float cm[2] = {-INFINITY, -INFINITY};  // column max per tb over this wave's 64 rows
+#pragma unroll
+    for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int i = m0 + wm * 64 + ta * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            float rm = -INFINITY;
+#pragma unroll
+            for (int tb = 0; tb < 2; ++tb) {
+                const int j = n0 + wn * 64 + tb * 32 + c;
+                const float v = acc[ta][tb][r];
+                if (j < L) rm = fmaxf(rm, v);
+                if (i < L) cm[tb] = fmaxf(cm[tb], v);
+            }
+            // row max across the 32 lanes of this half (columns c)
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) rm = fmaxf(rm, __shfl_xor(rm, o, 64));
+            if (c == 0) part[0][wn][wm * 64 + ta * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh] = rm;
+        }
+#pragma unroll
+    for (int tb = 0; tb < 2; ++tb) {
+        const float v = fmaxf(cm[tb], __shfl_xor(cm[tb], 32, 64));  // both row halves
+        if (hh == 0) part[1][wm][wn * 64 + tb * 32 + c] = v;
+    }
+    __syncthreads();
+    if (tid < SBM) {
+        const int i = m0 + tid;
+        if (i < L) rowp[((size_t)p * nct + ct) * L + i] = fmaxf(part[0][0][tid], part[0][1][tid]);
+    } else {
+        const int j = n0 + tid - SBM;
+        if (j < L) colp[((size_t)p * nrt + rt) * L + j] = fmaxf(part[1][0][tid - SBM], part[1][1][tid - SBM]);
+    }
+}
+
+// one workgroup per pair: maxima over the tiles, then k_xcorr_reduce's sums and root
+__global__ __launch_bounds__(256) void k_xcorr_finish(const float* __restrict__ rowp, const float* __restrict__ colp,
+                                                      int L, int nct, int nrt, float* __restrict__ score) {
+    __shared__ float red[2][256];
+    const int p = blockIdx.x;
+    float rs = 0.f, cs = 0.f;
+    for (int i = threadIdx.x; i < L; i += 256) {
+        float m = -INFINITY;
+        for (int t = 0; t < nct; ++t) m = fmaxf(m, rowp[((size_t)p * nct + t) * L + i]);
+        rs += m;
+    }
+    for (int j = threadIdx.x; j < L; j += 256) {
+        float m = -INFINITY;
+        for (int t = 0; t < nrt; ++t) m = fmaxf(m, colp[((size_t)p * nrt + t) * L + j]);
+        cs += m;
+    }
+    red[0][threadIdx.x] = rs;
+    red[1][threadIdx.x] = cs;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + o];
+            red[1][threadIdx.x] += red[1][threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) score[p] = sqrtf((red[0][0] / (float)L) * (red[1][0] / (float)L));
+}
+
 }  // namespace
+
+size_t mlg_xcorr_batch_ws_bytes(int F, int L, int D, int P) {
+    if (F <= 0 || L <= 0 || D <= 0 || P <= 0) return 0;
+    const size_t t = (size_t)((L + SBM - 1) / SBM);
+    return (((size_t)F * L * D * 4 + 255) & ~(size_t)255) + 2 * (size_t)P * t * L * 4;
+}
+
+int mlg_xcorr_batch_run(const float* feats, int F, int L, int D, const int32_t* qa, const int32_t* qb, int P,
+                        void* ws, size_t ws_bytes, float* score, hipStream_t s) {
+    if (P <= 0) return MLG_OK;
+    if (!feats || !qa || !qb || !ws || !score || F <= 0 || L <= 0 || D <= 0 || (D % 4)) return MLG_EINVAL;
+    if (ws_bytes < mlg_xcorr_batch_ws_bytes(F, L, D, P)) return MLG_ENOMEM;
+    float* fn = (float*)ws;
+    const int t = (L + SBM - 1) / SBM;
+    float* rowp = (float*)((char*)ws + (((size_t)F * L * D * 4 + 255) & ~(size_t)255));
+    float* colp = rowp + (size_t)P * t * L;
+    // the reference's q / (||q|| + 1e-8) per row, numpy-exact (one thread per row)
+    hipLaunchKernelGGL(k_row_normalize, dim3((F * L + 63) / 64), dim3(64), 0, s, feats, fn, F * L, D, D, nullptr);
+    hipLaunchKernelGGL(k_xcorr_tiles, dim3(t, t, P), dim3(256), 0, s, fn, L, D, qa, qb, rowp, colp);
+    hipLaunchKernelGGL(k_xcorr_finish, dim3(P), dim3(256), 0, s, rowp, colp, L, t, t, score);
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}
 
 int mlg_row_normalize(const float* X, float* Xn, int N, int D, float* norms, hipStream_t s) {
     if (N <= 0 || D <= 0) return MLG_EINVAL;
@@ -729,7 +880,7 @@ int mlg_topk_gate(const float* S, int lds, int N, int Q, const double* tq, const
                   const uint8_t* hfq, const int64_t* fdb, const uint8_t* hfdb, double min_gap, float thr, int k,
                   int gating, int32_t* idx, float* sim, uint8_t* valid, int32_t* count, unsigned long long* totals,
                   hipStream_t s) {
-    if (N <= 0 || Q <= 0 || k <= 0 || k > TOPK_LARGE || lds < N) return MLG_EINVAL;
+    if (N <= 0 || Q <= 0 || k <= 0 || lds < N) return MLG_EINVAL;
     if (gating && (!fq || !hfq || !fdb || !hfdb)) return MLG_EINVAL;
     if (k > 256)
         hipLaunchKernelGGL(k_topk_large, dim3(Q), dim3(256), 0, s, S, lds, N, Q, tq, tdb, fq, hfq, fdb, hfdb, min_gap,

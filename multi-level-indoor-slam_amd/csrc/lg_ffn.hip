@@ -103,19 +103,6 @@ __device__ __forceinline__ void gemm_phase(const bf16_t* __restrict__ W, int N, 
     }
 }
 
-// diagnostic build switch (tools/ffn_variants.sh): wait states between a GEMM phase's
-// last MFMA and the first VALU read of its accumulators
-#ifndef MLG_FFN_PAD
-#define MLG_FFN_PAD 0
-#endif
-__device__ __forceinline__ void mfma_pad() {
-#if MLG_FFN_PAD
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-}
-
 template <int NT, int MT>
 __device__ __forceinline__ void zero(f32x16 (&acc)[NT][MT]) {
 #pragma unroll
@@ -193,7 +180,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             f32x16 acc[NT1][MT];
             zero(acc);
             gemm_phase<NT1, MT, RING>(w.Wout, 256, 32 * NT1 * wave, 4, 32, lds, acc);
-            mfma_pad();
             __syncthreads();  // every wave has read the ctx half
     #pragma unroll
             for (int t = 0; t < NT1; ++t)
@@ -217,7 +203,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             f32x16 acc[NT2][MT];
             zero(acc);
             gemm_phase<NT2, MT, RING>(w.Wf1, 512, 32 * NT2 * wave, 8, 0, lds, acc);
-            mfma_pad();
     #pragma unroll
             for (int t = 0; t < NT2; ++t)
     #pragma unroll
@@ -319,7 +304,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             f32x16 acc[NT1][MT];
             zero(acc);
             gemm_phase<NT1, MT, RING>(w.Wf2, 256, 32 * NT1 * wave, 8, 0, lds, acc);
-            mfma_pad();
             __syncthreads();  // every wave has read the GELU output
     #pragma unroll
             for (int t = 0; t < NT1; ++t)

@@ -132,7 +132,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> knn_gate(const Tensor& desc, const Te
     TORCH_CHECK(desc.dim() == 2, "desc must be [N, D]");
     const int64_t N = desc.size(0), D = desc.size(1);
     TORCH_CHECK(t.numel() == N && floor.numel() == N && has_floor.numel() == N, "t / floor / has_floor must be [N]");
-    TORCH_CHECK(k >= 1 && k <= 4096, "k must be in [1, 4096]");
+    TORCH_CHECK(k >= 1, "k must be >= 1");
     TORCH_CHECK(q0 >= 0 && Q >= 0 && q0 + Q <= N, "query rows out of range");
     if (totals.has_value() && totals->defined()) {
         want(*totals, at::kLong, "totals");
@@ -160,7 +160,7 @@ std::tuple<Tensor, Tensor, Tensor> knn_query(const Tensor& db, const Tensor& q, 
     want(t_q, at::kDouble, "t_q");
     const int64_t N = db.size(0), D = db.size(1), Q = q.size(0);
     TORCH_CHECK(q.dim() == 2 && q.size(1) == D && t_db.numel() == N && t_q.numel() == Q, "knn_query shapes");
-    TORCH_CHECK(k >= 1 && k <= 4096, "k must be in [1, 4096]");
+    TORCH_CHECK(k >= 1, "k must be >= 1");
     c10::DeviceGuard g(db.device());
     auto o = db.options();
     Tensor idx = at::empty({Q, k}, o.dtype(at::kInt)), sim = at::empty({Q, k}, o.dtype(at::kFloat));
@@ -381,6 +381,24 @@ std::tuple<Tensor, Tensor, Tensor> superglue(const Tensor& kpts, const Tensor& s
                            stream_of(kpts)),
              "mlg_superglue");
     return {m, sc, n};
+}
+
+// CricaVPR.rerank_candidates at scale: feats f32 [F, L, D], query / cand int32 [P] -> scores f32 [P]
+Tensor xcorr_batch(const Tensor& feats, const Tensor& query, const Tensor& cand) {
+    want(feats, at::kFloat, "feats");
+    want(query, at::kInt, "query");
+    want(cand, at::kInt, "cand");
+    TORCH_CHECK(feats.dim() == 3 && feats.size(2) % 4 == 0, "feats [F, L, D] with D % 4 == 0");
+    TORCH_CHECK(query.numel() == cand.numel(), "query / cand [P]");
+    const int64_t F = feats.size(0), L = feats.size(1), D = feats.size(2), P = query.numel();
+    c10::DeviceGuard g(feats.device());
+    Tensor out = at::empty({P}, feats.options());
+    if (P == 0) return out;
+    Tensor ws = workspace(mlg_xcorr_batch_workspace_bytes((int)F, (int)L, (int)D, (int)P), feats);
+    check_rc(mlg_xcorr_batch(cp<float>(feats), (int)F, (int)L, (int)D, cp<int32_t>(query), cp<int32_t>(cand), (int)P,
+                             ws.data_ptr(), (size_t)ws.numel(), mp<float>(out), stream_of(feats)),
+             "mlg_xcorr_batch");
+    return out;
 }
 
 // --------------------------------------------------------------- LightGlue
@@ -725,6 +743,7 @@ TORCH_LIBRARY(mlgate, m) {
     m.def("row_normalize(Tensor X) -> Tensor");
     m.def("similarity(Tensor A, Tensor B) -> Tensor");
     m.def("xcorr_score(Tensor q, Tensor m) -> Tensor");
+    m.def("xcorr_batch(Tensor feats, Tensor query, Tensor cand) -> Tensor");
     m.def("superpoint(Tensor frames, Tensor[] weights, float detection_threshold, int max_keypoints, "
           "int nms_radius, int remove_borders, bool with_bf16) -> (Tensor, Tensor, Tensor, Tensor, Tensor)");
     m.def("lightglue(Tensor kpts, Tensor desc, Tensor counts, Tensor pair_a, Tensor pair_b, Tensor[] weights, "
@@ -762,6 +781,7 @@ TORCH_LIBRARY_IMPL(mlgate, CUDA, m) {
     m.impl("row_normalize", &row_normalize);
     m.impl("similarity", &similarity);
     m.impl("xcorr_score", &xcorr_score);
+    m.impl("xcorr_batch", &xcorr_batch);
     m.impl("superpoint", &superpoint);
     m.impl("lightglue", &lightglue);
     m.impl("ransac_epipolar", &ransac_epipolar);

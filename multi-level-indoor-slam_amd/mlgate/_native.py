@@ -16,7 +16,8 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmlgate.so")
 TORCH_LIB_PATH = os.path.join(_HERE, "libmlgate_torch.so")
-OPS = ("vit_forward_into", "knn_gate", "knn_query", "row_normalize", "similarity", "xcorr_score", "superpoint",
+OPS = ("vit_forward_into", "knn_gate", "knn_query", "row_normalize", "similarity", "xcorr_score", "xcorr_batch",
+       "superpoint",
        "lightglue", "ransac_epipolar", "recover_pose", "resnet50", "loftr_features", "loftr_match", "superglue", "pillow_resize_224", "plane_ransac", "proximity",
        "prof_enable", "prof_reset", "prof_read")
 
@@ -87,6 +88,9 @@ EXPORTS = {
     "mlg_prof_read": (c_int, [c_int, ctypes.POINTER(c_double), ctypes.POINTER(c_long)]),
     "mlg_prof_read_work": (c_int, [c_int, ctypes.POINTER(c_double)]),
     "mlg_lg_orient_matches": (c_int, [c_void_p] * 5 + [c_int, c_int] + [c_void_p] * 4),
+    "mlg_xcorr_batch_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "mlg_xcorr_batch": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_size_t,
+                                c_void_p, c_void_p]),
     "mlg_dbg_lg_trace_begin": (c_int, [c_void_p, c_size_t]),
     "mlg_dbg_lg_trace_end": (c_int, [c_void_p, c_void_p, c_int]),
     "mlg_dbg_fill_lds": (c_int, [ctypes.c_uint32, c_void_p, c_void_p]),

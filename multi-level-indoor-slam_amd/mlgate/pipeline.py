@@ -149,9 +149,10 @@ class DeviceGate:
     """The same chain on device arrays for a frame-sharded sequence: rank r of W owns
     keyframes [r N / W, (r + 1) N / W) -- its frames, ViT forwards and SuperPoint
     features -- and the query rows of the same range.  Exchange steps (RCCL over
-    xGMI): the [N, 768] descriptor all-gather before retrieval, the SuperPoint feature
-    all-gather before verification, and an 8-B-per-pair all-gather that re-balances the
-    gate-accepted pairs across ranks (mlgate.distributed.balanced_pairs).
+    xGMI; gloo through host copies): the [N, 768] descriptor all-gather before retrieval,
+    an 8-B-per-pair all-gather that re-balances the gate-accepted pairs across ranks
+    (mlgate.distributed.balanced_pairs), and the SuperPoint features of exactly the
+    keyframes each rank's pair slice touches (mlgate.distributed.FeatureExchange).
 
     One ``step()`` gates the whole sequence once and returns per-rank counts; the
     caller all-reduces them (bench.py)."""
@@ -181,12 +182,17 @@ class DeviceGate:
         self.min_inliers, self.min_inlier_ratio = min_inliers, min_inlier_ratio
         self.sp_batch, self.lg_chunk, self.kp = sp_batch, lg_chunk, max_keypoints
         self.t_all = torch.as_tensor(np.asarray(timestamps, np.float64), device=self.dev)
+        from .vpr import floor_codes
         self.labels = np.asarray(floor_labels)
-        codes = np.asarray(self.labels, np.int64)
-        if not np.array_equal(codes, self.labels):
-            raise ValueError("DeviceGate takes integer floor labels")
+        # equality codes for the retrieval floor check and the verifier skip (Python ==
+        # semantics: 1 == 1.0, NaN != NaN, None = no label), the numeric labels for the
+        # gate's |floor_i - floor_j| > limit (loop_closure_gate.py:91-98; NaN never rejects)
+        lab = list(self.labels.tolist()) if self.labels.dtype != object else list(self.labels)
+        codes, has = floor_codes(lab)
         self.f_all = torch.as_tensor(codes, device=self.dev)
-        self.hf_all = torch.ones(N, dtype=torch.uint8, device=self.dev)
+        self.hf_all = torch.as_tensor(has, dtype=torch.uint8, device=self.dev)
+        num = np.array([np.nan if v is None else float(v) for v in lab], np.float64)
+        self.f_num = torch.as_tensor(num, device=self.dev)
         sd = vit_state_dict if vit_state_dict is not None else synthetic_state_dict(0)
         self.eng = VitB14(sd, device=self.dev, max_batch=vit_batch)
         self.gather = mdist.RowGather(N, EMBED, world, self.dev)
@@ -199,15 +205,12 @@ class DeviceGate:
             KP = max_keypoints
             self.sp = SuperPointGPU(device=self.dev, max_num_keypoints=KP)
             self.lg = LightGlueGPU(device=self.dev)
-            self.g_kp = mdist.RowGather(N, KP * 2, world, self.dev)
-            self.g_ds = mdist.RowGather(N, KP * 256, world, self.dev)
-            self.g_cnt = mdist.RowGather(N, 1, world, self.dev, dtype=torch.int32)
-            if world == 1:
-                self.kp_loc, self.ds_loc, self.cnt_loc = self.g_kp.out, self.g_ds.out, self.g_cnt.out
-            else:
-                self.kp_loc = torch.empty(self.n_local, KP * 2, device=self.dev)
-                self.ds_loc = torch.empty(self.n_local, KP * 256, device=self.dev)
-                self.cnt_loc = torch.empty(self.n_local, 1, dtype=torch.int32, device=self.dev)
+            # this rank's keyframes' features; with world > 1 each rank then receives the
+            # features of exactly the keyframes its verification slice touches
+            self.kp_loc = torch.empty(self.n_local, KP * 2, device=self.dev)
+            self.ds_loc = torch.empty(self.n_local, KP * 256, device=self.dev)
+            self.cnt_loc = torch.empty(self.n_local, 1, dtype=torch.int32, device=self.dev)
+            self.fx = mdist.FeatureExchange(N, world, rank) if world > 1 else None
             Kc = np.asarray(K if K is not None else np.eye(3), np.float64)
             self.K = torch.from_numpy(Kc.reshape(9).copy()).to(self.dev) if K is not None else None
         self.last = {}
@@ -258,18 +261,14 @@ class DeviceGate:
             self.kp_loc[b0:b1].copy_(kp.view(b1 - b0, -1))
             self.ds_loc[b0:b1].copy_(ds.view(b1 - b0, -1))
             self.cnt_loc[b0:b1, 0].copy_(cnt)
-        if self.world > 1:
-            self.g_kp(self.kp_loc)
-            self.g_ds(self.ds_loc)
-            self.g_cnt(self.cnt_loc)
-        kp_all = self.g_kp.out.view(self.N, self.kp, 2)
-        ds_all = self.g_ds.out.view(self.N, self.kp, 256)
-        counts = self.g_cnt.out.view(-1).cpu().numpy()
         # matches handed to verify_with_semantics (is_valid ones), skip rule on floors
         qs, js = torch.nonzero(live & (valid != 0), as_tuple=True)
         pa_t, pb_t = (qs + self.lo).to(torch.int32), idx[qs, js].to(torch.int32)
         if self.verifier_floor_gating:
-            same = self.f_all[pa_t.long()] == self.f_all[pb_t.long()]
+            # verify_with_semantics skips when floor1 != floor2 in Python
+            # (geometric_verification.py:709-710): None == None only, NaN != NaN
+            ha, hb = self.hf_all[pa_t.long()] != 0, self.hf_all[pb_t.long()] != 0
+            same = (ha & hb & (self.f_all[pa_t.long()] == self.f_all[pb_t.long()])) | (~ha & ~hb)
             out["skipped_floor_mismatch"] = int((~same).sum())
             pa_t, pb_t = pa_t[same], pb_t[same]
         # pair-level load balance across ranks (features are all-gathered, so any rank
@@ -278,6 +277,20 @@ class DeviceGate:
         pa_t, pb_t = self.mdist.balanced_pairs(pa_t, pb_t, self.world, self.rank, group_reverse=dedup)
         pa, pb = pa_t.cpu().numpy(), pb_t.cpu().numpy()
         self.last_pairs = (pa, pb)
+        # features of the keyframes the pairs touch: the local table (world 1), or the
+        # need-driven exchange (row k of the compact tables = keyframe need[k])
+        if self.world > 1:
+            need = np.unique(np.concatenate([pa, pb]).astype(np.int64))
+            kp_c, ds_c, cnt_c = self.fx(need, [self.kp_loc, self.ds_loc, self.cnt_loc])
+            nf = len(need)
+            local = lambda x: np.searchsorted(need, x).astype(np.int32)  # noqa: E731
+            out["features_exchanged_bytes"] = self.fx.last_bytes
+        else:
+            kp_c, ds_c, cnt_c, nf = self.kp_loc, self.ds_loc, self.cnt_loc, self.N
+            local = lambda x: np.asarray(x, np.int32)  # noqa: E731
+        kp_all = kp_c.view(nf, self.kp, 2)
+        ds_all = ds_c.view(nf, self.kp, 256)
+        counts = cnt_c.view(-1).cpu().numpy()
         # LightGlue once per UNORDERED pair: it is symmetric in its two images (shared
         # weights; self / cross blocks, dual-softmax assignment, early stopping and pruning
         # treat both alike), so (b, a) is (a, b) with the image roles exchanged and the
@@ -294,6 +307,7 @@ class DeviceGate:
         order = np.argsort(inv, kind="stable")
         bounds = np.searchsorted(inv[order], np.arange(0, len(ua) + self.lg_chunk, self.lg_chunk))
         out["pairs_matched_lightglue"] = len(ua)
+        ua, ub = local(ua), local(ub)  # LightGlue indexes the feature tables
         # RANSAC of chunk c runs on a side stream while LightGlue matches chunk c + 1 on
         # this one (mlg_lightglue waits on its stream once per layer; the side stream
         # fills those gaps and the CUs the small RANSAC / assignment grids leave idle)
@@ -323,10 +337,12 @@ class DeviceGate:
                 P = len(ca)
                 lv = torch.arange(self.kp, device=self.dev)[None, :] < n[:, None]
                 pi, si = torch.nonzero(lv, as_tuple=True)
-                ta = torch.from_numpy(ca).to(self.dev).long()
+                ta = torch.from_numpy(ca).to(self.dev).long()  # global keyframe indices
                 tb = torch.from_numpy(cb).to(self.dev).long()
-                k1 = kp_all[ta[pi], m[pi, si, 0].long()].contiguous()
-                k2 = kp_all[tb[pi], m[pi, si, 1].long()].contiguous()
+                la = torch.from_numpy(local(ca)).to(self.dev).long()  # feature-table rows
+                lb = torch.from_numpy(local(cb)).to(self.dev).long()
+                k1 = kp_all[la[pi], m[pi, si, 0].long()].contiguous()
+                k2 = kp_all[lb[pi], m[pi, si, 1].long()].contiguous()
                 offs = torch.zeros(P + 1, dtype=torch.int32, device=self.dev)
                 offs[1:] = torch.cumsum(n, 0)
                 _, _, inl, _, _ = geometry.epipolar_ransac_device(k1, k2, offs, self.K, 0, 3.0)
@@ -336,7 +352,7 @@ class DeviceGate:
                 if rec is not None:
                     rec.append((sel, n, inl, ok))
                 # the floor gate on the geometrically valid pairs
-                gate_rej_t += (ok & ((self.f_all[ta] - self.f_all[tb]).abs() > self.limit)).sum()
+                gate_rej_t += (ok & ((self.f_num[ta] - self.f_num[tb]).abs() > self.limit)).sum()
         main.wait_stream(side)
         n_valid, gate_rej = int(n_valid_t), int(gate_rej_t)
         if rec is not None:

@@ -8,7 +8,8 @@ import numpy as np
 
 from . import _native
 
-MAX_K = 4096  # k <= 32: fused scan; <= 256: per-lane lists; <= 4096: radix select (knn.hip)
+# k <= 32: fused scan; <= 256: per-lane lists; beyond: radix select in windows of 4096 ranks
+# (knn.hip k_topk_large) -- no upper limit, as the reference's argsort()[:k] has none
 
 
 def knn_gate(desc, t, floor, has_floor, min_gap, thr, k, gating, q0=0, Q=None, totals=None):
@@ -18,8 +19,8 @@ def knn_gate(desc, t, floor, has_floor, min_gap, thr, k, gating, q0=0, Q=None, t
 
     Returns device tensors idx int32 [Q, k], sim f32 [Q, k], valid uint8 [Q, k], count int32 [Q].
     """
-    if not 1 <= k <= MAX_K:
-        raise ValueError(f"k must be in [1, {MAX_K}] (got {k})")
+    if k < 1:
+        raise ValueError(f"k must be >= 1 (got {k})")
     N = desc.shape[0]
     Q = N - q0 if Q is None else Q
     return _native.ops().knn_gate(desc, t, floor, has_floor, float(min_gap), float(thr), int(k), bool(gating),
@@ -50,8 +51,8 @@ def flatten_matches(idx, sim, valid, count, q0=0):
 def knn_query(db, qdesc, t_db, t_query, min_gap, k):
     """BasePlaceRecognition.query on the device: db f32 [N, D], qdesc f32 [Q, D], t_db f64 [N],
     t_query f64 [Q] (NaN = no timestamp).  Returns device idx int32 [Q, k], sim f32 [Q, k], count [Q]."""
-    if not 1 <= k <= MAX_K:
-        raise ValueError(f"k must be in [1, {MAX_K}] (got {k})")
+    if k < 1:
+        raise ValueError(f"k must be >= 1 (got {k})")
     return _native.ops().knn_query(db, qdesc, t_db, t_query, float(min_gap), int(k))
 
 

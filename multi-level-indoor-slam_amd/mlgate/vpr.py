@@ -204,9 +204,7 @@ class BasePlaceRecognition:
         tq = torch.tensor([float('nan') if timestamp is None else float(timestamp)], dtype=torch.float64,
                           device=dev)
         q = torch.from_numpy(np.asarray(qd, np.float32).reshape(1, -1)).to(dev)
-        if k > retrieval.MAX_K and len(self.descriptors) > retrieval.MAX_K:
-            raise ValueError(f"k={k} exceeds the device top-k limit of {retrieval.MAX_K}")
-        kk = max(1, min(k, len(self.descriptors), retrieval.MAX_K))
+        kk = max(1, min(k, len(self.descriptors)))
         idx, sim, cnt = retrieval.knn_query(db, q, t_db, tq, min_time_gap if timestamp is not None else 0.0, kk)
         c = int(cnt[0]) if k > 0 else 0
         idx, sim = idx[0, :c].cpu().numpy(), sim[0, :c].cpu().numpy()
@@ -339,17 +337,41 @@ class CricaVPR(_DinoEngineMixin, BasePlaceRecognition):
 
     def rerank_candidates(self, query_idx: int, candidates: List[Tuple[int, float]],
                           top_k: int = 5) -> List[Tuple[int, float]]:
+        """place_recognition.py:714-757: 0.5 global + 0.5 cross-correlation, sorted
+        (stable) by the combined score; every candidate of the query scored in ONE batched
+        pass (mlg_xcorr_batch) instead of one correlation per candidate."""
         if not self.use_reranking or query_idx not in self._feature_cache:
             return candidates[:top_k]
-        qf = self._feature_cache[query_idx]
-        scored = []
-        for j, g in candidates:
-            if j in self._feature_cache:
-                scored.append((j, 0.5 * g + 0.5 * self.compute_cross_correlation_score(qf, self._feature_cache[j])))
-            else:
-                scored.append((j, g))
-        scored.sort(key=lambda x: x[1], reverse=True)
-        return scored[:top_k]
+        return self.rerank_candidates_batch({query_idx: candidates}, top_k)[query_idx]
+
+    def rerank_candidates_batch(self, requests: Dict[int, List[Tuple[int, float]]],
+                                top_k: int = 5) -> Dict[int, List[Tuple[int, float]]]:
+        """rerank_candidates for many queries at once ({query_idx: [(match_idx,
+        global_sim), ...]}): all (query, candidate) cross-correlation scores of all
+        queries in one batched pass over the cached local features (one frame bank, no
+        [L, L] matrix per pair), then the reference's combination and stable sort per query."""
+        torch = _torch()
+        pairs = [(q, j) for q, cands in requests.items() if self.use_reranking and q in self._feature_cache
+                 for j, _ in cands if j in self._feature_cache]
+        scores = {}
+        if pairs:
+            frames = sorted({i for p in pairs for i in p})
+            pos = {f: k for k, f in enumerate(frames)}
+            bank = torch.cat([self._to_device_feats(self._feature_cache[f])[None] for f in frames])
+            dev = bank.device
+            qa = torch.tensor([pos[q] for q, _ in pairs], dtype=torch.int32, device=dev)
+            qb = torch.tensor([pos[j] for _, j in pairs], dtype=torch.int32, device=dev)
+            sc = _native.ops().xcorr_batch(bank.contiguous(), qa, qb).cpu().numpy()
+            scores = {p: float(v) for p, v in zip(pairs, sc)}
+        out = {}
+        for q, cands in requests.items():
+            if not self.use_reranking or q not in self._feature_cache:
+                out[q] = cands[:top_k]
+                continue
+            scored = [(j, 0.5 * g + 0.5 * scores[(q, j)]) if (q, j) in scores else (j, g) for j, g in cands]
+            scored.sort(key=lambda x: x[1], reverse=True)
+            out[q] = scored[:top_k]
+        return out
 
     def _append(self, descs, local, timestamps, floor_labels, image_paths):
         out = []
@@ -405,10 +427,9 @@ class SemanticPlaceRecognition:
         from . import retrieval
         if k <= 0:
             return []
-        # a row ranks all n entries (its own included when min_time_gap <= 0)
-        if k > retrieval.MAX_K and n > retrieval.MAX_K:
-            raise ValueError(f"k={k} exceeds the device top-k limit of {retrieval.MAX_K}")
-        kk = min(k, retrieval.MAX_K)
+        # a row ranks all n entries (its own included when min_time_gap <= 0): k beyond n
+        # returns what argsort()[:k] returns, every candidate
+        kk = min(k, n)
         X, dev = self.vpr._device_matrix()
         t = torch.tensor([float(d.timestamp) for d in descs], dtype=torch.float64, device=dev)
         codes, has = floor_codes([d.floor_label for d in descs])

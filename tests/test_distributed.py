@@ -131,3 +131,34 @@ def test_balanced_pairs_group_reverse(tmp_path):
     out = str(tmp_path / "pairs_rev.txt")
     mp.spawn(_pairs_rev_worker, args=(3, _free_port(), out), nprocs=3, join=True)
     assert open(out).read() == "ok"
+
+
+def _fx_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 53
+    full_kp = torch.arange(n * 6, dtype=torch.float32).view(n, 6) * 0.5
+    full_ds = torch.randn(n, 16, generator=torch.Generator().manual_seed(7))
+    full_cnt = torch.arange(n, dtype=torch.int32).view(n, 1) * 3
+    lo, hi = mdist.shard(n, world, rank)
+    rng = np.random.default_rng(100 + rank)
+    need = np.unique(rng.integers(0, n, [17, 0, 40][rank]))  # uneven, one rank needs nothing
+    fx = mdist.FeatureExchange(n, world, rank)
+    kp, ds, cnt = fx(need, [full_kp[lo:hi], full_ds[lo:hi], full_cnt[lo:hi]])
+    idx = torch.from_numpy(need.astype(np.int64))
+    ok = (torch.equal(kp, full_kp[idx]) and torch.equal(ds, full_ds[idx]) and torch.equal(cnt, full_cnt[idx])
+          and fx.last_bytes == len(need) * (6 * 4 + 16 * 4 + 4))
+    res = mdist.gather_objects_to_rank0(bool(ok), world, rank)
+    if rank == 0:
+        with open(out_path, "w") as f:
+            f.write("ok" if all(res) else f"mismatch {res}")
+    dist.destroy_process_group()
+
+
+def test_feature_exchange_delivers_exactly_the_needed_rows(tmp_path):
+    """FeatureExchange (the sharded gate's SuperPoint feature step): each rank receives the
+    rows of exactly the keyframes it asked for, in ascending global order, from whichever
+    ranks own them -- uneven needs, an empty need list, several dtypes."""
+    out = str(tmp_path / "fx.txt")
+    mp.spawn(_fx_worker, args=(3, _free_port(), out), nprocs=3, join=True)
+    assert open(out).read() == "ok"

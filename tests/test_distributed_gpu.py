@@ -1,0 +1,99 @@
+"""The frame-sharded full gate (DeviceGate with world 2) executed on the GPU: two ranks on
+cuda:0 over gloo (collectives staged through host copies -- the same code path RCCL runs
+on device tensors across GPUs), each owning a contiguous keyframe shard, its ViT and
+SuperPoint forwards and its query rows; the verification pairs re-balanced across ranks
+(balanced_pairs, unordered pairs kept on one rank) and the SuperPoint features of exactly
+the keyframes each rank's pairs touch exchanged (FeatureExchange).
+
+Bar (the reference's per-query loop is row-independent,
+place_recognition.py:873-909): the all-reduced counts and rejection terms, and every
+ordered pair's (matches, inliers, is_valid) gathered to rank 0, equal the world-1 run
+exactly."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _case(name):
+    from mlgate import synthetic
+    from mlgate.pipeline import floor_labels_from_imu
+    from oracle import geometry as ogeo
+    if name == "chain":  # the 40-keyframe gate-chain fixture (tests/golden/make_gate_chain.py)
+        g = np.load(os.path.join(ROOT, "tests", "golden", "gate_chain.npz"))
+        n, places, seed, k = (int(x) for x in g["params"])
+        plan = tuple((int(f), float(p)) for f, p in g["plan"])
+        seq = synthetic.make_sequence(n, places, seed, plan)
+        thr, gap = (float(x) for x in g["thr_gap"])
+        kw = dict(k=k, similarity_threshold=thr, min_time_gap=gap, vit_batch=64, lg_chunk=64)
+        return seq, np.asarray(g["labels"]), kw, ogeo.ISEC_K
+    seq = synthetic.make_sequence(1000, 120, 3)
+    labels, _ = floor_labels_from_imu(seq.t, synthetic.imu_log(seq), start_floor=5)
+    return seq, labels, dict(k=20, vit_batch=123, lg_chunk=512), ogeo.ISEC_K
+
+
+def _worker(rank, world, port, case, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mlgate import distributed as mdist
+    from mlgate import synthetic
+    from mlgate.pipeline import DeviceGate
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    seq, labels, kw, K = _case(case)
+    lo, hi = mdist.shard(seq.n, world, rank)
+    frames = torch.from_numpy(synthetic.frames_host(seq, np.arange(lo, hi))).to(dev)
+    g = DeviceGate(frames, seq.t, labels, world, rank, dev, K=K, record=True, **kw)
+    out = g.step()
+    xbytes = out.pop("features_exchanged_bytes", 0)
+    keys = sorted(out)
+    tot = torch.tensor([out[k_] for k_ in keys], dtype=torch.int64)
+    dist.all_reduce(tot)
+    r = g.last_pair_results
+    pairs = {(int(a), int(b)): (int(n), int(i), bool(v))
+             for a, b, n, i, v in zip(r["a"], r["b"], r["matches"], r["inliers"], r["is_valid"])}
+    parts = mdist.gather_objects_to_rank0((pairs, xbytes), world, rank)
+    if rank == 0:
+        g1 = DeviceGate(torch.from_numpy(synthetic.frames_host(seq)).to(dev), seq.t, labels, 1, 0, dev, K=K,
+                        record=True, **kw)
+        o1 = g1.step()
+        r1 = g1.last_pair_results
+        ref = {(int(a), int(b)): (int(n), int(i), bool(v))
+               for a, b, n, i, v in zip(r1["a"], r1["b"], r1["matches"], r1["inliers"], r1["is_valid"])}
+        merged, dup = {}, 0
+        for p, _ in parts:
+            dup += len(set(p) & set(merged))
+            merged.update(p)
+        res = {"counts_w2": dict(zip(keys, tot.tolist())), "counts_w1": {k_: o1[k_] for k_ in keys},
+               "pairs": len(ref), "dup": dup, "same_pairs": merged == ref,
+               "differing": [str(p) for p in ref if merged.get(p) != ref[p]][:10],
+               "exchanged_bytes": [b for _, b in parts], "valid": int(sum(v[2] for v in ref.values()))}
+        with open(out_path, "w") as f:
+            json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["chain", "seq1000"])
+def test_sharded_gate_equals_single_rank(tmp_path, case):
+    out = str(tmp_path / "res.json")
+    mp.spawn(_worker, args=(2, _free_port(), case, out), nprocs=2, join=True)
+    res = json.load(open(out))
+    print(json.dumps(res))
+    assert res["counts_w2"] == res["counts_w1"]
+    assert res["dup"] == 0 and res["same_pairs"], res["differing"]
+    assert res["pairs"] > 0 and res["valid"] > 0

@@ -108,9 +108,15 @@ def test_gate_nan_label_accepted_like_reference():
     assert len(v) == 2 and not rj
 
 
-def test_k_above_device_limit_raises_before_device_work():
+def test_large_k_has_no_limit_and_k0_needs_no_device():
+    """k has no upper limit (the reference's argsort()[:k]; k > 4096 runs the windowed
+    radix select, tests/test_retrieval_gpu.py::test_k_beyond_4096_windows): a large k
+    reaches the device (here: the no-device error, not a ValueError); k <= 0 returns the
+    reference's empty list before any device work."""
+    from mlgate._native import MlgateError
     spr = SemanticPlaceRecognition('cricavpr', device='cuda')
     spr.vpr.descriptors = [PlaceDescriptor(timestamp=float(i), descriptor=np.ones(4, np.float32), floor_label=1)
                            for i in range(4097)]
-    with pytest.raises(ValueError):
+    assert spr.find_loop_closures(k=0) == []
+    with pytest.raises(MlgateError):
         spr.find_loop_closures(k=5000)

@@ -210,3 +210,51 @@ def test_query_large_k(dev, k):
     assert np.max(np.abs(sim - rs)) <= SIM_TOL
     assert np.all((sim[:-1] > sim[1:]) | ((sim[:-1] == sim[1:]) & (idx[:-1] > idx[1:])))
     assert len(set(idx.tolist())) == c and np.all(np.abs(t[idx] - ts) >= gap)
+
+
+@pytest.mark.parametrize("L", [528, 200])
+def test_xcorr_batch_equals_single_pairs(dev, L):
+    """mlg_xcorr_batch (one pass over all (query, candidate) pairs, no [L, L] matrices)
+    gives every pair exactly the single-pair mlg_xcorr_score bits; plus the golden pairs."""
+    from mlgate import _native
+    rng = np.random.default_rng(L)
+    F, D = 7, 768
+    feats = torch.from_numpy(rng.standard_normal((F, L, D)).astype(np.float32)).to(dev)
+    qa = np.array([0, 0, 1, 3, 6, 2, 5, 4], np.int32)
+    qb = np.array([1, 2, 0, 3, 5, 6, 0, 4], np.int32)
+    got = _native.ops().xcorr_batch(feats, torch.from_numpy(qa).to(dev), torch.from_numpy(qb).to(dev)).cpu().numpy()
+    for p, (a, b) in enumerate(zip(qa, qb)):
+        ref = retrieval.xcorr_score(feats[a], feats[b]).item()
+        assert np.float32(got[p]).tobytes() == np.float32(ref).tobytes(), (p, got[p], ref)
+    g = load(os.path.join(os.path.dirname(__file__), "golden", "xcorr.npz"))
+    gf = torch.from_numpy(g["feats"].astype(np.float32)[:, 0]).to(dev)
+    pr = g["pairs"].astype(np.int32)
+    sc = _native.ops().xcorr_batch(gf, torch.from_numpy(pr[:, 0].copy()).to(dev),
+                                   torch.from_numpy(pr[:, 1].copy()).to(dev)).cpu().numpy()
+    assert np.max(np.abs(sc - g["scores"])) < 1e-5
+
+
+@pytest.mark.parametrize("k,thr", [(5000, -1.1), (20000, -1.1), (9000, -0.02)])
+def test_k_beyond_4096_windows(dev, k, thr):
+    """k > 4096 with N > 4096 (the reference's argsort()[:k] has no limit; k > N returns
+    every candidate): k_topk_large emits its ranks in windows of 4096 -- indices, order,
+    validity and similarities bit-exact against the oracle's per-row loop on the same S,
+    including a threshold that stops emission inside a window."""
+    from oracle import _lib
+    rng = np.random.default_rng(k)
+    n, d, q0, Q = 9000, 32, 4000, 64
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    t = np.arange(n, dtype=np.float64) * 0.7
+    fl = rng.integers(0, 4, n).astype(np.int64)
+    hf = (rng.random(n) > 0.1).astype(np.uint8)
+    Xd = torch.from_numpy(X).to(dev)
+    out = retrieval.knn_gate(Xd, torch.from_numpy(t).to(dev), torch.from_numpy(fl).to(dev),
+                             torch.from_numpy(hf).to(dev), 10.0, thr, k, True, q0=q0, Q=Q)
+    idx, sim, valid, count = (x.cpu().numpy() for x in out)
+    S = retrieval.pairwise_similarities(Xd)[q0:q0 + Q].cpu().numpy()
+    ri, rs, rv, rc = _lib.knn_rows(S, q0, t, fl, hf, 10.0, thr, k, True)
+    assert np.array_equal(count, rc) and count.max() > 4096
+    for r in range(Q):
+        c = int(count[r])
+        assert np.array_equal(idx[r, :c], ri[r, :c]) and np.array_equal(sim[r, :c], rs[r, :c])
+        assert np.array_equal(valid[r, :c].astype(bool), rv[r, :c].astype(bool))

@@ -169,9 +169,9 @@ def main():
     ua, ub = (key // gate.N).astype(np.int32), (key % gate.N).astype(np.int32)
     if a.max_pairs:
         ua, ub = ua[:a.max_pairs], ub[:a.max_pairs]
-    kp_all = gate.g_kp.out.view(gate.N, gate.kp, 2)
-    ds_all = gate.g_ds.out.view(gate.N, gate.kp, 256)
-    counts = gate.g_cnt.out.view(-1).cpu().numpy()
+    kp_all = gate.kp_loc.view(gate.N, gate.kp, 2)
+    ds_all = gate.ds_loc.view(gate.N, gate.kp, 256)
+    counts = gate.cnt_loc.view(-1).cpu().numpy()
     nch = (len(ua) + a.chunk - 1) // a.chunk
     print(json.dumps({"setup_s": round(time.time() - t0, 1), "unordered_pairs": int(len(ua)), "chunks": nch}),
           flush=True)

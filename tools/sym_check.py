@@ -44,9 +44,9 @@ def main():
     smp = sorted({(min(x, y), max(x, y)) for x, y in sym})[:a.sample]
     A = np.array([x for x, _ in smp], np.int32)
     B = np.array([y for _, y in smp], np.int32)
-    kp_all = gate.g_kp.out.view(gate.N, gate.kp, 2)
-    ds_all = gate.g_ds.out.view(gate.N, gate.kp, 256)
-    cnt = gate.g_cnt.out.view(-1).cpu().numpy()
+    kp_all = gate.kp_loc.view(gate.N, gate.kp, 2)
+    ds_all = gate.ds_loc.view(gate.N, gate.kp, 256)
+    cnt = gate.cnt_loc.view(-1).cpu().numpy()
     m1, s1, n1, st1 = gate.lg.match_device(kp_all, ds_all, cnt, A, B)
     m2, s2, n2, st2 = gate.lg.match_device(kp_all, ds_all, cnt, B, A)
     m1, s1, n1, m2, s2, n2 = (t.cpu().numpy() for t in (m1, s1, n1, m2, s2, n2))
