@@ -213,3 +213,27 @@ def test_ransac_inliers_equal_opencv_loop_on_gpu_matches(dev, chain, reports):
         # same sample stream and control flow; the two 5-point solvers' models differ in
         # the last bits, which can move a point sitting on the threshold (<= 0.3 %)
         assert abs(r.num_inliers - n_in) <= max(1, 0.003 * len(k1)), ((a, b), r.num_inliers, n_in)
+
+
+def test_device_gate_float_and_missing_labels(dev, chain):
+    """DeviceGate takes float labels with the reference's semantics: a non-integer floor,
+    a NaN (never equal to anything -- retrieval floor check, verifier skip -- and never
+    rejected by the gate's |df| > limit) -- the same four-term count as the drop-in
+    FullSemanticGate on the same labels.  (None labels are accepted by retrieval and the
+    verifier as the reference accepts them; the reference's gate cannot take them.)"""
+    frames = torch.from_numpy(chain["frames"]).to(dev)
+    lab = np.array([float(x) for x in chain["labels"]], np.float64)
+    lab[3] = np.nan
+    lab[lab == lab[0]] += 0.5
+    for rg, vg in ((True, True), (False, True), (False, False)):
+        fg = FullSemanticGate(device=str(dev), k=chain["k"], similarity_threshold=chain["thr"],
+                              min_time_gap=chain["gap"], retrieval_floor_gating=rg, verifier_floor_gating=vg)
+        rep = fg.run(frames, chain["seq"].t, K=ogeo.ISEC_K, floor_labels=lab)
+        g = DeviceGate(frames, chain["seq"].t, lab, device=str(dev), k=chain["k"], similarity_threshold=chain["thr"],
+                       min_time_gap=chain["gap"], retrieval_floor_gating=rg, verifier_floor_gating=vg,
+                       K=ogeo.ISEC_K, vit_batch=64, lg_chunk=64)
+        out = g.step()
+        got = {k: out[k] for k in ("retrieval_floor_rejected", "skipped_floor_mismatch", "verifier_invalid",
+                                   "gate_rejected_cross_floor")}
+        got["total"] = sum(got.values())
+        assert got == rep.rejections.as_dict(), (rg, vg, got, rep.rejections.as_dict())
