@@ -121,6 +121,74 @@ def cpu_baseline(budget_s=12.0, pairs_per_kf=0.0):
             "sample": sample}
 
 
+def loftr_flops_per_pair(L=4800, matches=0.0):
+    """Algorithmic FLOPs of LoFTR's matching for one pair at 640x480 (L = 80 x 60 coarse
+    cells): 8 coarse encoder layers (4 self + 4 cross) on both sides -- q / k / v, merge,
+    MLP 512 -> 512 -> 256 and the linear attention's KV and apply (8 heads x 32 x 32) per
+    token --, the coarse similarity L x L x 256, and per coarse match the fine stage (2
+    layers over 2 x 25 window tokens at d 128, 8 heads x 16 x 16)."""
+    def layer(d):
+        return 2 * (4 * d * d + 2 * d * 2 * d + 2 * d * d + 2 * 8 * (d // 8) ** 2)
+    return 8 * 2 * L * layer(256) + 2 * L * L * 256 + matches * 2 * 2 * 25 * layer(128)
+
+
+# algorithmic FLOPs per 640x480 keyframe of LoFTR's ResNetFPN_8_2 backbone (196-channel
+# stages counted at 196; the GPU runs them zero-padded to 256)
+def loftr_backbone_flops(H=480, W=640):
+    p2, p4, p8 = (H // 2) * (W // 2), (H // 4) * (W // 4), (H // 8) * (W // 8)
+    c = [p2 * 49 * 128, 4 * p2 * 9 * 128 * 128,                                   # stem, layer1
+         p4 * 9 * (128 * 196 + 3 * 196 * 196) + p4 * 128 * 196,                   # layer2
+         p8 * 9 * (196 * 256 + 3 * 256 * 256) + p8 * 196 * 256,                   # layer3
+         p8 * 256 * 256, p4 * (196 * 256 + 9 * 256 * 256 + 9 * 256 * 196),       # FPN 1/8, 1/4
+         p2 * (128 * 196 + 9 * 196 * 196 + 9 * 196 * 128)]                       # FPN 1/2
+    return 2.0 * sum(c)
+
+
+def loftr_bench(frames, seq, lo, dev, n_pairs=64, iters=3):
+    """configs[4] on the driver's clock (outside the gate's timed region): LoFTR backbone
+    over the keyframes of `n_pairs` revisit pairs of this rank's shard plus their
+    coarse / fine matching, HIP-event timed over `iters` runs after one warm-up."""
+    from mlgate.loftr import LoFTRGPU
+    n = frames.shape[0]
+    po = seq.place_of[lo:lo + n]
+    pairs = [(i, j) for i in range(n) for j in range(i + 1, n) if po[i] >= 0 and po[i] == po[j]][:n_pairs]
+    if not pairs:
+        return None
+    used = sorted({i for p in pairs for i in p})
+    pos = {f: k for k, f in enumerate(used)}
+    sel = frames[torch.as_tensor(used, device=dev)].contiguous()
+    lf = LoFTRGPU(device=dev, feature_batch=16)
+    pa, pb = [pos[a] for a, _ in pairs], [pos[b] for _, b in pairs]
+    H, W = int(sel.shape[1]) // 8 * 8, int(sel.shape[2]) // 8 * 8
+    coarse, fine = lf.features(sel)
+    cnt, *_ = lf.match_device(coarse, fine, H, W, pa, pb)
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record()
+    for _ in range(iters):
+        coarse, fine = lf.features(sel)
+    ev[1].record()
+    for _ in range(iters):
+        cnt, *_ = lf.match_device(coarse, fine, H, W, pa, pb)
+    ev[2].record()
+    torch.cuda.synchronize(dev)
+    t_feat, t_match = ev[0].elapsed_time(ev[1]) / iters, ev[1].elapsed_time(ev[2]) / iters
+    m = float(cnt.float().mean())
+    bf, mf = loftr_backbone_flops(H, W), loftr_flops_per_pair((H // 8) * (W // 8), m)
+    bt = bf * len(used) / (t_feat * 1e-3) / 1e12
+    mt = mf * len(pairs) / (t_match * 1e-3) / 1e12
+    return {"workload": "configs[4] LoFTR 640x480 (seeded synthetic weights): ResNetFPN_8_2 backbone per keyframe "
+                        "+ coarse linear-attention transformer, dual-softmax mutual-NN and 5x5 fine refinement "
+                        "per revisit pair",
+            "keyframes": len(used), "pairs": len(pairs), "matches_mean": round(m, 1),
+            "backbone_ms_per_keyframe": round(t_feat / len(used), 3), "backbone_tflops": round(bt, 1),
+            "backbone_frac": round(bt / MFMA_BF16_PEAK_TFLOPS, 4),
+            "match_ms_per_pair": round(t_match / len(pairs), 3), "match_tflops": round(mt, 1),
+            "match_frac": round(mt / MFMA_BF16_PEAK_TFLOPS, 4),
+            "pairs_per_s": round(len(pairs) / ((t_feat + t_match) * 1e-3), 1),
+            "flops": {"backbone_per_keyframe": bf, "match_per_pair": round(mf, 0)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -138,6 +206,7 @@ def main():
     ap.add_argument("--places", type=int, default=600)
     ap.add_argument("--verify", choices=["all", "none"], default="all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--loftr-pairs", type=int, default=64, help="configs[4] LoFTR sub-object (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -194,6 +263,7 @@ def main():
     steps = max(args.steps, 1)
     counts = {k_: int(v) // steps for k_, v in zip(keys, cv.cpu().tolist())}  # per step, all ranks
     N = args.keyframes
+    lft = loftr_bench(frames, seq, lo, dev, args.loftr_pairs) if args.loftr_pairs > 0 else None
 
     if rank == 0:
         avg_s = ms / 1e3 / max(cnt, 1)
@@ -240,6 +310,8 @@ def main():
                          "stage_rate": {SLOTS[s]: (f"{tflops[s] * 1e3:.0f} GB/s" if s in HBM_SLOTS else
                                                    f"{tflops[s]:.1f} TFLOP/s") for s in SLOTS}},
         }
+        if lft:
+            line["loftr"] = lft
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(pairs_per_kf=(counts["pairs_verified"] / N) if gate.verify else 0.0)
         print(json.dumps(line), flush=True)

@@ -184,6 +184,12 @@ int mlg_op_lg_ffn(const uint16_t* ctx, float* X, uint16_t* xcopy, int ldc, int M
 int mlg_op_lg_proj(int self_block, const uint16_t* xcopy, int ldx, const uint16_t* W, const float* bias,
                    const float* ecos, const float* esin, const uint8_t* live, uint16_t* Q, uint16_t* K, uint16_t* Vt,
                    int Npad, void* stream);
+/* Implicit-GEMM convolution of LoFTR's ResNetFPN (loftr.hip convs): k x k (k = 1 or 3,
+ * zero padding k / 2) stride-s conv of NHWC bf16 in [B, H, W, C] (C % 64 == 0) with
+ * weights bf16 [N][k * k * C] (k index tap * C + c, N % 128 == 0) plus bias -> f32 out
+ * [B, Ho, Wo, N], Ho = ceil(H / s); zero16 = 16 zero bytes on the device. */
+int mlg_op_conv2d_nhwc(const uint16_t* in, const uint16_t* zero16, int B, int H, int W, int C, int k, int s,
+                       const uint16_t* Wt, const float* bias, float* out, int N, void* stream);
 int mlg_op_preprocess_patches(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, int S,
                               uint16_t* patches, void* stream);
 

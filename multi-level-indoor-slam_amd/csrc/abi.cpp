@@ -458,6 +458,11 @@ int mlg_op_lg_proj(int self_block, const uint16_t* xcopy, int ldx, const uint16_
                    int Npad, void* stream) {
     return mlg_lg_proj(self_block != 0, xcopy, ldx, W, bias, ecos, esin, live, Q, K, Vt, Npad, (hipStream_t)stream);
 }
+int mlg_op_conv2d_nhwc(const uint16_t* in, const uint16_t* zero16, int B, int H, int W, int C, int k, int s,
+                       const uint16_t* Wt, const float* bias, float* out, int N, void* stream) {
+    return mlg_conv_implicit(in, zero16, B, H, W, C, k, s, Wt, bias, nullptr, 0, out, N, nullptr, 0, 0, N, N,
+                             (hipStream_t)stream);
+}
 int mlg_op_preprocess_patches(const uint8_t* frames, int B, int H, int W, int C, long frame_stride, int S,
                               uint16_t* patches, void* stream) {
     return mlg_preprocess_patches(frames, B, H, W, C, frame_stride, S, MLG_VIT_PATCH_K, 1, patches,

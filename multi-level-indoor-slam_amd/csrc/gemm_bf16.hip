@@ -687,6 +687,139 @@ __global__ __launch_bounds__(512, 2) void k_gemm256q(const bf16_t* __restrict__ 
     __builtin_amdgcn_s_waitcnt(0xF70);
 #undef Q256_DMA
 }
+// Implicit-GEMM convolution on the persistent 256 x TN x 64 tile of k_gemm256 (LoFTR's
+// ResNetFPN, loftr.hip): A[m, k] is never materialised.  Row m = output pixel (b, oy, ox)
+// of an NHWC bf16 input [B, H, W, C]; k = tap * C + c with C % 64 == 0, so a 64-wide
+// K-tile lies inside one tap (ty, tx) and its 16-B chunks are contiguous input channels
+// at pixel (oy * s - pad + ty, ox * s - pad + tx).  Each lane keeps its 4 rows' pixel
+// origin per output tile and LDS-DMAs from a per-lane 64-bit address; taps that fall in
+// the zero padding read a 16-B zero line (`zero`).  TN = 256: 8 waves 2 (M) x 4 (N) of
+// 128 x 64; TN = 128: 4 (M) x 2 (N) of 64 x 64.  Same MFMA k order as the explicit
+// im2col GEMM, so the same bits.
+struct ConvGeom {
+    const bf16_t* in; const bf16_t* zero; int H, W, C, kw, s, pad, Ho, Wo;
+};
+
+template <class Epi, int TN>
+__global__ __launch_bounds__(512, 2) void k_conv256(ConvGeom g, const bf16_t* __restrict__ W, int M, int N, int K,
+                                                    Epi epi) {
+    constexpr int BK = 64, TM = 256;
+    constexpr int WN = TN / 64, WM = 8 / WN, RM = TM / WM;  // waves along N / M, rows per wave
+    constexpr int JM = RM / 16;                             // 16-row m-tiles per wave
+    constexpr int A_BYTES = TM * BK * 2, STAGE = (TM + TN) * BK * 2;
+    constexpr int NA = 4, NB = TN / 64;  // DMAs per wave per K-tile
+    __shared__ __attribute__((aligned(16))) char st0[STAGE];
+    __shared__ __attribute__((aligned(16))) char st1[STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nN = N / TN, nM = (M + TM - 1) / TM, ntiles = nN * nM;
+    const int xcd = blockIdx.x & 7, per_xcd = gridDim.x >> 3;
+    const int tx = (ntiles + 7) >> 3;
+    const int tile_end = min((xcd + 1) * tx, ntiles);
+    int tile = xcd * tx + (blockIdx.x >> 3);
+    if (tile >= tile_end) return;
+
+    const int lr = lane >> 3, lp = lane & 7;
+    const int wm = wave % WM, wn = wave / WM;
+    const int da = NA * wave * 1024, db = A_BYTES + NB * wave * 1024;
+    const int nk = K / BK;  // even (checked by the launcher)
+
+    unsigned ob[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int row = (NB * wave + i) * 8 + lr;
+        ob[i] = (unsigned)(row * K + ((lp ^ ((row >> 1) & 7)) * 8)) * 2u;
+    }
+    // per row: (b, oy, ox) packed 10 / 11 / 11 bits (H, W <= 2048 and B <= 1024, checked
+    // by the launcher) -- one VGPR per row instead of three
+    unsigned pk[NA];
+    auto rows_of = [&](int t) {
+        const int m0 = (t / nN) * TM;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int row = (NA * wave + i) * 8 + lr;
+            const int m = min(m0 + row, M - 1);
+            const int ox = m % g.Wo, r = m / g.Wo, oy = r % g.Ho, b = r / g.Ho;
+            pk[i] = ((unsigned)b << 22) | ((unsigned)oy << 11) | (unsigned)ox;
+        }
+    };
+    auto a_src = [&](int i, int k0) -> const bf16_t* {
+        const int tap = k0 / g.C, c0 = k0 - tap * g.C;
+        const int ty = tap / g.kw, tx_ = tap - ty * g.kw;
+        const int b = (int)(pk[i] >> 22), oy = (int)((pk[i] >> 11) & 2047u), ox = (int)(pk[i] & 2047u);
+        const int iy = oy * g.s - g.pad + ty, ix = ox * g.s - g.pad + tx_;
+        const int row = (NA * wave + i) * 8 + lr;
+        const int ch = (lp ^ ((row >> 1) & 7)) * 8;
+        if ((unsigned)iy >= (unsigned)g.H || (unsigned)ix >= (unsigned)g.W) return g.zero;
+        return g.in + ((size_t)((b * g.H + iy) * g.W + ix)) * g.C + c0 + ch;
+    };
+    auto b_base = [&](int t) { return W + (size_t)((t % nN) * TN) * K; };
+    const bf16_t* sb = b_base(tile);
+    rows_of(tile);
+#define C256_DMA(ST, SB, k0)                                                                               \
+    {                                                                                                      \
+        const unsigned b_ = lds_addr(ST);                                                                  \
+        const bf16_t* sb_ = (SB) + (k0);                                                                   \
+        _Pragma("unroll") for (int i = 0; i < NA; ++i) dma16(a_src(i, k0), b_ + da + i * 1024);            \
+        _Pragma("unroll") for (int i = 0; i < NB; ++i) dma16s(ob[i], sb_, b_ + db + i * 1024);             \
+    }
+#define C256_COMPUTE(ST)                                                                                   \
+    _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                                        \
+        bf16x8 af[JM], wf[4];                                                                              \
+        const int ch = s * 4 + (lane >> 4);                                                                \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                    \
+            const int row = wn * 64 + i * 16 + (lane & 15);                                                \
+            wf[i] = *reinterpret_cast<const bf16x8*>((ST) + A_BYTES + soff<64>(row, ch));                  \
+        }                                                                                                  \
+        _Pragma("unroll") for (int j = 0; j < JM; ++j) {                                                   \
+            const int row = wm * RM + j * 16 + (lane & 15);                                                \
+            af[j] = *reinterpret_cast<const bf16x8*>((ST) + soff<64>(row, ch));                            \
+        }                                                                                                  \
+        _Pragma("unroll") for (int j = 0; j < JM; ++j) _Pragma("unroll") for (int i = 0; i < 4; ++i)       \
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], af[j], acc[i][j], 0, 0, 0);         \
+    }
+
+    C256_DMA(st0, sb, 0);
+    __builtin_amdgcn_s_waitcnt(0xF70);
+    __builtin_amdgcn_s_barrier();
+    for (; tile < tile_end; tile += per_xcd) {
+        const int next = tile + per_xcd < tile_end ? tile + per_xcd : tile;
+        const bf16_t* nsb = b_base(next);
+        const int kn = next != tile ? 0 : (nk - 1) * BK;  // no next tile: harmless re-read
+        f32x4 acc[4][JM];  // [n-tile][m-tile]
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < JM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < nk; t += 2) {
+            C256_DMA(st1, sb, (t + 1) * BK);
+            C256_COMPUTE(st0);
+            __builtin_amdgcn_s_waitcnt(0xF70);
+            __builtin_amdgcn_s_barrier();
+            if (t + 2 < nk) {
+                C256_DMA(st0, sb, (t + 2) * BK);
+            } else {
+                rows_of(next);  // this tile's A rows are no longer needed
+                C256_DMA(st0, nsb, kn);     // K-tile 0 of the next output tile
+            }
+            C256_COMPUTE(st1);
+            __builtin_amdgcn_s_waitcnt(0xF70);
+            __builtin_amdgcn_s_barrier();
+        }
+        const int mt = tile / nN, m0 = mt * TM, n0 = (tile - mt * nN) * TN;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < JM; ++j) {
+                const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4;
+                const int m = m0 + wm * RM + j * 16 + (lane & 15);
+                if (m < M) epi(m, n, acc[i][j]);
+            }
+        sb = nsb;
+    }
+    __builtin_amdgcn_s_waitcnt(0xF70);
+#undef C256_COMPUTE
+#undef C256_DMA
+}
 }  // namespace dma
 
 // 1: 128x128 register-staged; 2: 128x256 DMA BK=64 (3 stages); 3: 128x256 DMA BK=32 (2 WG/CU);
@@ -802,4 +935,30 @@ int mlg_gemm_patch(const bf16_t* A, const bf16_t* W, const float* bias, const fl
                    int Kpad, hipStream_t s) {
     if (M % P) return MLG_EINVAL;
     return launch(A, W, M, 768, Kpad, Kpad, Kpad, EpiPatch{X, bias, pos, P}, s);
+}
+int mlg_conv_implicit(const bf16_t* in, const bf16_t* zero, int B, int H, int W, int C, int k, int s,
+                      const bf16_t* Wt, const float* bias, const float* R, int ldr, float* X, int ldx, bf16_t* Cout,
+                      int ldc, int act, int act_cols, int N, hipStream_t st) {
+    if ((!X && !Cout) || act < 0 || act > 3 || !in || !zero || !Wt || B <= 0 || H <= 0 || W <= 0 || C % 64 ||
+        (k != 1 && k != 3) || s < 1 || N <= 0 || N % 128)
+        return MLG_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(zero) | reinterpret_cast<uintptr_t>(Wt)) & 15)
+        return MLG_EINVAL;
+    const int Ho = (H + s - 1) / s, Wo = (W + s - 1) / s, K = k * k * C;
+    if ((K / 64) % 2 || B > 1024 || H > 2048 || W > 2048 || (long)B * H * W >= (1L << 31)) return MLG_EINVAL;
+    const int M = B * Ho * Wo;
+    const dma::ConvGeom g{in, zero, H, W, C, k, s, k / 2, Ho, Wo};
+    const EpiConv epi{bias, R, ldr, X, ldx, Cout, ldc, act, act_cols};
+    const int cus = num_cus();
+    if (N % 256 == 0) {
+        const long ntiles = (long)(N / 256) * ((M + 255) / 256);
+        const long grid = std::min<long>(cus, (ntiles + 7) / 8 * 8);
+        hipLaunchKernelGGL((dma::k_conv256<EpiConv, 256>), dim3((unsigned)grid), dim3(512), 0, st, g, Wt, M, N, K, epi);
+    } else {
+        const long ntiles = (long)(N / 128) * ((M + 255) / 256);
+        const long grid = std::min<long>(cus, (ntiles + 7) / 8 * 8);
+        hipLaunchKernelGGL((dma::k_conv256<EpiConv, 128>), dim3((unsigned)grid), dim3(512), 0, st, g, Wt, M, N, K, epi);
+    }
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
 }

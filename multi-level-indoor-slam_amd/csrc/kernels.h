@@ -44,6 +44,11 @@ int mlg_gemm_bias_add_relu(const bf16_t* A, int lda, const bf16_t* W, const floa
 // -> f32 X and / or bf16 C (LoFTR convs on im2col rows and its transformer linears)
 int mlg_gemm_conv(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, int ldr, float* X,
                   int ldx, bf16_t* C, int ldc, int act, int act_cols, int M, int N, int K_, hipStream_t s);
+// implicit-GEMM k x k (k = 1 or 3, pad k / 2) stride-s convolution over NHWC bf16 [B, H, W, C]
+// (C % 64 == 0), weights [N][tap * C + c], EpiConv epilogue; `zero` = 16 zero bytes
+int mlg_conv_implicit(const bf16_t* in, const bf16_t* zero, int B, int H, int W, int C, int k, int s,
+                      const bf16_t* Wt, const float* bias, const float* R, int ldr, float* X, int ldx, bf16_t* Cout,
+                      int ldc, int act, int act_cols, int N, hipStream_t st);
 int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,
                          const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s);
 int mlg_gemm_bias_bf16(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K,

@@ -5,10 +5,11 @@
 // Features, once per keyframe (mlg_loftr_features), NHWC throughout:
 //   k_lf_stem     cv2 BGR2GRAY (fixed point) / 255 -> conv 7x7/2 (1 -> 128, BN folded) +
 //                 ReLU on the VALU (0.96 GFLOP per 640x480 frame); f32 + bf16 copy
-//   k_lf_im2col   3x3 / 1x1 patches (pad 1 / 0, stride 1 / 2) as bf16 GEMM rows,
-//                 k = tap * C + c
-//   mlg_gemm_conv every other conv of ResNetFPN_8_2 as a bf16 MFMA GEMM (gemm_bf16.hip,
-//                 persistent 256x256 LDS-DMA tiles), bias (folded BN) + shortcut + ReLU /
+//   convs         every other conv of ResNetFPN_8_2 as a bf16 MFMA GEMM, k = tap * C + c:
+//                 3x3 and strided 1x1 as implicit GEMMs (mlg_conv_implicit, gemm_bf16.hip:
+//                 the persistent 256 x 256 / 256 x 128 LDS-DMA tile gathering each K-tile's
+//                 16-B channel chunks straight from the NHWC input, padding taps from a zero
+//                 line), 1x1 stride 1 as plain GEMMs; bias (folded BN) + shortcut + ReLU /
 //                 LeakyReLU fused in the epilogue; 196-channel stages zero-padded to 256
 //   k_lf_up_add   FPN merge: lateral + bilinear x2 upsample (align_corners=True) -> bf16
 // Matching, per batch of pairs (mlg_loftr_match):
@@ -17,13 +18,16 @@
 //     q, k, v  one GEMM (self) or two (cross: q from x, k / v from the source side),
 //              elu + 1 fused on q, k;
 //     k_lf_kv    per (segment, head): KV = sum_s phi(k_s)^T (v_s / L), ksum = sum_s phi(k_s)
-//                (tokens staged through LDS, fixed summation order);
-//     k_lf_apply per (token, head): msg = (phi(q) KV) / (phi(q) . ksum + 1e-6) * L -> bf16;
+//                (fixed summation order; segments longer than 256 tokens as per-chunk
+//                partials k_lf_kv_part added in chunk order by k_lf_kv_combine);
+//     k_lf_apply per (token, head): msg = (phi(q) KV) / (phi(q) . ksum + 1e-6) * L -> bf16
+//                (one wave per segment tile and head: KV, ksum wave-uniform);
 //     merge GEMM -> k_lf_ln (norm1) -> bf16 into CAT's second half; MLP GEMMs
 //     (512 -> 512 ReLU, 512 -> 256); k_lf_ln_res: x += norm2(.), new bf16 copy;
 //   dual softmax: S = f0 . f1^T on the exact-f32 MFMA (knn.hip), sim = S / 256 / 0.1;
-//   k_lf_rowstats / k_lf_colstats (max, sum exp); k_lf_rowbest (row max of conf, first
-//   argmax) / k_lf_colmax (column max of conf) with conf recomputed identically in both;
+//   k_lf_rowstats / k_lf_colpart + k_lf_colfin (max, sum exp; columns in row chunks merged
+//   in chunk order); k_lf_rowbest (row max of conf, first argmax) / k_lf_colmaxpart +
+//   k_lf_colmaxfin (column max of conf) with conf recomputed identically in both;
 //   k_lf_select: conf > 0.2, 2-cell border, mutual max, compacted in row order;
 //   fine: k_lf_windows gathers the 5x5 windows (stride 4, zero padding) of the 1/2 maps
 //   as bf16, down_proj / merge_feat as GEMMs (the coarse half of merge_feat applied
@@ -146,27 +150,6 @@ __global__ void k_lf_gray_resize(const uint8_t* __restrict__ frames, long frame_
     out[e] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 
-// ---------------------------------------------------------------- im2col ----
-// out[(b, oy, ox)][tap * C + c] for a k x k (k = 1 or 3) conv with padding k / 2 and
-// stride s over bf16 NHWC [B, H, W, C]; 8 channels (16 B) per thread.
-__global__ void k_lf_im2col(const bf16_t* __restrict__ in, int B, int H, int W, int C, int k, int s,
-                            bf16_t* __restrict__ out) {
-    const int Ho = (H + s - 1) / s, Wo = (W + s - 1) / s, C8 = C / 8, taps = k * k;
-    const long total = (long)B * Ho * Wo * taps * C8;
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= total) return;
-    const int c8 = (int)(e % C8);
-    long r = e / C8;
-    const int tap = (int)(r % taps);
-    r /= taps;
-    const int ox = (int)(r % Wo), oy = (int)((r / Wo) % Ho), b = (int)(r / ((long)Wo * Ho));
-    const int pad = k / 2, iy = oy * s - pad + tap / k, ix = ox * s - pad + tap % k;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
-        v = *reinterpret_cast<const uint4*>(in + (((size_t)b * H + iy) * W + ix) * C + c8 * 8);
-    *reinterpret_cast<uint4*>(out + (size_t)r * taps * C + tap * C + c8 * 8) = v;
-}
-
 // ---------------------------------------------------------------- FPN add ---
 // out_bf16[b, y, x, c] = lat[b, y, x, c] + bilinear_x2(src)[b, y, x, c]  (align_corners:
 // source index = dst * (in - 1) / (out - 1) in f32, as torch's upsample_bilinear2d)
@@ -264,37 +247,113 @@ __global__ __launch_bounds__(256) void k_lf_kv(const float* __restrict__ k, cons
     if (tid < DH) ksum[((size_t)g * heads + h) * DH + tid] = ks;
 }
 
-// msg[row][h * DH + dv] = (sum_dk phiq[dk] KV[dk][dv]) * (1 / (phiq . ksum + 1e-6)) * L
+// Chunked form of k_lf_kv for long segments: one wave per (segment, head, chunk of
+// LF_KV_CHUNK tokens); lane (bk, bv) owns the B x B block (B = DH / 8) KV[bk B .., bv B ..]
+// and reads its k / v quads straight from the rows (the 8 lanes sharing bk read the same
+// bytes); ksum by the lanes with bv == 0.  Partial sums [seg, head, chunk][DH * DH + DH]
+// (tokens in order inside a chunk); k_lf_kv_combine adds the chunks in chunk order.
+constexpr int LF_KV_CHUNK = 256;
+template <int DH>
+__global__ __launch_bounds__(256) void k_lf_kv_part(const float* __restrict__ k, const float* __restrict__ v, int ldk,
+                                                    int ldv, int L, int heads, int nseg, int nch,
+                                                    float* __restrict__ part) {
+    constexpr int B = DH / 8;
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w >= nseg * heads * nch) return;
+    const int c = w % nch, gh = w / nch, h = gh % heads, g = gh / heads;
+    const int bk = lane >> 3, bv = lane & 7;
+    const int s0 = c * LF_KV_CHUNK, s1 = min(L, s0 + LF_KV_CHUNK);
+    float acc[B][B] = {};
+    float ks[B] = {};
+    const float fL = (float)L;
+    for (int s = s0; s < s1; ++s) {
+        const size_t row = (size_t)g * L + s;
+        const float* kr = k + row * ldk + h * DH + bk * B;
+        const float* vr = v + row * ldv + h * DH + bv * B;
+        float a[B], b[B];
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            a[i] = kr[i];
+            b[i] = vr[i] / fL;
+        }
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            ks[i] += a[i];
+#pragma unroll
+            for (int j = 0; j < B; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+        }
+    }
+    float* o = part + (size_t)w * (DH * DH + DH);
+#pragma unroll
+    for (int i = 0; i < B; ++i)
+#pragma unroll
+        for (int j = 0; j < B; ++j) o[(bk * B + i) * DH + bv * B + j] = acc[i][j];
+    if (bv == 0)
+#pragma unroll
+        for (int i = 0; i < B; ++i) o[DH * DH + bk * B + i] = ks[i];
+}
+
+template <int DH>
+__global__ __launch_bounds__(256) void k_lf_kv_combine(const float* __restrict__ part, int nsh, int nch,
+                                                       float* __restrict__ KV, float* __restrict__ ksum) {
+    constexpr int E = DH * DH + DH;
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (long)nsh * E) return;
+    const long gh = e / E;
+    const int i = (int)(e % E);
+    const float* p = part + gh * nch * E + i;
+    float s = p[0];
+    for (int c = 1; c < nch; ++c) s += p[(size_t)c * E];
+    if (i < DH * DH)
+        KV[gh * DH * DH + i] = s;
+    else
+        ksum[gh * DH + (i - DH * DH)] = s;
+}
+
+// msg[row][h * DH + dv] = (sum_dk phiq[dk] KV[dk][dv]) * (1 / (phiq . ksum + 1e-6)) * L.
+// One wave per (segment, 64-token tile, head), lane = token: the segment's KV and ksum
+// are wave-uniform (scalar loads, SGPR operands of the FMAs); sums over dk in order.
 template <int DH>
 __global__ __launch_bounds__(256) void k_lf_apply(const float* __restrict__ q, int ldq, const float* __restrict__ KV,
-                                                  const float* __restrict__ ksum, int L, int heads, long rows,
+                                                  const float* __restrict__ ksum, int L, int heads, int nseg,
                                                   bf16_t* __restrict__ msg) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (row, head)
-    if (e >= rows * heads) return;
-    const long row = e / heads;
-    const int h = (int)(e % heads);
-    const long g = row / L;
+    const int tiles = (L + 63) / 64;
+    const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (w >= nseg * tiles * heads) return;
+    const int h = w % heads, gt = w / heads, t = gt % tiles, g = gt / tiles;
+    const int s = t * 64 + (threadIdx.x & 63);
+    if (s >= L) return;
+    const size_t row = (size_t)g * L + s;
     const float* qr = q + row * ldq + h * DH;
     const float* kv = KV + ((size_t)g * heads + h) * DH * DH;
     const float* ks = ksum + ((size_t)g * heads + h) * DH;
     float qv[DH];
+#pragma unroll
+    for (int d = 0; d < DH; d += 4) {
+        const float4 x = *reinterpret_cast<const float4*>(qr + d);
+        qv[d] = x.x;
+        qv[d + 1] = x.y;
+        qv[d + 2] = x.z;
+        qv[d + 3] = x.w;
+    }
     float z = 0.f;
 #pragma unroll
-    for (int d = 0; d < DH; ++d) {
-        qv[d] = qr[d];
-        z = fmaf(qv[d], ks[d], z);
-    }
+    for (int d = 0; d < DH; ++d) z = fmaf(qv[d], ks[d], z);
     const float zi = 1.0f / (z + 1e-6f);
     bf16_t* o = msg + row * (heads * DH) + h * DH;
 #pragma unroll
-    for (int dv = 0; dv < DH; dv += 2) {
-        float a0 = 0.f, a1 = 0.f;
+    for (int dv0 = 0; dv0 < DH; dv0 += 8) {
+        float a[8] = {};
 #pragma unroll
-        for (int d = 0; d < DH; ++d) {
-            a0 = fmaf(qv[d], kv[d * DH + dv], a0);
-            a1 = fmaf(qv[d], kv[d * DH + dv + 1], a1);
-        }
-        *reinterpret_cast<uint32_t*>(o + dv) = pack_bf16x2(a0 * zi * (float)L, a1 * zi * (float)L);
+        for (int d = 0; d < DH; ++d)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] = fmaf(qv[d], kv[d * DH + dv0 + j], a[j]);
+        uint4 pk;
+        pk.x = pack_bf16x2(a[0] * zi * (float)L, a[1] * zi * (float)L);
+        pk.y = pack_bf16x2(a[2] * zi * (float)L, a[3] * zi * (float)L);
+        pk.z = pack_bf16x2(a[4] * zi * (float)L, a[5] * zi * (float)L);
+        pk.w = pack_bf16x2(a[6] * zi * (float)L, a[7] * zi * (float)L);
+        *reinterpret_cast<uint4*>(o + dv0) = pk;
     }
 }
 
@@ -359,28 +418,34 @@ __global__ __launch_bounds__(256) void k_lf_rowstats(const float* __restrict__ S
     }
 }
 
-// 64 columns per workgroup, 4 waves split the rows, partials combined through LDS
-__global__ __launch_bounds__(256) void k_lf_colstats(const float* __restrict__ S, int L, float* __restrict__ cmax,
-                                                     float* __restrict__ csum) {
-    __shared__ float red[4][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = blockIdx.x * 64 + lane;
-    const bool ok = col < L;
+// Column statistics in two steps so that the whole chip reads S: grid (column blocks of
+// 256, row chunks of LF_RCH); thread = column, coalesced 1 KiB row reads.  Chunk c's
+// (max, sum exp(x - max)) -> pm / pz [c][L]; k_lf_colfin merges the chunks in order
+// (max, then sum_c pz_c exp(pm_c - max)).
+constexpr int LF_RCH = 64;
+__global__ __launch_bounds__(256) void k_lf_colpart(const float* __restrict__ S, int L, float* __restrict__ pm,
+                                                    float* __restrict__ pz) {
+    const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
+    if (col >= L) return;
+    const int r0 = c * LF_RCH, r1 = min(L, r0 + LF_RCH);
     float m = -INFINITY;
-    if (ok)
-        for (int i = wave; i < L; i += 4) m = fmaxf(m, lf_sim(S[(size_t)i * L + col]));
-    red[wave][lane] = m;
-    __syncthreads();
-    m = fmaxf(fmaxf(red[0][lane], red[1][lane]), fmaxf(red[2][lane], red[3][lane]));
-    __syncthreads();
+    for (int i = r0; i < r1; ++i) m = fmaxf(m, lf_sim(S[(size_t)i * L + col]));
     float z = 0.f;
-    if (ok)
-        for (int i = wave; i < L; i += 4) z += expf(lf_sim(S[(size_t)i * L + col]) - m);
-    red[wave][lane] = z;
-    __syncthreads();
-    if (wave == 0 && ok) {
-        cmax[col] = m;
-        csum[col] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-    }
+    for (int i = r0; i < r1; ++i) z += expf(lf_sim(S[(size_t)i * L + col]) - m);
+    pm[(size_t)c * L + col] = m;
+    pz[(size_t)c * L + col] = z;
+}
+
+__global__ __launch_bounds__(256) void k_lf_colfin(const float* __restrict__ pm, const float* __restrict__ pz, int L,
+                                                   int nch, float* __restrict__ cmax, float* __restrict__ csum) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= L) return;
+    float m = -INFINITY;
+    for (int c = 0; c < nch; ++c) m = fmaxf(m, pm[(size_t)c * L + col]);
+    float z = 0.f;
+    for (int c = 0; c < nch; ++c) z += pz[(size_t)c * L + col] * expf(pm[(size_t)c * L + col] - m);
+    cmax[col] = m;
+    csum[col] = z;
 }
 
 // conf = softmax over dim 1 (column-wise) * softmax over dim 2 (row-wise), as torch
@@ -415,20 +480,27 @@ __global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S,
     }
 }
 
-__global__ __launch_bounds__(256) void k_lf_colmax(const float* __restrict__ S, int L, const float* __restrict__ rmax,
-                                                   const float* __restrict__ rsum, const float* __restrict__ cmax,
-                                                   const float* __restrict__ csum, float* __restrict__ cbest) {
-    __shared__ float red[4][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = blockIdx.x * 64 + lane;
-    const bool ok = col < L;
+// column max of conf, chunked like k_lf_colpart (max is exact in any order)
+__global__ __launch_bounds__(256) void k_lf_colmaxpart(const float* __restrict__ S, int L,
+                                                       const float* __restrict__ rmax, const float* __restrict__ rsum,
+                                                       const float* __restrict__ cmax, const float* __restrict__ csum,
+                                                       float* __restrict__ pb) {
+    const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
+    if (col >= L) return;
+    const int r0 = c * LF_RCH, r1 = min(L, r0 + LF_RCH);
+    const float cm = cmax[col], cz = csum[col];
     float m = -1.f;
-    if (ok) {
-        const float cm = cmax[col], cz = csum[col];
-        for (int i = wave; i < L; i += 4) m = fmaxf(m, lf_conf(S[(size_t)i * L + col], rmax[i], rsum[i], cm, cz));
-    }
-    red[wave][lane] = m;
-    __syncthreads();
-    if (wave == 0 && ok) cbest[col] = fmaxf(fmaxf(red[0][lane], red[1][lane]), fmaxf(red[2][lane], red[3][lane]));
+    for (int i = r0; i < r1; ++i) m = fmaxf(m, lf_conf(S[(size_t)i * L + col], rmax[i], rsum[i], cm, cz));
+    pb[(size_t)c * L + col] = m;
+}
+
+__global__ __launch_bounds__(256) void k_lf_colmaxfin(const float* __restrict__ pb, int L, int nch,
+                                                      float* __restrict__ cbest) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= L) return;
+    float m = -1.f;
+    for (int c = 0; c < nch; ++c) m = fmaxf(m, pb[(size_t)c * L + col]);
+    cbest[col] = m;
 }
 
 // Mutual-nearest selection with threshold and border, compacted in row order (one
@@ -585,7 +657,7 @@ constexpr ConvSpec CONVS[MLG_LOFTR_NCONV] = {
     {128, 256, 1, 1}, {256, 256, 3, 1}, {256, 128, 3, 1}};                                     // FPN 1/2
 
 struct FeatLayout {
-    size_t xf, xb, yb, rf, tf, col, c3, c2, gray, total;
+    size_t xf, xb, yb, rf, tf, zero, c3, c2, gray, total;
 };
 
 FeatLayout feat_layout(int B, int H, int W) {
@@ -602,7 +674,7 @@ FeatLayout feat_layout(int B, int H, int W) {
     L.yb = take(P2 * 256 * 2);   // block-internal bf16 activation
     L.rf = take(P2 * 256 * 4);   // shortcut / lateral f32
     L.tf = take(P2 * 256 * 4);   // FPN f32 temporaries
-    L.col = take(P2 * 9 * 256 * 2);  // im2col rows
+    L.zero = take(256);               // 16 zero bytes: the convs' padding taps
     L.c3 = take(P2 / 16 * 256 * 4 + 256);  // layer3 output f32 (1/8)
     L.c2 = take(P2 / 4 * 256 * 4 + 256);   // layer2 output f32 (1/4) kept for the FPN
     L.gray = take(P2 * 4);                  // resized gray frames (H, W not multiples of 8)
@@ -610,22 +682,15 @@ FeatLayout feat_layout(int B, int H, int W) {
     return L;
 }
 
-int conv(const mlg_loftr_weights& w, int idx, const bf16_t* in, int B, int H, int W, bf16_t* col, const float* R,
-         float* X, bf16_t* C, int act, hipStream_t s) {
+int conv(const mlg_loftr_weights& w, int idx, const bf16_t* in, int B, int H, int W, const bf16_t* zero,
+         const float* R, float* X, bf16_t* C, int act, hipStream_t s) {
     const ConvSpec sp = CONVS[idx];
-    const int Ho = (H + sp.s - 1) / sp.s, Wo = (W + sp.s - 1) / sp.s;
-    const long M = (long)B * Ho * Wo;
-    const bf16_t* A = in;
-    if (sp.k != 1 || sp.s != 1) {
-        const long items = M * sp.k * sp.k * (sp.cin / 8);
-        hipLaunchKernelGGL(k_lf_im2col, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, in, B, H, W, sp.cin,
-                           sp.k, sp.s, col);
-        MLG_LAUNCH_CHECK();
-        A = col;
-    }
-    const int K = sp.k * sp.k * sp.cin;
-    return mlg_gemm_conv(A, K, (const bf16_t*)w.conv_w[idx], w.conv_b[idx], R, sp.cout, X, sp.cout, C, sp.cout, act,
-                         sp.cout, (int)M, sp.cout, K, s);
+    if (sp.k != 1 || sp.s != 1)  // 3x3 and strided 1x1: implicit GEMM (no patch matrix)
+        return mlg_conv_implicit(in, zero, B, H, W, sp.cin, sp.k, sp.s, (const bf16_t*)w.conv_w[idx], w.conv_b[idx],
+                                 R, sp.cout, X, sp.cout, C, sp.cout, act, sp.cout, sp.cout, s);
+    const long M = (long)B * H * W;
+    return mlg_gemm_conv(in, sp.cin, (const bf16_t*)w.conv_w[idx], w.conv_b[idx], R, sp.cout, X, sp.cout, C, sp.cout,
+                         act, sp.cout, (int)M, sp.cout, sp.cin, s);
 }
 
 #define LF_TRY(x)                    \
@@ -636,16 +701,16 @@ int conv(const mlg_loftr_weights& w, int idx, const bf16_t* in, int B, int H, in
 
 // one BasicBlock: in (f32 x + bf16 xb) -> out (same buffers), stride 1 or 2
 int basic_block(const mlg_loftr_weights& w, int c1, int c2, int cds, int B, int H, int W, float* x, bf16_t* xb,
-                bf16_t* yb, float* rf, bf16_t* col, hipStream_t s) {
+                bf16_t* yb, float* rf, const bf16_t* zero, hipStream_t s) {
     const int st = CONVS[c1].s, Ho = (H + st - 1) / st, Wo = (W + st - 1) / st;
-    LF_TRY(conv(w, c1, xb, B, H, W, col, nullptr, nullptr, yb, 1, s));  // relu(bn1(conv1 x))
+    LF_TRY(conv(w, c1, xb, B, H, W, zero, nullptr, nullptr, yb, 1, s));  // relu(bn1(conv1 x))
     const float* R = x;
     if (cds >= 0) {  // bn(downsample x) -> rf
-        LF_TRY(conv(w, cds, xb, B, H, W, col, nullptr, rf, nullptr, 0, s));
+        LF_TRY(conv(w, cds, xb, B, H, W, zero, nullptr, rf, nullptr, 0, s));
         R = rf;
     }
     // relu(R + bn2(conv2 y)) -> x (f32) + xb; R may alias x (stride 1: same shape)
-    return conv(w, c2, yb, B, Ho, Wo, col, R, x, xb, 1, s);
+    return conv(w, c2, yb, B, Ho, Wo, zero, R, x, xb, 1, s);
 }
 
 }  // namespace
@@ -685,7 +750,8 @@ int mlg_loftr_features(const mlg_loftr_weights* wp, const uint8_t* frames_in, in
     bf16_t* yb = (bf16_t*)(base + L.yb);
     float* rf = (float*)(base + L.rf);
     float* tf = (float*)(base + L.tf);
-    bf16_t* col = (bf16_t*)(base + L.col);
+    const bf16_t* zero = (const bf16_t*)(base + L.zero);
+    if (hipMemsetAsync(base + L.zero, 0, 256, (hipStream_t)stream) != hipSuccess) return MLG_EHIP;
     float* c3 = (float*)(base + L.c3);
     float* c2 = (float*)(base + L.c2);
     const int H2 = H / 2, W2 = W / 2, H4 = H / 4, W4 = W / 4, H8 = H / 8, W8 = W / 8;
@@ -693,44 +759,44 @@ int mlg_loftr_features(const mlg_loftr_weights* wp, const uint8_t* frames_in, in
                        C, w.stem_w, w.stem_b, xf, xb);
     MLG_LAUNCH_CHECK();
     // layer1 (1/2, 128)
-    LF_TRY(basic_block(w, 0, 1, -1, B, H2, W2, xf, xb, yb, rf, col, s));
-    LF_TRY(basic_block(w, 2, 3, -1, B, H2, W2, xf, xb, yb, rf, col, s));
+    LF_TRY(basic_block(w, 0, 1, -1, B, H2, W2, xf, xb, yb, rf, zero, s));
+    LF_TRY(basic_block(w, 2, 3, -1, B, H2, W2, xf, xb, yb, rf, zero, s));
     // x1 (bf16) is needed by the FPN: kept in `fine` (scratch until the end: fine is
     // written last)
     bf16_t* x1b = (bf16_t*)fine;
     if (hipMemcpyAsync(x1b, xb, (size_t)B * H2 * W2 * 128 * 2, hipMemcpyDeviceToDevice, s) != hipSuccess)
         return MLG_EHIP;
     // layer2 (1/4, 256p)
-    LF_TRY(basic_block(w, 4, 5, 6, B, H2, W2, xf, xb, yb, rf, col, s));
-    LF_TRY(basic_block(w, 7, 8, -1, B, H4, W4, xf, xb, yb, rf, col, s));
+    LF_TRY(basic_block(w, 4, 5, 6, B, H2, W2, xf, xb, yb, rf, zero, s));
+    LF_TRY(basic_block(w, 7, 8, -1, B, H4, W4, xf, xb, yb, rf, zero, s));
     bf16_t* x2b = (bf16_t*)c2;  // bf16 copy of x2 (c2 is free until the FPN needs its f32 slot)
     if (hipMemcpyAsync(x2b, xb, (size_t)B * H4 * W4 * 256 * 2, hipMemcpyDeviceToDevice, s) != hipSuccess)
         return MLG_EHIP;
     // layer3 (1/8, 256)
-    LF_TRY(basic_block(w, 9, 10, 11, B, H4, W4, xf, xb, yb, rf, col, s));
-    LF_TRY(basic_block(w, 12, 13, -1, B, H8, W8, xf, xb, yb, rf, col, s));
+    LF_TRY(basic_block(w, 9, 10, 11, B, H4, W4, xf, xb, yb, rf, zero, s));
+    LF_TRY(basic_block(w, 12, 13, -1, B, H8, W8, xf, xb, yb, rf, zero, s));
     // FPN: x3_out = outconv3(x3) -> coarse output (f32)
-    LF_TRY(conv(w, 14, xb, B, H8, W8, col, nullptr, coarse, nullptr, 0, s));
+    LF_TRY(conv(w, 14, xb, B, H8, W8, zero, nullptr, coarse, nullptr, 0, s));
     // x2_out = outconv2(x2) + up(x3_out) -> bf16 -> conv + BN + leaky -> conv
-    LF_TRY(conv(w, 15, x2b, B, H4, W4, col, nullptr, tf, nullptr, 0, s));
+    LF_TRY(conv(w, 15, x2b, B, H4, W4, zero, nullptr, tf, nullptr, 0, s));
     {
         const long n = (long)B * H4 * W4 * 256;
         hipLaunchKernelGGL(k_lf_up_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tf, coarse, B, H8, W8, 256,
                            yb);
         MLG_LAUNCH_CHECK();
     }
-    LF_TRY(conv(w, 16, yb, B, H4, W4, col, nullptr, nullptr, xb, 2, s));
-    LF_TRY(conv(w, 17, xb, B, H4, W4, col, nullptr, c2, nullptr, 0, s));  // x2_out f32 (1/4, 256p)
+    LF_TRY(conv(w, 16, yb, B, H4, W4, zero, nullptr, nullptr, xb, 2, s));
+    LF_TRY(conv(w, 17, xb, B, H4, W4, zero, nullptr, c2, nullptr, 0, s));  // x2_out f32 (1/4, 256p)
     // x1_out = outconv1(x1) + up(x2_out) -> conv + BN + leaky -> conv -> fine
-    LF_TRY(conv(w, 18, x1b, B, H2, W2, col, nullptr, tf, nullptr, 0, s));
+    LF_TRY(conv(w, 18, x1b, B, H2, W2, zero, nullptr, tf, nullptr, 0, s));
     {
         const long n = (long)B * H2 * W2 * 256;
         hipLaunchKernelGGL(k_lf_up_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tf, c2, B, H4, W4, 256,
                            yb);
         MLG_LAUNCH_CHECK();
     }
-    LF_TRY(conv(w, 19, yb, B, H2, W2, col, nullptr, nullptr, xb, 2, s));
-    LF_TRY(conv(w, 20, xb, B, H2, W2, col, nullptr, fine, nullptr, 0, s));
+    LF_TRY(conv(w, 19, yb, B, H2, W2, zero, nullptr, nullptr, xb, 2, s));
+    LF_TRY(conv(w, 20, xb, B, H2, W2, zero, nullptr, fine, nullptr, 0, s));
     (void)c3;
     return MLG_OK;
 }
@@ -747,6 +813,7 @@ struct LayerBufs {
     bf16_t* h;    // [rows][2d]
     float* kv;    // [segs][8][dh][dh]
     float* ks;    // [segs][8][dh]
+    float* kvp;   // [segs][8][chunks][dh * dh + dh] partial sums (segments > LF_KV_CHUNK tokens)
 };
 
 // One LoFTREncoderLayer over `nseg` segments of L tokens (rows x0 .. of the buffers);
@@ -767,18 +834,38 @@ int encoder_layer(const mlg_loftr_layer& lw, const LayerBufs& b, int d, long x0,
     }
     float* kv = b.kv + (size_t)(x0 / L) * 8 * dh * dh;
     float* ks = b.ks + (size_t)(x0 / L) * 8 * dh;
+    const int nch = (L + LF_KV_CHUNK - 1) / LF_KV_CHUNK;
+    const unsigned apply_blocks = (unsigned)(((long)nseg * ((L + 63) / 64) * 8 + 3) / 4);
     if (d == 256) {
-        hipLaunchKernelGGL(k_lf_kv<32>, dim3(nseg * 8), dim3(256), 0, s, qkv + d, qkv + 2 * d, 3 * d, 3 * d, L, 8,
-                           (const int32_t*)nullptr, kv, ks);
+        if (nch > 1) {  // long segments: chunked partial sums, combined in chunk order
+            hipLaunchKernelGGL(k_lf_kv_part<32>, dim3((unsigned)((nseg * 8 * nch + 3) / 4)), dim3(256), 0, s, qkv + d,
+                               qkv + 2 * d, 3 * d, 3 * d, L, 8, nseg, nch, b.kvp);
+            MLG_LAUNCH_CHECK();
+            const long items = (long)nseg * 8 * (32 * 32 + 32);
+            hipLaunchKernelGGL(k_lf_kv_combine<32>, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, b.kvp,
+                               nseg * 8, nch, kv, ks);
+        } else {
+            hipLaunchKernelGGL(k_lf_kv<32>, dim3(nseg * 8), dim3(256), 0, s, qkv + d, qkv + 2 * d, 3 * d, 3 * d, L, 8,
+                               (const int32_t*)nullptr, kv, ks);
+        }
         MLG_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_lf_apply<32>, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, qkv, 3 * d, kv,
-                           ks, L, 8, rows, b.msg + x0 * d);
+        hipLaunchKernelGGL(k_lf_apply<32>, dim3(apply_blocks), dim3(256), 0, s, qkv, 3 * d, kv, ks, L, 8, nseg,
+                           b.msg + x0 * d);
     } else {
-        hipLaunchKernelGGL(k_lf_kv<16>, dim3(nseg * 8), dim3(256), 0, s, qkv + d, qkv + 2 * d, 3 * d, 3 * d, L, 8,
-                           (const int32_t*)nullptr, kv, ks);
+        if (nch > 1) {
+            hipLaunchKernelGGL(k_lf_kv_part<16>, dim3((unsigned)((nseg * 8 * nch + 3) / 4)), dim3(256), 0, s, qkv + d,
+                               qkv + 2 * d, 3 * d, 3 * d, L, 8, nseg, nch, b.kvp);
+            MLG_LAUNCH_CHECK();
+            const long items = (long)nseg * 8 * (16 * 16 + 16);
+            hipLaunchKernelGGL(k_lf_kv_combine<16>, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, b.kvp,
+                               nseg * 8, nch, kv, ks);
+        } else {
+            hipLaunchKernelGGL(k_lf_kv<16>, dim3(nseg * 8), dim3(256), 0, s, qkv + d, qkv + 2 * d, 3 * d, 3 * d, L, 8,
+                               (const int32_t*)nullptr, kv, ks);
+        }
         MLG_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_lf_apply<16>, dim3((unsigned)((rows * 8 + 255) / 256)), dim3(256), 0, s, qkv, 3 * d, kv,
-                           ks, L, 8, rows, b.msg + x0 * d);
+        hipLaunchKernelGGL(k_lf_apply<16>, dim3(apply_blocks), dim3(256), 0, s, qkv, 3 * d, kv, ks, L, 8, nseg,
+                           b.msg + x0 * d);
     }
     MLG_LAUNCH_CHECK();
     // merge -> norm1 -> bf16 into cat[:, d:]
@@ -824,9 +911,10 @@ int transformer(const mlg_loftr_layer* layers, int nl, const LayerBufs& b, int d
 }
 
 struct MatchLayout {
-    size_t cx, ccat, cqkv, cmsg, ct, ch, ckv, cks;  // coarse transformer (rows 2 P L, d 256)
+    size_t cx, ccat, cqkv, cmsg, ct, ch, ckv, cks, ckvp;  // coarse transformer (rows 2 P L, d 256)
     size_t fx, fcat, fqkv, fmsg, ft, fh, fkv, fks;  // fine transformer (rows 2 C 25, d 128)
-    size_t win, crow, cd, cm, S, rmax, rsum, cmax, csum, bval, bidx, cbest, mi, mj, mconf, cnt, frm, mp, ms, total;
+    size_t win, crow, cd, cm, S, rmax, rsum, cmax, csum, pm, pz, bval, bidx, cbest, mi, mj, mconf, cnt, frm, mp, ms,
+        total;
 };
 
 constexpr int FINE_CHUNK = 4096;  // matches per fine-stage pass
@@ -848,6 +936,7 @@ MatchLayout match_layout(int P, int L) {
     M.ch = take(rc * 512 * 2);
     M.ckv = take((size_t)2 * P * 8 * 32 * 32 * 4);
     M.cks = take((size_t)2 * P * 8 * 32 * 4);
+    M.ckvp = take((size_t)2 * P * 8 * ((L + LF_KV_CHUNK - 1) / LF_KV_CHUNK) * (32 * 32 + 32) * 4);
     M.fx = take(rf * 128 * 4);
     M.fcat = take(rf * 256 * 2);
     M.fqkv = take(rf * 384 * 4);
@@ -865,6 +954,9 @@ MatchLayout match_layout(int P, int L) {
     M.rsum = take((size_t)L * 4);
     M.cmax = take((size_t)L * 4);
     M.csum = take((size_t)L * 4);
+    const size_t nrch = (size_t)(L + LF_RCH - 1) / LF_RCH;
+    M.pm = take(nrch * L * 4);
+    M.pz = take(nrch * L * 4);
     M.bval = take((size_t)L * 4);
     M.bidx = take((size_t)L * 4);
     M.cbest = take((size_t)L * 4);
@@ -900,9 +992,9 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
     char* base = (char*)ws;
     auto at = [&](size_t off) { return (void*)(base + off); };
     const LayerBufs bc{(float*)at(ML.cx), (bf16_t*)at(ML.ccat), (float*)at(ML.cqkv), (bf16_t*)at(ML.cmsg),
-                       (float*)at(ML.ct), (bf16_t*)at(ML.ch), (float*)at(ML.ckv), (float*)at(ML.cks)};
+                       (float*)at(ML.ct), (bf16_t*)at(ML.ch), (float*)at(ML.ckv), (float*)at(ML.cks), (float*)at(ML.ckvp)};
     const LayerBufs bf{(float*)at(ML.fx), (bf16_t*)at(ML.fcat), (float*)at(ML.fqkv), (bf16_t*)at(ML.fmsg),
-                       (float*)at(ML.ft), (bf16_t*)at(ML.fh), (float*)at(ML.fkv), (float*)at(ML.fks)};
+                       (float*)at(ML.ft), (bf16_t*)at(ML.fh), (float*)at(ML.fkv), (float*)at(ML.fks), nullptr};
     bf16_t* win = (bf16_t*)at(ML.win);
     bf16_t* crow = (bf16_t*)at(ML.crow);
     bf16_t* cd = (bf16_t*)at(ML.cd);
@@ -912,6 +1004,9 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
     float* rsum = (float*)at(ML.rsum);
     float* cmax = (float*)at(ML.cmax);
     float* csum = (float*)at(ML.csum);
+    float* pm = (float*)at(ML.pm);
+    float* pz = (float*)at(ML.pz);
+    const int nrch = (L + LF_RCH - 1) / LF_RCH;
     float* bval = (float*)at(ML.bval);
     int32_t* bidx = (int32_t*)at(ML.bidx);
     float* cbest = (float*)at(ML.cbest);
@@ -942,9 +1037,12 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
         const float* f1 = bc.x + ((size_t)P + p) * L * 256;
         LF_TRY(mlg_similarity_f32(f0, L, f1, L, 256, S, L, s));
         hipLaunchKernelGGL(k_lf_rowstats, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum);
-        hipLaunchKernelGGL(k_lf_colstats, dim3((L + 63) / 64), dim3(256), 0, s, S, L, cmax, csum);
+        hipLaunchKernelGGL(k_lf_colpart, dim3((L + 255) / 256, nrch), dim3(256), 0, s, S, L, pm, pz);
+        hipLaunchKernelGGL(k_lf_colfin, dim3((L + 255) / 256), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum);
         hipLaunchKernelGGL(k_lf_rowbest, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, cmax, csum, bval, bidx);
-        hipLaunchKernelGGL(k_lf_colmax, dim3((L + 63) / 64), dim3(256), 0, s, S, L, rmax, rsum, cmax, csum, cbest);
+        hipLaunchKernelGGL(k_lf_colmaxpart, dim3((L + 255) / 256, nrch), dim3(256), 0, s, S, L, rmax, rsum, cmax, csum,
+                           pm);
+        hipLaunchKernelGGL(k_lf_colmaxfin, dim3((L + 255) / 256), dim3(256), 0, s, pm, L, nrch, cbest);
         hipLaunchKernelGGL(k_lf_select, dim3(1), dim3(1024), 0, s, bval, bidx, cbest, L, hc, wc, 0.2f, 2,
                            mi + (size_t)p * L, mj + (size_t)p * L, mconf + (size_t)p * L, cnt + p);
         MLG_LAUNCH_CHECK();

@@ -81,6 +81,7 @@ EXPORTS = {
                                         c_void_p, c_int, c_int, c_void_p]),
     "mlg_op_lg_ffn": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 8 + [c_void_p]),
     "mlg_op_lg_proj": (c_int, [c_int, c_void_p, c_int] + [c_void_p] * 8 + [c_int, c_void_p]),
+    "mlg_op_conv2d_nhwc": (c_int, [c_void_p, c_void_p] + [c_int] * 6 + [c_void_p] * 3 + [c_int, c_void_p]),
     "mlg_op_preprocess_patches": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_long, c_int, c_void_p,
                                           c_void_p]),
     "mlg_prof_enable": (c_int, [c_int]),

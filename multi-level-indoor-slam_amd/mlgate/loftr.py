@@ -115,7 +115,7 @@ def weight_list(sd, device):
 class LoFTRGPU:
     """Batched LoFTR on device-resident keyframes."""
 
-    def __init__(self, device="cuda", state_dict=None, seed=0, feature_batch=4):
+    def __init__(self, device="cuda", state_dict=None, seed=0, feature_batch=16):
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise _native.MlgateError("LoFTR runs on the HIP device only (no CPU path)")

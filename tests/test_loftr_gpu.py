@@ -149,3 +149,33 @@ def test_default_is_the_reference_lightglue_fallback(dev, monkeypatch):
     with pytest.warns(UserWarning, match="outdoor"):
         o._load_model()
     assert not o._is_native
+
+
+@pytest.mark.parametrize("B,H,W,C,k,s,N", [(2, 60, 80, 128, 3, 1, 128), (2, 61, 79, 128, 3, 2, 256),
+                                           (1, 37, 53, 256, 1, 2, 256), (3, 30, 40, 256, 3, 1, 256),
+                                           (1, 9, 7, 256, 3, 1, 128)])
+def test_implicit_conv_matches_float64_conv(dev, B, H, W, C, k, s, N):
+    """mlg_op_conv2d_nhwc (the backbone's implicit-GEMM conv, gemm_bf16.hip k_conv256) on
+    bf16 inputs / weights against torch's float64 conv2d of the same bf16 values: ragged
+    M (tiles of 256 output pixels), stride 2 (1x1 and 3x3), 256- and 128-wide N tiles,
+    zero-padding taps on every border.  Bar: f32 accumulation, |err| <= 1e-5 of the
+    output scale."""
+    from mlgate import _native
+    g = torch.Generator().manual_seed(B * 1000 + H + k + s)
+    x = torch.randn(B, H, W, C, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, k, k, C, generator=g) / (k * (C ** 0.5))).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g) * 0.1
+    Ho, Wo = (H + s - 1) // s, (W + s - 1) // s
+    xd, wd, bd = x.to(dev), w.reshape(N, -1).contiguous().to(dev), bias.to(dev)
+    zero = torch.zeros(8, dtype=torch.bfloat16, device=dev)
+    out = torch.full((B, Ho, Wo, N), float("nan"), device=dev)
+    P = _native.ptr
+    rc = _native.lib().mlg_op_conv2d_nhwc(P(xd), P(zero), B, H, W, C, k, s, P(wd), P(bd), P(out), N,
+                                          torch.cuda.current_stream(dev).cuda_stream)
+    assert rc == 0
+    ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2),
+                                     bias.double(), stride=s, padding=k // 2).permute(0, 2, 3, 1)
+    got = out.cpu().double()
+    assert got.shape == ref.shape and torch.isfinite(got).all()
+    err = float((got - ref).abs().max())
+    assert err <= 1e-5 * float(ref.abs().max()), err
