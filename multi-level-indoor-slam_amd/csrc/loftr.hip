@@ -155,12 +155,12 @@ __global__ void k_lf_gray_resize(const uint8_t* __restrict__ frames, long frame_
 // source index = dst * (in - 1) / (out - 1) in f32, as torch's upsample_bilinear2d)
 __global__ void k_lf_up_add(const float* __restrict__ lat, const float* __restrict__ src, int B, int h, int w, int C,
                             bf16_t* __restrict__ out) {
-    const int Ho = 2 * h, Wo = 2 * w;
-    const long total = (long)B * Ho * Wo * C;
+    const int Ho = 2 * h, Wo = 2 * w, C4 = C / 4;  // 4 channels (16 B of f32) per thread
+    const long total = (long)B * Ho * Wo * C4;
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= total) return;
-    const int c = (int)(e % C);
-    long r = e / C;
+    const int c = (int)(e % C4) * 4;
+    long r = e / C4;
     const int x = (int)(r % Wo), y = (int)((r / Wo) % Ho), b = (int)(r / ((long)Wo * Ho));
     const float sh = Ho > 1 ? (float)(h - 1) / (float)(Ho - 1) : 0.f;
     const float sw = Wo > 1 ? (float)(w - 1) / (float)(Wo - 1) : 0.f;
@@ -169,10 +169,15 @@ __global__ void k_lf_up_add(const float* __restrict__ lat, const float* __restri
     const int y1 = y0 < h - 1 ? y0 + 1 : y0, x1 = x0 < w - 1 ? x0 + 1 : x0;
     const float ly1 = fy - (float)y0, lx1 = fx - (float)x0, ly0 = 1.f - ly1, lx0 = 1.f - lx1;
     const float* s0 = src + ((size_t)b * h * w) * C + c;
-    const float v00 = s0[((size_t)y0 * w + x0) * C], v01 = s0[((size_t)y0 * w + x1) * C];
-    const float v10 = s0[((size_t)y1 * w + x0) * C], v11 = s0[((size_t)y1 * w + x1) * C];
-    const float up = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
-    out[e] = f32_to_bf16(lat[e] + up);
+    const float4 v00 = *reinterpret_cast<const float4*>(s0 + ((size_t)y0 * w + x0) * C);
+    const float4 v01 = *reinterpret_cast<const float4*>(s0 + ((size_t)y0 * w + x1) * C);
+    const float4 v10 = *reinterpret_cast<const float4*>(s0 + ((size_t)y1 * w + x0) * C);
+    const float4 v11 = *reinterpret_cast<const float4*>(s0 + ((size_t)y1 * w + x1) * C);
+    const float4 l = *reinterpret_cast<const float4*>(lat + r * C + c);
+    auto up = [&](float a, float b_, float c_, float d) { return ly0 * (lx0 * a + lx1 * b_) + ly1 * (lx0 * c_ + lx1 * d); };
+    const float o0 = l.x + up(v00.x, v01.x, v10.x, v11.x), o1 = l.y + up(v00.y, v01.y, v10.y, v11.y);
+    const float o2 = l.z + up(v00.z, v01.z, v10.z, v11.z), o3 = l.w + up(v00.w, v01.w, v10.w, v11.w);
+    *reinterpret_cast<uint2*>(out + r * C + c) = make_uint2(pack_bf16x2(o0, o1), pack_bf16x2(o2, o3));
 }
 
 // ------------------------------------------------------- tokens + PE --------
@@ -266,7 +271,31 @@ __global__ __launch_bounds__(256) void k_lf_kv_part(const float* __restrict__ k,
     float acc[B][B] = {};
     float ks[B] = {};
     const float fL = (float)L;
-    for (int s = s0; s < s1; ++s) {
+    // 8 tokens' k / v loads in flight before their FMAs (tokens still summed in order)
+    int s = s0;
+    for (; s + 8 <= s1; s += 8) {
+        float a[8][B], b[8][B];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const size_t row = (size_t)g * L + s + u;
+            const float* kr = k + row * ldk + h * DH + bk * B;
+            const float* vr = v + row * ldv + h * DH + bv * B;
+#pragma unroll
+            for (int i = 0; i < B; ++i) {
+                a[u][i] = kr[i];
+                b[u][i] = vr[i] / fL;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+            for (int i = 0; i < B; ++i) {
+                ks[i] += a[u][i];
+#pragma unroll
+                for (int j = 0; j < B; ++j) acc[i][j] = fmaf(a[u][i], b[u][j], acc[i][j]);
+            }
+    }
+    for (; s < s1; ++s) {
         const size_t row = (size_t)g * L + s;
         const float* kr = k + row * ldk + h * DH + bk * B;
         const float* vr = v + row * ldv + h * DH + bv * B;
@@ -406,12 +435,27 @@ __global__ __launch_bounds__(256) void k_lf_rowstats(const float* __restrict__ S
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= L) return;
     const float* s = S + (size_t)row * L;
-    float m = -INFINITY;
-    for (int j = lane; j < L; j += 64) m = fmaxf(m, lf_sim(s[j]));
-    m = wave_max(m);
-    float z = 0.f;
-    for (int j = lane; j < L; j += 64) z += expf(lf_sim(s[j]) - m);
-    z = wave_sum(z);
+    float m = -INFINITY, z = 0.f;  // online per lane, merged across the wave
+    auto add = [&](float v) {
+        const float x = lf_sim(v), mn = fmaxf(m, x);
+        z = z * expf(m - mn) + expf(x - mn);
+        m = mn;
+    };
+    if ((L & 3) == 0) {
+        const float4* s4 = reinterpret_cast<const float4*>(s);
+        for (int j = lane; j < L / 4; j += 64) {
+            const float4 v = s4[j];
+            add(v.x);
+            add(v.y);
+            add(v.z);
+            add(v.w);
+        }
+    } else {
+        for (int j = lane; j < L; j += 64) add(s[j]);
+    }
+    const float mw = wave_max(m);
+    z = wave_sum(m == -INFINITY ? 0.f : z * expf(m - mw));
+    m = mw;
     if (lane == 0) {
         rmax[row] = m;
         rsum[row] = z;
@@ -428,10 +472,13 @@ __global__ __launch_bounds__(256) void k_lf_colpart(const float* __restrict__ S,
     const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
     if (col >= L) return;
     const int r0 = c * LF_RCH, r1 = min(L, r0 + LF_RCH);
-    float m = -INFINITY;
-    for (int i = r0; i < r1; ++i) m = fmaxf(m, lf_sim(S[(size_t)i * L + col]));
-    float z = 0.f;
-    for (int i = r0; i < r1; ++i) z += expf(lf_sim(S[(size_t)i * L + col]) - m);
+    float m = -INFINITY, z = 0.f;  // online: one read of S
+#pragma unroll 8
+    for (int i = r0; i < r1; ++i) {
+        const float x = lf_sim(S[(size_t)i * L + col]), mn = fmaxf(m, x);
+        z = z * expf(m - mn) + expf(x - mn);
+        m = mn;
+    }
     pm[(size_t)c * L + col] = m;
     pz[(size_t)c * L + col] = z;
 }
@@ -440,10 +487,13 @@ __global__ __launch_bounds__(256) void k_lf_colfin(const float* __restrict__ pm,
                                                    int nch, float* __restrict__ cmax, float* __restrict__ csum) {
     const int col = blockIdx.x * 256 + threadIdx.x;
     if (col >= L) return;
-    float m = -INFINITY;
-    for (int c = 0; c < nch; ++c) m = fmaxf(m, pm[(size_t)c * L + col]);
-    float z = 0.f;
-    for (int c = 0; c < nch; ++c) z += pz[(size_t)c * L + col] * expf(pm[(size_t)c * L + col] - m);
+    float m = -INFINITY, z = 0.f;  // chunks merged in order
+#pragma unroll 8
+    for (int c = 0; c < nch; ++c) {
+        const float pmc = pm[(size_t)c * L + col], mn = fmaxf(m, pmc);
+        z = z * expf(m - mn) + pz[(size_t)c * L + col] * expf(pmc - mn);
+        m = mn;
+    }
     cmax[col] = m;
     csum[col] = z;
 }
@@ -499,6 +549,7 @@ __global__ __launch_bounds__(256) void k_lf_colmaxfin(const float* __restrict__ 
     const int col = blockIdx.x * 256 + threadIdx.x;
     if (col >= L) return;
     float m = -1.f;
+#pragma unroll 8
     for (int c = 0; c < nch; ++c) m = fmaxf(m, pb[(size_t)c * L + col]);
     cbest[col] = m;
 }
@@ -780,7 +831,7 @@ int mlg_loftr_features(const mlg_loftr_weights* wp, const uint8_t* frames_in, in
     // x2_out = outconv2(x2) + up(x3_out) -> bf16 -> conv + BN + leaky -> conv
     LF_TRY(conv(w, 15, x2b, B, H4, W4, zero, nullptr, tf, nullptr, 0, s));
     {
-        const long n = (long)B * H4 * W4 * 256;
+        const long n = (long)B * H4 * W4 * 64;
         hipLaunchKernelGGL(k_lf_up_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tf, coarse, B, H8, W8, 256,
                            yb);
         MLG_LAUNCH_CHECK();
@@ -790,7 +841,7 @@ int mlg_loftr_features(const mlg_loftr_weights* wp, const uint8_t* frames_in, in
     // x1_out = outconv1(x1) + up(x2_out) -> conv + BN + leaky -> conv -> fine
     LF_TRY(conv(w, 18, x1b, B, H2, W2, zero, nullptr, tf, nullptr, 0, s));
     {
-        const long n = (long)B * H2 * W2 * 256;
+        const long n = (long)B * H2 * W2 * 64;
         hipLaunchKernelGGL(k_lf_up_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tf, c2, B, H4, W4, 256,
                            yb);
         MLG_LAUNCH_CHECK();

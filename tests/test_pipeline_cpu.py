@@ -120,3 +120,19 @@ def test_large_k_has_no_limit_and_k0_needs_no_device():
     assert spr.find_loop_closures(k=0) == []
     with pytest.raises(MlgateError):
         spr.find_loop_closures(k=5000)
+
+
+def test_decision_fixture_one_pair_fp32(golden_dir):
+    """tests/golden/decision_sample.npz (tools/decision_sample.py on the GPU +
+    tools/decision_check_cpu.py here): its fp32 columns are the oracle chain's -- one
+    valid sampled pair recomputed from pixels -- and the GPU decisions flip none of them."""
+    import bench
+    from mlgate.weights import lightglue_state_dict, superpoint_state_dict
+    d = np.load(f"{golden_dir}/decision_sample.npz")
+    assert len(d["a"]) == 600 and int(np.sum(d["is_valid"] != d["fp32_is_valid"])) == 0
+    i = int(np.flatnonzero(d["fp32_is_valid"])[0])
+    seq, _ = bench.sequence(int(d["keyframes"]), int(d["places"]))
+    fr = synthetic.frames_host(seq, [int(d["a"][i]), int(d["b"][i])])
+    r = opipe.verify_pair(fr[0], fr[1], superpoint_state_dict(0), opipe.make_matcher(lightglue_state_dict(0)),
+                          ogeo.ISEC_K)
+    assert r["is_valid"] and r["num_matches"] == d["fp32_matches"][i] and r["num_inliers"] == d["fp32_inliers"][i]
