@@ -239,6 +239,39 @@ __device__ __forceinline__ float swap_sum(float v) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// max of the 16 scores of each query tile, both chains interleaved in ONE asm statement:
+// hipcc pads every inline-asm statement with an s_nop (it cannot see inside), so eight
+// separate v_max3 statements per tile cost eight nops; v_max3_f32 directly (no
+// NaN-canonicalising v_max_f32 on the MFMA results: scores are finite or -inf).
+__device__ __forceinline__ void block_max2(const f32x16 (&v)[2], float (&m)[2]) {
+    float a, b;
+    asm("v_max3_f32 %0, %2, %3, %4\n\t"
+        "v_max3_f32 %1, %18, %19, %20\n\t"
+        "v_max3_f32 %0, %0, %5, %6\n\t"
+        "v_max3_f32 %1, %1, %21, %22\n\t"
+        "v_max3_f32 %0, %0, %7, %8\n\t"
+        "v_max3_f32 %1, %1, %23, %24\n\t"
+        "v_max3_f32 %0, %0, %9, %10\n\t"
+        "v_max3_f32 %1, %1, %25, %26\n\t"
+        "v_max3_f32 %0, %0, %11, %12\n\t"
+        "v_max3_f32 %1, %1, %27, %28\n\t"
+        "v_max3_f32 %0, %0, %13, %14\n\t"
+        "v_max3_f32 %1, %1, %29, %30\n\t"
+        "v_max3_f32 %0, %0, %15, %16\n\t"
+        "v_max3_f32 %1, %1, %31, %32\n\t"
+        "v_max3_f32 %0, %0, %17, %17\n\t"
+        "v_max3_f32 %1, %1, %33, %33"
+        : "=&v"(a), "=&v"(b)
+        : "v"(v[0][0]), "v"(v[0][1]), "v"(v[0][2]), "v"(v[0][3]), "v"(v[0][4]), "v"(v[0][5]), "v"(v[0][6]),
+          "v"(v[0][7]), "v"(v[0][8]), "v"(v[0][9]), "v"(v[0][10]), "v"(v[0][11]), "v"(v[0][12]), "v"(v[0][13]),
+          "v"(v[0][14]), "v"(v[0][15]),
+          "v"(v[1][0]), "v"(v[1][1]), "v"(v[1][2]), "v"(v[1][3]), "v"(v[1][4]), "v"(v[1][5]), "v"(v[1][6]),
+          "v"(v[1][7]), "v"(v[1][8]), "v"(v[1][9]), "v"(v[1][10]), "v"(v[1][11]), "v"(v[1][12]), "v"(v[1][13]),
+          "v"(v[1][14]), "v"(v[1][15]));
+    m[0] = a;
+    m[1] = b;
+}
+
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 
@@ -267,10 +300,15 @@ __device__ __forceinline__ void qk_half(const char* kb, const PipeCtx& c, const 
 
 // half-step H of stage j: consume `cur` (keys 64 j + 32 H ..), produce `nxt`.  kcur /
 // knext: K ring slots of stages j / j + 1; kw: slot for K_{j+2}.
-template <int H, bool LASTSTAGE>
+template <int H, bool LASTSTAGE, int R>
 __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)[2], const PipeCtx& c,
                                           const bf16x8 (&qf)[2][4], f32x16 (&o)[2][2], float (&mrun)[2],
-                                          float (&lsum)[2][2], int kcur, int knext, int kw, uint4 (&stage)[4]) {
+                                          float (&lsum)[2][2], uint4 (&stage)[4], int rr = 0) {
+    // ring slots are compile-time constants (stage j uses K slot j % 3 = R, V slot R), so
+    // every LDS fragment address is a lane offset plus an immediate; R < 0: slot rr at run
+    // time (the last stage only)
+    const int rs = R >= 0 ? R : rr;
+    const int kcur = rs * KTILE_BYTES, knext = ((rs + 1) % 3) * KTILE_BYTES, kw = ((rs + 2) % 3) * KTILE_BYTES;
     constexpr float C = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
     const int hh = (threadIdx.x & 63) >> 5;
     if (!LASTSTAGE && H == 0) {  // K_{j+2} (clamped), V_{j+1} -> registers, into LDS at the stage end
@@ -291,13 +329,11 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
     }
     float mnew[2];
     bool grow = false;
+    float bm[2];
+    block_max2(cur, bm);
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-        float bm = max3_raw(cur[qt][0], cur[qt][1], cur[qt][2]);
-#pragma unroll
-        for (int r = 3; r < 15; r += 2) bm = max3_raw(bm, cur[qt][r], cur[qt][r + 1]);
-        bm = fmaxf(bm, cur[qt][15]);
-        mnew[qt] = fmaxf(mrun[qt], swap_max(bm));
+        mnew[qt] = fmaxf(mrun[qt], swap_max(bm[qt]));
         grow |= (mnew[qt] - mrun[qt]) * C > 8.0f;
     }
     if (__any(grow)) {
@@ -316,7 +352,7 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
     const char* kring = c.smem;
     if (!(LASTSTAGE && H == 1)) qk_half(kring + (H == 0 ? kcur : knext), c, qf, H ^ 1, nxt);
     // P of this half-block [st][qt]: keys 16 st + 8 hh .. + 7, then O^T += V^T . P^T
-    const char* vb = c.smem + 3 * KTILE_BYTES + (j & 1) * VTILE_BYTES;
+    const char* vb = c.smem + 3 * KTILE_BYTES + rs * VTILE_BYTES;
     bf16x8 pf[2][2];
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
@@ -345,7 +381,7 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
     }
     if (!LASTSTAGE && H == 1) {
         char* kwp = c.smem + kw;
-        char* vw = c.smem + 3 * KTILE_BYTES + ((j + 1) & 1) * VTILE_BYTES;
+        char* vw = c.smem + 3 * KTILE_BYTES + ((rs + 1) % 3) * VTILE_BYTES;
         *reinterpret_cast<uint4*>(kwp + c.sk0) = stage[0];
         *reinterpret_cast<uint4*>(kwp + c.sk1) = stage[1];
         *reinterpret_cast<uint2*>(vw + c.sv0a) = make_uint2(stage[2].x, stage[2].y);
@@ -423,17 +459,29 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
     float mrun[2] = {-INFINITY, -INFINITY};
     float lsum[2][2] = {{0.f, 0.f}, {0.f, 0.f}};  // per lane half, two partial sums each
     uint4 stage[4];
-    int k0 = 0, k1 = KTILE_BYTES, k2 = 2 * KTILE_BYTES;  // ring slots of K_j, K_{j+1}, K_{j+2}
-    for (int j = 0; j + 1 < c.nkb; ++j) {
-        pipe_half<0, false>(j, sA, sB, c, qf, o, mrun, lsum, k0, k1, k2, stage);
-        pipe_half<1, false>(j, sB, sA, c, qf, o, mrun, lsum, k0, k1, k2, stage);
-        const int t = k0;
-        k0 = k1;
-        k1 = k2;
-        k2 = t;
+    // stages unrolled by 3 (K and V ring slot of stage j = j % 3, compile-time)
+#define PIPE_STAGE(J, R, LAST)                                                      \
+    {                                                                               \
+        pipe_half<0, LAST, R>(J, sA, sB, c, qf, o, mrun, lsum, stage, (J) % 3);     \
+        pipe_half<1, LAST, R>(J, sB, sA, c, qf, o, mrun, lsum, stage, (J) % 3);     \
     }
-    pipe_half<0, true>(c.nkb - 1, sA, sB, c, qf, o, mrun, lsum, k0, k1, k2, stage);
-    pipe_half<1, true>(c.nkb - 1, sB, sA, c, qf, o, mrun, lsum, k0, k1, k2, stage);
+    const int last = c.nkb - 1;
+    int j = 0;
+    for (; j + 3 <= last; j += 3) {
+        PIPE_STAGE(j, 0, false)
+        PIPE_STAGE(j + 1, 1, false)
+        PIPE_STAGE(j + 2, 2, false)
+    }
+    if (j < last) {  // j % 3 == 0 here
+        PIPE_STAGE(j, 0, false)
+        ++j;
+        if (j < last) {
+            PIPE_STAGE(j, 1, false)
+            ++j;
+        }
+    }
+    PIPE_STAGE(last, -1, true)  // slot last % 3 at run time
+#undef PIPE_STAGE
 
     // O staged through LDS (the K / V rings are dead once every wave is past its last
     // stage) as this wave's [64 queries][64 d] bf16, 16-B chunk c of row r at c ^ (r & 7),
@@ -481,7 +529,7 @@ __global__ __launch_bounds__(256, 1) void k_attention_varlen(const bf16_t* __res
                                                              int ldo, int Npad, const int4* __restrict__ tasks,
                                                              const int* __restrict__ out_off, int nqb, int heads,
                                                              int total) {
-    __shared__ __attribute__((aligned(16))) char smem[3 * KTILE_BYTES + 2 * VTILE_BYTES];
+    __shared__ __attribute__((aligned(16))) char smem[3 * KTILE_BYTES + 3 * VTILE_BYTES];
     const int per_xcd = (int)gridDim.x >> 3;
     const int logical = ((int)blockIdx.x & 7) * per_xcd + ((int)blockIdx.x >> 3);
     if (logical >= total) return;
