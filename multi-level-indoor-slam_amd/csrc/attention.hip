@@ -203,14 +203,6 @@ __global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__
                    blockIdx.x, O + (size_t)b * T * 768 + h * 64, 768);
 }
 
-// v_max3_f32 without the NaN-canonicalising v_max_f32 hipcc puts in front of every
-// MFMA-produced operand of fmaxf (scores are finite or -inf here).
-__device__ __forceinline__ float max3_raw(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-
 // Software-pipelined wide tile for the ragged (LightGlue) path: one workgroup = 4 waves
 // = 256 query rows of one (task, head), one wave per SIMD, each wave 64 queries as two
 // 32-column MFMA tiles.  The softmax runs over 32-key half-blocks: while the VALU
@@ -228,27 +220,24 @@ __device__ __forceinline__ float max3_raw(float a, float b, float c) {
 // precede its exponentials, and all earlier P V MFMAs have been
 // issued by then.
 // LDS, per 64-key stage: K ring of 3 (the current stage's K is still read for its second
-// half while K_{j+1} is read and K_{j+2} lands), V ring of 2; global loads issued at the
+// half while K_{j+1} is read and K_{j+2} lands), V ring of 3 (slot j % 3 like K: the stage
+// loop is unrolled by 3 so every ring address is a constant); global loads issued at the
 // top of a stage land in LDS at its end, one barrier per stage.
-__device__ __forceinline__ float swap_max(float v) {  // max(v, v of lane ^ 32)
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
 __device__ __forceinline__ float swap_sum(float v) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// max of the 16 scores of each query tile, both chains interleaved in ONE asm statement:
-// hipcc pads every inline-asm statement with an s_nop (it cannot see inside), so eight
-// separate v_max3 statements per tile cost eight nops; v_max3_f32 directly (no
-// NaN-canonicalising v_max_f32 on the MFMA results: scores are finite or -inf).
+// Row max of each query tile's 16 scores, merged with the other lane half (permlane32
+// swap) -- ONE asm statement: hipcc pads every inline-asm statement with an s_nop (it
+// cannot see inside) and puts a NaN-canonicalising v_max_f32 in front of every fmaxf
+// operand it did not produce, so per-instruction statements or fmaxf on the swap results
+// cost as much again as the maxima.  The two chains interleave; `s_nop 1`: the VALU-write
+// -> permlane32_swap-read wait states.  Scores are finite or -inf.
 __device__ __forceinline__ void block_max2(const f32x16 (&v)[2], float (&m)[2]) {
-    float a, b;
-    asm("v_max3_f32 %0, %2, %3, %4\n\t"
-        "v_max3_f32 %1, %18, %19, %20\n\t"
-        "v_max3_f32 %0, %0, %5, %6\n\t"
-        "v_max3_f32 %1, %1, %21, %22\n\t"
+    float a, b, t0, t1;
+    asm("v_max3_f32 %0, %4, %5, %6\n\t"
+        "v_max3_f32 %1, %20, %21, %22\n\t"
         "v_max3_f32 %0, %0, %7, %8\n\t"
         "v_max3_f32 %1, %1, %23, %24\n\t"
         "v_max3_f32 %0, %0, %9, %10\n\t"
@@ -259,9 +248,18 @@ __device__ __forceinline__ void block_max2(const f32x16 (&v)[2], float (&m)[2]) 
         "v_max3_f32 %1, %1, %29, %30\n\t"
         "v_max3_f32 %0, %0, %15, %16\n\t"
         "v_max3_f32 %1, %1, %31, %32\n\t"
-        "v_max3_f32 %0, %0, %17, %17\n\t"
-        "v_max3_f32 %1, %1, %33, %33"
-        : "=&v"(a), "=&v"(b)
+        "v_max3_f32 %0, %0, %17, %18\n\t"
+        "v_max3_f32 %1, %1, %33, %34\n\t"
+        "v_max3_f32 %0, %0, %19, %19\n\t"
+        "v_max3_f32 %1, %1, %35, %35\n\t"
+        "v_mov_b32 %2, %0\n\t"
+        "v_mov_b32 %3, %1\n\t"
+        "s_nop 1\n\t"
+        "v_permlane32_swap_b32 %0, %2\n\t"
+        "v_permlane32_swap_b32 %1, %3\n\t"
+        "v_max_f32 %0, %0, %2\n\t"
+        "v_max_f32 %1, %1, %3"
+        : "=&v"(a), "=&v"(b), "=&v"(t0), "=&v"(t1)
         : "v"(v[0][0]), "v"(v[0][1]), "v"(v[0][2]), "v"(v[0][3]), "v"(v[0][4]), "v"(v[0][5]), "v"(v[0][6]),
           "v"(v[0][7]), "v"(v[0][8]), "v"(v[0][9]), "v"(v[0][10]), "v"(v[0][11]), "v"(v[0][12]), "v"(v[0][13]),
           "v"(v[0][14]), "v"(v[0][15]),
@@ -330,10 +328,10 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
     float mnew[2];
     bool grow = false;
     float bm[2];
-    block_max2(cur, bm);
+    block_max2(cur, bm);  // both lane halves
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-        mnew[qt] = fmaxf(mrun[qt], swap_max(bm[qt]));
+        mnew[qt] = fmaxf(mrun[qt], bm[qt]);
         grow |= (mnew[qt] - mrun[qt]) * C > 8.0f;
     }
     if (__any(grow)) {

@@ -12,8 +12,11 @@ The fixture holds 0 decision flips in 600 (214 valid both ways).
 
 GPU test: the sampled pairs re-verified through the drop-in GeometricVerifier
 (verify_frames_batch: SuperPoint per keyframe, one ragged LightGlue call, batched RANSAC)
-give the fixture's GPU (matches, inliers, decision) exactly -- a pair's result does not
-depend on the batch it runs in -- and so the fp32 chain's decision on every pair."""
+give the fp32 chain's decision on every pair, and match / inlier counts within the bf16
+chain's spread of the fixture (median relative match-count difference <= 2 %, 99th
+percentile <= 15 %, inliers of valid pairs within 10 %).  The fixture's own GPU columns
+(the kernels of its generation) are kept for reference; a kernel change that moves
+rounding is expected to move counts slightly, never the decisions."""
 import numpy as np
 import pytest
 import torch
@@ -40,5 +43,9 @@ def test_sampled_bench_pairs_reproduce_and_match_fp32_decisions(dev, golden_dir)
     got_i = np.array([r.num_inliers for r in res])
     got_v = np.array([r.is_valid for r in res])
     assert np.array_equal(got_v, d["fp32_is_valid"]), np.flatnonzero(got_v != d["fp32_is_valid"])[:10]
-    assert np.array_equal(got_m, d["matches"]), np.flatnonzero(got_m != d["matches"])[:10]
-    assert np.array_equal(got_i, d["inliers"]), np.flatnonzero(got_i != d["inliers"])[:10]
+    fm, fi = d["fp32_matches"].astype(np.float64), d["fp32_inliers"].astype(np.float64)
+    rel_m = np.abs(got_m - fm) / np.maximum(fm, 1.0)
+    assert np.median(rel_m) <= 0.02 and np.quantile(rel_m, 0.99) <= 0.15, (np.median(rel_m), np.quantile(rel_m, 0.99))
+    v = d["fp32_is_valid"]
+    rel_i = np.abs(got_i[v] - fi[v]) / np.maximum(fi[v], 1.0)
+    assert rel_i.max() <= 0.10, rel_i.max()
