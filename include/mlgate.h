@@ -88,6 +88,41 @@ int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, 
                     long frame_stride, int image_size, int flags, void* workspace, size_t workspace_bytes,
                     float* desc_out, float* local_out, void* stream);
 
+/* ------------------------------------------------------------------- SALAD --
+ * SALAD's native branch (place_recognition.py:357-368, 380-391): serizba/salad's
+ * aggregator over the same DINOv2 ViT-B/14 (all final-LayerNorm tokens).  Weights in
+ * kernel layout (mlgate/vpr.py SaladGPU._pack):
+ *   w1 bf16 [1024, 768]  rows 0..511 cluster_features.0, 512..1023 score.0 (1x1 convs)
+ *   w2 bf16 [256, 1024]  rows 0..127 [cluster_features.3 | 0], 128..191 [0 | score.3],
+ *                        192..255 zero; b1 [1024], b2 [256] float32
+ *   wt1 [512, 768], wt2 [256, 512] float32 token_features.0 / .2 (+ biases)
+ *   dust_bin             the learned dust-bin score
+ */
+typedef struct mlg_salad_weights {
+    const uint16_t* w1;
+    const float* b1;
+    const uint16_t* w2;
+    const float* b2;
+    const float *wt1, *bt1, *wt2, *bt2;
+    float dust_bin;
+} mlg_salad_weights;
+
+#define MLG_SALAD_DIM 8448 /* 256 token + 64 clusters x 128 */
+
+size_t mlg_salad_workspace_bytes(int batch, int image_size);
+
+/*
+ * SALAD descriptors for a batch of frames at image_size 322 (SALAD's evaluation size;
+ * the hub PatchEmbed rejects the reference's 480 x 640 resize): preprocessing without a
+ * channel swap, the ViT forward, the final LayerNorm over every token, then per frame
+ * the token MLP, 3 log-domain Sinkhorn iterations over the [64 + dust-bin, 529] score
+ * matrix, the cluster aggregation and the L2 normalisations.  desc_out float32
+ * [batch, MLG_SALAD_DIM].
+ */
+int mlg_salad_forward(const mlg_vit_weights* w, const mlg_salad_weights* sw, const uint8_t* frames, int batch,
+                      int H, int W, int C, long frame_stride, int image_size, void* workspace,
+                      size_t workspace_bytes, float* desc_out, void* stream);
+
 /* --------------------------------------------------------------- retrieval --
  * SemanticPlaceRecognition.find_loop_closures (place_recognition.py:851-911) for
  * query rows [q0, q0 + Q) against all N descriptors:
@@ -476,10 +511,9 @@ int mlg_prof_read_work(int slot, double* flops);
 typedef struct mlg_orb_params {
     int level_w[MLG_ORB_LEVELS], level_h[MLG_ORB_LEVELS];
     int level_features[MLG_ORB_LEVELS]; /* nfeaturesPerLevel */
-    int level_vec_end[MLG_ORB_LEVELS];  /* cv2.resize SIMD/scalar split of each level row */
     float level_scale[MLG_ORB_LEVELS];
     int umax[16];
-    int gauss[7]; /* 7-tap Gaussian, 8 fractional bits, sum 256 */
+    float gauss[7]; /* getGaussianKernel(7, 2, CV_32F) of the per-level GaussianBlur */
     int fast_threshold, edge_threshold;
 } mlg_orb_params;
 size_t mlg_orb_workspace_bytes(const mlg_orb_params* p, int F, int H, int W, int max_kp);

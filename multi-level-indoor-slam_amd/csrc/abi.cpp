@@ -126,18 +126,12 @@ size_t mlg_vit_workspace_bytes(int batch, int image_size) {
     return carve(VitGeom(batch, image_size), nullptr, nullptr);
 }
 
-int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, int H, int W, int C,
-                    long frame_stride, int image_size, int flags, void* workspace, size_t workspace_bytes,
-                    float* desc_out, float* local_out, void* stream) {
-    if (!w || !frames || !workspace || !desc_out || batch <= 0 || image_size % PATCH) return MLG_EINVAL;
-    const VitGeom g(batch, image_size);
-    VitWorkspace ws;
-    if (carve(g, (char*)workspace, &ws) > workspace_bytes) return MLG_ENOMEM;
-    hipStream_t s = (hipStream_t)stream;
-    const int M = g.B * g.T;
+}  // extern "C"
 
-    const int swap_rb = (flags & MLG_VIT_KEEP_CHANNELS) ? 0 : 1;
-    const int mean_pool = (flags & MLG_VIT_POOL_MEAN) ? 1 : 0;
+// Preprocess + patch embedding + the 12 blocks; leaves the residual stream in ws->x.
+static int vit_trunk(const mlg_vit_weights* w, const uint8_t* frames, const VitGeom& g, int H, int W, int C,
+                     long frame_stride, int swap_rb, const VitWorkspace& ws, hipStream_t s) {
+    const int M = g.B * g.T;
     TRY(mlg_preprocess_patches(frames, g.B, H, W, C, frame_stride, g.S, MLG_VIT_PATCH_K, swap_rb, ws.patches, s));
     TRY(mlg_gemm_patch(ws.patches, w->patch_w, w->patch_b, w->pos, ws.x, g.B * g.P, g.P, MLG_VIT_PATCH_K, s));
     TRY(mlg_cls_rows(ws.x, w->cls, w->pos, g.B, g.T, s));
@@ -169,7 +163,48 @@ int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, 
             TRY(mlg_gemm_residual(ws.h, bl.fc2_w, bl.fc2_b, bl.ls2, ws.x, M, 768, 3072, s));
         }
     }
+    return MLG_OK;
+}
+
+extern "C" {
+
+int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, int H, int W, int C,
+                    long frame_stride, int image_size, int flags, void* workspace, size_t workspace_bytes,
+                    float* desc_out, float* local_out, void* stream) {
+    if (!w || !frames || !workspace || !desc_out || batch <= 0 || image_size % PATCH) return MLG_EINVAL;
+    const VitGeom g(batch, image_size);
+    VitWorkspace ws;
+    if (carve(g, (char*)workspace, &ws) > workspace_bytes) return MLG_ENOMEM;
+    hipStream_t s = (hipStream_t)stream;
+    const int swap_rb = (flags & MLG_VIT_KEEP_CHANNELS) ? 0 : 1;
+    const int mean_pool = (flags & MLG_VIT_POOL_MEAN) ? 1 : 0;
+    TRY(vit_trunk(w, frames, g, H, W, C, frame_stride, swap_rb, ws, s));
     TRY(mlg_final_norm_gem(ws.x, w->norm_w, w->norm_b, local_out, ws.partial, desc_out, g.B, g.T, mean_pool, s));
+    return MLG_OK;
+}
+
+size_t mlg_salad_workspace_bytes(int batch, int image_size) {
+    // the head reuses the ViT buffers: hidden [B*T, 1024] bf16 in `h`, scores / cluster
+    // features [B*T, 256] f32 in `x` once the final LayerNorm has read it
+    return mlg_vit_workspace_bytes(batch, image_size);
+}
+
+int mlg_salad_forward(const mlg_vit_weights* w, const mlg_salad_weights* sw, const uint8_t* frames, int batch,
+                      int H, int W, int C, long frame_stride, int image_size, void* workspace,
+                      size_t workspace_bytes, float* desc_out, void* stream) {
+    if (!w || !sw || !frames || !workspace || !desc_out || batch <= 0 || image_size % PATCH) return MLG_EINVAL;
+    const VitGeom g(batch, image_size);
+    VitWorkspace ws;
+    if (carve(g, (char*)workspace, &ws) > workspace_bytes) return MLG_ENOMEM;
+    hipStream_t s = (hipStream_t)stream;
+    const int M = g.B * g.T;
+    // SALAD._preprocess keeps the stored channel order (place_recognition.py:395-397)
+    TRY(vit_trunk(w, frames, g, H, W, C, frame_stride, /*swap_rb=*/0, ws, s));
+    TRY(mlg_layernorm_bf16(ws.x, w->norm_w, w->norm_b, ws.xn, M, s));  // backbone norm_layer, all tokens
+    TRY(mlg_gemm_bias_relu_bf16(ws.xn, 768, sw->w1, sw->b1, ws.h, 1024, 1024, M, 1024, 768, s));
+    float* y = ws.x;  // [M, 256]
+    TRY(mlg_gemm_bias_f32_ld(ws.h, 1024, sw->w2, sw->b2, y, 256, M, 256, 1024, s));
+    TRY(mlg_salad_head(ws.xn, y, g.B, g.T, sw->wt1, sw->bt1, sw->wt2, sw->bt2, sw->dust_bin, desc_out, s));
     return MLG_OK;
 }
 

@@ -75,6 +75,10 @@ int mlg_final_norm_gem(const float* X, const float* g, const float* b, float* lo
                        int B, int T, int mean_pool, hipStream_t s);
 size_t mlg_gem_partial_bytes(int B);
 
+// salad.hip -- SALAD head per frame (token MLP, Sinkhorn, aggregation, normalisation)
+int mlg_salad_head(const bf16_t* xn, const float* Y, int B, int T, const float* wt1, const float* bt1,
+                   const float* wt2, const float* bt2, float dust, float* desc, hipStream_t s);
+
 // knn.hip
 int mlg_row_normalize(const float* X, float* Xn, int N, int D, float* norms, hipStream_t s);
 int mlg_similarity_f32(const float* A, int Q, const float* B, int N, int D, float* S, int lds, hipStream_t s);

@@ -7,7 +7,7 @@
 // Restated from OpenCV's ORB (orb.cpp) -- the algorithm and its deviations are listed in
 // oracle/csrc/orb.c, which this file matches bit for bit.  MI355X shape:
 //   * a batch of F frames at once; every pixel stage is one launch per pyramid level
-//     over all frames (gray, INTER_LINEAR pyramid, FAST-9 score map, 3x3 NMS + border
+//     over all frames (gray, INTER_LINEAR_EXACT pyramid, FAST-9 score map, 3x3 NMS + border
 //     + per-(frame, level) candidate lists and FAST-score histograms, 7x7 Gaussian);
 //   * retainBest twice without a global sort: the FAST-score threshold of the 2n best
 //     comes from the 256-bin histogram (ties at it kept, as retainBest keeps them), the
@@ -30,7 +30,7 @@ constexpr int SORT_CAP = 8192;  // survivors of the FAST retainBest per (frame, 
 
 struct OrbGeom {
     int H, W, F, nfeat_total, max_kp;
-    int lw[NL], lh[NL], nfeat[NL], vend[NL];
+    int lw[NL], lh[NL], nfeat[NL];
     long loff[NL];   // byte offset of level l inside one frame's pyramid image
     long lcap[NL];   // candidate capacity of level l
     long coff[NL];   // candidate-list offset of level l inside one frame's lists
@@ -39,10 +39,9 @@ struct OrbGeom {
     long cand_per_frame;
     int fast_t, edge;
     int umax[16];
-    int gc[7];
+    float gk[7];
 };
 
-__device__ __forceinline__ int16_t sat16(int v) { return (int16_t)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v)); }
 
 __global__ void k_orb_gray(const uint8_t* __restrict__ frames, long stride, int C, OrbGeom g,
                            uint8_t* __restrict__ pyr) {
@@ -56,40 +55,41 @@ __global__ void k_orb_gray(const uint8_t* __restrict__ frames, long stride, int 
         (uint8_t)(C >= 3 ? (p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + 8192) >> 14 : p[0]);
 }
 
-// cv2.resize INTER_LINEAR (fixed-point generic path; oracle.c orc_resize_linear_u8) of
-// level l - 1 into level l.
+// cv::resize(..., INTER_LINEAR_EXACT) of level l - 1 into level l (OpenCV resize.cpp
+// resize_bitExact on 8U; oracle/csrc/orb.c resize_linear_exact_u8): binary64 source
+// coordinate, 8-bit tap weights, 16-bit horizontal sums, (h0 c0 + h1 c1 + 2^15) >> 16.
+__device__ __forceinline__ void exact_tap(int d, int dsize, int ssize, int& i0, uint32_t& c1) {
+    const double inv = __ddiv_rn((double)dsize, (double)ssize), scale = __ddiv_rn(1.0, inv);
+    const double f = __dsub_rn(__dmul_rn(scale, __dadd_rn((double)d, 0.5)), 0.5);
+    const int i = (int)floor(f);
+    if (i < 0 || ssize <= 1) {
+        i0 = 0;
+        c1 = 0;
+    } else if (i >= ssize - 1) {
+        i0 = ssize - 1;
+        c1 = 0;
+    } else {
+        i0 = i;
+        c1 = (uint32_t)__double2int_rn(__dmul_rn(__dsub_rn(f, (double)i), 256.0));
+    }
+}
+
 __global__ void k_orb_resize(OrbGeom g, int l, uint8_t* __restrict__ pyr) {
     const int W = g.lw[l - 1], H = g.lh[l - 1], DW = g.lw[l], DH = g.lh[l];
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (long)g.F * DH * DW) return;
     const int dx = (int)(e % DW), dy = (int)((e / DW) % DH), f = (int)(e / ((long)DW * DH));
-    const double sxs = 1.0 / ((double)DW / W);
-    float fx = (float)((dx + 0.5) * sxs - 0.5);
-    int sx = (int)floorf(fx);
-    fx -= (float)sx;
-    if (sx < 0) { fx = 0.f; sx = 0; }
-    if (sx >= W - 1) { fx = 0.f; sx = W - 1; }
-    const int ax0 = sat16(__float2int_rn((1.f - fx) * 2048.f)), ax1 = sat16(__float2int_rn(fx * 2048.f));
-    const double sys = 1.0 / ((double)DH / H);
-    float fy = (float)((dy + 0.5) * sys - 0.5);
-    const int sy = (int)floorf(fy);
-    fy -= (float)sy;
-    const int by0 = sat16(__float2int_rn((1.f - fy) * 2048.f)), by1 = sat16(__float2int_rn(fy * 2048.f));
-    const int sy0 = min(max(sy, 0), H - 1), sy1 = min(max(sy + 1, 0), H - 1);
-    const int sx1 = sx + 1 < W ? sx + 1 : sx;
+    int x0, y0;
+    uint32_t cx1, cy1;
+    exact_tap(dx, DW, W, x0, cx1);
+    exact_tap(dy, DH, H, y0, cy1);
+    const int x1 = x0 + 1 < W ? x0 + 1 : x0, y1 = y0 + 1 < H ? y0 + 1 : y0;
+    const uint32_t cx0 = 256u - cx1, cy0 = 256u - cy1;
     const uint8_t* src = pyr + (long)f * g.pyr_bytes + g.loff[l - 1];
-    const uint8_t* r0 = src + (long)sy0 * W;
-    const uint8_t* r1 = src + (long)sy1 * W;
-    const int s0 = r0[sx] * ax0 + r0[sx1] * ax1, s1 = r1[sx] * ax0 + r1[sx1] * ax1;
-    int v;
-    if (dx < g.vend[l]) {
-        const int a0 = sat16(s0 >> 4), a1 = sat16(s1 >> 4);
-        v = (int)(int16_t)(((a0 * by0) >> 16) + ((a1 * by1) >> 16));
-        v = (v + 2) >> 2;
-    } else {
-        v = (s0 * by0 + s1 * by1 + (1 << 21)) >> 22;
-    }
-    pyr[(long)f * g.pyr_bytes + g.loff[l] + e % ((long)DW * DH)] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+    const uint8_t* r0 = src + (long)y0 * W;
+    const uint8_t* r1 = src + (long)y1 * W;
+    const uint32_t h0 = cx0 * r0[x0] + cx1 * r0[x1], h1 = cx0 * r1[x0] + cx1 * r1[x1];
+    pyr[(long)f * g.pyr_bytes + g.loff[l] + e % ((long)DW * DH)] = (uint8_t)((h0 * cy0 + h1 * cy1 + 32768u) >> 16);
 }
 
 __constant__ int8_t CIRC[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1}, {2, -2}, {1, -3},
@@ -154,8 +154,17 @@ __global__ void k_orb_nms(OrbGeom g, int l, const uint8_t* __restrict__ score, u
 
 __device__ __forceinline__ int reflect101(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
 
-// 7x7 Gaussian (sigma 2), separable fixed point: 8-bit coefficients summing to 256,
-// 16-bit horizontal sums, (v + 2^15) >> 16; BORDER_REFLECT_101.
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) as OpenCV runs it on ORB's pyramid
+// submatrices: sepFilter2D with the float kernel -- row pass k0 x0 + ... + k6 x6 left to
+// right, symmetric column pass k3 c + k4 (u1 + d1) + k5 (u2 + d2) + k6 (u3 + d3), round
+// half to even, saturate (every operation rounded separately, as oracle/csrc/orb.c).
+__device__ __forceinline__ float blur_row(const uint8_t* row, const int* xs, const float* k) {
+    float s = __fmul_rn(k[0], (float)row[xs[0]]);
+#pragma unroll
+    for (int t = 1; t < 7; ++t) s = __fadd_rn(s, __fmul_rn(k[t], (float)row[xs[t]]));
+    return s;
+}
+
 __global__ void k_orb_blur(OrbGeom g, int l, const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur) {
     const int w = g.lw[l], h = g.lh[l];
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -166,16 +175,15 @@ __global__ void k_orb_blur(OrbGeom g, int l, const uint8_t* __restrict__ pyr, ui
     int xs[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) xs[k] = reflect101(x + k - 3, w);
-    uint32_t v = 0;
+    float s = __fmul_rn(g.gk[3], blur_row(img + (long)y * w, xs, g.gk));
 #pragma unroll
-    for (int r = 0; r < 7; ++r) {
-        const uint8_t* row = img + (long)reflect101(y + r - 3, h) * w;
-        uint32_t hs = 0;
-#pragma unroll
-        for (int k = 0; k < 7; ++k) hs += (uint32_t)g.gc[k] * row[xs[k]];
-        v += (uint32_t)g.gc[r] * (hs & 0xffffu);
+    for (int t = 1; t <= 3; ++t) {
+        const float up = blur_row(img + (long)reflect101(y - t, h) * w, xs, g.gk);
+        const float dn = blur_row(img + (long)reflect101(y + t, h) * w, xs, g.gk);
+        s = __fadd_rn(s, __fmul_rn(g.gk[3 + t], __fadd_rn(dn, up)));
     }
-    blur[base + (long)y * w + x] = (uint8_t)((v + 32768u) >> 16);
+    const int v = __float2int_rn(s);
+    blur[base + (long)y * w + x] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
 }
 
 __device__ __forceinline__ float harris_resp(const uint8_t* img, int W, int x, int y) {
@@ -497,7 +505,6 @@ bool make_geom(const mlg_orb_params* p, int F, int H, int W, int max_kp, OrbGeom
         g.lw[l] = p->level_w[l];
         g.lh[l] = p->level_h[l];
         g.nfeat[l] = p->level_features[l];
-        g.vend[l] = p->level_vec_end[l];
         g.lscale[l] = p->level_scale[l];
         if (g.lw[l] < 1 || g.lh[l] < 1 || g.nfeat[l] < 0) return false;
         g.loff[l] = off;
@@ -511,7 +518,7 @@ bool make_geom(const mlg_orb_params* p, int F, int H, int W, int max_kp, OrbGeom
     g.pyr_bytes = (off + 255) & ~255L;
     g.cand_per_frame = coff;
     for (int i = 0; i < 16; ++i) g.umax[i] = p->umax[i];
-    for (int i = 0; i < 7; ++i) g.gc[i] = p->gauss[i];
+    for (int i = 0; i < 7; ++i) g.gk[i] = p->gauss[i];
     return true;
 }
 

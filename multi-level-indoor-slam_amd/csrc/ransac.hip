@@ -35,6 +35,9 @@
 //   k_ransac_hyp     : one thread per hypothesis: solve (<= 10 models)
 //   k_ransac_score   : one thread per hypothesis: inlier count (or LMedS median) of
 //                      each model over the pair's points, staged in LDS
+//   (hyp / hyp5 / score run in two rounds: hypotheses [0, 256) of every pair, then
+//   k_ransac_probe replays the sequential scan over them and only the pairs whose
+//   adaptive stop lies beyond get hypotheses [256, H))
 //   k_ransac_select  : one workgroup per pair: OpenCV's sequential best-model scan,
 //                      inlier mask
 //   k_recover_pose   : one workgroup per pair: E -> [R|t] by cheirality on the inliers
@@ -47,6 +50,7 @@ namespace {
 
 constexpr int MAXSOL = 10;
 constexpr int RS_CHUNK = 1024;  // points per LDS stage in scoring (4 doubles each = 32 KB)
+constexpr int RS_ROUND1 = 256;  // hypotheses of the first round (inlier ratio >= 0.5 stops inside it)
 
 // ------------------------------------------------------------------ small linear algebra
 
@@ -873,11 +877,13 @@ __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict_
                                                      const double4* __restrict__ ptsn, int H,
                                                      const int32_t* __restrict__ subsets,
                                                      const int32_t* __restrict__ nsub, double* __restrict__ models,
-                                                     int8_t* __restrict__ nsol) {
+                                                     int8_t* __restrict__ nsol, int h0,
+                                                     const uint8_t* __restrict__ done) {
     __shared__ double snb[16][4][9];
     const int g = threadIdx.x >> 4, r = threadIdx.x & 15, gl = threadIdx.x & 48;  // group, lane in group, base
     const int p = blockIdx.y;
-    const int h = blockIdx.x * 16 + g;
+    const int h = h0 + blockIdx.x * 16 + g;
+    if (done && done[p]) return;  // uniform per block
     const PairInfo pi = info[p];
     const bool ess = pi.mode == 1 || pi.mode == 5;
     // whole groups are active or not (shuffles stay inside a group)
@@ -1142,10 +1148,10 @@ __global__ __launch_bounds__(64) void k_ransac_subsets(const PairInfo* __restric
 __global__ __launch_bounds__(64) void k_ransac_hyp(const PairInfo* __restrict__ info, const double4* __restrict__ ptsn,
                                                    int H, uint64_t seed, const int32_t* __restrict__ subsets,
                                                    const int32_t* __restrict__ nsub, double* __restrict__ models,
-                                                   int8_t* __restrict__ nsol) {
+                                                   int8_t* __restrict__ nsol, int h0, const uint8_t* __restrict__ done) {
     const int p = blockIdx.y;
-    const int h = blockIdx.x * blockDim.x + threadIdx.x;
-    if (h >= H) return;
+    const int h = h0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= H || (done && done[p])) return;
     const PairInfo pi = info[p];
     double* out = models + ((size_t)p * H + h) * MAXSOL * 9;
     int ns = 0;
@@ -1204,10 +1210,12 @@ __global__ __launch_bounds__(64) void k_ransac_hyp(const PairInfo* __restrict__ 
 __global__ __launch_bounds__(256) void k_ransac_score(const PairInfo* __restrict__ info, const double4* __restrict__ ptsn,
                                                       const double4* __restrict__ ptsr, int H,
                                                       const double* __restrict__ models,
-                                                      const int8_t* __restrict__ nsol, float* __restrict__ score) {
+                                                      const int8_t* __restrict__ nsol, float* __restrict__ score,
+                                                      int h0, const uint8_t* __restrict__ done) {
     __shared__ double4 sp[RS_CHUNK];
     const int p = blockIdx.y;
-    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    const int h = h0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (done && done[p]) return;  // uniform per block: the barrier count stays uniform
     const PairInfo pi = info[p];
     if (pi.mode == 0) {
         if (h < H)
@@ -1430,6 +1438,38 @@ RS_HD bool cheiral(const double (&R)[3][3], const double (&t)[3], double x1, dou
     return z2 > 0 && z2 < dist;
 }
 
+// Adaptive early stop across two launch rounds: after hypotheses [0, H1) are solved and
+// scored, replay OpenCV's sequential scan over them (as k_ransac_select does); a pair is
+// done when the scan stops inside the first H1 -- its adaptive iteration budget or its
+// subset count fell to <= H1 -- so the scan never reads a hypothesis >= H1 and round two
+// skips the pair.  Only the sequential modes (5-point E, 7-point F) can finish early.
+__global__ __launch_bounds__(256) void k_ransac_probe(const PairInfo* __restrict__ info, int P, int H, int H1,
+                                                      const float* __restrict__ score,
+                                                      const int8_t* __restrict__ nsol,
+                                                      const int32_t* __restrict__ nsub, uint8_t* __restrict__ done) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const PairInfo pi = info[p];
+    uint8_t d = 0;
+    if (pi.mode == 1 || pi.mode == 2) {
+        const int mp = pi.mode == 1 ? 5 : 7;
+        const int ns_it = nsub[p], total = H * MAXSOL;
+        int niters = H, max_good = 0;
+        for (int it = 0; it < niters && it < ns_it && it < H1; ++it) {
+            const int ns = nsol[(size_t)p * H + it];
+            for (int s = 0; s < ns; ++s) {
+                const int g = (int)score[(size_t)p * total + it * MAXSOL + s];
+                if (g > max(max_good, mp - 1)) {
+                    max_good = g;
+                    niters = ransac_update_iters(RANSAC_CONFIDENCE, (double)(pi.count - g) / pi.count, mp, niters);
+                }
+            }
+        }
+        d = (niters <= H1 || ns_it <= H1) ? 1 : 0;
+    }
+    done[p] = d;
+}
+
 __global__ __launch_bounds__(256) void k_ransac_select(const PairInfo* __restrict__ info,
                                                        const double4* __restrict__ ptsn,
                                                        const double4* __restrict__ ptsr, int H,
@@ -1598,7 +1638,7 @@ __global__ __launch_bounds__(256) void k_recover_pose(const float* __restrict__ 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct RsLayout {
-    size_t info, ptsn, ptsr, models, nsol, score, subsets, nsub, total;
+    size_t info, ptsn, ptsr, models, nsol, score, subsets, nsub, done, total;
 };
 
 RsLayout rs_layout(int P, long S_total, int H) {
@@ -1611,7 +1651,8 @@ RsLayout rs_layout(int P, long S_total, int H) {
     L.score = L.nsol + align256((size_t)P * H);
     L.subsets = L.score + align256(sizeof(float) * MAXSOL * (size_t)P * H);
     L.nsub = L.subsets + align256(sizeof(int32_t) * 7 * (size_t)P * H);
-    L.total = L.nsub + align256(sizeof(int32_t) * (size_t)P);
+    L.done = L.nsub + align256(sizeof(int32_t) * (size_t)P);
+    L.total = L.done + align256((size_t)P);
     return L;
 }
 
@@ -1641,15 +1682,29 @@ int mlg_ransac_run(const float* kp1, const float* kp2, const int32_t* offs, int 
     MLG_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_ransac_subsets, dim3((P + 63) / 64), dim3(64), 0, s, info, P, H, kp1, kp2, subsets, nsub);
     MLG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ransac_hyp, dim3((H + 63) / 64, P), dim3(64), 0, s, info, ptsn, H, seed, subsets, nsub,
-                       models, nsol);
-    MLG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ransac_hyp5, dim3((H + 15) / 16, P), dim3(256), 0, s, info, ptsn, H, subsets, nsub, models,
-                       nsol);
-    MLG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_ransac_score, dim3((H + 255) / 256, P), dim3(256), 0, s, info, ptsn, ptsr, H, models, nsol,
-                       score);
-    MLG_LAUNCH_CHECK();
+    uint8_t* done = (uint8_t*)(w + L.done);
+    // round one: hypotheses [0, H1) of every pair; round two: [H1, H) of the pairs whose
+    // sequential scan has not stopped inside round one (k_ransac_probe)
+    const int H1 = std::min(H, RS_ROUND1);
+    for (int round = 0; round < 2; ++round) {
+        const int h0 = round ? H1 : 0, hn = round ? H - H1 : H1;
+        const uint8_t* skip = round ? done : nullptr;
+        if (hn <= 0) break;
+        hipLaunchKernelGGL(k_ransac_hyp, dim3((hn + 63) / 64, P), dim3(64), 0, s, info, ptsn, H, seed, subsets, nsub,
+                           models, nsol, h0, skip);
+        MLG_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_ransac_hyp5, dim3((hn + 15) / 16, P), dim3(256), 0, s, info, ptsn, H, subsets, nsub,
+                           models, nsol, h0, skip);
+        MLG_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_ransac_score, dim3((hn + 255) / 256, P), dim3(256), 0, s, info, ptsn, ptsr, H, models,
+                           nsol, score, h0, skip);
+        MLG_LAUNCH_CHECK();
+        if (round == 0 && H1 < H) {
+            hipLaunchKernelGGL(k_ransac_probe, dim3((P + 255) / 256), dim3(256), 0, s, info, P, H, H1, score, nsol,
+                               nsub, done);
+            MLG_LAUNCH_CHECK();
+        }
+    }
     hipLaunchKernelGGL(k_ransac_select, dim3(P), dim3(256), 0, s, info, ptsn, ptsr, H, models, score, nsol, nsub, model_out,
                        mask, inliers, status);
     MLG_LAUNCH_CHECK();

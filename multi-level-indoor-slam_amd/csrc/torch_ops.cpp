@@ -120,6 +120,44 @@ void vit_forward_into(const Tensor& frames, at::TensorList w, int64_t image_size
     }
 }
 
+// SALAD: frames uint8 [B, H, W, C] -> desc f32 [B, 8448]; salad = [w1, b1, w2, b2, wt1, bt1, wt2, bt2]
+Tensor salad_forward(const Tensor& frames, at::TensorList w, at::TensorList salad, double dust_bin,
+                     int64_t image_size, int64_t max_batch) {
+    want(frames, at::kByte, "frames");
+    TORCH_CHECK(frames.dim() == 4, "frames must be [B, H, W, C]");
+    TORCH_CHECK(salad.size() == 8, "salad weights: expected 8 tensors");
+    TORCH_CHECK(max_batch > 0, "max_batch must be positive");
+    const int64_t B = frames.size(0), H = frames.size(1), W = frames.size(2), C = frames.size(3);
+    std::vector<Tensor> wv(w.begin(), w.end());
+    const mlg_vit_weights s = vit_weights(wv);
+    const at::ScalarType kinds[8] = {at::kBFloat16, at::kFloat, at::kBFloat16, at::kFloat,
+                                     at::kFloat,    at::kFloat, at::kFloat,    at::kFloat};
+    const int64_t numel[8] = {1024 * 768, 1024, 256 * 1024, 256, 512 * 768, 512, 256 * 512, 256};
+    for (int i = 0; i < 8; ++i) {
+        want(salad[i], kinds[i], "salad weight");
+        TORCH_CHECK(salad[i].numel() == numel[i], "salad weight ", i, ": expected ", numel[i], " elements");
+    }
+    mlg_salad_weights sw;
+    sw.w1 = cp<uint16_t>(salad[0]); sw.b1 = cp<float>(salad[1]);
+    sw.w2 = cp<uint16_t>(salad[2]); sw.b2 = cp<float>(salad[3]);
+    sw.wt1 = cp<float>(salad[4]); sw.bt1 = cp<float>(salad[5]);
+    sw.wt2 = cp<float>(salad[6]); sw.bt2 = cp<float>(salad[7]);
+    sw.dust_bin = (float)dust_bin;
+    c10::DeviceGuard g(frames.device());
+    Tensor desc = at::empty({B, MLG_SALAD_DIM}, frames.options().dtype(at::kFloat));
+    const int64_t nb_max = std::min(B, max_batch);
+    Tensor ws = workspace(mlg_salad_workspace_bytes((int)nb_max, (int)image_size), frames);
+    const long stride = (long)(H * W * C);
+    for (int64_t b0 = 0; b0 < B; b0 += max_batch) {
+        const int nb = (int)std::min(max_batch, B - b0);
+        check_rc(mlg_salad_forward(&s, &sw, cp<uint8_t>(frames) + b0 * stride, nb, (int)H, (int)W, (int)C, stride,
+                                   (int)image_size, ws.data_ptr(), (size_t)ws.numel(),
+                                   mp<float>(desc) + b0 * MLG_SALAD_DIM, stream_of(frames)),
+                 "mlg_salad_forward");
+    }
+    return desc;
+}
+
 // --------------------------------------------------------------- retrieval
 std::tuple<Tensor, Tensor, Tensor, Tensor> knn_gate(const Tensor& desc, const Tensor& t, const Tensor& floor,
                                                     const Tensor& has_floor, double min_gap, double thr, int64_t k,
@@ -636,24 +674,25 @@ std::tuple<double, int64_t, double> prof_read(int64_t slot) {
 // ------------------------------------------------------------------ ORB fallback
 // iparams: int32 [57] = level_w[8], level_h[8], level_features[8], level_vec_end[8],
 // umax[16], gauss[7], fast_threshold, edge_threshold; scales: float32 [8] (host tensors)
-mlg_orb_params orb_params(const Tensor& ip, const Tensor& sc) {
+mlg_orb_params orb_params(const Tensor& ip, const Tensor& fp) {
     want(ip, at::kInt, "orb iparams", false);
-    want(sc, at::kFloat, "orb scales", false);
-    TORCH_CHECK(ip.numel() == 57 && sc.numel() == MLG_ORB_LEVELS, "orb params: expected 57 ints and 8 scales");
+    want(fp, at::kFloat, "orb fparams", false);
+    TORCH_CHECK(ip.numel() == 42 && fp.numel() == MLG_ORB_LEVELS + 7,
+                "orb params: expected 42 ints and 8 scales + 7 Gaussian taps");
     const int32_t* v = ip.data_ptr<int32_t>();
+    const float* f = fp.data_ptr<float>();
     mlg_orb_params p;
     std::memset(&p, 0, sizeof(p));
     for (int l = 0; l < MLG_ORB_LEVELS; ++l) {
         p.level_w[l] = v[l];
         p.level_h[l] = v[8 + l];
         p.level_features[l] = v[16 + l];
-        p.level_vec_end[l] = v[24 + l];
-        p.level_scale[l] = sc.data_ptr<float>()[l];
+        p.level_scale[l] = f[l];
     }
-    for (int i = 0; i < 16; ++i) p.umax[i] = v[32 + i];
-    for (int i = 0; i < 7; ++i) p.gauss[i] = v[48 + i];
-    p.fast_threshold = v[55];
-    p.edge_threshold = v[56];
+    for (int i = 0; i < 16; ++i) p.umax[i] = v[24 + i];
+    for (int i = 0; i < 7; ++i) p.gauss[i] = f[MLG_ORB_LEVELS + i];
+    p.fast_threshold = v[40];
+    p.edge_threshold = v[41];
     return p;
 }
 
@@ -737,6 +776,8 @@ std::tuple<Tensor, Tensor> png_decode(std::vector<Tensor> blobs, int64_t H, int6
 TORCH_LIBRARY(mlgate, m) {
     m.def("vit_forward_into(Tensor frames, Tensor[] weights, int image_size, int flags, int max_batch, "
           "Tensor(a!) desc, Tensor(b!)? local) -> ()");
+    m.def("salad_forward(Tensor frames, Tensor[] weights, Tensor[] salad, float dust_bin, int image_size, "
+          "int max_batch) -> Tensor");
     m.def("knn_gate(Tensor desc, Tensor t, Tensor floor, Tensor has_floor, float min_gap, float thr, int k, "
           "bool gating, int q0, int Q, Tensor(a!)? totals) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("knn_query(Tensor db, Tensor q, Tensor t_db, Tensor t_q, float min_gap, int k) -> (Tensor, Tensor, Tensor)");
@@ -776,6 +817,7 @@ TORCH_LIBRARY(mlgate, m) {
 
 TORCH_LIBRARY_IMPL(mlgate, CUDA, m) {
     m.impl("vit_forward_into", &vit_forward_into);
+    m.impl("salad_forward", &salad_forward);
     m.impl("knn_gate", &knn_gate);
     m.impl("knn_query", &knn_query);
     m.impl("row_normalize", &row_normalize);

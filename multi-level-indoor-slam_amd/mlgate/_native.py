@@ -16,7 +16,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmlgate.so")
 TORCH_LIB_PATH = os.path.join(_HERE, "libmlgate_torch.so")
-OPS = ("vit_forward_into", "knn_gate", "knn_query", "row_normalize", "similarity", "xcorr_score", "xcorr_batch",
+OPS = ("vit_forward_into", "salad_forward", "knn_gate", "knn_query", "row_normalize", "similarity", "xcorr_score", "xcorr_batch",
        "superpoint",
        "lightglue", "ransac_epipolar", "recover_pose", "resnet50", "loftr_features", "loftr_match", "superglue", "pillow_resize_224", "plane_ransac", "proximity",
        "prof_enable", "prof_reset", "prof_read")
@@ -31,6 +31,9 @@ EXPORTS = {
     "mlg_vit_workspace_bytes": (c_size_t, [c_int, c_int]),
     "mlg_vit_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_long, c_int, c_int, c_void_p,
                                 c_size_t, c_void_p, c_void_p, c_void_p]),
+    "mlg_salad_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "mlg_salad_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_long, c_int,
+                                  c_void_p, c_size_t, c_void_p, c_void_p]),
     "mlg_knn_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mlg_knn_workspace_bytes_k": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     "mlg_knn_gate": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_double, c_float, c_int,

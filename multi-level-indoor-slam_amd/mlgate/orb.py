@@ -8,12 +8,14 @@ pairs, through ``torch.ops.mlgate.orb_detect`` / ``orb_match``.
 
 The ORB_Impl geometry is computed here, once per frame size: OpenCV's defaults
 (scaleFactor 1.2, nlevels 8, edgeThreshold 31, patchSize 31, fastThreshold 20), level
-sizes cvRound(cols / scale), nfeaturesPerLevel in float32, the u_max circle, and the
+sizes cvRound(cols / scale), nfeaturesPerLevel in float32, the u_max circle, the float32
+Gaussian kernel of the per-level GaussianBlur(7x7, sigma 2), and the
 point pattern: OpenCV's makeRandomPattern(31) stream (cv::RNG(0x34985739)) unless
 MLGATE_ORB_PATTERN names an int [512, 2] .npy holding OpenCV's bit_pattern_31_ table
 (not shipped: OpenCV is not installed here).  Deviations from OpenCV (parity unpinned):
 see oracle/csrc/orb.c.
 """
+import math
 import os
 from functools import lru_cache
 
@@ -24,19 +26,10 @@ from . import _native
 SCALE_FACTOR, NLEVELS, EDGE, PATCH, FAST_T = 1.2, 8, 31, 31, 20
 
 
-def _vec_end(width_bytes):
-    """First byte of a row that cv2.resize's vertical pass handles in its scalar tail."""
-    x = 0
-    while x <= width_bytes - 16:
-        x += 16
-    while x < width_bytes - 8:
-        x += 8
-    return x
-
-
 @lru_cache(maxsize=None)
 def geometry(H, W, nfeatures):
-    """(int32 [57] parameter block of mlg_orb_params, float32 [8] level scales)."""
+    """(int32 [42] block of mlg_orb_params: level widths, heights, features, umax[16],
+    FAST threshold, edge threshold; float32 [15]: level scales, Gaussian kernel)."""
     f32 = np.float32
     scales = np.array([f32(np.power(np.float64(SCALE_FACTOR), l)) for l in range(NLEVELS)], np.float32)
     ws = [int(np.rint(f32(W) / s)) for s in scales]
@@ -61,12 +54,26 @@ def geometry(H, W, nfeatures):
             v0 += 1
         umax[v] = v0
         v0 += 1
-    x = np.arange(7) - 3
-    g = np.exp(-(x * x) / 8.0)
-    gc = np.rint(g / g.sum() * 256).astype(np.int64)
-    gc[3] += 256 - int(gc.sum())
-    ip = ws + hs + per + [_vec_end(w) for w in ws] + umax[:16] + gc.tolist() + [FAST_T, EDGE]
-    return np.array(ip, np.int32), scales
+    ip = ws + hs + per + umax[:16] + [FAST_T, EDGE]
+    return np.array(ip, np.int32), np.concatenate([scales, gaussian_kernel()]).astype(np.float32)
+
+
+def gaussian_kernel(ksize=7, sigma=2.0):
+    """cv::getGaussianKernel(7, 2, CV_32F) as OpenCV 4.x builds it (getGaussianKernelBitExact:
+    t_i = exp(x^2 * (-0.125 / sigma^2)) for x = 2 i - (n - 1), scaled by 1 / (2 sum t_i + 1),
+    centre tap = that factor), rounded to float32 -- ORB's GaussianBlur(7x7, 2, 2)."""
+    scale2 = -0.125 / (float(sigma) * float(sigma))
+    n2 = (ksize - 1) // 2
+    vals, s = [], 0.0
+    for i in range(n2):
+        x = 1 - ksize + 2 * i
+        vals.append(math.exp(float(x * x) * scale2))
+        s += vals[-1]
+    mul1 = 1.0 / (s * 2.0 + 1.0)
+    k = [mul1] * ksize
+    for i in range(n2):
+        k[i] = k[ksize - 1 - i] = vals[i] * mul1
+    return np.array(k, np.float32)
 
 
 def random_pattern(npoints=512):

@@ -13,11 +13,13 @@ behaviour as the reference; the compute runs on the mlgate HIP kernels:
   * MixVPR / SALAD -> the reference resolves both to a torchvision ResNet-50 GAP
     fallback (place_recognition.py:241-306, 370-378); here that network runs on the
     GPU (mlgate.resnet: Pillow-exact resize, HIP stem, MFMA bottlenecks, GAP, zero-pad).
+    SALAD's native branch (DINOv2 + Sinkhorn aggregation) is opt-in: mlgate.salad.
 
 Weights: the hub checkpoint cannot be fetched offline.  ``pretrained_path`` (or
 MLGATE_DINOV2_WEIGHTS) may point at a local hub-format dinov2_vitb14 state_dict;
 otherwise seeded synthetic weights are used and a warning says so.
 """
+import os
 import warnings
 from dataclasses import dataclass
 from pathlib import Path
@@ -252,8 +254,41 @@ class MixVPR(_ResNetFallback):
 
 
 class SALAD(_ResNetFallback):
+    """place_recognition.py:335-410.  By default what the reference executes: the
+    ``salad`` package does not import, so SALAD warns and runs the MixVPR fallback
+    (:370-378).  ``MLGATE_SALAD_NATIVE=1`` (or ``.native = True``) selects the model its
+    native branch names (:357-368): serizba/salad's DINOv2 ViT-B/14 + optimal-transport
+    aggregator (64 clusters x 128 + 256 token dims = 8448) on the GPU (mlgate.salad,
+    csrc/salad.hip); weights from ``pretrained_path`` / MLGATE_SALAD_WEIGHTS, else seeded
+    synthetic ones."""
+
     def __init__(self, descriptor_dim: int = 8448, device: str = 'cuda', pretrained_path: Optional[str] = None):
         super().__init__(descriptor_dim, device, pretrained_path)
+        self.native = None  # None: MLGATE_SALAD_NATIVE decides; True / False force it
+        self._salad = None
+
+    def _load_model(self):
+        if self._model_loaded:
+            return
+        native = self.native if self.native is not None else os.environ.get("MLGATE_SALAD_NATIVE") == "1"
+        if not native:
+            warnings.warn("SALAD not installed. Using MixVPR fallback. For SALAD: pip install salad-vpr")
+            return super()._load_model()
+        from .salad import DESC_DIM, SaladGPU
+        if self.descriptor_dim != DESC_DIM:
+            raise ValueError(f"native SALAD produces {DESC_DIM}-dim descriptors, not {self.descriptor_dim}")
+        self._salad = SaladGPU(device=self.device, pretrained_path=self.pretrained_path)
+        if self._salad.weights_source.startswith("synthetic"):
+            warnings.warn("SALAD weights not configured (pretrained_path / MLGATE_SALAD_WEIGHTS); using seeded "
+                          "synthetic weights")
+        self._model_loaded = True
+        self._is_fallback = False
+
+    def extract_descriptors(self, images) -> np.ndarray:
+        self._load_model()
+        if self._salad is None:
+            return super().extract_descriptors(images)
+        return self._salad.forward(_device_frames(images, self._salad.device)).cpu().numpy()
 
 
 class _DinoEngineMixin:

@@ -560,3 +560,66 @@ def resolve_superglue_state_dict(path=None, seed=0):
     if path:
         return load_superglue_state_dict(path), path
     return superglue_state_dict(seed), f"synthetic(seed={seed})"
+
+
+# ----------------------------------------------------------------- SALAD
+# serizba/salad VPRModel state dict (SALAD, place_recognition.py:357-368): the hub
+# DINOv2 backbone under ``backbone.model.`` and the SALAD aggregator (num_channels 768,
+# num_clusters 64, cluster_dim 128, token_dim 256).
+SALAD_CLUSTERS, SALAD_CLUSTER_DIM, SALAD_TOKEN_DIM = 64, 128, 256
+
+
+def salad_aggregator_shapes():
+    c = EMBED
+    return {"token_features.0.weight": (512, c), "token_features.0.bias": (512,),
+            "token_features.2.weight": (SALAD_TOKEN_DIM, 512), "token_features.2.bias": (SALAD_TOKEN_DIM,),
+            "cluster_features.0.weight": (512, c, 1, 1), "cluster_features.0.bias": (512,),
+            "cluster_features.3.weight": (SALAD_CLUSTER_DIM, 512, 1, 1),
+            "cluster_features.3.bias": (SALAD_CLUSTER_DIM,),
+            "score.0.weight": (512, c, 1, 1), "score.0.bias": (512,),
+            "score.3.weight": (SALAD_CLUSTERS, 512, 1, 1), "score.3.bias": (SALAD_CLUSTERS,),
+            "dust_bin": ()}
+
+
+def salad_keys():
+    return ["backbone.model." + k for k in hub_keys()] + ["aggregator." + k for k in salad_aggregator_shapes()]
+
+
+def salad_state_dict(seed=0, score_gain=2.0):
+    """Seeded float32 weights with serizba/salad's key names and shapes (He-normal hidden
+    layers; ``score_gain`` widens the cluster scores so the Sinkhorn plan is not flat)."""
+    sd = {"backbone.model." + k: v for k, v in synthetic_state_dict(seed).items()}
+    rng = np.random.default_rng(seed + 7)
+    for k, shp in salad_aggregator_shapes().items():
+        if k == "dust_bin":
+            sd["aggregator.dust_bin"] = np.float32(1.0).reshape(())
+            continue
+        if k.endswith("bias"):
+            sd["aggregator." + k] = (rng.standard_normal(shp, dtype=np.float32) * np.float32(0.02))
+            continue
+        fan_in = int(np.prod(shp[1:]))
+        std = np.sqrt(2.0 / fan_in) if k.split(".")[1] == "0" else np.sqrt(1.0 / fan_in)
+        if k.startswith("score.3"):
+            std *= score_gain
+        sd["aggregator." + k] = rng.standard_normal(shp, dtype=np.float32) * np.float32(std)
+    return sd
+
+
+def load_salad_state_dict(path):
+    """serizba/salad checkpoint (VPRModel state dict, optionally under 'state_dict') from a
+    local file, weights only."""
+    import torch
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if "state_dict" in sd and isinstance(sd["state_dict"], dict):
+        sd = sd["state_dict"]
+    missing = [k for k in salad_keys() if k not in sd]
+    if missing:
+        raise KeyError(f"checkpoint {path} lacks SALAD keys, e.g. {missing[:3]}")
+    return {k: sd[k].float().cpu().numpy() for k in salad_keys()}
+
+
+def resolve_salad_state_dict(path=None, seed=0):
+    path = path or os.environ.get("MLGATE_SALAD_WEIGHTS")
+    if path:
+        return load_salad_state_dict(path), path
+    return salad_state_dict(seed), f"synthetic(seed={seed})"

@@ -7,17 +7,31 @@
  *   cv2.cvtColor(BGR2GRAY); cv2.ORB_create(nfeatures=max_keypoints).detectAndCompute;
  *   cv2.BFMatcher(NORM_HAMMING, crossCheck=True).match; sorted by distance;
  *   confidence = 1 - distance / max distance.
- * OpenCV is not installed here, so this is a restatement of OpenCV's published ORB
- * (orb.cpp: scale pyramid, FAST-9 with 3x3 non-maximum suppression, edge-threshold
- * border filter, retainBest by FAST score (2n, ties kept), Harris response (block 7,
- * k 0.04), retainBest by Harris (n, ties kept), intensity-centroid angle with the
- * umax circle and fastAtan2, 7x7 sigma-2 Gaussian, rBRIEF over 256 rotated point
- * pairs) and BFMatcher's cross-checked Hamming match.  PARITY UNPINNED against OpenCV
- * itself; the known deviations (pyramid by INTER_LINEAR rather than
- * INTER_LINEAR_EXACT, Gaussian coefficients rounded to 8 fractional bits, the point
- * pattern of OpenCV's makeRandomPattern rather than its bit_pattern_31_ table, ties in
- * retainBest ordered by (response desc, y, x) where OpenCV leaves nth_element order)
- * are shared with the HIP path (csrc/orb.hip), which this file pins bit for bit.
+ * OpenCV is not installed here, so this is a restatement of OpenCV 4.x's published ORB
+ * (orb.cpp: scale pyramid by resize(..., INTER_LINEAR_EXACT), FAST-9 with 3x3
+ * non-maximum suppression, edge-threshold border filter, retainBest by FAST score (2n,
+ * ties kept), Harris response (block 7, k 0.04), retainBest by Harris (n, ties kept),
+ * intensity-centroid angle with the umax circle and fastAtan2, GaussianBlur(7x7,
+ * sigma 2, BORDER_REFLECT_101) of each level, rBRIEF over 256 rotated point pairs) and
+ * BFMatcher's cross-checked Hamming match.
+ *   - INTER_LINEAR_EXACT on 8U (resize.cpp resize_bitExact / interpolationLinear): per
+ *     output coordinate f = (1 / (dst / src)) * (d + 0.5) - 0.5 in binary64, i = floor f,
+ *     weight of i + 1 = cvRound((f - i) * 256) (8 fractional bits, ufixedpoint16), of i
+ *     = 256 minus that; coordinates left of the image take pixel 0, right of it the last
+ *     pixel; horizontal sums c0 a + c1 b (16 bit), vertical (h0 c0 + h1 c1 + 2^15) >> 16.
+ *   - GaussianBlur: ORB blurs a submatrix of its bordered pyramid image without
+ *     BORDER_ISOLATED, which routes 8U through sepFilter2D with the float kernel (the
+ *     bit-exact fixed-point path requires an isolated source); kernel =
+ *     getGaussianKernel(7, 2, CV_32F) = getGaussianKernelBitExact rounded to float; row
+ *     pass s = k0 x0 + k1 x1 + ... + k6 x6 (float, left to right), column pass (symmetric
+ *     filter) s = k3 c + k4 (u1 + d1) + k5 (u2 + d2) + k6 (u3 + d3), cvRound (half to
+ *     even), saturated to 8 bits; the level's border is REFLECT_101 (its copyMakeBorder).
+ * PARITY UNPINNED against OpenCV itself; the remaining deviations (the point pattern
+ * of makeRandomPattern rather than the bit_pattern_31_ table, which is not available
+ * here -- loadable through MLGATE_ORB_PATTERN --; ties in retainBest ordered by
+ * (response desc, y, x) where OpenCV leaves nth_element order; OpenCV's SIMD builds may
+ * fuse the blur's multiply-adds, which moves a sum by <= 1 ulp before the rounding) are
+ * shared with the HIP path (csrc/orb.hip), which this file pins bit for bit.
  *
  * The per-frame geometry (level sizes and scales, features per level, pattern, umax,
  * Gaussian coefficients) is computed once by the caller (mlgate/orb.py) and passed in.
@@ -29,7 +43,48 @@
 
 #define CV_PI 3.1415926535897932384626433832795
 
-int orc_resize_linear_u8(const uint8_t *src, int H, int W, int C, uint8_t *dst, int DH, int DW);
+/* INTER_LINEAR_EXACT weights along one axis: source index of the left tap and the
+   8-bit weight of the right tap (0 where the coordinate is clamped). */
+static void exact_axis(int dsize, int ssize, int *ofs, int *c1) {
+    const double inv = (double)dsize / (double)ssize, scale = 1.0 / inv;
+    for (int d = 0; d < dsize; ++d) {
+        const double f = scale * ((double)d + 0.5) - 0.5;
+        const int i = (int)floor(f);
+        if (i < 0 || ssize <= 1) {
+            ofs[d] = 0;
+            c1[d] = 0;
+        } else if (i >= ssize - 1) {
+            ofs[d] = ssize - 1;
+            c1[d] = 0;
+        } else {
+            ofs[d] = i;
+            c1[d] = (int)nearbyint((f - (double)i) * 256.0);
+        }
+    }
+}
+
+/* cv::resize(src, dst, Size(DW, DH), 0, 0, INTER_LINEAR_EXACT), one 8-bit channel. */
+void orc_resize_exact_u8(const uint8_t *src, int H, int W, uint8_t *dst, int DH, int DW) {
+    int *xo = (int *)malloc(sizeof(int) * DW), *xc = (int *)malloc(sizeof(int) * DW);
+    int *yo = (int *)malloc(sizeof(int) * DH), *yc = (int *)malloc(sizeof(int) * DH);
+    exact_axis(DW, W, xo, xc);
+    exact_axis(DH, H, yo, yc);
+    for (int y = 0; y < DH; ++y) {
+        const int y0 = yo[y], y1 = y0 + 1 < H ? y0 + 1 : y0;
+        const uint32_t cy1 = (uint32_t)yc[y], cy0 = 256u - cy1;
+        for (int x = 0; x < DW; ++x) {
+            const int x0 = xo[x], x1 = x0 + 1 < W ? x0 + 1 : x0;
+            const uint32_t cx1 = (uint32_t)xc[x], cx0 = 256u - cx1;
+            const uint32_t h0 = cx0 * src[(size_t)y0 * W + x0] + cx1 * src[(size_t)y0 * W + x1];
+            const uint32_t h1 = cx0 * src[(size_t)y1 * W + x0] + cx1 * src[(size_t)y1 * W + x1];
+            dst[(size_t)y * DW + x] = (uint8_t)((h0 * cy0 + h1 * cy1 + 32768u) >> 16);
+        }
+    }
+    free(xo);
+    free(xc);
+    free(yo);
+    free(yc);
+}
 
 typedef struct {
     int x, y, level;
@@ -124,19 +179,20 @@ static float ic_angle(const uint8_t *img, int W, int x, int y, const int *umax) 
 
 static int refl(int i, int n) { return i < 0 ? -i : (i >= n ? 2 * n - 2 - i : i); }
 
-static void gauss7(const uint8_t *src, int H, int W, const int *gc, uint8_t *dst) {
-    uint16_t *h = (uint16_t *)malloc(sizeof(uint16_t) * H * W);
+void orc_gauss7(const uint8_t *src, int H, int W, const float *k, uint8_t *dst) {
+    float *h = (float *)malloc(sizeof(float) * H * W);
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
-            int s = 0;
-            for (int k = 0; k < 7; ++k) s += gc[k] * src[y * W + refl(x + k - 3, W)];
-            h[y * W + x] = (uint16_t)s;
+            float s = k[0] * (float)src[y * W + refl(x - 3, W)];
+            for (int t = 1; t < 7; ++t) s = s + k[t] * (float)src[y * W + refl(x + t - 3, W)];
+            h[y * W + x] = s;
         }
     for (int y = 0; y < H; ++y)
         for (int x = 0; x < W; ++x) {
-            uint32_t s = 0;
-            for (int k = 0; k < 7; ++k) s += (uint32_t)gc[k] * h[refl(y + k - 3, H) * W + x];
-            dst[y * W + x] = (uint8_t)((s + 32768u) >> 16);
+            float s = k[3] * h[y * W + x];
+            for (int t = 1; t <= 3; ++t) s = s + k[3 + t] * (h[refl(y + t, H) * W + x] + h[refl(y - t, H) * W + x]);
+            const int v = (int)nearbyintf(s);
+            dst[y * W + x] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
         }
     free(h);
 }
@@ -144,7 +200,7 @@ static void gauss7(const uint8_t *src, int H, int W, const int *gc, uint8_t *dst
 /* One grayscale frame -> keypoints (level-0 coordinates), levels, responses, angles,
    32-byte descriptors; returns the count (<= max_out) or -1. */
 int orc_orb_detect(const uint8_t *gray, int H, int W, int nlev, const int *lw, const int *lh, const float *lscale,
-                   const int *nfeat, const int *pattern, const int *umax, const int *gc, int fast_t, int edge,
+                   const int *nfeat, const int *pattern, const int *umax, const float *gk, int fast_t, int edge,
                    float *kx, float *ky, int *klev, float *kresp, float *kang, uint8_t *kdesc, int max_out) {
     uint8_t **lv = (uint8_t **)calloc(nlev, sizeof(uint8_t *));
     lv[0] = (uint8_t *)malloc((size_t)H * W);
@@ -152,7 +208,7 @@ int orc_orb_detect(const uint8_t *gray, int H, int W, int nlev, const int *lw, c
     if (lw[0] != W || lh[0] != H) return -1;
     for (int l = 1; l < nlev; ++l) {
         lv[l] = (uint8_t *)malloc((size_t)lw[l] * lh[l]);
-        orc_resize_linear_u8(lv[l - 1], lh[l - 1], lw[l - 1], 1, lv[l], lh[l], lw[l]);
+        orc_resize_exact_u8(lv[l - 1], lh[l - 1], lw[l - 1], lv[l], lh[l], lw[l]);
     }
     int out = 0;
     for (int l = 0; l < nlev; ++l) {
@@ -197,7 +253,7 @@ int orc_orb_detect(const uint8_t *gray, int H, int W, int nlev, const int *lw, c
             }
         }
         uint8_t *bl = (uint8_t *)malloc((size_t)w * h);
-        gauss7(img, h, w, gc, bl);
+        orc_gauss7(img, h, w, gk, bl);
         for (int i = 0; i < fin && out < max_out; ++i, ++out) {
             const int x = cs[i].x, y = cs[i].y;
             const float ang = ic_angle(img, w, x, y, umax);

@@ -9,6 +9,7 @@ nlevels 8, edgeThreshold 31, patchSize 31, fastThreshold 20, WTA_K 2, HARRIS_SCO
 and the reference's Python around the two OpenCV calls.
 """
 import ctypes
+import math
 
 import numpy as np
 
@@ -69,13 +70,40 @@ def umax_table(half=PATCH // 2):
     return umax
 
 
-def gauss_coeffs(ksize=7, sigma=2.0):
-    """7-tap Gaussian in 8 fractional bits, summing to exactly 256."""
-    x = np.arange(ksize) - ksize // 2
-    g = np.exp(-(x * x) / (2.0 * sigma * sigma))
-    c = np.rint(g / g.sum() * 256).astype(np.int32)
-    c[ksize // 2] += 256 - int(c.sum())
-    return c
+def gauss_kernel(ksize=7, sigma=2.0):
+    """cv::getGaussianKernel(ksize, sigma, CV_32F) of OpenCV 4.x: getGaussianKernelBitExact
+    (x = 2 i - (n - 1), t_i = exp(x^2 * (-0.125 / sigma^2)), normaliser 1 / (2 sum t_i + 1),
+    centre = the normaliser) rounded to float32."""
+    scale2 = -0.125 / (float(sigma) * float(sigma))
+    n2 = (ksize - 1) // 2
+    vals, s = [], 0.0
+    for i in range(n2):
+        x = 1 - ksize + 2 * i
+        t = math.exp(float(x * x) * scale2)
+        vals.append(t)
+        s += t
+    mul1 = 1.0 / (s * 2.0 + 1.0)
+    k = [mul1] * ksize
+    for i in range(n2):
+        k[i] = k[ksize - 1 - i] = vals[i] * mul1
+    return np.array(k, np.float32)
+
+
+def resize_exact(img, DH, DW):
+    """cv::resize(img, (DW, DH), INTER_LINEAR_EXACT) on one 8-bit channel (orb.c)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.empty((DH, DW), np.uint8)
+    _lib.lib().orc_resize_exact_u8(_lib.ptr(img), img.shape[0], img.shape[1], _lib.ptr(out), DH, DW)
+    return out
+
+
+def blur(img):
+    """ORB's GaussianBlur(7x7, 2, 2, BORDER_REFLECT_101) of one level (orb.c)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.empty_like(img)
+    k = gauss_kernel()
+    _lib.lib().orc_gauss7(_lib.ptr(img), img.shape[0], img.shape[1], _lib.ptr(k), _lib.ptr(out))
+    return out
 
 
 def gray(img):
@@ -94,13 +122,13 @@ def detect_and_compute(gray_img, nfeatures, pattern=None):
     H, W = g.shape
     scales, ws, hs, per = level_geometry(H, W, nfeatures)
     pat = np.ascontiguousarray(random_pattern() if pattern is None else pattern, np.int32)
-    um, gc = umax_table(), gauss_coeffs()
+    um, gk = umax_table(), gauss_kernel()
     cap = int(per.sum()) * 4 + 64
     kx, ky, kr, ka = (np.zeros(cap, np.float32) for _ in range(4))
     kl = np.zeros(cap, np.int32)
     kd = np.zeros((cap, 32), np.uint8)
     p = _lib.ptr
-    n = _lib.lib().orc_orb_detect(p(g), H, W, NLEVELS, p(ws), p(hs), p(scales), p(per), p(pat), p(um), p(gc),
+    n = _lib.lib().orc_orb_detect(p(g), H, W, NLEVELS, p(ws), p(hs), p(scales), p(per), p(pat), p(um), p(gk),
                                   FAST_T, EDGE, p(kx), p(ky), p(kl), p(kr), p(ka), p(kd), cap)
     assert n >= 0
     return np.stack([kx[:n], ky[:n]], 1), kl[:n], kr[:n], ka[:n], kd[:n]

@@ -74,6 +74,13 @@ def interpolate_pos_embed(pos_embed, grid):
 @torch.no_grad()
 def forward_tokens(x, sd):
     """get_intermediate_layers(x, n=1, norm=True)[0]: [B, 3, S, S] -> [B, (S/14)^2, 768]."""
+    return forward_tokens_with_cls(x, sd)[:, 1:]
+
+
+@torch.no_grad()
+def forward_tokens_with_cls(x, sd):
+    """The hub forward through the final LayerNorm, CLS kept: [B, 1 + (S/14)^2, 768]
+    (SALAD's DINOv2 backbone with norm_layer / return_token)."""
     B, _, S, _ = x.shape
     grid = S // PATCH
     t = F.conv2d(x, _t(sd, "patch_embed.proj.weight"), _t(sd, "patch_embed.proj.bias"), stride=PATCH)
@@ -97,8 +104,7 @@ def forward_tokens(x, sd):
         h = F.gelu(F.linear(h, _t(sd, p + "mlp.fc1.weight"), _t(sd, p + "mlp.fc1.bias")))
         h = F.linear(h, _t(sd, p + "mlp.fc2.weight"), _t(sd, p + "mlp.fc2.bias"))
         t = t + h * _t(sd, p + "ls2.gamma")
-    t = F.layer_norm(t, (EMBED,), _t(sd, "norm.weight"), _t(sd, "norm.bias"), eps=1e-6)
-    return t[:, 1:]
+    return F.layer_norm(t, (EMBED,), _t(sd, "norm.weight"), _t(sd, "norm.bias"), eps=1e-6)
 
 
 def gem(features, p=3.0):

@@ -30,10 +30,9 @@ def test_product_geometry_equals_oracle():
         scales, ws, hs, per = oorb.level_geometry(H, W, n)
         assert ip[:8].tolist() == ws.tolist() and ip[8:16].tolist() == hs.tolist()
         assert ip[16:24].tolist() == per.tolist()
-        assert np.array_equal(sc, scales)
-        assert ip[32:48].tolist() == oorb.umax_table()[:16].tolist()
-        assert ip[48:55].tolist() == oorb.gauss_coeffs().tolist()
-        assert ip[55:].tolist() == [20, 31]
+        assert np.array_equal(sc[:8], scales) and np.array_equal(sc[8:], oorb.gauss_kernel())
+        assert ip[24:40].tolist() == oorb.umax_table()[:16].tolist()
+        assert ip[40:].tolist() == [20, 31]
     assert np.array_equal(porb.random_pattern().astype(np.int32), oorb.random_pattern())
 
 
@@ -46,7 +45,83 @@ def test_pattern_and_umax():
     assert pat[0, 0] == (s & 0xFFFFFFFF) % 31 - 15
     um = oorb.umax_table()
     assert um[0] == 15 and um[15] == 3 and (np.diff(um[:16]) <= 0).all()
-    assert oorb.gauss_coeffs().sum() == 256
+    k = oorb.gauss_kernel().astype(np.float64)
+    assert abs(k.sum() - 1) < 1e-6 and np.array_equal(k, k[::-1]) and k.argmax() == 3
+
+
+def test_gauss_kernel_is_opencv_bitexact_kernel():
+    """getGaussianKernelBitExact(7, 2) in float64 rounded to float32; the taps are the
+    sigma-2 Gaussian normalised to sum 1 (the old per-tap float path agrees to 1 ulp)."""
+    x = np.arange(7) - 3.0
+    g = np.exp(-x * x / 8.0)
+    k = oorb.gauss_kernel()
+    assert k.dtype == np.float32
+    assert np.allclose(k, g / g.sum(), rtol=2e-7, atol=0)
+    assert k[3] == np.float32(1.0 / (2 * g[:3].sum() + 1.0))
+
+
+def _resize_exact_py(src, DH, DW):
+    """INTER_LINEAR_EXACT on 8U restated with Python ints / floats (resize_bitExact)."""
+    H, W = src.shape
+
+    def axis(d, dsize, ssize):
+        scale = 1.0 / (dsize / ssize)
+        f = scale * (d + 0.5) - 0.5
+        i = int(np.floor(f))
+        if i < 0 or ssize <= 1:
+            return 0, 0
+        if i >= ssize - 1:
+            return ssize - 1, 0
+        return i, int(round((f - i) * 256.0))  # Python round: half to even, as cvRound
+
+    out = np.zeros((DH, DW), np.uint8)
+    for y in range(DH):
+        y0, cy1 = axis(y, DH, H)
+        y1 = min(y0 + 1, H - 1)
+        for x in range(DW):
+            x0, cx1 = axis(x, DW, W)
+            x1 = min(x0 + 1, W - 1)
+            h0 = (256 - cx1) * int(src[y0, x0]) + cx1 * int(src[y0, x1])
+            h1 = (256 - cx1) * int(src[y1, x0]) + cx1 * int(src[y1, x1])
+            out[y, x] = (h0 * (256 - cy1) + h1 * cy1 + 32768) >> 16
+    return out
+
+
+def _blur_py(img, k):
+    """sepFilter2D(8U, float kernel) with REFLECT_101 restated in numpy float32."""
+    H, W = img.shape
+    k = k.astype(np.float32)
+    xs = np.abs(np.arange(-3, W + 3))
+    xs = np.where(xs >= W, 2 * W - 2 - xs, xs)
+    src = img.astype(np.float32)
+    h = k[0] * src[:, xs[0:W]]
+    for t in range(1, 7):
+        h = h + k[t] * src[:, xs[t:t + W]]
+    ys = np.abs(np.arange(-3, H + 3))
+    ys = np.where(ys >= H, 2 * H - 2 - ys, ys)
+    s = k[3] * h
+    for t in range(1, 4):
+        s = s + k[3 + t] * (h[ys[3 + t:3 + t + H]] + h[ys[3 - t:3 - t + H]])
+    return np.clip(np.rint(s), 0, 255).astype(np.uint8)
+
+
+def test_pyramid_and_blur_restated_twice():
+    """The C oracle's INTER_LINEAR_EXACT pyramid and float GaussianBlur equal the Python
+    restatements above on a frame where every level and the borders are exercised."""
+    rng = np.random.default_rng(7)
+    img = rng.integers(0, 256, (61, 83), dtype=np.uint8)
+    img[10:30, 20:50] = 200
+    scales, ws, hs, _ = oorb.level_geometry(61, 83, 500)
+    prev = img
+    k = oorb.gauss_kernel()
+    for l in range(1, 4):
+        cur = _resize_exact_py(prev, int(hs[l]), int(ws[l]))
+        assert np.array_equal(cur, oorb.resize_exact(prev, int(hs[l]), int(ws[l]))), l
+        assert np.array_equal(_blur_py(cur, k), oorb.blur(cur)), l
+        prev = cur
+    # upscale edges clamp to the first / last pixel
+    tiny = np.array([[0, 100], [200, 255]], np.uint8)
+    assert np.array_equal(_resize_exact_py(tiny, 4, 4), oorb.resize_exact(tiny, 4, 4))
 
 
 def _fast_slow(img, x, y, t):
