@@ -192,8 +192,11 @@ int mlg_op_gemm_bias_gelu(const uint16_t* A, const uint16_t* W, const float* bia
 int mlg_op_gemm_residual(const uint16_t* A, const uint16_t* W, const float* bias, const float* gamma, float* X,
                          int M, int N, int K, void* stream);
 int mlg_op_layernorm_bf16(const float* X, const float* g, const float* b, uint16_t* Y, int M, void* stream);
+/* ViT attention (hub Attention.forward, 12 heads x 64) on the pipelined tile: Q, K bf16
+ * [12][B * Tpad][64], Vt bf16 [12][B * Tpad / 64][64 d][64 keys] (keys >= T finite), O bf16
+ * [B * T][768]; task_ws: 5 * B int32 of device scratch. */
 int mlg_op_attention(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, uint16_t* O, int B, int T, int Tpad,
-                     void* stream);
+                     int32_t* task_ws, void* stream);
 /* Ragged multi-head attention (LightGlue self / cross, geometric_verification.py:263-312
  * via upstream SelfBlock / CrossBlock).  Task t = int32 x4 (q_off, q_len, kv_off, kv_len)
  * over a flat token layout; Q, K bf16 [heads][Npad][64] (Q pre-scaled by 1/8 is NOT

@@ -26,7 +26,8 @@ struct VitGeom {
 struct VitWorkspace {
     bf16_t *patches, *xn, *q, *k, *vt, *o, *h;
     float *x, *partial;
-    size_t vt_bytes;
+    int32_t* tasks;  // attention tasks + output offsets, 5 * B int32
+    size_t q_bytes, vt_bytes;
 };
 
 size_t carve(const VitGeom& g, char* base, VitWorkspace* ws) {
@@ -42,13 +43,15 @@ size_t carve(const VitGeom& g, char* base, VitWorkspace* ws) {
     w.patches = (bf16_t*)take((size_t)g.B * g.P * MLG_VIT_PATCH_K * 2);
     w.x = (float*)take(rows * 768 * 4);
     w.xn = (bf16_t*)take(rows * 768 * 2);
-    w.q = (bf16_t*)take(heads * g.Tpad * 64 * 2);
+    w.q_bytes = heads * g.Tpad * 64 * 2;
+    w.q = (bf16_t*)take(w.q_bytes);
     w.k = (bf16_t*)take(heads * g.Tpad * 64 * 2);
     w.vt_bytes = heads * 64 * g.Tpad * 2;
     w.vt = (bf16_t*)take(w.vt_bytes);
     w.o = (bf16_t*)take(rows * 768 * 2);
     w.h = (bf16_t*)take(rows * 3072 * 2);
     w.partial = (float*)take(mlg_gem_partial_bytes(g.B));
+    w.tasks = (int32_t*)take((size_t)g.B * 5 * 4);
     if (ws) *ws = w;
     return off;
 }
@@ -135,8 +138,10 @@ static int vit_trunk(const mlg_vit_weights* w, const uint8_t* frames, const VitG
     TRY(mlg_preprocess_patches(frames, g.B, H, W, C, frame_stride, g.S, MLG_VIT_PATCH_K, swap_rb, ws.patches, s));
     TRY(mlg_gemm_patch(ws.patches, w->patch_w, w->patch_b, w->pos, ws.x, g.B * g.P, g.P, MLG_VIT_PATCH_K, s));
     TRY(mlg_cls_rows(ws.x, w->cls, w->pos, g.B, g.T, s));
-    // padded key columns of V^T must be finite: masked keys multiply them by p = 0
+    // padded key columns of V^T must be finite (masked keys multiply them by p = 0); padded
+    // query rows are never stored but are zeroed too, so no lane computes on stale bits
     if (hipMemsetAsync(ws.vt, 0, ws.vt_bytes, s) != hipSuccess) return MLG_EHIP;
+    if (hipMemsetAsync(ws.q, 0, ws.q_bytes, s) != hipSuccess) return MLG_EHIP;
 
     for (int l = 0; l < MLG_VIT_DEPTH; ++l) {
         const mlg_vit_block& bl = w->blocks[l];
@@ -147,7 +152,7 @@ static int vit_trunk(const mlg_vit_weights* w, const uint8_t* frames, const VitG
         }
         {
             MlgProfScope p(4, s, 4.0 * g.B * 12 * (double)g.T * g.T * 64);
-            TRY(mlg_attention(ws.q, ws.k, ws.vt, ws.o, g.B, g.T, g.Tpad, s));
+            TRY(mlg_attention(ws.q, ws.k, ws.vt, ws.o, g.B, g.T, g.Tpad, ws.tasks, s));
         }
         {
             MlgProfScope p(3, s, 2.0 * M * 768 * 768);
@@ -472,8 +477,8 @@ int mlg_op_layernorm_bf16(const float* X, const float* g, const float* b, uint16
     return mlg_layernorm_bf16(X, g, b, Y, M, (hipStream_t)stream);
 }
 int mlg_op_attention(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, uint16_t* O, int B, int T, int Tpad,
-                     void* stream) {
-    return mlg_attention(Q, K, Vt, O, B, T, Tpad, (hipStream_t)stream);
+                     int32_t* task_ws, void* stream) {
+    return mlg_attention(Q, K, Vt, O, B, T, Tpad, task_ws, (hipStream_t)stream);
 }
 int mlg_op_attention_varlen(const uint16_t* Q, const uint16_t* K, const uint16_t* Vt, uint16_t* O, int ldo, int Npad,
                             int heads, const int32_t* tasks, const int32_t* out_off, int ntasks, int max_q,

@@ -1,19 +1,19 @@
-// Fused multi-head self-attention for ViT-B/14 (12 heads x 64, T = 530 tokens at 322^2).
+// Fused multi-head attention on gfx950: one software-pipelined tile (k_attention_varlen)
+// serves the ViT-B/14 (12 heads x 64, T = 530 tokens at 322^2; hub Attention.forward
+//   O[b, t, h*64 + d] = softmax_k( q_t . k_k / 8 ) . v_k )
+// and LightGlue's ragged self / cross attention (4 heads x 64).
 //
-//   O[b, t, h*64 + d] = softmax_k( q_t . k_k / 8 ) . v_k         (hub Attention.forward)
-//
-// One workgroup = 4 waves = 128 query rows of one (image, head); each wave owns 32
-// query rows and streams the keys in blocks of 64 with an online softmax.
 // Scores are computed transposed, S^T = K . Q^T, with v_mfma_f32_32x32x16_bf16 so
 // that a lane owns one query column: the softmax row statistics are lane-local plus
 // one cross-half exchange, and the S^T accumulator feeds the next MFMA directly as
 // its B operand (O^T = V^T . P^T) with no LDS round trip.  O^T keeps the query on
 // the lane too, so the online-softmax rescale is lane-local.
 //
-// Layouts (written by the QKV GEMM epilogue, gemm_bf16.hip EpiQKV):
-//   Q, K : bf16 [B, 12, Tpad, 64];   Vt : bf16 [B, 12, 64, Tpad]  (V transposed)
-//   rows/cols T..Tpad-1 must be finite (zeroed once at workspace creation).
-// Q is pre-scaled by 1/8 (exact in bf16).  Output O: bf16 [B*T, 768].
+// Layouts (ViT: written by the QKV GEMM epilogue, gemm_bf16.hip EpiQKV; one task per
+// image over the segment b * Tpad of every head):
+//   Q, K : bf16 [heads][Npad][64];   Vt : bf16 [heads][Npad / 64][64 d][64 keys]
+//   V^T columns of keys >= T must be finite (zeroed per forward); keys >= T are masked.
+// Output O: bf16 rows of ldo elements, head h at column h * 64.
 #include "common.h"
 #include "kernels.h"
 
@@ -31,176 +31,6 @@ __device__ __forceinline__ int k_off(int key, int chunk) {  // K image [key][d],
 // ds_read2st64_b64 (which banks mod 32 dwords and would 2-way conflict).
 __device__ __forceinline__ int v_off(int d, int gran) {
     return d * 128 + ((gran ^ (((d >> 1) ^ (d >> 5)) & 15)) << 3);
-}
-
-// One (image, head, 128-query block) tile.  Qh / Kh: [rows][64] of this head; Vh: the
-// V^T rows [64][vstride] of this head; T keys; nq query rows (rows nq..qpad-1 must be
-// finite); output row r goes to orow + r * ldo.
-template <bool VTILED>
-__device__ __forceinline__ void attention_tile(char* smem, const bf16_t* __restrict__ Qh,
-                                               const bf16_t* __restrict__ Kh, const bf16_t* __restrict__ Vh,
-                                               int vstride, int T, int nq, int qmax, int qblock,
-                                               bf16_t* __restrict__ orow, int ldo) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, col = lane & 31;
-    const int Tpad = vstride;
-    const int qrow = qblock * 128 + wave * 32 + col;
-    const int qld = min(qrow, qmax - 1);
-    bf16x8 qf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        bf16x8 v = *reinterpret_cast<const bf16x8*>(Qh + (size_t)qld * 64 + s * 16 + hh * 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)  // x 1/8: exponent - 3 (exact; zero / subnormal-free inputs)
-            v[j] = (short)f32_to_bf16(bf16_to_f32((bf16_t)v[j]) * 0.125f);
-        qf[s] = v;
-    }
-
-    // staging: K block 64 x 8 chunks, V^T block 64 x 8 chunks -> 2 + 2 per thread
-    // staging: thread -> (row tid>>3 and tid>>3 + 32, 16-B chunk tid&7) of the K block
-    // [key][d] and of the V^T block [d][key]
-    const int srow = tid >> 3, sch = tid & 7;
-    const int sk0 = k_off(srow, sch), sk1 = k_off(srow + 32, sch);
-    const int sv0a = v_off(srow, 2 * sch), sv0b = v_off(srow, 2 * sch + 1);
-    const int sv1a = v_off(srow + 32, 2 * sch), sv1b = v_off(srow + 32, 2 * sch + 1);
-    uint4 rk0, rk1, rv0, rv1;
-#define ATT_GLOAD(kb)                                                                        \
-    {                                                                                        \
-        rk0 = *reinterpret_cast<const uint4*>(Kh + (size_t)((kb) + srow) * 64 + sch * 8);      \
-        rk1 = *reinterpret_cast<const uint4*>(Kh + (size_t)((kb) + srow + 32) * 64 + sch * 8); \
-        if (VTILED) {  /* [key block][64 d][64 keys]: one contiguous 8 KB tile per block */     \
-            const bf16_t* vb_ = Vh + (size_t)((kb) >> 6) * 4096 + sch * 8;                    \
-            rv0 = *reinterpret_cast<const uint4*>(vb_ + srow * 64);                            \
-            rv1 = *reinterpret_cast<const uint4*>(vb_ + (srow + 32) * 64);                     \
-        } else {                                                                               \
-            rv0 = *reinterpret_cast<const uint4*>(Vh + (size_t)srow * Tpad + (kb) + sch * 8);  \
-            rv1 = *reinterpret_cast<const uint4*>(Vh + (size_t)(srow + 32) * Tpad + (kb) + sch * 8); \
-        }                                                                                      \
-    }
-#define ATT_LSTORE(buf)                                                                      \
-    {                                                                                        \
-        char* kb_ = smem + (buf) * (KTILE_BYTES + VTILE_BYTES);                              \
-        char* vb_ = kb_ + KTILE_BYTES;                                                       \
-        *reinterpret_cast<uint4*>(kb_ + sk0) = rk0;                                          \
-        *reinterpret_cast<uint4*>(kb_ + sk1) = rk1;                                          \
-        *reinterpret_cast<uint2*>(vb_ + sv0a) = make_uint2(rv0.x, rv0.y);                    \
-        *reinterpret_cast<uint2*>(vb_ + sv0b) = make_uint2(rv0.z, rv0.w);                    \
-        *reinterpret_cast<uint2*>(vb_ + sv1a) = make_uint2(rv1.x, rv1.y);                    \
-        *reinterpret_cast<uint2*>(vb_ + sv1b) = make_uint2(rv1.z, rv1.w);                    \
-    }
-
-    f32x16 o[2];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { o[0][i] = 0.f; o[1][i] = 0.f; }
-    float mrun = -INFINITY, lrun = 0.f;
-
-    const int nkb = (T + KB - 1) / KB;
-    ATT_GLOAD(0);
-    ATT_LSTORE(0);
-    __syncthreads();
-    int cur = 0;
-    for (int kb = 0; kb < nkb; ++kb) {
-        if (kb + 1 < nkb) { ATT_GLOAD((kb + 1) * KB); }
-        const char* kbase = smem + cur * (KTILE_BYTES + VTILE_BYTES);
-        const char* vbase = kbase + KTILE_BYTES;
-
-        // S^T tiles: keys kt*32 .. +32 of this block  x  this wave's 32 queries
-        f32x16 s[2];
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) s[kt][i] = 0.f;
-#pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kbase + k_off(kt * 32 + col, 2 * st + hh));
-                s[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[st], s[kt], 0, 0, 0);
-            }
-        }
-        // mask keys >= T, block max
-        float bm = -INFINITY;
-        const int key0 = kb * KB;
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int key = key0 + kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                if (key >= T) s[kt][r] = -INFINITY;
-                bm = fmaxf(bm, s[kt][r]);
-            }
-        bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-        const float mnew = fmaxf(mrun, bm);
-        const float alpha = __expf(mrun - mnew);
-        float ps = 0.f;
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float p = __expf(s[kt][r] - mnew);
-                s[kt][r] = p;
-                ps += p;
-            }
-        ps += __shfl_xor(ps, 32, 64);
-        lrun = lrun * alpha + ps;
-        mrun = mnew;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { o[0][i] *= alpha; o[1][i] *= alpha; }
-
-        // O^T += V^T . P^T : B operand = P from the S^T registers (8s .. 8s+7 -> k-step s)
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int st = 0; st < 2; ++st) {
-                bf16x8 pf;
-#pragma unroll
-                for (int j = 0; j < 8; j += 2) {
-                    const uint32_t w = pack_bf16x2(s[kt][8 * st + j], s[kt][8 * st + j + 1]);
-                    pf[j] = (short)(w & 0xffff);
-                    pf[j + 1] = (short)(w >> 16);
-                }
-                const int g0 = kt * 8 + st * 4 + hh;  // 8-B granule of keys 16st + 4hh .. +3
-#pragma unroll
-                for (int dt = 0; dt < 2; ++dt) {
-                    const int d = dt * 32 + col;
-                    const uint2 lo = *reinterpret_cast<const uint2*>(vbase + v_off(d, g0));
-                    const uint2 hi = *reinterpret_cast<const uint2*>(vbase + v_off(d, g0 + 2));
-                    bf16x8 vf;
-                    vf[0] = (short)(lo.x & 0xffff); vf[1] = (short)(lo.x >> 16);
-                    vf[2] = (short)(lo.y & 0xffff); vf[3] = (short)(lo.y >> 16);
-                    vf[4] = (short)(hi.x & 0xffff); vf[5] = (short)(hi.x >> 16);
-                    vf[6] = (short)(hi.y & 0xffff); vf[7] = (short)(hi.y >> 16);
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
-                }
-            }
-        if (kb + 1 < nkb) { ATT_LSTORE(cur ^ 1); }
-        __syncthreads();
-        cur ^= 1;
-    }
-
-    if (qrow < nq) {
-        const float inv = 1.0f / lrun;
-        bf16_t* out = orow + (size_t)qrow * ldo;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int d = dt * 32 + 8 * g + 4 * hh;
-                uint2 w;
-                w.x = pack_bf16x2(o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv);
-                w.y = pack_bf16x2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-                *reinterpret_cast<uint2*>(out + d) = w;
-            }
-    }
-#undef ATT_GLOAD
-#undef ATT_LSTORE
-}
-
-__global__ __launch_bounds__(256, 2) void k_attention(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
-                                                      const bf16_t* __restrict__ Vt, bf16_t* __restrict__ O, int T,
-                                                      int Tpad) {
-    __shared__ __attribute__((aligned(16))) char smem[2 * (KTILE_BYTES + VTILE_BYTES)];
-    const int h = blockIdx.y, b = blockIdx.z;
-    const size_t head = (size_t)b * 12 + h;
-    attention_tile<false>(smem, Q + head * Tpad * 64, K + head * Tpad * 64, Vt + head * 64 * Tpad, Tpad, T, T, Tpad,
-                   blockIdx.x, O + (size_t)b * T * 768 + h * 64, 768);
 }
 
 // Software-pipelined wide tile for the ragged (LightGlue) path: one workgroup = 4 waves
@@ -234,8 +64,16 @@ __device__ __forceinline__ float swap_sum(float v) {
 // operand it did not produce, so per-instruction statements or fmaxf on the swap results
 // cost as much again as the maxima.  The two chains interleave; `s_nop 1`: the VALU-write
 // -> permlane32_swap-read wait states.  Scores are finite or -inf.
-__device__ __forceinline__ void block_max2(const f32x16 (&v)[2], float (&m)[2]) {
+// The scores are MFMA results read by the asm: an XDL write -> VALU read needs 12 wait
+// states after an 8-pass v_mfma_f32_32x32x16_bf16, and hipcc inserts none for a consumer
+// inside an asm string.  Wherever the scheduler put the producing MFMAs close to this
+// read, the max came from accumulators not yet written, on some waves, under load: up to
+// ~0.1 % of output rows differed run to run (tools/attn_det_probe.py, 0 with the pad;
+// the pad costs ~0.8 % of the tile's time).  The pad is tied to the inputs so it sits
+// between their producers and this read.
+__device__ __forceinline__ void block_max2(f32x16 (&v)[2], float (&m)[2]) {
     float a, b, t0, t1;
+    asm volatile("s_nop 11" : "+v"(v[0][15]), "+v"(v[1][15]));
     asm("v_max3_f32 %0, %4, %5, %6\n\t"
         "v_max3_f32 %1, %20, %21, %22\n\t"
         "v_max3_f32 %0, %0, %7, %8\n\t"
@@ -542,15 +380,25 @@ __global__ __launch_bounds__(256, 1) void k_attention_varlen(const bf16_t* __res
                         ldo);
 }
 
+// ViT tasks: image b attends its own segment [b * Tpad, b * Tpad + T) in every head;
+// output rows b * T ..
+__global__ void k_vit_tasks(int4* __restrict__ tasks, int* __restrict__ out_off, int B, int T, int Tpad) {
+    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+        tasks[b] = make_int4(b * Tpad, T, b * Tpad, T);
+        out_off[b] = b * T;
+    }
+}
+
 }  // namespace
 
 int mlg_attention(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int B, int T, int Tpad,
-                  hipStream_t s) {
-    if (B <= 0 || T <= 0 || Tpad < ((T + KB - 1) / KB) * KB || (Tpad % 8)) return MLG_EINVAL;
-    dim3 grid((T + 127) / 128, 12, B);
-    hipLaunchKernelGGL(k_attention, grid, dim3(256), 0, s, Q, K, Vt, O, T, Tpad);
+                  int32_t* task_ws, hipStream_t s) {
+    if (B <= 0 || T <= 0 || Tpad % 64 || Tpad < T || !task_ws || (long)B * Tpad * 64 >= (1L << 31)) return MLG_EINVAL;
+    int4* tasks = reinterpret_cast<int4*>(task_ws);
+    int* out_off = task_ws + 4 * B;
+    hipLaunchKernelGGL(k_vit_tasks, dim3(1), dim3(256), 0, s, tasks, out_off, B, T, Tpad);
     MLG_LAUNCH_CHECK();
-    return MLG_OK;
+    return mlg_attention_varlen(Q, K, Vt, O, 768, B * Tpad, 12, tasks, out_off, B, T, s);
 }
 
 int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,

@@ -105,30 +105,29 @@ struct EpiResidual {  // X += gamma * (acc + b)   (attn.proj / mlp.fc2 + LayerSc
     }
 };
 
-struct EpiQKV {  // qkv -> Q, K bf16 [B, 12, Tpad, 64] and V^T bf16 [B, 12, 64, Tpad]
-    bf16_t* Q; bf16_t* K; bf16_t* Vt; const float* bias; int T, Tpad;
+// qkv -> Q, K bf16 [12][B * Tpad][64] and V^T bf16 tiled [12][B * Tpad / 64][64 d][64 keys]
+// (the layouts k_attention_varlen reads; image b is the segment b * Tpad of each head)
+struct EpiQKV {
+    bf16_t* Q; bf16_t* K; bf16_t* Vt; const float* bias; int T, Tpad, Np;
     __device__ void operator()(int m, int n, const f32x4& v) const {
         const float4 b = *reinterpret_cast<const float4*>(bias + n);
         const int bi = m / T, t = m - bi * T;
         const int which = n / 768, c = n - which * 768, h = c >> 6, d = c & 63;
-        const size_t head = (size_t)bi * 12 + h;
+        const size_t key = (size_t)bi * Tpad + t;
         if (which < 2) {
             uint2 o;
             o.x = pack_bf16x2(v[0] + b.x, v[1] + b.y);
             o.y = pack_bf16x2(v[2] + b.z, v[3] + b.w);
-            *reinterpret_cast<uint2*>((which == 0 ? Q : K) + (head * Tpad + t) * 64 + d) = o;
-        } else {  // transposed so attention streams V^T rows (key-contiguous)
-            bf16_t* p = Vt + (head * 64 + d) * Tpad + t;
+            *reinterpret_cast<uint2*>((which == 0 ? Q : K) + ((size_t)h * Np + key) * 64 + d) = o;
+        } else {  // transposed per 64-key block so attention streams V^T rows (key-contiguous)
+            bf16_t* p = Vt + (((size_t)h * (Np >> 6) + (key >> 6)) * 64 + d) * 64 + (key & 63);
             p[0] = f32_to_bf16(v[0] + b.x);
-            p[Tpad] = f32_to_bf16(v[1] + b.y);
-            p[2 * Tpad] = f32_to_bf16(v[2] + b.z);
-            p[3 * Tpad] = f32_to_bf16(v[3] + b.w);
+            p[64] = f32_to_bf16(v[1] + b.y);
+            p[128] = f32_to_bf16(v[2] + b.z);
+            p[192] = f32_to_bf16(v[3] + b.w);
         }
     }
 };
-
-
-
 
 // relu(acc + b) -> bf16, columns >= nvalid dropped (N padded to the tile width)
 struct EpiBiasReluBF16 {
@@ -928,8 +927,8 @@ int mlg_gemm_residual(const bf16_t* A, const bf16_t* W, const float* bias, const
 }
 int mlg_gemm_qkv(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* Q, bf16_t* Kh, bf16_t* V, int M,
                  int T, int Tpad, hipStream_t s) {
-    if (M % T) return MLG_EINVAL;
-    return launch(A, W, M, 3 * 768, 768, 768, 768, EpiQKV{Q, Kh, V, bias, T, Tpad}, s);
+    if (M % T || Tpad % 64 || Tpad < T) return MLG_EINVAL;
+    return launch(A, W, M, 3 * 768, 768, 768, 768, EpiQKV{Q, Kh, V, bias, T, Tpad, (M / T) * Tpad}, s);
 }
 int mlg_gemm_patch(const bf16_t* A, const bf16_t* W, const float* bias, const float* pos, float* X, int M, int P,
                    int Kpad, hipStream_t s) {

@@ -63,8 +63,10 @@ int mlg_gemm_patch(const bf16_t* A, const bf16_t* W, const float* bias, const fl
                    int Kpad, hipStream_t s);
 
 // attention.hip
+// ViT self-attention through k_attention_varlen (Q, K [12][B * Tpad][64], V^T tiled
+// [12][B * Tpad / 64][64][64], O [B * T][768]); task_ws: 5 * B int32 of device memory
 int mlg_attention(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int B, int T, int Tpad,
-                  hipStream_t s);
+                  int32_t* task_ws, hipStream_t s);
 
 // vit_ops.hip
 int mlg_preprocess_patches(const uint8_t* img, int B, int H, int W, int C, long img_stride, int S, int Kpad,

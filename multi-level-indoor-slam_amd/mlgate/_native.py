@@ -79,7 +79,7 @@ EXPORTS = {
     "mlg_op_gemm_residual": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                      c_void_p]),
     "mlg_op_layernorm_bf16": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
-    "mlg_op_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mlg_op_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "mlg_op_attention_varlen": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                                         c_void_p, c_int, c_int, c_void_p]),
     "mlg_op_lg_ffn": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int] + [c_void_p] * 8 + [c_void_p]),

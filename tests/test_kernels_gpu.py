@@ -105,15 +105,18 @@ def test_attention(dev, B, T):
     g = torch.Generator().manual_seed(T)
     q, k, v = (torch.randn(B, 12, T, 64, generator=g) * 1.5 for _ in range(3))
     q, k, v = (bf16_bits(x) for x in (q, k, v))
-    Qd = torch.zeros(B, 12, Tpad, 64, dtype=torch.bfloat16)
-    Kd = torch.zeros(B, 12, Tpad, 64, dtype=torch.bfloat16)
-    Vt = torch.zeros(B, 12, 64, Tpad, dtype=torch.bfloat16)
-    Qd[:, :, :T] = q
-    Kd[:, :, :T] = k
-    Vt[:, :, :, :T] = v.transpose(-1, -2)
+    # head-major segments (image b at rows b * Tpad of each head), V^T tiled per 64 keys
+    Qd = torch.zeros(12, B, Tpad, 64, dtype=torch.bfloat16)
+    Kd = torch.zeros(12, B, Tpad, 64, dtype=torch.bfloat16)
+    Vp = torch.zeros(12, B, Tpad, 64, dtype=torch.bfloat16)
+    Qd[:, :, :T] = q.transpose(0, 1)
+    Kd[:, :, :T] = k.transpose(0, 1)
+    Vp[:, :, :T] = v.transpose(0, 1)
+    Vt = Vp.reshape(12, B * Tpad // 64, 64, 64).transpose(-1, -2).contiguous()
     Qd, Kd, Vt = Qd.to(dev), Kd.to(dev), Vt.to(dev)
     O = torch.empty(B * T, 768, dtype=torch.bfloat16, device=dev)
-    _native.check(_native.lib().mlg_op_attention(P(Qd), P(Kd), P(Vt), P(O), B, T, Tpad, S(dev)), "attn")
+    tw = torch.empty(5 * B, dtype=torch.int32, device=dev)
+    _native.check(_native.lib().mlg_op_attention(P(Qd), P(Kd), P(Vt), P(O), B, T, Tpad, P(tw), S(dev)), "attn")
     a = ((q.float() * 0.125) @ k.float().transpose(-1, -2)).softmax(-1)
     ref = (a @ v.float()).transpose(1, 2).reshape(B * T, 768)
     torch.cuda.synchronize()
