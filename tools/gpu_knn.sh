@@ -1,7 +1,7 @@
 #!/bin/bash
 # kNN: parity tests, timing, rocprof kernel stats and one FETCH_SIZE / WRITE_SIZE pass each
 set -u
-cd "${GRAFT_REPO_ROOT}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/knn
 timeout -k 10 300 python -u -m pytest tests/test_retrieval_gpu.py tests/test_api_gpu.py tests/test_pipeline_gpu.py -m gpu -q -rf --timeout 120 --timeout-method thread > gpurun_out/knn/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/knn/pytest.log
