@@ -47,6 +47,38 @@ __device__ __forceinline__ int cat_off(int row, int chunk) { return row * ROWB +
 
 __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+// The tile's token rows are read once and the residual written once per block: they go
+// through non-temporal (streaming) accesses so they do not evict the block's weights,
+// which every tile of the launch re-reads from L2 (same-box A/B: 385.6 -> 379.6 ms of FFN
+// per 4096-pair call, profiles/r03ac_ab_ffn_nontemporal.txt).
+#ifndef MLG_FFN_NT
+#define MLG_FFN_NT 1
+#endif
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+__device__ __forceinline__ uint4 stream_ld(const uint4* p) {
+#if MLG_FFN_NT
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ float4 stream_ld(const float4* p) {
+#if MLG_FFN_NT
+    const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void stream_st(float4* p, const float4& v) {
+#if MLG_FFN_NT
+    __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(p));
+#else
+    *p = v;
+#endif
+}
+
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 // log(sigmoid(x)) = min(x, 0) - log1p(exp(-|x|))  (torch's stable form)
 __device__ __forceinline__ float logsigmoid_f(float x) { return fminf(x, 0.f) - log1pf(expf(-fabsf(x))); }
@@ -163,8 +195,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             for (int i = 0; i < PASSES; ++i) {
                 const int row = 2 * NW * i + 2 * wave + hh;
                 const size_t gr = (size_t)min(m0 + row, M - 1);
-                rx[i] = *reinterpret_cast<const uint4*>(xcopy + gr * ldc + c * 8);
-                rc[i] = *reinterpret_cast<const uint4*>(ctx + gr * 256 + c * 8);
+                rx[i] = stream_ld(reinterpret_cast<const uint4*>(xcopy + gr * ldc + c * 8));
+                rc[i] = stream_ld(reinterpret_cast<const uint4*>(ctx + gr * 256 + c * 8));
             }
     #pragma unroll
             for (int i = 0; i < PASSES; ++i) {
@@ -299,7 +331,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             float4 xr[R / NW];
     #pragma unroll
             for (int i = 0; i < R / NW; ++i)
-                xr[i] = reinterpret_cast<const float4*>(X + (size_t)min(m0 + wave * (R / NW) + i, M - 1) * 256)[lane];
+                xr[i] = stream_ld(reinterpret_cast<const float4*>(X + (size_t)min(m0 + wave * (R / NW) + i, M - 1) * 256) + lane);
             __builtin_amdgcn_sched_barrier(0);
             f32x16 acc[NT1][MT];
             zero(acc);
@@ -340,7 +372,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                 x.y += y.y;
                 x.z += y.z;
                 x.w += y.w;
-                *px = x;
+                stream_st(px, x);
                 *reinterpret_cast<uint2*>(xcopy + (size_t)m * ldc + 4 * lane) =
                     make_uint2(pack_bf16x2(x.x, x.y), pack_bf16x2(x.z, x.w));
                 if (heads) pz[i] = x.x * wm4.x + x.y * wm4.y + x.z * wm4.z + x.w * wm4.w;
