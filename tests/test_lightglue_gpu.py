@@ -103,7 +103,7 @@ def test_lightglue_empty_side(lg):
 def test_lightglue_against_fp32_reference(dev, lg, sd):
     """The GPU matcher (bf16 GEMM / attention operands) against the reference's arithmetic
     -- the fp32 forward without bf16 emulation -- on SuperPoint features of a synthetic
-    revisit pair (true correspondences): match sets overlap >= 90 %, scores of common
+    revisit pair (true correspondences): match sets overlap >= 99 %, scores of common
     matches within 5e-2."""
     from mlgate import synthetic
     from mlgate.superpoint import SuperPointGPU
@@ -119,7 +119,7 @@ def test_lightglue_against_fp32_reference(dev, lg, sd):
     common = set(g) & set(r)
     overlap = len(common) / max(len(g), len(r), 1)
     print(f"fp32 LightGlue: {len(g)} vs {len(r)} matches, overlap {overlap:.4f}, stop {gstop} vs {ref['stop']}")
-    assert len(r) > 100 and overlap >= 0.90
+    assert len(r) > 100 and overlap >= 0.99  # measured 0.9976 (profiles/r03ae_tolerances.log)
     gi = np.array([g[c] for c in common])
     ri = np.array([r[c] for c in common])
     np.testing.assert_allclose(gs[gi], ref["scores"].numpy()[ri], atol=5e-2)

@@ -11,7 +11,7 @@ Bar (north star: identical false-loop-closure rejection count, identical decisio
     every retrieval decision >= 5e-5 away from a flip);
   * verification: the cross-floor skip and is_valid of every pair identical to the fp32
     chain (SuperPoint + LightGlue fp32, OpenCV's RANSAC loop); inlier counts within
-    15 % of the fp32 chain's (bf16 matches differ from fp32 ones in a few percent);
+    3 % (at least 1) of the fp32 chain's (measured max 1.1 %: bf16 matches differ from fp32 ones);
   * floor gate verdicts and all four terms of the rejection count: identical.
 Three configurations exercise every term: A (retrieval and verifier floor gating on),
 B (retrieval gating off: the verifier skip engages), C (both off: aliased cross-floor
@@ -105,7 +105,10 @@ def test_verification_and_gate_match_oracle(chain, reports, cfg):
             inl_ref.append(int(chain["pair_inliers"][i]))
     inl_got, inl_ref = np.array(inl_got), np.array(inl_ref)
     if len(inl_ref):
-        assert np.all(np.abs(inl_got - inl_ref) <= 0.15 * inl_ref), list(zip(inl_got, inl_ref))
+        rel = np.abs(inl_got - inl_ref) / inl_ref
+        print(f"{cfg}: {len(inl_ref)} valid pairs, inlier |diff| / ref max {rel.max():.4f} mean {rel.mean():.4f}")
+        # measured max 0.011 (profiles/r03ae_tolerances.log): bf16 matches vs the fp32 chain
+        assert np.all(np.abs(inl_got - inl_ref) <= np.maximum(1, 0.03 * inl_ref)), list(zip(inl_got, inl_ref))
     # the gate on the geometrically valid pairs
     ok = [(m.query_idx, m.match_idx) for m, r in zip(rep.verified, rep.results) if r.is_valid]
     gv = chain[f"{cfg}_gate_valid"]

@@ -84,6 +84,28 @@ def test_superglue_matches_oracle(sg, sd, m, n):
         assert len(got_m) >= 0.5 * int(0.6 * min(m, n))  # the shared points are found
 
 
+@pytest.mark.parametrize("m,n", [(700, 650), (2048, 1900)])
+def test_superglue_against_fp32_reference(sg, sd, m, n):
+    """The GPU SuperGlue (bf16 GNN, f32 Sinkhorn) against the float32 restatement
+    (oracle/superglue.py with emulate_bf16=False): match-set overlap and score error."""
+    rng = np.random.default_rng(7 * m + n)
+    case = feats(rng, m, n)
+    got_m, got_s = _run_gpu(sg, [case])[0]
+    rm, rs = Oracle(sd, emulate_bf16=False).match(*case, W, H)
+    g = {tuple(x): i for i, x in enumerate(got_m.tolist())}
+    r = {tuple(x): i for i, x in enumerate(rm.tolist())}
+    common = set(g) & set(r)
+    overlap = len(common) / max(len(g), len(r), 1)
+    err = 0.0
+    if common:
+        gi = np.array([g[c] for c in common], int)
+        ri = np.array([r[c] for c in common], int)
+        err = float(np.abs(got_s[gi] - rs[ri]).max())
+    print(f"fp32 SuperGlue {m}x{n}: {len(g)} vs {len(r)} matches, overlap {overlap:.4f}, max score err {err:.4f}")
+    assert len(r) > 50 and overlap >= 0.99  # measured 1.0000 / 1.0000 (profiles/r03ae_tolerances.log)
+    assert err < 1e-2  # measured 0.0012 / 0.0017
+
+
 def test_superglue_batch_equals_single_and_empty_sides(sg):
     rng = np.random.default_rng(11)
     cases = [feats(rng, 900, 800), feats(rng, 130, 1200), feats(rng, 400, 410)]
