@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--len", type=int, default=2048)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--ragged", action="store_true")
+    ap.add_argument("--clock", type=float, default=0.0,
+                    help="seconds of back-to-back launches, then the in-kernel clock of a "
+                         "tools/clock_probe_build.py library (mlg_probe_clock)")
     ap.add_argument("--exp2", action="store_true",
                     help="q in exp2 units (x log2(e) / 8, as lg_proj writes it for the current kernel)")
     args = ap.parse_args()
@@ -89,6 +92,20 @@ def main():
             got = O[int(outs[ti]):int(outs[ti]) + ql].float().view(ql, H, 64).transpose(0, 1)
             err = max(err, float((got - ref).abs().max()))
         res[kind] = {"ms": round(ms, 3), "tflops": round(flops / ms / 1e9, 1), "max_abs_err": err}
+        if args.clock > 0:
+            import ctypes
+            import time
+            t_end = time.time() + args.clock
+            while time.time() < t_end:
+                for _ in range(10):
+                    run()
+                torch.cuda.synchronize()
+            ghz, n = ctypes.c_double(0.0), ctypes.c_int(0)
+            rc = L.mlg_probe_clock(ctypes.byref(ghz), ctypes.byref(n))
+            res[kind]["clock_ghz"] = round(ghz.value, 3) if rc == 0 else None
+            res[kind]["clock_wgs"] = n.value
+            if rc == 0:  # TFLOP/s per GHz: the issue efficiency with the clock taken out
+                res[kind]["tflops_at_2.4"] = round(flops / ms / 1e9 * 2.4 / ghz.value, 1)
     print(json.dumps(res), flush=True)
 
 
