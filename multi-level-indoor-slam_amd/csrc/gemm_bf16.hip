@@ -823,7 +823,12 @@ __global__ __launch_bounds__(512, 2) void k_conv256(ConvGeom g, const bf16_t* __
 
 // 1: 128x128 register-staged; 2: 128x256 DMA BK=64 (3 stages); 3: 128x256 DMA BK=32 (2 WG/CU);
 // 4: persistent 256x256 DMA where N allows (N % 256 == 0, K / 64 even), else 2.
-int g_variant = 4;
+// Fixed per build (MLG_GEMM_VARIANT; A/B arms are separate builds loaded through
+// tools/ab_run.py) or per process through mlg_gemm_set_variant (tools/gemm_bench.py).
+#ifndef MLG_GEMM_VARIANT
+#define MLG_GEMM_VARIANT 4
+#endif
+int g_variant = MLG_GEMM_VARIANT;
 int g_num_cus = 256;  // multiple of 8 (refreshed from the device on first use)
 
 int num_cus() {
@@ -840,14 +845,6 @@ int num_cus() {
 template <class Epi>
 int launch(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int ldw, Epi epi, hipStream_t s,
            int variant = -1) {
-    static const bool env_read = [] {  // A/B knob for whole runs (tools/gpu_ab_gemm.sh)
-        if (const char* v = getenv("MLG_GEMM_VARIANT")) {
-            const int x = atoi(v);
-            if (x >= 1 && x <= 5) g_variant = x;
-        }
-        return true;
-    }();
-    (void)env_read;
     if (variant < 0) variant = g_variant;
     g_num_cus = num_cus();
     if (M <= 0 || N <= 0 || K <= 0 || (K % BK) || (lda % 8) || (ldw % 8) || lda < K || ldw < K)

@@ -54,6 +54,15 @@ __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_ca
 #ifndef MLG_FFN_NT
 #define MLG_FFN_NT 1
 #endif
+// Launch form, fixed per build (A/B arms are separate builds loaded through
+// tools/ab_run.py): MLG_FFN_GRID = workgroups per CU of a persistent grid (0: one
+// workgroup per tile), MLG_FFN_ROWS = token rows per workgroup (64: 4 waves, 128: 8).
+#ifndef MLG_FFN_GRID
+#define MLG_FFN_GRID 0
+#endif
+#ifndef MLG_FFN_ROWS
+#define MLG_FFN_ROWS 64
+#endif
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 __device__ __forceinline__ uint4 stream_ld(const uint4* p) {
 #if MLG_FFN_NT
@@ -422,12 +431,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
     }
 }
 
-int ffn_env(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : dflt;
-}
-
-int ffn_num_cus() {
+[[maybe_unused]] int ffn_num_cus() {
     static const int n = [] {
         int dev = 0, c = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
@@ -446,30 +450,19 @@ int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const
     if (ldc < 256 || (ldc % 8)) return MLG_EINVAL;
     mlg_lg_conf_i cf{};
     if (conf) cf = *conf;
-    // A/B knob (tools/ffn_ab.sh): MLG_FFN_GRID = workgroups per CU of the persistent grid
-    // (0: one workgroup per tile)
-    static const int per_cu = ffn_env("MLG_FFN_GRID", 0);
-    // timing probe only (tools/gpu_ab_ffn_epi.sh): ReLU instead of LayerNorm + GELU, to
-    // price the LightGlue epilogue; results are then NOT LightGlue's
-    static const int probe_relu = ffn_env("MLG_FFN_PROBE_RELU", 0);
-    if (probe_relu) relu = 1;
-    // A/B knob: MLG_FFN_ROWS = token rows per workgroup (64: 4 waves, 128: 8 waves)
-    static const int rows = ffn_env("MLG_FFN_ROWS", 64) == 128 ? 128 : 64;
-    if (rows == 128) {
-        hipLaunchKernelGGL((k_lg_ffn<false, 128, 8>), dim3((unsigned)((M + 127) / 128)), dim3(512), 0, s, ctx, X, xcopy,
-                           ldc, M, w, cf, relu);
-        MLG_LAUNCH_CHECK();
-        return MLG_OK;
-    }
+#if MLG_FFN_ROWS == 128
+    hipLaunchKernelGGL((k_lg_ffn<false, 128, 8>), dim3((unsigned)((M + 127) / 128)), dim3(512), 0, s, ctx, X, xcopy, ldc,
+                       M, w, cf, relu);
+#elif MLG_FFN_GRID > 0
     const long ntiles = (M + 63) / 64;
-    if (per_cu > 0) {
-        const long grid = std::min<long>(ntiles, (long)per_cu * ffn_num_cus());
-        hipLaunchKernelGGL((k_lg_ffn<true, 64, 4>), dim3((unsigned)grid), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf,
-                           relu);
-    } else {
-        hipLaunchKernelGGL((k_lg_ffn<false, 64, 4>), dim3((unsigned)ntiles), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w,
-                           cf, relu);
-    }
+    const long grid = std::min<long>(ntiles, (long)MLG_FFN_GRID * ffn_num_cus());
+    hipLaunchKernelGGL((k_lg_ffn<true, 64, 4>), dim3((unsigned)grid), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf,
+                       relu);
+#else
+    const long ntiles = (M + 63) / 64;
+    hipLaunchKernelGGL((k_lg_ffn<false, 64, 4>), dim3((unsigned)ntiles), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf,
+                       relu);
+#endif
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

@@ -23,6 +23,18 @@
 #include "common.h"
 #include "kernels.h"
 
+// Build-time A/B knobs (separate builds loaded through tools/ab_run.py; the defaults are
+// the product): tile height, persistent weights-resident form, timing probes.
+#ifndef MLG_PROJ_MT
+#define MLG_PROJ_MT 2
+#endif
+#ifndef MLG_PROJ_RES
+#define MLG_PROJ_RES 1
+#endif
+#ifndef MLG_PROJ_PROBE
+#define MLG_PROJ_PROBE 0
+#endif
+
 namespace {
 
 constexpr int ROWB = 512;  // LDS bytes per token row: 256 bf16
@@ -344,20 +356,13 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
 int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,
                 const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s) {
     if (Npad <= 0 || (Npad % 64) || ldx < 256 || (ldx % 8)) return MLG_EINVAL;
-    // A/B knob: MLG_PROJ_MT = 32-token m-tiles per workgroup (2: 64 tokens, 4: 128).
+    // Build-time A/B knob: MLG_PROJ_MT = 32-token m-tiles per workgroup (2: 64 tokens, 4: 128).
     // 128-token tiles halve the weight bytes per FLOP but measured 2-7 % slower on one
     // box (tools/gpu_ab_ffn_proj.sh: self 2.39 vs 2.35 ms, cross 1.27 vs 1.19 ms at 2 M
     // tokens): the weight stream is not what bounds this kernel.
-    static const int mt = [] {
-        const char* v = getenv("MLG_PROJ_MT");
-        return v && atoi(v) == 4 ? 4 : 2;
-    }();
-    // default: the weights-resident persistent form; MLG_PROJ_RES=0 selects the tiled form
-    static const int res = [] {
-        const char* v = getenv("MLG_PROJ_RES");
-        return v ? atoi(v) : 1;
-    }();
-    if (res) {
+    constexpr int mt = MLG_PROJ_MT == 4 ? 4 : 2;
+    // default: the weights-resident persistent form; MLG_PROJ_RES=0 builds the tiled form
+    if (MLG_PROJ_RES) {
         static const int cus = [] {
             int dev = 0, c = 0;
             if (hipGetDevice(&dev) != hipSuccess ||
@@ -365,12 +370,9 @@ int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, 
                 return 256;
             return c;
         }();
-        // timing probes only (results wrong): 1 no GEMM, 2 no epilogue, 4 no DMA, 8 no factor DMA,
+        // timing-probe builds only (MLG_PROJ_PROBE, results wrong; 0 in the product): 1 no GEMM, 2 no epilogue, 4 no DMA, 8 no factor DMA,
         // 16 no copy-out stores
-        static const int probe = [] {
-            const char* v = getenv("MLG_PROJ_PROBE");
-            return v ? atoi(v) : 0;
-        }();
+        constexpr int probe = MLG_PROJ_PROBE;
         const int npart = self_block ? 3 : 2, ntiles = Npad / 64;
         // one workgroup per CU (256 VGPRs, 64-96 KiB LDS), `slots` part-groups per XCD
         const int slots = std::max(1, std::min((cus / 8) / npart, (ntiles + 7) / 8));
