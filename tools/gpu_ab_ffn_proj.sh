@@ -1,4 +1,9 @@
 #!/bin/bash
+# HISTORICAL (kept as the recipe of the profiles it produced): it switches arms through
+# runtime knobs (MLG_FFN_* / MLG_PROJ_* / MLG_GEMM_VARIANT env vars, MLGATE_LIB_DIR) that the
+# library no longer reads, so both arms would now run the same build.  Build each arm
+# with -D flags instead and load it through tools/ab_run.py --lib-dir (tools/gpu_r03ag.sh).
+echo "$0: historical recipe; its runtime A/B knobs are gone (see header)" >&2; exit 2
 # Same-box A/B: FFN launch form (MLG_FFN_GRID 0 = one workgroup per tile, 2 = persistent)
 # x projection tile (MLG_PROJ_MT 2 = 64 tokens, 4 = 128), then the kernel tests and a
 # short bench with the defaults.

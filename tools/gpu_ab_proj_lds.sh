@@ -1,4 +1,9 @@
 #!/bin/bash
+# HISTORICAL (kept as the recipe of the profiles it produced): it switches arms through
+# runtime knobs (MLG_FFN_* / MLG_PROJ_* / MLG_GEMM_VARIANT env vars, MLGATE_LIB_DIR) that the
+# library no longer reads, so both arms would now run the same build.  Build each arm
+# with -D flags instead and load it through tools/ab_run.py --lib-dir (tools/gpu_r03ag.sh).
+echo "$0: historical recipe; its runtime A/B knobs are gone (see header)" >&2; exit 2
 # Same-box A/B of the LightGlue projection kernel: ab_old/ (baseline build, loaded through
 # MLGATE_LIB_DIR) against the in-tree build; projection / LightGlue parity tests first.
 set -u

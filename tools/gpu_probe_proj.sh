@@ -1,4 +1,9 @@
 #!/bin/bash
+# HISTORICAL (kept as the recipe of the profiles it produced): it switches arms through
+# runtime knobs (MLG_FFN_* / MLG_PROJ_* / MLG_GEMM_VARIANT env vars, MLGATE_LIB_DIR) that the
+# library no longer reads, so both arms would now run the same build.  Build each arm
+# with -D flags instead and load it through tools/ab_run.py --lib-dir (tools/gpu_r03ag.sh).
+echo "$0: historical recipe; its runtime A/B knobs are gone (see header)" >&2; exit 2
 set -u
 cd "${GRAFT_REPO_ROOT}"
 mkdir -p gpurun_out
