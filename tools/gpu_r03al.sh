@@ -1,0 +1,8 @@
+#!/bin/bash
+# r03al: build-time knobs refactor (no kernel change for the defaults): full GPU suite, smoke, bench
+set -u
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 250 --timeout-method thread > gpurun_out/r03al_pytest.log 2>&1; rc=$?; tail -2 gpurun_out/r03al_pytest.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03al_smoke.log 2>&1 || { tail -5 gpurun_out/r03al_smoke.log; exit 1; }
+timeout -k 10 600 python -u bench.py > gpurun_out/r03al_bench.json 2> gpurun_out/r03al_bench.err || { tail -5 gpurun_out/r03al_bench.err; exit 1; }
+python3 -c "import json; l=json.loads(open('gpurun_out/r03al_bench.json').read().strip().splitlines()[-1]); print(l['value'], l['ms_per_step'], l['config']['false_loop_closure_rejections']['total'], l['roofline']['frac'], l['roofline']['avg_launch_us'])"

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--no-prune", action="store_true")
+    ap.add_argument("--clock", type=float, default=0.0,
+                    help="seconds of back-to-back calls, then the in-kernel clocks of a "
+                         "tools/clock_probe_build.py library (attention, fused FFN, projections)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     seq = synthetic.make_sequence(args.frames, max(2, args.frames // 4), 0)
@@ -64,6 +67,18 @@ def main():
         rate = work.value / (ms.value * 1e9) if ms.value else None  # TFLOP/s, or TB/s for slot 8
         res[name] = {"ms_per_call": round(ms.value / args.iters, 2),
                      ("tb_per_s" if slot == 8 else "tflops"): round(rate, 2) if rate else None}
+    if args.clock > 0:
+        import time
+        t_end = time.time() + args.clock
+        while time.time() < t_end:
+            lg.match_device(kp, ds, counts, pa, pb)
+            torch.cuda.synchronize()
+        for name, fn in (("attention", "mlg_probe_clock"), ("ffn_fused", "mlg_probe_clock_ffn"),
+                         ("qkv_proj", "mlg_probe_clock_proj")):
+            ghz, nwg = ctypes.c_double(0.0), ctypes.c_int(0)
+            rc = getattr(L, fn)(ctypes.byref(ghz), ctypes.byref(nwg))
+            res[name]["clock_ghz"] = round(ghz.value, 3) if rc == 0 else None
+            res[name]["clock_wgs"] = nwg.value
     print(json.dumps(res), flush=True)
 
 
