@@ -63,6 +63,12 @@ __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_ca
 #ifndef MLG_FFN_ROWS
 #define MLG_FFN_ROWS 64
 #endif
+#ifndef MLG_FFN_RING1
+#define MLG_FFN_RING1 2
+#endif
+#ifndef MLG_FFN_RING2
+#define MLG_FFN_RING2 4
+#endif
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 __device__ __forceinline__ uint4 stream_ld(const uint4* p) {
 #if MLG_FFN_NT
@@ -169,7 +175,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                                                   bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w,
                                                   mlg_lg_conf_i cf, int relu) {
     constexpr int MT = R / 32, NT1 = 256 / NW / 32, NT2 = 512 / NW / 32, NTH = 64 * NW;
-    constexpr int RING = NW == 8 ? 8 : 4;  // weight k-steps in flight per wave
+    constexpr int RING = NW == 8 ? 8 : MLG_FFN_RING2;  // weight k-steps in flight per wave (ffn1)
+    // ring of the msg / ffn2 phases (NT1 column tiles, half the MFMAs per k-step of ffn1).
+    // Same-box sweep (profiles/r03an_ab_ffn_ring.txt, identical matches in every arm): msg /
+    // ffn2 ring 2 / 4 / 8 / 16 -> 374 / 376 / 379 / 432 ms of FFN per 4096-pair call, ffn1
+    // ring 2 / 4 / 8 -> 382 / 376 / 506 ms: more loads in flight only cost, so the L2
+    // latency of the weight stream is covered already.
+    constexpr int RING1 = NW == 8 ? 8 : MLG_FFN_RING1;
     __shared__ __attribute__((aligned(16))) char lds[R * ROWB];
     __shared__ float red[2][NW][R];
     // biases and LayerNorm affine, staged in LDS: epilogue reads never wait on VMEM
@@ -220,7 +232,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
         {
             f32x16 acc[NT1][MT];
             zero(acc);
-            gemm_phase<NT1, MT, RING>(w.Wout, 256, 32 * NT1 * wave, 4, 32, lds, acc);
+            gemm_phase<NT1, MT, RING1>(w.Wout, 256, 32 * NT1 * wave, 4, 32, lds, acc);
             __syncthreads();  // every wave has read the ctx half
     #pragma unroll
             for (int t = 0; t < NT1; ++t)
@@ -344,7 +356,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             __builtin_amdgcn_sched_barrier(0);
             f32x16 acc[NT1][MT];
             zero(acc);
-            gemm_phase<NT1, MT, RING>(w.Wf2, 256, 32 * NT1 * wave, 8, 0, lds, acc);
+            gemm_phase<NT1, MT, RING1>(w.Wf2, 256, 32 * NT1 * wave, 8, 0, lds, acc);
             __syncthreads();  // every wave has read the GELU output
     #pragma unroll
             for (int t = 0; t < NT1; ++t)
