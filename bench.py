@@ -200,8 +200,9 @@ def main():
     ap.add_argument("--batch", type=int, default=123)
     ap.add_argument("--sp-batch", type=int, default=64)
     # pairs per LightGlue call: 4096 (131 GB of workspace) measured 547 vs 529 kf/s at 1024
-    # (profiles/r02t_chunk_sweep.txt); 8192 would need 260 GB
-    ap.add_argument("--lg-chunk", type=int, default=4096)
+    # (profiles/r02t_chunk_sweep.txt); 5120 (164 GB, 5 calls per step instead of 6) another
+    # +0.3-0.5 % and 6144 (196 GB) no more (profiles/r03as_chunk_sweep.txt); 8192 would need 260 GB
+    ap.add_argument("--lg-chunk", type=int, default=5120)
     ap.add_argument("--k", type=int, default=20)  # configs[2]: top-20 candidates per query
     ap.add_argument("--places", type=int, default=600)
     ap.add_argument("--verify", choices=["all", "none"], default="all")
