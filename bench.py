@@ -24,6 +24,7 @@ and each rank receives the SuperPoint features of exactly the keyframes its pair
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -58,17 +59,24 @@ def sequence(n, places, seed=0):
     return seq, labels
 
 
-def pmc_traffic(slot_name):
+def pmc_traffic(slot_name, lg_chunk):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from separate
-    `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` runs of this bench, with the
-    gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md), or None if absent."""
+    `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` runs of one LightGlue call of this
+    bench's size, with the gfx950 FETCH_SIZE x2 correction of MI355X_MICROARCH.md), or None
+    if absent or measured on a call of another size than --lg-chunk."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         entry = json.load(f).get(slot_name)
-    return entry.get("bytes_per_launch") if entry else None
+    if not entry:
+        return None
+    pairs = entry.get("pairs")
+    if pairs is None:
+        m = re.search(r"--pairs (\d+)", entry.get("source", ""))
+        pairs = int(m.group(1)) if m else None
+    return entry.get("bytes_per_launch") if pairs == lg_chunk else None
 
 
 def cpu_baseline(budget_s=12.0, pairs_per_kf=0.0):
@@ -304,7 +312,7 @@ def main():
                          "achieved": round(achieved, 2) if achieved else None,
                          "peak": peak, "unit": "GB/s" if hbm else "TFLOP/s",
                          "frac": round(achieved / peak, 4) if achieved else None,
-                         "traffic": pmc_traffic(SLOTS[dom]), "avg_launch_us": round(avg_s * 1e6, 2),
+                         "traffic": pmc_traffic(SLOTS[dom], args.lg_chunk), "avg_launch_us": round(avg_s * 1e6, 2),
                          "launches": cnt,
                          ("bytes_per_launch" if hbm else "flops_per_launch"): round(flops, 1),
                          "stage_ms_per_step": {SLOTS[s]: round(tot[s], 2) for s in SLOTS},

@@ -39,7 +39,8 @@ def main():
         pairs = int(os.environ.get("PAIRS", "4096"))
         fb = 2.0 * 1024 * sum(fetch) / len(fetch)
         wb = 1024.0 * sum(write) / len(write)
-        res[slot] = {"kernel": pat.rstrip("("), "dispatches": len(fetch), "fetch_bytes_per_launch": round(fb),
+        res[slot] = {"kernel": pat.rstrip("("), "dispatches": len(fetch), "pairs": pairs,
+                     "fetch_bytes_per_launch": round(fb),
                      "write_bytes_per_launch": round(wb), "bytes_per_launch": round(fb + wb),
                      "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs) of "
                                f"tools/lg_bench.py --iters 1 --pairs {pairs} (one {pairs}-pair LightGlue call = "
