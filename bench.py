@@ -203,9 +203,11 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--keyframes", type=int, default=5000)
-    # 123 frames = 65,190 tokens = 255 M-tiles of 256: the 256x256 GEMM tiles of every
-    # ViT layer (3 / 9 / 12 N-tiles) then fill 256 CUs in whole waves (99.6 %).
-    ap.add_argument("--batch", type=int, default=123)
+    # 246 frames = 130,380 tokens = 510 M-tiles of 256: the 256x256 GEMM tiles of every
+    # ViT layer (3 / 9 / 12 N-tiles) then fill 256 CUs in whole waves (99.6 %); against 123
+    # frames (255 M-tiles) the ViT stages take 700 vs 728 ms per step on one box
+    # (profiles/r03aw_vit_batch_sweep.txt)
+    ap.add_argument("--batch", type=int, default=246)
     ap.add_argument("--sp-batch", type=int, default=64)
     # pairs per LightGlue call: 4096 (131 GB of workspace) measured 547 vs 529 kf/s at 1024
     # (profiles/r02t_chunk_sweep.txt); 5120 (164 GB, 5 calls per step instead of 6) another
