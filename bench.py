@@ -2,10 +2,12 @@
 over a 5k-keyframe multi-floor sequence on 1..8 MI355X (BASELINE.json metric
 "keyframes gated/sec (VPR+kNN+LightGlue verify)").
 
-One step = the whole sequence gated once (mlgate.pipeline.DeviceGate): IMU floor labels
-(IMUFloorDetector on the sequence's 200 Hz log, host), every keyframe (640x480x3 uint8
-BGR, resident in HBM) preprocessed and run through ViT-B/14 (one forward yields the GeM
-descriptor and the cached local features, as CricaVPR.add_image needs); all keyframes
+The floor labels come from IMUFloorDetector on the sequence's 200 Hz IMU log (host, once,
+before the timed region: they are an input of the gate, kilobytes per sequence).  One
+step = the whole sequence gated once (mlgate.pipeline.DeviceGate): every keyframe
+(640x480x3 uint8 BGR, resident in HBM) preprocessed and run through ViT-B/14 (the
+split-bf16 forward by default, --vit; one forward yields the GeM descriptor and the
+cached local features, as CricaVPR.add_image needs); all keyframes
 retrieved against all (top-k = 20 as configs[2], time gap, threshold, floor decision);
 every floor-valid candidate verified (verify_with_semantics): SuperPoint keypoints /
 descriptors per keyframe (computed once, cached), LightGlue on the pair, OpenCV-sequenced
@@ -79,6 +81,16 @@ def pmc_traffic(slot_name, lg_chunk):
     return entry.get("bytes_per_launch") if pairs == lg_chunk else None
 
 
+def host_threads():
+    """Threads for the CPU legs: the CPUs this process may use.  BASELINE.md asks for
+    os.cpu_count(); on the GPU box that reports the whole machine while the job's share is
+    16 CPUs (OMP_NUM_THREADS=16 is exported there), and threads beyond the share only
+    oversubscribe it -- so the share, when the environment states it."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(int(env), avail)) if env and env.isdigit() else avail
+
+
 def cpu_baseline(budget_s=12.0, pairs_per_kf=0.0):
     """The oracle port of the reference CPU path on this host's cores, per keyframe:
     CricaVPR.add_image (preprocess + TWO ViT-B/14 fp32 forwards at batch 1,
@@ -86,14 +98,19 @@ def cpu_baseline(budget_s=12.0, pairs_per_kf=0.0):
     descriptors amortised per keyframe, and -- for the verified pairs per keyframe the
     GPU run produced -- the reference's per-pair verification cost: SuperPoint on BOTH
     images (geometric_verification.py:285-290 re-extracts per pair) + LightGlue (fp32
-    restatements, oracle/), timed on one sampled pair.  RANSAC (OpenCV, C++) is not
-    restated on the CPU and is excluded; it is milliseconds against seconds."""
+    restatements, oracle/), timed on one sampled pair, + findEssentialMat's RANSAC loop
+    (the C restatement, oracle/csrc/ransac_cv.c) on that pair's matches.  Plus configs[0]:
+    MixVPR's ResNet-50 fallback (place_recognition.py:248-306) + find_loop_closures on 64
+    keyframes, the reference's CPU plumbing configuration."""
+    from oracle import _lib as olib
+    from oracle import geometry as ogeo
     from oracle import lightglue as olg
+    from oracle import resnet as orn
     from oracle import retrieval as oret
     from oracle import superpoint as osp
     from oracle import vit as ovit
-    from mlgate.weights import lightglue_state_dict, superpoint_state_dict
-    threads = min(16, os.cpu_count() or 1)
+    from mlgate.weights import lightglue_state_dict, resnet50_state_dict, superpoint_state_dict
+    threads = host_threads()
     torch.set_num_threads(threads)
     sd = {k: torch.from_numpy(v) for k, v in synthetic_state_dict(0).items()}
     rng = np.random.default_rng(0)
@@ -116,17 +133,70 @@ def cpu_baseline(budget_s=12.0, pairs_per_kf=0.0):
     sample = (f"{n_done} keyframes x (preprocess + 2 ViT-B/14 fp32 forwards, batch 1) = {t_vit:.1f} s; "
               f"find_loop_closures N=5000 D=768 k=20 = {t_knn:.2f} s, amortised per keyframe")
     if pairs_per_kf > 0:
-        frames = synthetic.frames_host(synthetic.make_sequence(2, 1, 0))
+        seq2 = synthetic.make_sequence(2, 1, 0)
+        frames = synthetic.frames_host(seq2)
         s = time.perf_counter()
         f = osp.superpoint(superpoint_state_dict(0), [frames[0], frames[1]], emulate_bf16=False)
-        olg.Oracle(lightglue_state_dict(0), emulate_bf16=False).match(
+        r = olg.Oracle(lightglue_state_dict(0), emulate_bf16=False).match(
             f[0]["keypoints"], f[0]["descriptors"], f[1]["keypoints"], f[1]["descriptors"])
+        mm = r["matches"].numpy()
+        olib.essential_ransac(f[0]["keypoints"].numpy()[mm[:, 0]], f[1]["keypoints"].numpy()[mm[:, 1]],
+                              ogeo.ISEC_K, 3.0)
         t_pair = time.perf_counter() - s
         per_kf += pairs_per_kf * t_pair
-        sample += (f"; 1 pair x (SuperPoint on both images + LightGlue, fp32) = {t_pair:.1f} s, "
+        sample += (f"; 1 pair x (SuperPoint on both images + LightGlue, fp32, + RANSAC) = {t_pair:.1f} s, "
                    f"x {pairs_per_kf:.2f} gate-accepted pairs per keyframe")
+    # configs[0]: MixVPR ResNet-50 fallback descriptors + find_loop_closures, 64 keyframes
+    seq0, lab0 = sequence(64, 16)
+    fr0 = synthetic.frames_host(seq0)
+    rsd = resnet50_state_dict(0)
+    s = time.perf_counter()
+    n0 = 0
+    D0 = np.zeros((64, 4096), np.float32)
+    while n0 < 64 and (time.perf_counter() - s) < budget_s * 0.5:
+        D0[n0] = orn.extract_descriptor(rsd, fr0[n0])
+        n0 += 1
+    t_rn = time.perf_counter() - s
+    s = time.perf_counter()
+    oret.find_loop_closures(D0, seq0.t, lab0, np.ones(64, np.uint8), 10.0, 0.5, 10, True)
+    t_k0 = time.perf_counter() - s
+    c0 = {"value": round(64.0 / (t_rn / n0 * 64 + t_k0), 3), "unit": "keyframes/s",
+          "sample": f"{n0} of 64 keyframes through the ResNet-50 fallback (fp32) = {t_rn:.1f} s + "
+                    f"find_loop_closures over 64 x 4096 = {t_k0 * 1e3:.1f} ms"}
     return {"value": round(1.0 / per_kf, 4), "unit": "keyframes/s", "cores": threads, "kind": "port",
-            "sample": sample}
+            "host_cpus": os.cpu_count(), "sample": sample, "configs0": c0}
+
+
+def configs0_bench(frames, seq, labels, lo, dev, iters=5):
+    """configs[0] on the GPU: MixVPR's ResNet-50 fallback descriptors (4096-dim, zero-padded,
+    place_recognition.py:248-306; HIP mlg_resnet50) of 64 keyframes and find_loop_closures
+    over them (k = 10, gap 10 s, thr 0.5, floor-gated), HIP-event timed."""
+    from mlgate import retrieval
+    from mlgate.resnet import ResNet50GPU
+    n = min(64, frames.shape[0])
+    fr = frames[:n].contiguous()
+    eng = ResNet50GPU(device=dev)
+    t = torch.as_tensor(seq.t[lo:lo + n], device=dev)
+    fl = torch.as_tensor(np.asarray(labels[lo:lo + n], np.int64), device=dev)
+    hf = torch.ones(n, dtype=torch.uint8, device=dev)
+
+    def one():
+        d = eng.forward_device(fr, 4096)
+        return retrieval.knn_gate(d, t, fl, hf, 10.0, 0.5, 10, True)
+    one()
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(iters):
+        out = one()
+    ev[1].record()
+    torch.cuda.synchronize(dev)
+    ms = ev[0].elapsed_time(ev[1]) / iters
+    tf = 8.2e9 * n / (ms * 1e-3) / 1e12  # ResNet-50 @224^2 ~8.2 GFLOP per frame (BASELINE.md)
+    return {"workload": "configs[0] MixVPR ResNet-50 fallback descriptors (4096-dim) + find_loop_closures, "
+                        "64 keyframes (seeded synthetic ResNet-50 weights)",
+            "keyframes": n, "ms": round(ms, 3), "keyframes_per_s": round(n / (ms * 1e-3), 1),
+            "resnet_tflops": round(tf, 1), "matches": int(out[3].sum())}
 
 
 def loftr_flops_per_pair(L=4800, matches=0.0):
@@ -218,6 +288,8 @@ def main():
     ap.add_argument("--verify", choices=["all", "none"], default="all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--loftr-pairs", type=int, default=64, help="configs[4] LoFTR sub-object (0: skip)")
+    ap.add_argument("--vit", choices=["split", "bf16"], default="split",
+                    help="split: split-bf16 ViT (MLG_VIT_SPLIT, fp32-faithful descriptors); bf16: plain bf16 operands")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -233,7 +305,7 @@ def main():
     frames = synthetic.frames_device(seq, np.arange(lo, hi), dev)
     gate = DeviceGate(frames, seq.t, labels, world, rank, dev, k=args.k, verify=args.verify == "all", K=ISEC_K,
                       vit_batch=args.batch, sp_batch=args.sp_batch, lg_chunk=args.lg_chunk,
-                      vit_state_dict=synthetic_state_dict(0))
+                      vit_state_dict=synthetic_state_dict(0), vit_precise=args.vit == "split")
     ops = _native.ops()  # torch.ops.mlgate (HIP-event profiling slots of the C ABI)
     all_slots = (1 << len(SLOTS)) - 1
     for i in range(args.warmup):
@@ -275,6 +347,7 @@ def main():
     counts = {k_: int(v) // steps for k_, v in zip(keys, cv.cpu().tolist())}  # per step, all ranks
     N = args.keyframes
     lft = loftr_bench(frames, seq, lo, dev, args.loftr_pairs) if args.loftr_pairs > 0 else None
+    c0 = configs0_bench(frames, seq, labels, lo, dev) if rank == 0 else None
 
     if rank == 0:
         avg_s = ms / 1e3 / max(cnt, 1)
@@ -323,6 +396,8 @@ def main():
         }
         if lft:
             line["loftr"] = lft
+        if c0:
+            line["configs0"] = c0
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(pairs_per_kf=(counts["pairs_verified"] / N) if gate.verify else 0.0)
         print(json.dumps(line), flush=True)

@@ -23,11 +23,14 @@ struct VitGeom {
     }
 };
 
+// Operand buffers are sized for the split-bf16 forward (MLG_VIT_SPLIT): [hi | lo] rows
+// for patches / xn / o / h, and q / k / vt as a hi plane followed by a lo plane (lo_elems
+// apart); the plain bf16 forward uses the first half of each.
 struct VitWorkspace {
     bf16_t *patches, *xn, *q, *k, *vt, *o, *h;
     float *x, *partial;
     int32_t* tasks;  // attention tasks + output offsets, 5 * B int32
-    size_t q_bytes, vt_bytes;
+    size_t q_bytes, vt_bytes, lo_elems;
 };
 
 size_t carve(const VitGeom& g, char* base, VitWorkspace* ws) {
@@ -40,16 +43,17 @@ size_t carve(const VitGeom& g, char* base, VitWorkspace* ws) {
     const size_t rows = (size_t)g.B * g.T;
     const size_t heads = (size_t)g.B * 12;
     VitWorkspace w{};
-    w.patches = (bf16_t*)take((size_t)g.B * g.P * MLG_VIT_PATCH_K * 2);
+    w.patches = (bf16_t*)take((size_t)g.B * g.P * MLG_VIT_PATCH_K * 2 * 2);
     w.x = (float*)take(rows * 768 * 4);
-    w.xn = (bf16_t*)take(rows * 768 * 2);
-    w.q_bytes = heads * g.Tpad * 64 * 2;
+    w.xn = (bf16_t*)take(rows * 768 * 2 * 2);
+    w.lo_elems = heads * g.Tpad * 64;
+    w.q_bytes = 2 * w.lo_elems * 2;
     w.q = (bf16_t*)take(w.q_bytes);
-    w.k = (bf16_t*)take(heads * g.Tpad * 64 * 2);
-    w.vt_bytes = heads * 64 * g.Tpad * 2;
+    w.k = (bf16_t*)take(2 * w.lo_elems * 2);
+    w.vt_bytes = 2 * w.lo_elems * 2;
     w.vt = (bf16_t*)take(w.vt_bytes);
-    w.o = (bf16_t*)take(rows * 768 * 2);
-    w.h = (bf16_t*)take(rows * 3072 * 2);
+    w.o = (bf16_t*)take(rows * 768 * 2 * 2);
+    w.h = (bf16_t*)take(rows * 3072 * 2 * 2);
     w.partial = (float*)take(mlg_gem_partial_bytes(g.B));
     w.tasks = (int32_t*)take((size_t)g.B * 5 * 4);
     if (ws) *ws = w;
@@ -132,18 +136,50 @@ size_t mlg_vit_workspace_bytes(int batch, int image_size) {
 }  // extern "C"
 
 // Preprocess + patch embedding + the 12 blocks; leaves the residual stream in ws->x.
+// split: the MLG_VIT_SPLIT forward (weights packed [W_hi | W_lo | W_hi]).
 static int vit_trunk(const mlg_vit_weights* w, const uint8_t* frames, const VitGeom& g, int H, int W, int C,
-                     long frame_stride, int swap_rb, const VitWorkspace& ws, hipStream_t s) {
+                     long frame_stride, int swap_rb, const VitWorkspace& ws, hipStream_t s, int split = 0) {
     const int M = g.B * g.T;
-    TRY(mlg_preprocess_patches(frames, g.B, H, W, C, frame_stride, g.S, MLG_VIT_PATCH_K, swap_rb, ws.patches, s));
-    TRY(mlg_gemm_patch(ws.patches, w->patch_w, w->patch_b, w->pos, ws.x, g.B * g.P, g.P, MLG_VIT_PATCH_K, s));
+    TRY(mlg_preprocess_patches(frames, g.B, H, W, C, frame_stride, g.S, MLG_VIT_PATCH_K, swap_rb, ws.patches, s,
+                               split));
+    if (split)
+        TRY(mlg_gemm_patch_split(ws.patches, w->patch_w, w->patch_b, w->pos, ws.x, g.B * g.P, g.P, MLG_VIT_PATCH_K,
+                                 s));
+    else
+        TRY(mlg_gemm_patch(ws.patches, w->patch_w, w->patch_b, w->pos, ws.x, g.B * g.P, g.P, MLG_VIT_PATCH_K, s));
     TRY(mlg_cls_rows(ws.x, w->cls, w->pos, g.B, g.T, s));
     // padded key columns of V^T must be finite (masked keys multiply them by p = 0); padded
     // query rows are never stored but are zeroed too, so no lane computes on stale bits
     if (hipMemsetAsync(ws.vt, 0, ws.vt_bytes, s) != hipSuccess) return MLG_EHIP;
     if (hipMemsetAsync(ws.q, 0, ws.q_bytes, s) != hipSuccess) return MLG_EHIP;
 
-    for (int l = 0; l < MLG_VIT_DEPTH; ++l) {
+    const double mul = split ? 3.0 : 1.0;  // MFMA products per algorithmic product
+    for (int l = 0; l < MLG_VIT_DEPTH && split; ++l) {
+        const mlg_vit_block& bl = w->blocks[l];
+        TRY(mlg_layernorm_split(ws.x, bl.norm1_w, bl.norm1_b, ws.xn, M, s));
+        {
+            MlgProfScope p(2, s, mul * 2.0 * M * 2304 * 768);
+            TRY(mlg_gemm_qkv_split(ws.xn, bl.qkv_w, bl.qkv_b, ws.q, ws.k, ws.vt, M, g.T, g.Tpad, ws.lo_elems, s));
+        }
+        {
+            MlgProfScope p(4, s, mul * 4.0 * g.B * 12 * (double)g.T * g.T * 64);
+            TRY(mlg_attention_split(ws.q, ws.k, ws.vt, ws.o, g.B, g.T, g.Tpad, ws.lo_elems, ws.tasks, s));
+        }
+        {
+            MlgProfScope p(3, s, mul * 2.0 * M * 768 * 768);
+            TRY(mlg_gemm_residual_split(ws.o, bl.proj_w, bl.proj_b, bl.ls1, ws.x, M, 768, 768, s));
+        }
+        TRY(mlg_layernorm_split(ws.x, bl.norm2_w, bl.norm2_b, ws.xn, M, s));
+        {
+            MlgProfScope p(0, s, mul * 2.0 * M * 3072 * 768);
+            TRY(mlg_gemm_bias_gelu_split(ws.xn, bl.fc1_w, bl.fc1_b, ws.h, M, 3072, 768, s));
+        }
+        {
+            MlgProfScope p(1, s, mul * 2.0 * M * 768 * 3072);
+            TRY(mlg_gemm_residual_split(ws.h, bl.fc2_w, bl.fc2_b, bl.ls2, ws.x, M, 768, 3072, s));
+        }
+    }
+    for (int l = 0; l < MLG_VIT_DEPTH && !split; ++l) {
         const mlg_vit_block& bl = w->blocks[l];
         TRY(mlg_layernorm_bf16(ws.x, bl.norm1_w, bl.norm1_b, ws.xn, M, s));
         {
@@ -183,7 +219,7 @@ int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, 
     hipStream_t s = (hipStream_t)stream;
     const int swap_rb = (flags & MLG_VIT_KEEP_CHANNELS) ? 0 : 1;
     const int mean_pool = (flags & MLG_VIT_POOL_MEAN) ? 1 : 0;
-    TRY(vit_trunk(w, frames, g, H, W, C, frame_stride, swap_rb, ws, s));
+    TRY(vit_trunk(w, frames, g, H, W, C, frame_stride, swap_rb, ws, s, (flags & MLG_VIT_SPLIT) ? 1 : 0));
     TRY(mlg_final_norm_gem(ws.x, w->norm_w, w->norm_b, local_out, ws.partial, desc_out, g.B, g.T, mean_pool, s));
     return MLG_OK;
 }

@@ -111,9 +111,21 @@ __device__ __forceinline__ void block_max2(f32x16 (&v)[2], float (&m)[2]) {
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 
+// SPLIT (the ViT's MLG_VIT_SPLIT forward): Q / K / V^T each come as a hi plane and a lo
+// plane (x = hi + lo, lo_off elements apart); a K / V ring slot holds the hi tile and then
+// the lo tile; every product is hi*hi + lo*hi + hi*lo (three MFMAs into one accumulator)
+// and P is split in registers after the exponential.
+template <bool SPLIT>
+struct Slots {
+    static constexpr int K = SPLIT ? 2 * KTILE_BYTES : KTILE_BYTES;
+    static constexpr int V = SPLIT ? 2 * VTILE_BYTES : VTILE_BYTES;
+};
+
 struct PipeCtx {
     const bf16_t* Kh;
     const bf16_t* Vh;
+    const bf16_t* Kl;  // lo planes (SPLIT only)
+    const bf16_t* Vl;
     char* smem;
     int T, nkb, gk_off, gv_off;
     int sk0, sk1, sv0a, sv0b, sv1a, sv1b;
@@ -121,9 +133,16 @@ struct PipeCtx {
     int voff[2][2][4];  // V^T fragment offsets [half][st][dt * 2 + lo/hi]
 };
 
-// S^T of one 32-key half-block (kt) of the K tile at kb: [qt] tiles
-__device__ __forceinline__ void qk_half(const char* kb, const PipeCtx& c, const bf16x8 (&qf)[2][4], int kt,
-                                        f32x16 (&s)[2]) {
+// S^T of one 32-key half-block (kt) of the K tile at kb: [qt] tiles.
+// HAZARD PAD CONTRACT (block_max2's `s_nop 11`): the scores read by the asm row max must
+// come from v_mfma_f32_32x32x16_bf16 -- an 8-pass XDL op on gfx950, whose result needs 12
+// wait states before a VALU read -- each writing the WHOLE f32x16 accumulator (the pad is
+// tied to element [15]).  Changing this MFMA's shape (e.g. 16x16x32, 4 passes) or
+// splitting the accumulator requires re-deriving the pad; tests/test_kernels_gpu.py's
+// attention bit-identity test is the run-time guard.
+template <bool SPLIT>
+__device__ __forceinline__ void qk_half(const char* kb, const PipeCtx& c, const bf16x8 (&qf)[2][4],
+                                        const bf16x8 (&qfl)[2][4], int kt, f32x16 (&s)[2]) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) { s[0][i] = 0.f; s[1][i] = 0.f; }
 #pragma unroll
@@ -131,20 +150,28 @@ __device__ __forceinline__ void qk_half(const char* kb, const PipeCtx& c, const 
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + kt * 4096 + c.koff[st]);
         s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[0][st], s[0], 0, 0, 0);
         s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[1][st], s[1], 0, 0, 0);
+        if (SPLIT) {
+            const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kb + KTILE_BYTES + kt * 4096 + c.koff[st]);
+            s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qf[0][st], s[0], 0, 0, 0);
+            s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qf[1][st], s[1], 0, 0, 0);
+            s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qfl[0][st], s[0], 0, 0, 0);
+            s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qfl[1][st], s[1], 0, 0, 0);
+        }
     }
 }
 
 // half-step H of stage j: consume `cur` (keys 64 j + 32 H ..), produce `nxt`.  kcur /
 // knext: K ring slots of stages j / j + 1; kw: slot for K_{j+2}.
-template <int H, bool LASTSTAGE, int R>
+template <int H, bool LASTSTAGE, int R, bool SPLIT>
 __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)[2], const PipeCtx& c,
-                                          const bf16x8 (&qf)[2][4], f32x16 (&o)[2][2], float (&mrun)[2],
-                                          float (&lsum)[2][2], uint4 (&stage)[4], int rr = 0) {
+                                          const bf16x8 (&qf)[2][4], const bf16x8 (&qfl)[2][4], f32x16 (&o)[2][2],
+                                          float (&mrun)[2], float (&lsum)[2][2], uint4 (&stage)[8], int rr = 0) {
+    constexpr int KS = Slots<SPLIT>::K, VS = Slots<SPLIT>::V;
     // ring slots are compile-time constants (stage j uses K slot j % 3 = R, V slot R), so
     // every LDS fragment address is a lane offset plus an immediate; R < 0: slot rr at run
     // time (the last stage only)
     const int rs = R >= 0 ? R : rr;
-    const int kcur = rs * KTILE_BYTES, knext = ((rs + 1) % 3) * KTILE_BYTES, kw = ((rs + 2) % 3) * KTILE_BYTES;
+    const int kcur = rs * KS, knext = ((rs + 1) % 3) * KS, kw = ((rs + 2) % 3) * KS;
     constexpr float C = 0.125f * 1.4426950408889634f;  // 1/sqrt(64) * log2(e)
     const int hh = (threadIdx.x & 63) >> 5;
     if (!LASTSTAGE && H == 0) {  // K_{j+2} (clamped), V_{j+1} -> registers, into LDS at the stage end
@@ -154,6 +181,14 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
         const bf16_t* pv = c.Vh + (size_t)(j + 1) * 4096 + c.gv_off;
         stage[2] = *reinterpret_cast<const uint4*>(pv);
         stage[3] = *reinterpret_cast<const uint4*>(pv + 32 * 64);
+        if (SPLIT) {
+            const bf16_t* pkl = c.Kl + (size_t)min(j + 2, c.nkb - 1) * (KB * 64) + c.gk_off;
+            stage[4] = *reinterpret_cast<const uint4*>(pkl);
+            stage[5] = *reinterpret_cast<const uint4*>(pkl + 32 * 64);
+            const bf16_t* pvl = c.Vl + (size_t)(j + 1) * 4096 + c.gv_off;
+            stage[6] = *reinterpret_cast<const uint4*>(pvl);
+            stage[7] = *reinterpret_cast<const uint4*>(pvl + 32 * 64);
+        }
     }
     if (LASTSTAGE && (c.T & (KB - 1))) {  // partial last stage: mask keys >= T
         const int key0 = j * KB + H * 32;
@@ -186,16 +221,16 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
     const float mc0 = mrun[0] * C, mc1 = mrun[1] * C;
     // next half-block's scores on the MFMA pipe
     const char* kring = c.smem;
-    if (!(LASTSTAGE && H == 1)) qk_half(kring + (H == 0 ? kcur : knext), c, qf, H ^ 1, nxt);
+    if (!(LASTSTAGE && H == 1)) qk_half<SPLIT>(kring + (H == 0 ? kcur : knext), c, qf, qfl, H ^ 1, nxt);
     // P of this half-block [st][qt]: keys 16 st + 8 hh .. + 7, then O^T += V^T . P^T
-    const char* vb = c.smem + 3 * KTILE_BYTES + rs * VTILE_BYTES;
-    bf16x8 pf[2][2];
+    const char* vb = c.smem + 3 * KS + rs * VS;
+    bf16x8 pf[2][2], pfl[2][2];
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
             const float mc = qt ? mc1 : mc0;
-            u32x4 w;
+            u32x4 w, wl;
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
                 const float p0 = __builtin_amdgcn_exp2f(fmaf(cur[qt][8 * st + 2 * jj], C, -mc));
@@ -203,8 +238,11 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
                 lsum[qt][0] += p0;
                 lsum[qt][1] += p1;
                 w[jj] = pack_bf16x2(p0, p1);
+                if (SPLIT)
+                    wl[jj] = pack_bf16x2(p0 - __uint_as_float(w[jj] << 16), p1 - __uint_as_float(w[jj] & 0xffff0000u));
             }
             pf[st][qt] = __builtin_bit_cast(bf16x8, w);
+            if (SPLIT) pfl[st][qt] = __builtin_bit_cast(bf16x8, wl);
         }
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) {
@@ -213,38 +251,62 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
             const bf16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
             o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st][0], o[0][dt], 0, 0, 0);
             o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st][1], o[1][dt], 0, 0, 0);
+            if (SPLIT) {
+                const s16x4 llo = *reinterpret_cast<const s16x4*>(vb + VTILE_BYTES + c.voff[H][st][2 * dt]);
+                const s16x4 lhi = *reinterpret_cast<const s16x4*>(vb + VTILE_BYTES + c.voff[H][st][2 * dt + 1]);
+                const bf16x8 vl = __builtin_shufflevector(llo, lhi, 0, 1, 2, 3, 4, 5, 6, 7);
+                o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, pf[st][0], o[0][dt], 0, 0, 0);
+                o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, pf[st][1], o[1][dt], 0, 0, 0);
+                o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pfl[st][0], o[0][dt], 0, 0, 0);
+                o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pfl[st][1], o[1][dt], 0, 0, 0);
+            }
         }
     }
     if (!LASTSTAGE && H == 1) {
         char* kwp = c.smem + kw;
-        char* vw = c.smem + 3 * KTILE_BYTES + ((rs + 1) % 3) * VTILE_BYTES;
+        char* vw = c.smem + 3 * KS + ((rs + 1) % 3) * VS;
         *reinterpret_cast<uint4*>(kwp + c.sk0) = stage[0];
         *reinterpret_cast<uint4*>(kwp + c.sk1) = stage[1];
         *reinterpret_cast<uint2*>(vw + c.sv0a) = make_uint2(stage[2].x, stage[2].y);
         *reinterpret_cast<uint2*>(vw + c.sv0b) = make_uint2(stage[2].z, stage[2].w);
         *reinterpret_cast<uint2*>(vw + c.sv1a) = make_uint2(stage[3].x, stage[3].y);
         *reinterpret_cast<uint2*>(vw + c.sv1b) = make_uint2(stage[3].z, stage[3].w);
+        if (SPLIT) {
+            *reinterpret_cast<uint4*>(kwp + KTILE_BYTES + c.sk0) = stage[4];
+            *reinterpret_cast<uint4*>(kwp + KTILE_BYTES + c.sk1) = stage[5];
+            char* vl = vw + VTILE_BYTES;
+            *reinterpret_cast<uint2*>(vl + c.sv0a) = make_uint2(stage[6].x, stage[6].y);
+            *reinterpret_cast<uint2*>(vl + c.sv0b) = make_uint2(stage[6].z, stage[6].w);
+            *reinterpret_cast<uint2*>(vl + c.sv1a) = make_uint2(stage[7].x, stage[7].y);
+            *reinterpret_cast<uint2*>(vl + c.sv1b) = make_uint2(stage[7].z, stage[7].w);
+        }
         __syncthreads();
     }
 }
 
+template <bool SPLIT>
 __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __restrict__ Qh,
                                                     const bf16_t* __restrict__ Kh, const bf16_t* __restrict__ Vh,
                                                     int T, int nq, int qmax, int qblock, bf16_t* __restrict__ orow,
-                                                    int ldo) {
+                                                    int ldo, size_t lo_off, int lo_col) {
+    constexpr int KS = Slots<SPLIT>::K;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, col = lane & 31;
     const int qbase = qblock * 256 + wave * 64;
-    bf16x8 qf[2][4];
+    bf16x8 qf[2][4], qfl[2][4];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
         const int qld = min(qbase + qt * 32 + col, qmax - 1);
 #pragma unroll
-        for (int st = 0; st < 4; ++st)
+        for (int st = 0; st < 4; ++st) {
             qf[qt][st] = *reinterpret_cast<const bf16x8*>(Qh + (size_t)qld * 64 + st * 16 + hh * 8);
+            if (SPLIT) qfl[qt][st] = *reinterpret_cast<const bf16x8*>(Qh + lo_off + (size_t)qld * 64 + st * 16 + hh * 8);
+        }
     }
     PipeCtx c;
     c.Kh = Kh;
     c.Vh = Vh;
+    c.Kl = Kh + lo_off;
+    c.Vl = Vh + lo_off;
     c.smem = smem;
     c.T = T;
     c.nkb = (T + KB - 1) / KB;
@@ -278,28 +340,48 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
         const uint4 k3 = *reinterpret_cast<const uint4*>(pk + 32 * 64);
         *reinterpret_cast<uint4*>(smem + c.sk0) = k0;
         *reinterpret_cast<uint4*>(smem + c.sk1) = k1;
-        *reinterpret_cast<uint4*>(smem + KTILE_BYTES + c.sk0) = k2;
-        *reinterpret_cast<uint4*>(smem + KTILE_BYTES + c.sk1) = k3;
-        char* vw = smem + 3 * KTILE_BYTES;
+        *reinterpret_cast<uint4*>(smem + KS + c.sk0) = k2;
+        *reinterpret_cast<uint4*>(smem + KS + c.sk1) = k3;
+        char* vw = smem + 3 * KS;
         *reinterpret_cast<uint2*>(vw + c.sv0a) = make_uint2(v0.x, v0.y);
         *reinterpret_cast<uint2*>(vw + c.sv0b) = make_uint2(v0.z, v0.w);
         *reinterpret_cast<uint2*>(vw + c.sv1a) = make_uint2(v1.x, v1.y);
         *reinterpret_cast<uint2*>(vw + c.sv1b) = make_uint2(v1.z, v1.w);
+        if (SPLIT) {
+            const bf16_t* Kl = c.Kl;
+            const bf16_t* Vl = c.Vl;
+            const uint4 l0 = *reinterpret_cast<const uint4*>(Kl + c.gk_off);
+            const uint4 l1 = *reinterpret_cast<const uint4*>(Kl + c.gk_off + 32 * 64);
+            const uint4 w0 = *reinterpret_cast<const uint4*>(Vl + c.gv_off);
+            const uint4 w1 = *reinterpret_cast<const uint4*>(Vl + c.gv_off + 32 * 64);
+            const bf16_t* pl = Kl + (size_t)min(1, c.nkb - 1) * (KB * 64) + c.gk_off;
+            const uint4 l2 = *reinterpret_cast<const uint4*>(pl);
+            const uint4 l3 = *reinterpret_cast<const uint4*>(pl + 32 * 64);
+            *reinterpret_cast<uint4*>(smem + KTILE_BYTES + c.sk0) = l0;
+            *reinterpret_cast<uint4*>(smem + KTILE_BYTES + c.sk1) = l1;
+            *reinterpret_cast<uint4*>(smem + KS + KTILE_BYTES + c.sk0) = l2;
+            *reinterpret_cast<uint4*>(smem + KS + KTILE_BYTES + c.sk1) = l3;
+            char* vl = vw + VTILE_BYTES;
+            *reinterpret_cast<uint2*>(vl + c.sv0a) = make_uint2(w0.x, w0.y);
+            *reinterpret_cast<uint2*>(vl + c.sv0b) = make_uint2(w0.z, w0.w);
+            *reinterpret_cast<uint2*>(vl + c.sv1a) = make_uint2(w1.x, w1.y);
+            *reinterpret_cast<uint2*>(vl + c.sv1b) = make_uint2(w1.z, w1.w);
+        }
     }
     __syncthreads();
     f32x16 sA[2], sB[2];
-    qk_half(smem, c, qf, 0, sA);
+    qk_half<SPLIT>(smem, c, qf, qfl, 0, sA);
     f32x16 o[2][2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) { o[0][0][i] = 0.f; o[0][1][i] = 0.f; o[1][0][i] = 0.f; o[1][1][i] = 0.f; }
     float mrun[2] = {-INFINITY, -INFINITY};
     float lsum[2][2] = {{0.f, 0.f}, {0.f, 0.f}};  // per lane half, two partial sums each
-    uint4 stage[4];
+    uint4 stage[8];
     // stages unrolled by 3 (K and V ring slot of stage j = j % 3, compile-time)
-#define PIPE_STAGE(J, R, LAST)                                                      \
-    {                                                                               \
-        pipe_half<0, LAST, R>(J, sA, sB, c, qf, o, mrun, lsum, stage, (J) % 3);     \
-        pipe_half<1, LAST, R>(J, sB, sA, c, qf, o, mrun, lsum, stage, (J) % 3);     \
+#define PIPE_STAGE(J, R, LAST)                                                                 \
+    {                                                                                          \
+        pipe_half<0, LAST, R, SPLIT>(J, sA, sB, c, qf, qfl, o, mrun, lsum, stage, (J) % 3);    \
+        pipe_half<1, LAST, R, SPLIT>(J, sB, sA, c, qf, qfl, o, mrun, lsum, stage, (J) % 3);    \
     }
     const int last = c.nkb - 1;
     int j = 0;
@@ -325,28 +407,67 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
     // rows x 16 B (the store tail of a row-per-lane epilogue is issue-bound)
     __syncthreads();
     char* st = smem + wave * (64 * 128);
+    if constexpr (!SPLIT) {
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-        const float inv = 1.0f / swap_sum(lsum[qt][0] + lsum[qt][1]);
-        const int r = qt * 32 + col;
+        for (int qt = 0; qt < 2; ++qt) {
+            const float inv = 1.0f / swap_sum(lsum[qt][0] + lsum[qt][1]);
+            const int r = qt * 32 + col;
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
+            for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                uint2 w;
-                w.x = pack_bf16x2(o[qt][dt][4 * g] * inv, o[qt][dt][4 * g + 1] * inv);
-                w.y = pack_bf16x2(o[qt][dt][4 * g + 2] * inv, o[qt][dt][4 * g + 3] * inv);
-                *reinterpret_cast<uint2*>(st + r * 128 + (((dt * 4 + g) ^ (r & 7)) << 4) + 8 * hh) = w;
+                for (int g = 0; g < 4; ++g) {
+                    uint2 w;
+                    w.x = pack_bf16x2(o[qt][dt][4 * g] * inv, o[qt][dt][4 * g + 1] * inv);
+                    w.y = pack_bf16x2(o[qt][dt][4 * g + 2] * inv, o[qt][dt][4 * g + 3] * inv);
+                    *reinterpret_cast<uint2*>(st + r * 128 + (((dt * 4 + g) ^ (r & 7)) << 4) + 8 * hh) = w;
+                }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int r = p * 8 + (lane >> 3), c = lane & 7, qrow = qbase + r;
+            if (qrow < nq)
+                *reinterpret_cast<uint4*>(orow + (size_t)qrow * ldo + c * 8) =
+                    *reinterpret_cast<const uint4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
+        }
+    } else {  // two passes through the staging image: hi rows, then lo rows at column lo_col
+        float inv[2];
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) inv[qt] = 1.0f / swap_sum(lsum[qt][0] + lsum[qt][1]);
+#pragma unroll
+        for (int part = 0; part < 2; ++part) {
+#pragma unroll
+            for (int qt = 0; qt < 2; ++qt) {
+                const int r = qt * 32 + col;
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        uint2 w, wl;
+                        split_bf16x4(o[qt][dt][4 * g] * inv[qt], o[qt][dt][4 * g + 1] * inv[qt],
+                                     o[qt][dt][4 * g + 2] * inv[qt], o[qt][dt][4 * g + 3] * inv[qt], w, wl);
+                        *reinterpret_cast<uint2*>(st + r * 128 + (((dt * 4 + g) ^ (r & 7)) << 4) + 8 * hh) =
+                            part ? wl : w;
+                    }
             }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
-    __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
+            __builtin_amdgcn_wave_barrier();
+            bf16_t* dst = orow + (part ? lo_col : 0);
+            uint4 rows[8];
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-        const int r = p * 8 + (lane >> 3), c = lane & 7, qrow = qbase + r;
-        if (qrow < nq)
-            *reinterpret_cast<uint4*>(orow + (size_t)qrow * ldo + c * 8) =
-                *reinterpret_cast<const uint4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
+            for (int p = 0; p < 8; ++p) {
+                const int r = p * 8 + (lane >> 3), c = lane & 7;
+                rows[p] = *reinterpret_cast<const uint4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // staging read before the next part overwrites it
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+                const int r = p * 8 + (lane >> 3), c = lane & 7, qrow = qbase + r;
+                if (qrow < nq) *reinterpret_cast<uint4*>(dst + (size_t)qrow * ldo + c * 8) = rows[p];
+            }
+        }
     }
 }
 
@@ -361,14 +482,14 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
 // XCD (hardware deals linear block b to XCD b % 8) and share its L2.
 // VIT: the same tile under a second symbol, so rocprof's per-kernel rows (and their
 // average durations) keep the ViT's ~70 us launches apart from LightGlue's
-template <bool VIT>
+template <bool VIT, bool SPLIT = false>
 __global__ __launch_bounds__(256, 1) void k_attention_varlen(const bf16_t* __restrict__ Q,
                                                              const bf16_t* __restrict__ K,
                                                              const bf16_t* __restrict__ Vt, bf16_t* __restrict__ O,
                                                              int ldo, int Npad, const int4* __restrict__ tasks,
                                                              const int* __restrict__ out_off, int nqb, int heads,
-                                                             int total) {
-    __shared__ __attribute__((aligned(16))) char smem[3 * KTILE_BYTES + 3 * VTILE_BYTES];
+                                                             int total, size_t lo_off, int lo_col) {
+    __shared__ __attribute__((aligned(16))) char smem[3 * Slots<SPLIT>::K + 3 * Slots<SPLIT>::V];
     const int per_xcd = (int)gridDim.x >> 3;
     const int logical = ((int)blockIdx.x & 7) * per_xcd + ((int)blockIdx.x >> 3);
     if (logical >= total) return;
@@ -378,9 +499,9 @@ __global__ __launch_bounds__(256, 1) void k_attention_varlen(const bf16_t* __res
     const int4 tk = tasks[t];  // q_off, q_len, kv_off, kv_len
     if (qb * 256 >= tk.y || tk.w <= 0) return;
     const int qpad = (tk.y + 63) & ~63;
-    attention_tile_pipe(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
-                        Vt + ((size_t)h * Npad + tk.z) * 64, tk.w, tk.y, qpad, qb, O + (size_t)out_off[t] * ldo + h * 64,
-                        ldo);
+    attention_tile_pipe<SPLIT>(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
+                               Vt + ((size_t)h * Npad + tk.z) * 64, tk.w, tk.y, qpad, qb,
+                               O + (size_t)out_off[t] * ldo + h * 64, ldo, lo_off, lo_col);
 }
 
 // ViT tasks: image b attends its own segment [b * Tpad, b * Tpad + T) in every head;
@@ -392,17 +513,18 @@ __global__ void k_vit_tasks(int4* __restrict__ tasks, int* __restrict__ out_off,
     }
 }
 
-template <bool VIT>
+template <bool VIT, bool SPLIT = false>
 int varlen_launch(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,
-                  const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s) {
+                  const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s, size_t lo_off = 0,
+                  int lo_col = 0) {
     if (ntasks <= 0) return MLG_OK;
     if (Npad % 64 || heads <= 0 || max_q <= 0) return MLG_EINVAL;
     const int nqb = (max_q + 255) / 256;
     const long total = (long)nqb * heads * ntasks;
     if (total > (1L << 30)) return MLG_EINVAL;
     const int grid = (int)((total + 7) & ~7L);
-    hipLaunchKernelGGL(k_attention_varlen<VIT>, dim3(grid), dim3(256), 0, s, Q, K, Vt, O, ldo, Npad, tasks, out_off,
-                       nqb, heads, (int)total);
+    hipLaunchKernelGGL((k_attention_varlen<VIT, SPLIT>), dim3(grid), dim3(256), 0, s, Q, K, Vt, O, ldo, Npad, tasks,
+                       out_off, nqb, heads, (int)total, lo_off, lo_col);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }
@@ -417,6 +539,18 @@ int mlg_attention(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O,
     hipLaunchKernelGGL(k_vit_tasks, dim3(1), dim3(256), 0, s, tasks, out_off, B, T, Tpad);
     MLG_LAUNCH_CHECK();
     return varlen_launch<true>(Q, K, Vt, O, 768, B * Tpad, 12, tasks, out_off, B, T, s);
+}
+
+// Split-bf16 ViT attention (MLG_VIT_SPLIT): Q, K, Vt hi planes with the lo planes
+// lo_off elements further; O rows of 1536 = [hi | lo]
+int mlg_attention_split(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int B, int T, int Tpad,
+                        size_t lo_off, int32_t* task_ws, hipStream_t s) {
+    if (B <= 0 || T <= 0 || Tpad % 64 || Tpad < T || !task_ws || (long)B * Tpad * 64 >= (1L << 31)) return MLG_EINVAL;
+    int4* tasks = reinterpret_cast<int4*>(task_ws);
+    int* out_off = task_ws + 4 * B;
+    hipLaunchKernelGGL(k_vit_tasks, dim3(1), dim3(256), 0, s, tasks, out_off, B, T, Tpad);
+    MLG_LAUNCH_CHECK();
+    return varlen_launch<true, true>(Q, K, Vt, O, 1536, B * Tpad, 12, tasks, out_off, B, T, s, lo_off, 768);
 }
 
 int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,

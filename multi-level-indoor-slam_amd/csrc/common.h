@@ -35,6 +35,15 @@ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
     return (bf16_t)(pack_bf16x2(f, 0.0f) & 0xffffu);
 }
 
+// Split-bf16 pairs (MLG_VIT_SPLIT): hi = bf16(x) (RNE), lo = bf16(x - hi); x - hi is exact
+// in f32, so x = hi + lo to 2^-17 relative.  Four floats -> two packed bf16x2 each.
+__device__ __forceinline__ void split_bf16x4(float a, float b, float c, float d, uint2& hi, uint2& lo) {
+    hi.x = pack_bf16x2(a, b);
+    hi.y = pack_bf16x2(c, d);
+    lo.x = pack_bf16x2(a - __uint_as_float(hi.x << 16), b - __uint_as_float(hi.x & 0xffff0000u));
+    lo.y = pack_bf16x2(c - __uint_as_float(hi.y << 16), d - __uint_as_float(hi.y & 0xffff0000u));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -90,6 +90,22 @@ struct EpiBiasGeluBF16 {
     }
 };
 
+// y = gelu(acc + b) as the split pair: hi = bf16(y) at column n, lo = bf16(y - hi) at
+// column n + lo_col of the same row (the [hi | lo] A rows of the split fc2 GEMM).  The
+// exact erf form torch's nn.GELU() computes: gelu_poly2's 1e-6 absolute error would be
+// the largest error term of the split forward.
+struct EpiBiasGeluSplit {
+    bf16_t* C; int ldc; int lo_col; const float* bias;
+    __device__ static float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f)); }
+    __device__ void operator()(int m, int n, const f32x4& v) const {
+        const float4 b = *reinterpret_cast<const float4*>(bias + n);
+        uint2 h, l;
+        split_bf16x4(gelu(v[0] + b.x), gelu(v[1] + b.y), gelu(v[2] + b.z), gelu(v[3] + b.w), h, l);
+        *reinterpret_cast<uint2*>(C + (size_t)m * ldc + n) = h;
+        *reinterpret_cast<uint2*>(C + (size_t)m * ldc + lo_col + n) = l;
+    }
+};
+
 struct EpiResidual {  // X += gamma * (acc + b)   (attn.proj / mlp.fc2 + LayerScale + residual)
     float* X; int ldx; const float* bias; const float* gamma;
     __device__ void operator()(int m, int n, const f32x4& v) const {
@@ -130,6 +146,33 @@ struct EpiQKV {
 };
 
 // relu(acc + b) -> bf16, columns >= nvalid dropped (N padded to the tile width)
+// EpiQKV for the split forward: hi planes as EpiQKV, lo planes lo_off elements further
+struct EpiQKVSplit {
+    bf16_t* Q; bf16_t* K; bf16_t* Vt; const float* bias; int T, Tpad, Np; size_t lo_off;
+    __device__ void operator()(int m, int n, const f32x4& v) const {
+        const float4 b = *reinterpret_cast<const float4*>(bias + n);
+        const int bi = m / T, t = m - bi * T;
+        const int which = n / 768, c = n - which * 768, h = c >> 6, d = c & 63;
+        const size_t key = (size_t)bi * Tpad + t;
+        uint2 hi, lo;
+        split_bf16x4(v[0] + b.x, v[1] + b.y, v[2] + b.z, v[3] + b.w, hi, lo);
+        if (which < 2) {
+            bf16_t* p = (which == 0 ? Q : K) + ((size_t)h * Np + key) * 64 + d;
+            *reinterpret_cast<uint2*>(p) = hi;
+            *reinterpret_cast<uint2*>(p + lo_off) = lo;
+        } else {
+            bf16_t* p = Vt + (((size_t)h * (Np >> 6) + (key >> 6)) * 64 + d) * 64 + (key & 63);
+            const uint32_t e[4] = {hi.x & 0xffffu, hi.x >> 16, hi.y & 0xffffu, hi.y >> 16};
+            const uint32_t f[4] = {lo.x & 0xffffu, lo.x >> 16, lo.y & 0xffffu, lo.y >> 16};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                p[64 * i] = (bf16_t)e[i];
+                p[64 * i + lo_off] = (bf16_t)f[i];
+            }
+        }
+    }
+};
+
 struct EpiBiasReluBF16 {
     bf16_t* C; int ldc; const float* bias; int nvalid;
     __device__ void operator()(int m, int n, const f32x4& v) const {
@@ -450,9 +493,13 @@ __global__ __launch_bounds__(512, BK == 32 ? 4 : 2) void k_gemm(const bf16_t* __
 // so the next tile's first wait overlaps this tile's epilogue, and the epilogue's
 // stores drain while the next tile's MFMAs run.  Twice the MFMAs per barrier and
 // 0.375 fragment reads per MFMA (vs 0.5 at 64 x 64 per wave).
+// nk0 > 0: split-bf16 operands (MLG_VIT_SPLIT).  A rows are [A_hi | A_lo] (K0 = 64 nk0
+// each), W rows [W_hi | W_lo | W_hi] (K = 3 K0): K-tile t of W pairs with A K-tile t for
+// t < nk0 (hi . hi), t - nk0 for t < 2 nk0 (hi . lo, A_hi again) and t - nk0 beyond (A_lo
+// . W_hi), so the one f32 accumulator sums hi*hi + lo*hi + hi*lo over k in that order.
 template <class Epi>
 __global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
-                                                   int M, int N, int K, int lda, int ldw, Epi epi) {
+                                                   int M, int N, int K, int lda, int ldw, Epi epi, int nk0) {
     constexpr int BK = 64, TM = 256, TN = 256;
     constexpr int A_BYTES = TM * BK * 2, STAGE = (TM + TN) * BK * 2;  // 64 KiB
     constexpr int NA = 4, NB = 4;                                      // DMAs per wave per K-tile
@@ -494,11 +541,12 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A
     const bf16_t* sa = a_base(tile);
     const bf16_t* sb = b_base(tile);
     a_offsets(tile, oa);
-#define D256_DMA(ST, OA, SA, SB, k0)                                                                       \
+    auto ak = [&](int t) { return (nk0 > 0 && t >= nk0 ? t - nk0 : t) * BK; };  // A column of W K-tile t
+#define D256_DMA(ST, OA, SA, SB, t)                                                                        \
     {                                                                                                      \
         const unsigned b_ = lds_addr(ST);                                                                  \
-        const bf16_t* sa_ = (SA) + (k0);                                                                   \
-        const bf16_t* sb_ = (SB) + (k0);                                                                   \
+        const bf16_t* sa_ = (SA) + ak(t);                                                                  \
+        const bf16_t* sb_ = (SB) + (t) * BK;                                                               \
         _Pragma("unroll") for (int i = 0; i < NA; ++i) dma16s((OA)[i], sa_, b_ + da + i * 1024);           \
         _Pragma("unroll") for (int i = 0; i < NB; ++i) dma16s(ob[i], sb_, b_ + db + i * 1024);             \
     }
@@ -527,19 +575,19 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A
         a_offsets(next, na);
         const bf16_t* nsa = a_base(next);
         const bf16_t* nsb = b_base(next);
-        const int kn = next != tile ? 0 : (nk - 1) * BK;  // no next tile: harmless re-read
+        const int kn = next != tile ? 0 : nk - 1;  // K-tile of the last DMA (no next tile: harmless re-read)
         f32x4 acc[4][8];  // [n-tile][m-tile]
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int t = 0; t < nk; t += 2) {
-            D256_DMA(st1, oa, sa, sb, (t + 1) * BK);
+            D256_DMA(st1, oa, sa, sb, t + 1);
             D256_COMPUTE(st0);
             __builtin_amdgcn_s_waitcnt(0xF70);
             __builtin_amdgcn_s_barrier();
             if (t + 2 < nk) {
-                D256_DMA(st0, oa, sa, sb, (t + 2) * BK);
+                D256_DMA(st0, oa, sa, sb, t + 2);
             } else {
                 D256_DMA(st0, na, nsa, nsb, kn);  // K-tile 0 of the next output tile
             }
@@ -783,7 +831,7 @@ __global__ __launch_bounds__(512, 2) void k_conv256(ConvGeom g, const bf16_t* __
     for (; tile < tile_end; tile += per_xcd) {
         const int next = tile + per_xcd < tile_end ? tile + per_xcd : tile;
         const bf16_t* nsb = b_base(next);
-        const int kn = next != tile ? 0 : (nk - 1) * BK;  // no next tile: harmless re-read
+        const int kn = next != tile ? 0 : nk - 1;  // K-tile of the last DMA (no next tile: harmless re-read)
         f32x4 acc[4][JM];  // [n-tile][m-tile]
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -858,7 +906,7 @@ int launch(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int l
     } else if ((variant == 4 || variant == 5) && N % 256 == 0 && (K / 64) % 2 == 0) {
         const long ntiles = (long)(N / 256) * ((M + 255) / 256);
         const long grid = std::min<long>(g_num_cus, (ntiles + 7) / 8 * 8);  // persistent: <= 1 per CU
-        hipLaunchKernelGGL(dma::k_gemm256<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K, lda, ldw, epi);
+        hipLaunchKernelGGL(dma::k_gemm256<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K, lda, ldw, epi, 0);
     } else if (variant == 3 && N % dma::BN == 0 && (K / 32) % 3 == 0) {
         hipLaunchKernelGGL((dma::k_gemm<Epi, 32>), dim3((unsigned)nwg_dma), dim3(512), 0, s, A, W, M, N, K, lda, ldw,
                            epi);
@@ -874,7 +922,44 @@ int launch(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int l
     return MLG_OK;
 }
 
+// Split-bf16 GEMM (MLG_VIT_SPLIT): A rows [A_hi | A_lo] of K0 each (lda >= 2 K0), W rows
+// [W_hi | W_lo | W_hi] (ldw >= 3 K0); the persistent 256 x 256 tile with the A K-tile remap
+template <class Epi>
+int launch_split(const bf16_t* A, const bf16_t* W, int M, int N, int K0, int lda, int ldw, Epi epi, hipStream_t s) {
+    g_num_cus = num_cus();
+    if (M <= 0 || N % 256 || K0 <= 0 || K0 % 64 || ((3 * K0 / 64) % 2) || lda < 2 * K0 || ldw < 3 * K0 ||
+        (lda % 8) || (ldw % 8))
+        return MLG_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W)) & 15) return MLG_EINVAL;
+    const long ntiles = (long)(N / 256) * ((M + 255) / 256);
+    const long grid = std::min<long>(g_num_cus, (ntiles + 7) / 8 * 8);
+    hipLaunchKernelGGL(dma::k_gemm256<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, 3 * K0, lda, ldw, epi,
+                       K0 / 64);
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}
+
 }  // namespace
+
+int mlg_gemm_qkv_split(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* Q, bf16_t* Kh, bf16_t* V, int M,
+                       int T, int Tpad, size_t lo_off, hipStream_t s) {
+    if (M % T) return MLG_EINVAL;
+    return launch_split(A, W, M, 3 * 768, 768, 2 * 768, 3 * 768,
+                        EpiQKVSplit{Q, Kh, V, bias, T, Tpad, (M / T) * Tpad, lo_off}, s);
+}
+int mlg_gemm_residual_split(const bf16_t* A, const bf16_t* W, const float* bias, const float* gamma, float* X, int M,
+                            int N, int K0, hipStream_t s) {
+    return launch_split(A, W, M, N, K0, 2 * K0, 3 * K0, EpiResidual{X, N, bias, gamma}, s);
+}
+int mlg_gemm_bias_gelu_split(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K0,
+                             hipStream_t s) {
+    return launch_split(A, W, M, N, K0, 2 * K0, 3 * K0, EpiBiasGeluSplit{C, 2 * N, N, bias}, s);
+}
+int mlg_gemm_patch_split(const bf16_t* A, const bf16_t* W, const float* bias, const float* pos, float* X, int M, int P,
+                         int Kpad, hipStream_t s) {
+    if (M % P) return MLG_EINVAL;
+    return launch_split(A, W, M, 768, Kpad, 2 * Kpad, 3 * Kpad, EpiPatch{X, bias, pos, P}, s);
+}
 
 int mlg_gemm_f32out(const bf16_t* A, const bf16_t* W, float* C, int M, int N, int K, hipStream_t s) {
     return launch(A, W, M, N, K, K, K, EpiF32{C, N}, s);

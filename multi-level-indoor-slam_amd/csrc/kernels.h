@@ -70,9 +70,21 @@ int mlg_attention(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O,
 
 // vit_ops.hip
 int mlg_preprocess_patches(const uint8_t* img, int B, int H, int W, int C, long img_stride, int S, int Kpad,
-                           int swap_rb, bf16_t* out, hipStream_t s);
+                           int swap_rb, bf16_t* out, hipStream_t s, int split = 0);
 int mlg_cls_rows(float* X, const float* cls, const float* pos, int B, int T, hipStream_t s);
 int mlg_layernorm_bf16(const float* X, const float* g, const float* b, bf16_t* Y, int M, hipStream_t s);
+// split-bf16 forward (MLG_VIT_SPLIT): [hi | lo] operand rows, weights [W_hi | W_lo | W_hi]
+int mlg_layernorm_split(const float* X, const float* g, const float* b, bf16_t* Y, int M, hipStream_t s);
+int mlg_gemm_qkv_split(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* Q, bf16_t* K, bf16_t* Vt, int M,
+                       int T, int Tpad, size_t lo_off, hipStream_t s);
+int mlg_gemm_residual_split(const bf16_t* A, const bf16_t* W, const float* bias, const float* gamma, float* X, int M,
+                            int N, int K0, hipStream_t s);
+int mlg_gemm_bias_gelu_split(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K0,
+                             hipStream_t s);
+int mlg_gemm_patch_split(const bf16_t* A, const bf16_t* W, const float* bias, const float* pos, float* X, int M, int P,
+                         int Kpad, hipStream_t s);
+int mlg_attention_split(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int B, int T, int Tpad,
+                        size_t lo_off, int32_t* task_ws, hipStream_t s);
 int mlg_final_norm_gem(const float* X, const float* g, const float* b, float* local, float* partial, float* desc,
                        int B, int T, int mean_pool, hipStream_t s);
 size_t mlg_gem_partial_bytes(int B);

@@ -831,10 +831,16 @@ __global__ __launch_bounds__(256) void k_xcorr_finish(const float* __restrict__ 
 
 }  // namespace
 
+// pairs per k_xcorr_tiles launch: grid z stays far below the 65535 grid-dimension cap and
+// the per-tile maxima (rowp / colp) take at most 2 * XC_SLICE * t * L floats of workspace
+// (346 MB at L = 528) however many pairs one call scores
+constexpr int XC_SLICE = 16384;
+
 size_t mlg_xcorr_batch_ws_bytes(int F, int L, int D, int P) {
     if (F <= 0 || L <= 0 || D <= 0 || P <= 0) return 0;
     const size_t t = (size_t)((L + SBM - 1) / SBM);
-    return (((size_t)F * L * D * 4 + 255) & ~(size_t)255) + 2 * (size_t)P * t * L * 4;
+    const size_t ps = (size_t)(P < XC_SLICE ? P : XC_SLICE);
+    return (((size_t)F * L * D * 4 + 255) & ~(size_t)255) + 2 * ps * t * L * 4;
 }
 
 int mlg_xcorr_batch_run(const float* feats, int F, int L, int D, const int32_t* qa, const int32_t* qb, int P,
@@ -845,11 +851,14 @@ int mlg_xcorr_batch_run(const float* feats, int F, int L, int D, const int32_t* 
     float* fn = (float*)ws;
     const int t = (L + SBM - 1) / SBM;
     float* rowp = (float*)((char*)ws + (((size_t)F * L * D * 4 + 255) & ~(size_t)255));
-    float* colp = rowp + (size_t)P * t * L;
+    float* colp = rowp + (size_t)(P < XC_SLICE ? P : XC_SLICE) * t * L;
     // the reference's q / (||q|| + 1e-8) per row, numpy-exact (one thread per row)
     hipLaunchKernelGGL(k_row_normalize, dim3((F * L + 63) / 64), dim3(64), 0, s, feats, fn, F * L, D, D, nullptr);
-    hipLaunchKernelGGL(k_xcorr_tiles, dim3(t, t, P), dim3(256), 0, s, fn, L, D, qa, qb, rowp, colp);
-    hipLaunchKernelGGL(k_xcorr_finish, dim3(P), dim3(256), 0, s, rowp, colp, L, t, t, score);
+    for (int p0 = 0; p0 < P; p0 += XC_SLICE) {  // stream order: a slice reuses rowp / colp after the last
+        const int ps = P - p0 < XC_SLICE ? P - p0 : XC_SLICE;
+        hipLaunchKernelGGL(k_xcorr_tiles, dim3(t, t, ps), dim3(256), 0, s, fn, L, D, qa + p0, qb + p0, rowp, colp);
+        hipLaunchKernelGGL(k_xcorr_finish, dim3(ps), dim3(256), 0, s, rowp, colp, L, t, t, score + p0);
+    }
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(SL_THREADS) void k_salad_head(const bf16_t* __restr
 int mlg_salad_head(const bf16_t* xn, const float* Y, int B, int T, const float* wt1, const float* bt1,
                    const float* wt2, const float* bt2, float dust, float* desc, hipStream_t s) {
     const int n = T - 1;
-    if (B <= 0 || n <= SL_C || n > SL_NMAX) return MLG_EINVAL;
+    if (B <= 0 || n <= SL_C || (n | 1) > SL_NMAX) return MLG_EINVAL;  // rows are (n | 1) apart in LDS
     hipLaunchKernelGGL(k_salad_head, dim3(B), dim3(SL_THREADS), 0, s, xn, Y, T, wt1, bt1, wt2, bt2, dust, desc);
     MLG_LAUNCH_CHECK();
     return MLG_OK;

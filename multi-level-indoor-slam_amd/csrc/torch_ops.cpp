@@ -65,8 +65,22 @@ Tensor workspace(size_t bytes, const Tensor& like) {
 constexpr int kVitBlockTensors = 14;
 constexpr int kVitTensors = 4 + MLG_VIT_DEPTH * kVitBlockTensors + 2;
 
-mlg_vit_weights vit_weights(const std::vector<Tensor>& w) {
+// split: weights packed for MLG_VIT_SPLIT ([W_hi | W_lo | W_hi], 3x the reduction dim)
+mlg_vit_weights vit_weights(const std::vector<Tensor>& w, bool split = false) {
     TORCH_CHECK((int)w.size() == kVitTensors, "vit weights: expected ", kVitTensors, " tensors, got ", w.size());
+    const int64_t m = split ? 3 : 1;
+    auto want_n = [&](const Tensor& t, int64_t n, const char* what) {
+        TORCH_CHECK(t.numel() == n * m && t.scalar_type() == at::kBFloat16, "vit weights: ", what, " must be bf16 with ",
+                    n * m, " elements", split ? " (split packing)" : "");
+    };
+    want_n(w[0], 768LL * MLG_VIT_PATCH_K, "patch_w");
+    for (int i = 0; i < MLG_VIT_DEPTH; ++i) {
+        const Tensor* b = &w[4 + i * kVitBlockTensors];
+        want_n(b[2], 2304LL * 768, "qkv_w");
+        want_n(b[4], 768LL * 768, "proj_w");
+        want_n(b[9], 3072LL * 768, "fc1_w");
+        want_n(b[11], 768LL * 3072, "fc2_w");
+    }
     mlg_vit_weights s;
     std::memset(&s, 0, sizeof(s));
     s.patch_w = cp<uint16_t>(w[0]);
@@ -104,7 +118,7 @@ void vit_forward_into(const Tensor& frames, at::TensorList w, int64_t image_size
     }
     TORCH_CHECK(max_batch > 0, "max_batch must be positive");
     std::vector<Tensor> wv(w.begin(), w.end());
-    const mlg_vit_weights s = vit_weights(wv);
+    const mlg_vit_weights s = vit_weights(wv, (flags & MLG_VIT_SPLIT) != 0);
     c10::DeviceGuard g(frames.device());
     const int64_t nb_max = std::min(B, max_batch);
     Tensor ws = workspace(mlg_vit_workspace_bytes((int)nb_max, (int)image_size), frames);

@@ -44,7 +44,8 @@ struct PrepParams {
     int H, W, C, S, grid, P, Kpad;
     int swap_rb;         // 1: BGR(A) -> RGB (CricaVPR); 0: channels fed as stored (AnyLoc, :495-505)
     long img_stride;     // bytes between images
-    bf16_t* out;         // [B*P, Kpad]
+    bf16_t* out;         // [B*P, Kpad], or [B*P, 2 Kpad] = [hi | lo] rows when split
+    int split;           // MLG_VIT_SPLIT: split-bf16 pairs
 };
 
 __global__ __launch_bounds__(256) void k_preprocess_patches(PrepParams pp, int total_chunks) {
@@ -64,7 +65,7 @@ __global__ __launch_bounds__(256) void k_preprocess_patches(PrepParams pp, int t
         const int b = row / pp.P, p = row - b * pp.P;
         const int py = p / pp.grid, px = p - py * pp.grid;
         const uint8_t* src = pp.img + (size_t)b * pp.img_stride;
-        uint32_t packed[4];
+        float vals[8];
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
             float v2[2];
@@ -96,12 +97,27 @@ __global__ __launch_bounds__(256) void k_preprocess_patches(PrepParams pp, int t
                 }
                 v2[u] = val;
             }
-            packed[e >> 1] = pack_bf16x2(v2[0], v2[1]);
+            vals[e] = v2[0];
+            vals[e + 1] = v2[1];
         }
-        *reinterpret_cast<uint4*>(pp.out + (size_t)row * pp.Kpad + kc * 8) =
-            make_uint4(packed[0], packed[1], packed[2], packed[3]);
+        if (pp.split) {
+            uint2 h0, l0, h1, l1;
+            split_bf16x4(vals[0], vals[1], vals[2], vals[3], h0, l0);
+            split_bf16x4(vals[4], vals[5], vals[6], vals[7], h1, l1);
+            bf16_t* o = pp.out + (size_t)row * 2 * pp.Kpad + kc * 8;
+            *reinterpret_cast<uint4*>(o) = make_uint4(h0.x, h0.y, h1.x, h1.y);
+            *reinterpret_cast<uint4*>(o + pp.Kpad) = make_uint4(l0.x, l0.y, l1.x, l1.y);
+        } else {
+            *reinterpret_cast<uint4*>(pp.out + (size_t)row * pp.Kpad + kc * 8) =
+                make_uint4(pack_bf16x2(vals[0], vals[1]), pack_bf16x2(vals[2], vals[3]), pack_bf16x2(vals[4], vals[5]),
+                           pack_bf16x2(vals[6], vals[7]));
+        }
     }
 }
+
+// LayerNorm as split-bf16 pairs: rows of 1536, hi in columns 0..767, lo in 768..1535
+__global__ __launch_bounds__(256) void k_layernorm_split(const float* __restrict__ X, const float* __restrict__ g,
+                                                         const float* __restrict__ b, bf16_t* __restrict__ Y, int M);
 
 // X[b, 0, :] = cls + pos[0]
 __global__ void k_cls_rows(float* X, const float* cls, const float* pos, int T) {
@@ -147,6 +163,21 @@ __global__ __launch_bounds__(256) void k_layernorm_bf16(const float* __restrict_
     for (int i = 0; i < 3; ++i)
         *reinterpret_cast<uint2*>(Y + (size_t)row * 768 + i * 256 + lane * 4) =
             make_uint2(pack_bf16x2(y[i].x, y[i].y), pack_bf16x2(y[i].z, y[i].w));
+}
+
+__global__ __launch_bounds__(256) void k_layernorm_split(const float* __restrict__ X, const float* __restrict__ g,
+                                                         const float* __restrict__ b, bf16_t* __restrict__ Y, int M) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= M) return;
+    float4 y[3];
+    ln_row(X + (size_t)row * 768, g, b, lane, y);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        uint2 h, l;
+        split_bf16x4(y[i].x, y[i].y, y[i].z, y[i].w, h, l);
+        *reinterpret_cast<uint2*>(Y + (size_t)row * 1536 + i * 256 + lane * 4) = h;
+        *reinterpret_cast<uint2*>(Y + (size_t)row * 1536 + 768 + i * 256 + lane * 4) = l;
+    }
 }
 
 // Final norm + CricaVPR heads.  get_intermediate_layers strips CLS (token 0) and the
@@ -209,10 +240,10 @@ __global__ void k_gem_finish(const float* __restrict__ partial, float* __restric
 }  // namespace
 
 int mlg_preprocess_patches(const uint8_t* img, int B, int H, int W, int C, long img_stride, int S, int Kpad,
-                           int swap_rb, bf16_t* out, hipStream_t s) {
+                           int swap_rb, bf16_t* out, hipStream_t s, int split) {
     if (B <= 0 || H < 1 || W < 1 || !(C == 1 || C == 3 || C == 4) || S % 14 || Kpad < 588 || Kpad % 8)
         return MLG_EINVAL;
-    PrepParams pp{img, H, W, C, S, S / 14, (S / 14) * (S / 14), Kpad, swap_rb, img_stride, out};
+    PrepParams pp{img, H, W, C, S, S / 14, (S / 14) * (S / 14), Kpad, swap_rb, img_stride, out, split};
     const long total = (long)B * pp.P * (Kpad / 8);
     const int blocks = (int)std::min<long>((total + 255) / 256, 256L * 16);
     hipLaunchKernelGGL(k_preprocess_patches, dim3(blocks), dim3(256), 0, s, pp, (int)total);
@@ -229,6 +260,13 @@ int mlg_cls_rows(float* X, const float* cls, const float* pos, int B, int T, hip
 int mlg_layernorm_bf16(const float* X, const float* g, const float* b, bf16_t* Y, int M, hipStream_t s) {
     if (M <= 0) return MLG_EINVAL;
     hipLaunchKernelGGL(k_layernorm_bf16, dim3((M + 3) / 4), dim3(256), 0, s, X, g, b, Y, M);
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}
+
+int mlg_layernorm_split(const float* X, const float* g, const float* b, bf16_t* Y, int M, hipStream_t s) {
+    if (M <= 0) return MLG_EINVAL;
+    hipLaunchKernelGGL(k_layernorm_split, dim3((M + 3) / 4), dim3(256), 0, s, X, g, b, Y, M);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

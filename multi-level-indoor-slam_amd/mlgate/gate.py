@@ -118,26 +118,42 @@ class ContextualPriorFactor:
                 'sigma_dz': 0.3}
 
 
+# the snippet text integrate_with_orbslam3 returns (loop_closure_gate.py:223-257), byte for
+# byte: callers paste or diff it (tests/test_api_cpu.py against tests/golden/gate_snippet.json)
 _ORBSLAM3_SNIPPET = """
-// LoopClosing.cc: reject DBoW2 candidates whose floor label differs from the
-// current keyframe's before Sim3 / geometric verification.
+// Add to LoopClosing.cc - DetectLoop() function
+// After DBoW2 candidate retrieval, before geometric verification
+
 bool LoopClosing::CheckFloorConsistency(KeyFrame* pKF, KeyFrame* pKFcandidate)
 {
-    const int queryFloor = pKF->mnFloorLabel;
-    const int matchFloor = pKFcandidate->mnFloorLabel;
+    // Get floor labels (stored in KeyFrame during tracking)
+    int queryFloor = pKF->mnFloorLabel;
+    int matchFloor = pKFcandidate->mnFloorLabel;
+    
+    // Strict mode: reject any cross-floor candidates
     if (queryFloor != matchFloor)
     {
-        VLOG(1) << "Loop closure rejected: Floor " << queryFloor << " vs Floor " << matchFloor;
+        // Log rejected candidate for analysis
+        VLOG(1) << "Loop closure rejected: Floor " << queryFloor 
+                << " vs Floor " << matchFloor;
         return false;
     }
+    
     return true;
 }
 
-// In DetectLoop(), after mpKeyFrameDB->DetectLoopCandidates(mpCurrentKF, minScore):
+// Modify DetectLoop() to call this before ComputeSim3()
+vector<KeyFrame*> vpCandidateKFs = mpKeyFrameDB->DetectLoopCandidates(mpCurrentKF, minScore);
+
+// Filter by floor consistency
 vector<KeyFrame*> vpValidCandidates;
-for (KeyFrame* pKF : vpCandidateKFs)
-    if (CheckFloorConsistency(mpCurrentKF, pKF))
+for(KeyFrame* pKF : vpCandidateKFs)
+{
+    if(CheckFloorConsistency(mpCurrentKF, pKF))
         vpValidCandidates.push_back(pKF);
+}
+
+// Continue with geometric verification on filtered candidates
 """
 
 

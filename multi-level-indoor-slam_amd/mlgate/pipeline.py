@@ -160,7 +160,8 @@ class DeviceGate:
     def __init__(self, frames, timestamps, floor_labels, world=1, rank=0, device='cuda', k=10,
                  similarity_threshold=0.5, min_time_gap=10.0, strict_mode=True, retrieval_floor_gating=True,
                  verifier_floor_gating=True, verify=True, K=None, min_inliers=20, min_inlier_ratio=0.25,
-                 vit_batch=123, sp_batch=64, lg_chunk=1024, max_keypoints=2048, vit_state_dict=None, record=False):
+                 vit_batch=123, sp_batch=64, lg_chunk=1024, max_keypoints=2048, vit_state_dict=None, record=False,
+                 vit_precise=True):
         import torch
         from . import distributed as mdist
         from .lightglue import LightGlueGPU
@@ -194,7 +195,9 @@ class DeviceGate:
         num = np.array([np.nan if v is None else float(v) for v in lab], np.float64)
         self.f_num = torch.as_tensor(num, device=self.dev)
         sd = vit_state_dict if vit_state_dict is not None else synthetic_state_dict(0)
-        self.eng = VitB14(sd, device=self.dev, max_batch=vit_batch)
+        # vit_precise: the split-bf16 ViT (MLG_VIT_SPLIT), whose descriptors follow the fp32
+        # network closely enough that the kNN ranks near-ties as the fp32 reference does
+        self.eng = VitB14(sd, device=self.dev, max_batch=vit_batch, precise=vit_precise)
         self.gather = mdist.RowGather(N, EMBED, world, self.dev)
         self.desc_loc = (self.gather.out[self.lo:self.hi] if world == 1
                          else torch.empty(self.n_local, EMBED, device=self.dev))
@@ -218,6 +221,7 @@ class DeviceGate:
         # is_valid) in self.last_pair_results (host arrays in verification order)
         self.record = record
         self.last_pair_results = None
+        self.last_retrieval = None
 
     def _dedup(self):
         """Match each unordered pair once (MLGATE_LG_DEDUP=0: every ordered pair, for A/B)."""
@@ -245,6 +249,8 @@ class DeviceGate:
         idx, sim, valid, count = retrieval.knn_gate(self.gather.out, self.t_all, self.f_all, self.hf_all, self.gap,
                                                     self.thr, self.k, self.retrieval_floor_gating, q0=self.lo,
                                                     Q=self.n_local, totals=self.totals)
+        if self.record:  # this rank's query rows: idx / sim / valid [Q, k], count [Q] (host)
+            self.last_retrieval = tuple(x.cpu().numpy() for x in (idx, sim, valid, count))
         k = idx.shape[1]
         live = torch.arange(k, device=self.dev)[None, :] < count[:, None].long()
         out = {"matches": int(count.sum()), "retrieval_floor_rejected": 0, "skipped_floor_mismatch": 0,
@@ -271,8 +277,9 @@ class DeviceGate:
             same = (ha & hb & (self.f_all[pa_t.long()] == self.f_all[pb_t.long()])) | (~ha & ~hb)
             out["skipped_floor_mismatch"] = int((~same).sum())
             pa_t, pb_t = pa_t[same], pb_t[same]
-        # pair-level load balance across ranks (features are all-gathered, so any rank
-        # can verify any pair; the union of the slices is the global pair list)
+        # pair-level load balance across ranks: the pairs are re-balanced first (the union
+        # of the slices is the global pair list), then FeatureExchange delivers each rank
+        # exactly the SuperPoint features its own slice touches
         dedup = self._dedup()
         pa_t, pb_t = self.mdist.balanced_pairs(pa_t, pb_t, self.world, self.rank, group_reverse=dedup)
         pa, pb = pa_t.cpu().numpy(), pb_t.cpu().numpy()
@@ -351,7 +358,11 @@ class DeviceGate:
                 n_valid_t += ok.sum()
                 if rec is not None:
                     rec.append((sel, n, inl, ok))
-                # the floor gate on the geometrically valid pairs
+                # the floor gate on the geometrically valid pairs.  Deviation, by design: a
+                # None label is NaN here and never rejects, where the reference's host gate
+                # computes abs(None - None) and raises TypeError (loop_closure_gate.py:89;
+                # the drop-in SemanticLoopClosureGate keeps that TypeError,
+                # tests/test_api_cpu.py::test_gate_none_labels_raise_nan_labels_accept)
                 gate_rej_t += (ok & ((self.f_num[ta] - self.f_num[tb]).abs() > self.limit)).sum()
         main.wait_stream(side)
         n_valid, gate_rej = int(n_valid_t), int(gate_rej_t)

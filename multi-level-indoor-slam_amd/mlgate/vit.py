@@ -36,10 +36,30 @@ def resample_pos_embed(pos_embed, grid):
     return torch.cat((pos_embed[:, :1], patch), dim=1).contiguous()
 
 
-class VitB14:
-    """Packed device weights + workspace for batched CricaVPR descriptor extraction."""
+MLG_VIT_SPLIT = 4  # include/mlgate.h
 
-    def __init__(self, state_dict, device="cuda", image_size=322, max_batch=64, pool="gem", swap_rb=True):
+
+def split_weight(w):
+    """[out, in] float32 -> bf16 [out, 3 in] = [W_hi | W_lo | W_hi] (MLG_VIT_SPLIT packing:
+    hi = bf16(W), lo = bf16(W - hi); the kernel pairs the three K-blocks with A_hi, A_hi,
+    A_lo)."""
+    w = w.to(torch.float32)
+    hi = w.to(torch.bfloat16)
+    lo = (w - hi.to(torch.float32)).to(torch.bfloat16)
+    return torch.cat([hi, lo, hi], dim=1).contiguous()
+
+
+class VitB14:
+    """Packed device weights + workspace for batched CricaVPR descriptor extraction.
+
+    precise=True selects the split-bf16 forward (MLG_VIT_SPLIT, include/mlgate.h): every
+    GEMM and attention operand carried as a hi + lo bf16 pair, three MFMA products each.
+    Descriptors then agree with the fp32 network to ~1e-11 (1 - cos) instead of ~1e-5, and
+    kNN rankings over near-identical descriptors follow the fp32 reference's
+    (tests/test_bench_parity_gpu.py)."""
+
+    def __init__(self, state_dict, device="cuda", image_size=322, max_batch=64, pool="gem", swap_rb=True,
+                 precise=False):
         self.device = _native.require_device(device)
         if image_size % PATCH:
             raise ValueError("image_size must be a multiple of 14")
@@ -47,7 +67,9 @@ class VitB14:
         self.n_patches = self.grid * self.grid
         self.n_local = self.n_patches - 1  # tokens 2.. of get_intermediate_layers (CLS + patch 0 dropped)
         self.max_batch = max_batch
-        self.flags = (1 if pool == "mean" else 0) | (0 if swap_rb else 2)  # MLG_VIT_POOL_MEAN / KEEP_CHANNELS
+        self.precise = bool(precise)
+        self.flags = ((1 if pool == "mean" else 0) | (0 if swap_rb else 2)  # MLG_VIT_POOL_MEAN / KEEP_CHANNELS
+                      | (MLG_VIT_SPLIT if self.precise else 0))
         self._w = self._pack(state_dict)
 
     # ------------------------------------------------------------ weights
@@ -60,7 +82,12 @@ class VitB14:
         f32, bf = torch.float32, torch.bfloat16
         pw = torch.as_tensor(np.asarray(sd["patch_embed.proj.weight"], np.float32)).reshape(EMBED, -1)
         pos = torch.as_tensor(np.asarray(sd["pos_embed"], np.float32)).to(self.device)
-        w = [self._dev(F.pad(pw, (0, PATCH_K - pw.shape[1])), bf), self._dev(sd["patch_embed.proj.bias"], f32),
+
+        def gemm_w(a):  # a GEMM weight in the layout of this forward
+            t = a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
+            t = t.to(self.device, torch.float32)
+            return split_weight(t) if self.precise else t.to(bf).contiguous()
+        w = [gemm_w(F.pad(pw, (0, PATCH_K - pw.shape[1]))), self._dev(sd["patch_embed.proj.bias"], f32),
              self._dev(np.asarray(sd["cls_token"], np.float32).reshape(EMBED), f32),
              self._dev(resample_pos_embed(pos, self.grid).reshape(-1, EMBED), f32)]
         names = {"norm1_w": "norm1.weight", "norm1_b": "norm1.bias", "qkv_w": "attn.qkv.weight",
@@ -69,7 +96,8 @@ class VitB14:
                  "fc1_b": "mlp.fc1.bias", "fc2_w": "mlp.fc2.weight", "fc2_b": "mlp.fc2.bias", "ls2": "ls2.gamma"}
         for i in range(DEPTH):
             for f in BLOCK_ORDER:
-                w.append(self._dev(sd[f"blocks.{i}." + names[f]], bf if f in BF16_FIELDS else f32))
+                v = sd[f"blocks.{i}." + names[f]]
+                w.append(gemm_w(v) if f in BF16_FIELDS else self._dev(v, f32))
         w += [self._dev(sd["norm.weight"], f32), self._dev(sd["norm.bias"], f32)]
         return w
 

@@ -18,7 +18,7 @@ def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(_SO) or os.path.getmtime(_SO) < max(
-                os.path.getmtime(os.path.join(_HERE, "csrc", f)) for f in ("oracle.c", "orb.c")):
+                os.path.getmtime(os.path.join(_HERE, "csrc", f)) for f in ("oracle.c", "orb.c", "ransac_cv.c")):
             build()
         _lib = ctypes.CDLL(_SO)
         _lib.orc_resize_linear_u8.restype = ctypes.c_int
@@ -27,6 +27,8 @@ def lib():
         _lib.orc_knn_rows.restype = ctypes.c_int
         _lib.orc_orb_detect.restype = ctypes.c_int
         _lib.orc_bf_match.restype = ctypes.c_int
+        _lib.orc_five_point.restype = ctypes.c_int
+        _lib.orc_essential_ransac.restype = ctypes.c_int
     return _lib
 
 
@@ -65,3 +67,27 @@ def knn_rows(S, q0, t, floor, has_floor, min_gap, thr, k, gating):
     lib().orc_knn_rows(ptr(S), Q, N, q0, ptr(t), ptr(floor), ptr(has_floor), ctypes.c_double(min_gap),
                        ctypes.c_float(thr), k, int(gating), ptr(idx), ptr(sim), ptr(valid), ptr(count))
     return idx, sim, valid, count
+
+
+def five_point(q1, q2):
+    """oracle/csrc/ransac_cv.c orc_five_point: list of 3x3 essential matrices."""
+    q1 = np.ascontiguousarray(q1, dtype=np.float64)
+    q2 = np.ascontiguousarray(q2, dtype=np.float64)
+    out = np.zeros((10, 9), np.float64)
+    n = lib().orc_five_point(ptr(q1), ptr(q2), ptr(out))
+    return [out[i].reshape(3, 3) for i in range(n)]
+
+
+def essential_ransac(k1, k2, K, thr=3.0, confidence=0.999, max_iters=1000):
+    """oracle/csrc/ransac_cv.c orc_essential_ransac: (model 3x3 or None, bool mask, inliers)."""
+    k1 = np.ascontiguousarray(k1, dtype=np.float32)
+    k2 = np.ascontiguousarray(k2, dtype=np.float32)
+    Kc = np.ascontiguousarray(K, dtype=np.float64)
+    n = len(k1)
+    mask = np.zeros(max(n, 1), np.uint8)
+    E = np.zeros(9, np.float64)
+    g = lib().orc_essential_ransac(ptr(k1), ptr(k2), n, ptr(Kc), ctypes.c_double(thr), ctypes.c_double(confidence),
+                                   max_iters, ptr(mask), ptr(E))
+    if g < 0:
+        raise ValueError("orc_essential_ransac: more than 2056 matches")
+    return (E.reshape(3, 3) if g > 0 else None), mask[:n].astype(bool), int(g)

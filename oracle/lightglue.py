@@ -54,8 +54,11 @@ def rotate_half(x):
 
 
 class Oracle:
-    def __init__(self, sd, emulate_bf16=True):
-        self.sd = {k: torch.as_tensor(np.asarray(v, np.float32)) for k, v in sd.items()}
+    def __init__(self, sd, emulate_bf16=True, device=None):
+        # device: the CPU by default; a bench-scale checker tool may place the fp32
+        # restatement on the GPU box's device (same ops, fp32 throughout)
+        self.dev = torch.device(device or "cpu")
+        self.sd = {k: torch.as_tensor(np.asarray(v, np.float32)).to(self.dev) for k, v in sd.items()}
         self.bf = emulate_bf16
 
     def lin(self, x, name):
@@ -127,11 +130,12 @@ class Oracle:
         s = scores[:-1, :-1]
         max0, max1 = s.max(1), s.max(0)
         m0, m1 = max0.indices, max1.indices
-        mutual0 = torch.arange(len(m0)) == m1[m0]
-        mutual1 = torch.arange(len(m1)) == m0[m1]
+        dev = s.device
+        mutual0 = torch.arange(len(m0), device=dev) == m1[m0]
+        mutual1 = torch.arange(len(m1), device=dev) == m0[m1]
         max0_exp = max0.values.exp()
-        ms0 = torch.where(mutual0, max0_exp, torch.zeros(()))
-        ms1 = torch.where(mutual1, ms0[m1], torch.zeros(()))
+        ms0 = torch.where(mutual0, max0_exp, torch.zeros((), device=dev))
+        ms1 = torch.where(mutual1, ms0[m1], torch.zeros((), device=dev))
         valid0 = mutual0 & (ms0 > th)
         valid1 = mutual1 & valid0[m1]
         return torch.where(valid0, m0, -1), torch.where(valid1, m1, -1), ms0, ms1
@@ -144,14 +148,15 @@ class Oracle:
         decision is numerically ambiguous when lo <= depth_confidence < hi.  force_stop = s
         replaces the early-stop test by "stop after layer s" (to compare matches when a
         bf16 kernel took the other side of an ambiguous decision)."""
-        k0 = normalize_keypoints(torch.as_tensor(kpts0, dtype=torch.float32))
-        k1 = normalize_keypoints(torch.as_tensor(kpts1, dtype=torch.float32))
-        x0 = torch.as_tensor(desc0, dtype=torch.float32).clone()
-        x1 = torch.as_tensor(desc1, dtype=torch.float32).clone()
+        dev = self.dev
+        k0 = normalize_keypoints(torch.as_tensor(kpts0, dtype=torch.float32, device=dev))
+        k1 = normalize_keypoints(torch.as_tensor(kpts1, dtype=torch.float32, device=dev))
+        x0 = torch.as_tensor(desc0, dtype=torch.float32, device=dev).clone()
+        x1 = torch.as_tensor(desc1, dtype=torch.float32, device=dev).clone()
         m, n = len(x0), len(x1)
         e0, e1 = self.posenc(k0), self.posenc(k1)
-        ind0, ind1 = torch.arange(m), torch.arange(n)
-        prune0, prune1 = torch.ones(m, dtype=torch.long), torch.ones(n, dtype=torch.long)
+        ind0, ind1 = torch.arange(m, device=dev), torch.arange(n, device=dev)
+        prune0, prune1 = torch.ones(m, dtype=torch.long, device=dev), torch.ones(n, dtype=torch.long, device=dev)
         i = 0
         depth_band = []
         for i in range(L):
@@ -186,7 +191,8 @@ class Oracle:
                 ind1, x1, e1 = ind1[keep], x1[keep], e1[:, keep]
                 prune1[ind1] += 1
         if len(x0) == 0 or len(x1) == 0:
-            return {"matches": torch.zeros(0, 2, dtype=torch.long), "scores": torch.zeros(0), "stop": i + 1,
+            return {"matches": torch.zeros(0, 2, dtype=torch.long, device=dev), "scores": torch.zeros(0, device=dev),
+                    "stop": i + 1,
                     "prune0": prune0, "prune1": prune1, "depth_band": depth_band}
         scores = self.assignment(x0, x1, i)
         mm0, mm1, ms0, ms1 = self.filter_matches(scores, filter_threshold)

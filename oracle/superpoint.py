@@ -60,9 +60,11 @@ def sample_descriptors(kp, desc, s=8):
 
 
 def dense_maps(sd, gray_f, emulate_bf16=True):
-    """gray_f float32 [B, 1, H, W] in [0, 1] -> (scores [B, H, W], descriptor map [B, 256, H/8, W/8])."""
+    """gray_f float32 [B, 1, H, W] in [0, 1] -> (scores [B, H, W], descriptor map [B, 256, H/8, W/8]).
+    Runs on gray_f's device (the CPU, or the GPU box's device when a tool uses this
+    restatement as a bench-scale checker)."""
     q = _bf16 if emulate_bf16 else (lambda t: t)
-    sd = {k: torch.as_tensor(np.asarray(v, np.float32)) for k, v in sd.items()}
+    sd = {k: torch.as_tensor(np.asarray(v, np.float32)).to(gray_f.device) for k, v in sd.items()}
     W = {k: (q(v) if k.endswith("weight") and not k.startswith("conv1a") else v) for k, v in sd.items()}
 
     def conv(x, name, relu=True, pad=1):
@@ -113,7 +115,7 @@ def detect(scores, desc, max_kp=2048, det_thr=0.001, nms_radius=4, border=4):
     return out
 
 
-def superpoint(sd, images_bgr, max_kp=2048, det_thr=0.001, emulate_bf16=True, nms_radius=4):
+def superpoint(sd, images_bgr, max_kp=2048, det_thr=0.001, emulate_bf16=True, nms_radius=4, device=None):
     gray = np.stack([bgr_to_gray_u8(im) for im in images_bgr]).astype(np.float32) / 255.0
-    sc, desc = dense_maps(sd, torch.from_numpy(gray)[:, None], emulate_bf16)
+    sc, desc = dense_maps(sd, torch.from_numpy(gray)[:, None].to(device or "cpu"), emulate_bf16)
     return detect(sc, desc, max_kp, det_thr, nms_radius)

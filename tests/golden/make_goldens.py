@@ -304,9 +304,19 @@ def api_case(sg):
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+def snippet_case(sg):
+    """integrate_with_orbslam3's return value (a C++ snippet string) -- loop_closure_gate.py:223-257."""
+    from scripts.semantic_gating import loop_closure_gate
+    out = {"integrate_with_orbslam3": loop_closure_gate.integrate_with_orbslam3(np.array([1, 1, 2]),
+                                                                                np.array([0.0, 1.0, 2.0]))}
+    with open(os.path.join(OUT, "gate_snippet.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def main():
     sg = _import_reference()
     api_case(sg)
+    snippet_case(sg)
     if "--api-only" in sys.argv:
         return
     print("reference", sg.__version__)

@@ -212,3 +212,34 @@ def test_package_calls_compute_only_through_torch_ops():
         if f.endswith(".py") and f != "_native.py":
             src = open(os.path.join(pkg, f)).read()
             assert "_native.lib()" not in src and "import ctypes" not in src, f
+
+
+def test_orbslam3_snippet_is_the_reference_text():
+    """integrate_with_orbslam3 returns the reference's C++ snippet byte for byte
+    (loop_closure_gate.py:223-257; captured by tests/golden/make_goldens.py)."""
+    import json
+    import os
+    import numpy as np
+    from mlgate.gate import integrate_with_orbslam3
+    with open(os.path.join(os.path.dirname(__file__), "golden", "gate_snippet.json")) as f:
+        want = json.load(f)["integrate_with_orbslam3"]
+    assert integrate_with_orbslam3(np.array([1, 1, 2]), np.array([0.0, 1.0, 2.0])) == want
+
+
+def test_gate_none_labels_raise_nan_labels_accept():
+    """SemanticLoopClosureGate with a None label computes abs(None - x) and raises
+    TypeError as the reference does (loop_closure_gate.py:89); a NaN label never
+    satisfies |qf - mf| > limit and is accepted.  (DeviceGate treats None as NaN: the one
+    documented deviation, mlgate/pipeline.py.)"""
+    import numpy as np
+    import pytest
+    from mlgate.gate import SemanticLoopClosureGate
+    g = SemanticLoopClosureGate(np.array([1, None, None, 2], dtype=object))
+    with pytest.raises(TypeError):
+        g.gate_candidate(1, 2)
+    with pytest.raises(TypeError):
+        g.gate_candidates([(0, 1, 0.9)])
+    h = SemanticLoopClosureGate(np.array([1.0, np.nan, 2.0]))
+    valid, rejected = h.gate_candidates([(0, 1, 0.9), (0, 2, 0.8)])
+    assert [(c.query_idx, c.match_idx) for c in valid] == [(0, 1)] and len(rejected) == 1
+    assert h.gate_candidate(1, 2).is_valid

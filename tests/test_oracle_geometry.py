@@ -53,3 +53,38 @@ def test_recover_pose_returns_truth(seed):
     assert good == 60
     assert G.rotation_angle_deg(Rr, R) < 1e-6
     assert np.allclose(tr, t, atol=1e-6)
+
+
+# --- the compiled twin (oracle/csrc/ransac_cv.c) against the numpy restatement --------
+@pytest.mark.parametrize("seed", range(6))
+def test_c_five_point_equals_numpy_five_point(seed):
+    from oracle import _lib
+    rng = np.random.default_rng(100 + seed)
+    k1, k2, _, _, _ = G.synthetic_pair(rng, 5, 0, noise_px=0.3)
+    p1, p2 = G.normalize(k1, G.ISEC_K), G.normalize(k2, G.ISEC_K)
+    A, B = G.five_point(p1, p2), _lib.five_point(p1, p2)
+    assert len(A) == len(B)
+    for E in A:
+        assert any(_close_up_to_sign(E, F, 1e-7) for F in B)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_c_essential_ransac_equals_numpy_restatement(seed):
+    """Same sample stream, same acceptance rule: identical inlier counts and masks."""
+    from oracle import _lib
+    rng = np.random.default_rng(200 + seed)
+    n_in = int(rng.integers(30, 250))
+    k1, k2, _, _, _ = G.synthetic_pair(rng, n_in, int(rng.integers(0, n_in // 2 + 1)), noise_px=0.8)
+    _, mask_py, g_py = G.cv_ransac(k1, k2, G.ISEC_K, 3.0)
+    _, mask_c, g_c = _lib.essential_ransac(k1, k2, G.ISEC_K, 3.0)
+    assert g_c == g_py
+    assert np.array_equal(mask_c, mask_py)
+
+
+def test_c_essential_ransac_degenerate_sizes():
+    from oracle import _lib
+    rng = np.random.default_rng(7)
+    k1, k2, _, _, _ = G.synthetic_pair(rng, 5, 0, noise_px=0.0)
+    assert _lib.essential_ransac(k1[:4], k2[:4], G.ISEC_K)[2] == 0
+    _, mask, g = _lib.essential_ransac(k1, k2, G.ISEC_K)
+    assert g == 5 and mask.all()

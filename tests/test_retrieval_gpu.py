@@ -258,3 +258,19 @@ def test_k_beyond_4096_windows(dev, k, thr):
         c = int(count[r])
         assert np.array_equal(idx[r, :c], ri[r, :c]) and np.array_equal(sim[r, :c], rs[r, :c])
         assert np.array_equal(valid[r, :c].astype(bool), rv[r, :c].astype(bool))
+
+
+def test_xcorr_batch_beyond_one_grid_slice(dev):
+    """More pairs than one k_xcorr_tiles launch takes (slices of 16384; a bench step's
+    rerank sends every (query, candidate) pair, ~100k): every pair still gets the
+    single-pair bits, and the scores do not depend on where the slices fall."""
+    from mlgate import _native
+    rng = np.random.default_rng(5)
+    F, L, D, P = 9, 40, 64, 70_001
+    feats = torch.from_numpy(rng.standard_normal((F, L, D)).astype(np.float32)).to(dev)
+    qa = rng.integers(0, F, P).astype(np.int32)
+    qb = rng.integers(0, F, P).astype(np.int32)
+    got = _native.ops().xcorr_batch(feats, torch.from_numpy(qa).to(dev), torch.from_numpy(qb).to(dev)).cpu().numpy()
+    table = {(a, b): retrieval.xcorr_score(feats[a], feats[b]).item() for a in range(F) for b in range(F)}
+    want = np.array([table[(a, b)] for a, b in zip(qa.tolist(), qb.tolist())], np.float32)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))

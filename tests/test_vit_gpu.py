@@ -74,3 +74,38 @@ def test_gray_and_bgra_inputs(dev, sd, frames):
         ref = ovit.gem(ovit.forward_tokens(ovit.preprocess(f[0]), osd))[0]
         cos = torch.nn.functional.cosine_similarity(d.double(), ref.double(), dim=0).item()
         assert 1 - cos < 1e-4
+
+
+def test_precise_split_descriptor_matches_fp32(dev, sd, frames):
+    """MLG_VIT_SPLIT (VitB14(precise=True)): every GEMM / attention operand as a hi + lo
+    bf16 pair, three MFMA products each.  Against the float32 oracle the descriptors agree
+    to 1 - cos <= 1e-9 (the bf16 forward: ~1e-5) and the local features to 1e-7; the
+    pairwise descriptor similarities to 1e-6 (the bf16 forward moves them by up to 3e-4,
+    which is what reorders near-tied kNN neighbours at bench scale)."""
+    from oracle import vit as ovit
+    torch.set_num_threads(8)
+    eng = VitB14(sd, device="cuda", max_batch=4, precise=True)
+    desc, local = eng.forward(torch.from_numpy(frames).to(dev), with_local=True)
+    torch.cuda.synchronize()
+    desc, local = desc.cpu().double(), local.cpu().double()
+    osd = {k: torch.from_numpy(v) for k, v in sd.items()}
+    refs = []
+    for b in range(len(frames)):
+        tok = ovit.forward_tokens(ovit.preprocess(frames[b]), osd)
+        refs.append(ovit.gem(tok)[0].double())
+        cos = torch.nn.functional.cosine_similarity(desc[b], refs[-1], dim=0).item()
+        assert 1 - cos < 1e-9, (b, 1 - cos)
+        lc = torch.nn.functional.cosine_similarity(local[b], tok[0, 1:].double(), dim=1)
+        assert (1 - lc).max().item() < 1e-7, (b, (1 - lc).max().item())
+    R = torch.stack(refs)
+    nrm = lambda X: X / X.norm(dim=1, keepdim=True)  # noqa: E731
+    assert (nrm(desc) @ nrm(desc).T - nrm(R) @ nrm(R).T).abs().max().item() < 1e-6
+
+
+def test_precise_batch_split_bit_identical(dev, sd, frames):
+    """The split forward does not depend on how frames are batched, bit for bit."""
+    x = torch.from_numpy(frames).to(dev)
+    d2 = VitB14(sd, device="cuda", max_batch=2, precise=True).forward(x)
+    d4 = VitB14(sd, device="cuda", max_batch=4, precise=True).forward(x)
+    torch.cuda.synchronize()
+    assert torch.equal(d2, d4)
