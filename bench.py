@@ -199,6 +199,52 @@ def configs0_bench(frames, seq, labels, lo, dev, iters=5):
             "resnet_tflops": round(tf, 1), "matches": int(out[3].sum())}
 
 
+def ingest_bench(dev, n_files=1024, distinct=64):
+    """Row f2: keyframe ingestion throughput.  `distinct` synthetic bench
+    keyframes are written as bag_utils.extract_images writes them (scripts/utils/
+    bag_utils.py:222-271: '{t:.6f}.png', bgr8 through cv2.imwrite, whose PNG default is
+    zlib level 1) -- here with Pillow at compress_level 1 -- and mlgate.ingest.KeyframeStream
+    (the loader process_image_sequence uses, place_recognition.py:936-991) streams n_files
+    paths over them into HBM (host decode pool -> pinned buffer -> side-stream upload).
+    Files repeat, so they are read from the page cache: the number is decode + upload."""
+    import shutil
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    from PIL import Image
+    from mlgate import ingest
+    threads = host_threads()
+    d = tempfile.mkdtemp(prefix="mlg_ingest_")
+    try:
+        seq = synthetic.make_sequence(distinct, 16, 3)
+        fr = synthetic.frames_host(seq)
+        names = [os.path.join(d, f"{t:.6f}.png") for t in seq.t]
+
+        def enc(i):
+            Image.fromarray(np.ascontiguousarray(fr[i][..., ::-1])).save(names[i], compress_level=1)
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(enc, range(distinct)))
+        paths = [names[i % distinct] for i in range(n_files)]
+        stream = ingest.KeyframeStream(paths, device=dev, batch=128, threads=threads)
+        for _ in stream:  # warm-up pass (page cache, pinned buffers)
+            break
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        n = 0
+        for idx, frames in stream:
+            n += len(idx)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        size = float(np.mean([os.path.getsize(x) for x in names]))
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return {"workload": "f2 keyframe ingestion: 640x480 bgr8 PNG keyframes (zlib level 1, bag_utils format) -> "
+                        "uint8 frames in HBM via mlgate.ingest.KeyframeStream (host inflate + unfilter pool, "
+                        "pinned buffer, side-stream upload)",
+            "keyframes": n, "seconds": round(dt, 3), "ingest_kf_per_s": round(n / dt, 1), "threads": threads,
+            "host_cpus": os.cpu_count(), "png_bytes_mean": round(size), "distinct_files": distinct,
+            "source": "page cache (files repeat)"}
+
+
 def loftr_flops_per_pair(L=4800, matches=0.0):
     """Algorithmic FLOPs of LoFTR's matching for one pair at 640x480 (L = 80 x 60 coarse
     cells): 8 coarse encoder layers (4 self + 4 cross) on both sides -- q / k / v, merge,
@@ -222,49 +268,75 @@ def loftr_backbone_flops(H=480, W=640):
     return 2.0 * sum(c)
 
 
-def loftr_bench(frames, seq, lo, dev, n_pairs=64, iters=3):
-    """configs[4] on the driver's clock (outside the gate's timed region): LoFTR backbone
-    over the keyframes of `n_pairs` revisit pairs of this rank's shard plus their
-    coarse / fine matching, HIP-event timed over `iters` runs after one warm-up."""
+def loftr_bench(frames, seq, labels, lo, dev, world, rank, n_pairs=1024, chunk=128, kernel_pairs=256):
+    """configs[4]: GeometricVerifier('loftr') as the gate's matcher, batched across the ranks.
+    (1) gate level -- DeviceGate(matcher='loftr') verifies the first n_pairs floor-valid
+    candidate pairs of the sequence (the same kNN as the main gate), the pairs split over
+    the ranks (balanced_pairs) and each rank receiving the raw frames its pairs touch;
+    pairs/s = n_pairs / the slowest rank's verification time (backbone per keyframe +
+    coarse / fine matching + RANSAC + decision, HIP work synchronised).  (2) kernel level,
+    rank 0 -- LoFTRGPU on `kernel_pairs` revisit pairs of its shard, HIP-event timed:
+    backbone and matching rates against the bf16 peak."""
     from mlgate.loftr import LoFTRGPU
+    g = DeviceGate(frames, seq.t, labels, world, rank, dev, k=20, verify=True, K=ISEC_K, vit_batch=246,
+                   matcher="loftr", loftr_chunk=chunk, max_pairs=n_pairs, vit_state_dict=synthetic_state_dict(0))
+    g.step()  # warm-up
+    out = g.step()
+    vt = torch.tensor([g.last_verify_s], dtype=torch.float64, device=dev)
+    cnt = torch.tensor([out["pairs_verified"], out["verified_valid"]], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(vt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(cnt)
+    del g
+    torch.cuda.empty_cache()
+    res = {"workload": "configs[4] LoFTR 640x480 (seeded synthetic weights) as the gate's matcher: "
+                       "ResNetFPN_8_2 backbone per keyframe + coarse linear-attention transformer, dual-softmax "
+                       "mutual-NN, 5x5 fine refinement + E-RANSAC + decision per ordered pair, pairs split over "
+                       f"{world} rank(s)",
+           "gate_pairs": int(cnt[0]), "gate_valid": int(cnt[1]), "gate_verify_s": round(float(vt), 3),
+           "gate_pairs_per_s": round(int(cnt[0]) / float(vt), 1)}
+    if rank != 0:
+        return res
     n = frames.shape[0]
     po = seq.place_of[lo:lo + n]
-    pairs = [(i, j) for i in range(n) for j in range(i + 1, n) if po[i] >= 0 and po[i] == po[j]][:n_pairs]
+    pairs = [(i, j) for i in range(n) for j in range(i + 1, n) if po[i] >= 0 and po[i] == po[j]][:kernel_pairs]
     if not pairs:
-        return None
+        return res
     used = sorted({i for p in pairs for i in p})
     pos = {f: k for k, f in enumerate(used)}
     sel = frames[torch.as_tensor(used, device=dev)].contiguous()
     lf = LoFTRGPU(device=dev, feature_batch=16)
     pa, pb = [pos[a] for a, _ in pairs], [pos[b] for _, b in pairs]
     H, W = int(sel.shape[1]) // 8 * 8, int(sel.shape[2]) // 8 * 8
+
+    def match_all(coarse, fine):
+        ms = []
+        for c0 in range(0, len(pairs), chunk):
+            c, *_ = lf.match_device(coarse, fine, H, W, pa[c0:c0 + chunk], pb[c0:c0 + chunk])
+            ms.append(c)
+        return torch.cat(ms)
     coarse, fine = lf.features(sel)
-    cnt, *_ = lf.match_device(coarse, fine, H, W, pa, pb)
+    cntm = match_all(coarse, fine)
     torch.cuda.synchronize(dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     ev[0].record()
-    for _ in range(iters):
-        coarse, fine = lf.features(sel)
+    coarse, fine = lf.features(sel)
     ev[1].record()
-    for _ in range(iters):
-        cnt, *_ = lf.match_device(coarse, fine, H, W, pa, pb)
+    cntm = match_all(coarse, fine)
     ev[2].record()
     torch.cuda.synchronize(dev)
-    t_feat, t_match = ev[0].elapsed_time(ev[1]) / iters, ev[1].elapsed_time(ev[2]) / iters
-    m = float(cnt.float().mean())
+    t_feat, t_match = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+    m = float(cntm.float().mean())
     bf, mf = loftr_backbone_flops(H, W), loftr_flops_per_pair((H // 8) * (W // 8), m)
     bt = bf * len(used) / (t_feat * 1e-3) / 1e12
     mt = mf * len(pairs) / (t_match * 1e-3) / 1e12
-    return {"workload": "configs[4] LoFTR 640x480 (seeded synthetic weights): ResNetFPN_8_2 backbone per keyframe "
-                        "+ coarse linear-attention transformer, dual-softmax mutual-NN and 5x5 fine refinement "
-                        "per revisit pair",
-            "keyframes": len(used), "pairs": len(pairs), "matches_mean": round(m, 1),
-            "backbone_ms_per_keyframe": round(t_feat / len(used), 3), "backbone_tflops": round(bt, 1),
-            "backbone_frac": round(bt / MFMA_BF16_PEAK_TFLOPS, 4),
-            "match_ms_per_pair": round(t_match / len(pairs), 3), "match_tflops": round(mt, 1),
-            "match_frac": round(mt / MFMA_BF16_PEAK_TFLOPS, 4),
-            "pairs_per_s": round(len(pairs) / ((t_feat + t_match) * 1e-3), 1),
-            "flops": {"backbone_per_keyframe": bf, "match_per_pair": round(mf, 0)}}
+    res.update({"kernel_keyframes": len(used), "kernel_pairs": len(pairs), "matches_mean": round(m, 1),
+                "backbone_ms_per_keyframe": round(t_feat / len(used), 3), "backbone_tflops": round(bt, 1),
+                "backbone_frac": round(bt / MFMA_BF16_PEAK_TFLOPS, 4),
+                "match_ms_per_pair": round(t_match / len(pairs), 3), "match_tflops": round(mt, 1),
+                "match_frac": round(mt / MFMA_BF16_PEAK_TFLOPS, 4),
+                "flops": {"backbone_per_keyframe": bf, "match_per_pair": round(mf, 0)}})
+    return res
 
 
 def main():
@@ -287,7 +359,8 @@ def main():
     ap.add_argument("--places", type=int, default=600)
     ap.add_argument("--verify", choices=["all", "none"], default="all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--loftr-pairs", type=int, default=64, help="configs[4] LoFTR sub-object (0: skip)")
+    ap.add_argument("--no-ingest", action="store_true", help="skip the f2 ingestion sub-object")
+    ap.add_argument("--loftr-pairs", type=int, default=1024, help="configs[4] LoFTR sub-object: gate pairs (0: skip)")
     ap.add_argument("--vit", choices=["split", "bf16"], default="split",
                     help="split: split-bf16 ViT (MLG_VIT_SPLIT, fp32-faithful descriptors); bf16: plain bf16 operands")
     args = ap.parse_args()
@@ -346,8 +419,10 @@ def main():
     steps = max(args.steps, 1)
     counts = {k_: int(v) // steps for k_, v in zip(keys, cv.cpu().tolist())}  # per step, all ranks
     N = args.keyframes
-    lft = loftr_bench(frames, seq, lo, dev, args.loftr_pairs) if args.loftr_pairs > 0 else None
+    torch.cuda.empty_cache()  # the main gate's LightGlue workspace
+    lft = loftr_bench(frames, seq, labels, lo, dev, world, rank, args.loftr_pairs) if args.loftr_pairs > 0 else None
     c0 = configs0_bench(frames, seq, labels, lo, dev) if rank == 0 else None
+    ing = ingest_bench(dev) if rank == 0 and not args.no_ingest else None
 
     if rank == 0:
         avg_s = ms / 1e3 / max(cnt, 1)
@@ -398,6 +473,8 @@ def main():
             line["loftr"] = lft
         if c0:
             line["configs0"] = c0
+        if ing:
+            line["ingest"] = ing
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(pairs_per_kf=(counts["pairs_verified"] / N) if gate.verify else 0.0)
         print(json.dumps(line), flush=True)

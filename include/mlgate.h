@@ -71,8 +71,8 @@ typedef struct mlg_vit_weights {
 /* Split-bf16 ("precise") forward: every GEMM / attention operand x is carried as the
  * bf16 pair hi = bf16(x), lo = bf16(x - hi) (x = hi + lo to ~2^-17) and every product as
  * hi*hi + hi*lo + lo*hi with f32 accumulation (three MFMAs).  The GEMM weights must then
- * be packed [out, 3 * in] = [W_hi | W_lo | W_hi] along the reduction dimension (the
- * patch weight [768, 3 * MLG_VIT_PATCH_K]).  Descriptor error against the fp32 network
+ * be packed [out, 2 * in] = [W_hi | W_lo] along the reduction dimension (the patch weight
+ * [768, 2 * MLG_VIT_PATCH_K]).  Descriptor error against the fp32 network
  * drops from ~1e-5 to ~1e-11 (1 - cos), so kNN rankings follow the fp32 reference's to
  * its own near-tie level. */
 #define MLG_VIT_SPLIT 4

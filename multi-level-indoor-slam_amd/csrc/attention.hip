@@ -41,6 +41,9 @@ __device__ __forceinline__ int v_off(int d, int gran) {
 // VALU work (a one-phase tile leaves the VALU idle during QK^T and the MFMA pipe idle
 // during the max / exp chain: 865 vs 936 TFLOP/s on bench.py's LightGlue stage).  Two 32-key score sets (64 VGPRs) are live.
 // VALU per score, the bound of a d = 64 attention: no key mask except in the last stage;
+// (written as packed f32 -- f32x2 fma / adds, round 4 -- hipcc allocates the pairs out of the
+// MFMA accumulators with 418 extra v_mov_b64 and 238 v_accvgpr_read per kernel: 3882 vs
+// 3460 VALU instructions, so the scalar forms stay)
 // exponent as one fma + one v_exp (log2 domain, 1/8 folded into the constant); row sums
 // as f32 adds per lane half (a 16x16x32 ones-MFMA for them measured slower); the running
 // max moves lazily -- P and the O / l

@@ -493,13 +493,9 @@ __global__ __launch_bounds__(512, BK == 32 ? 4 : 2) void k_gemm(const bf16_t* __
 // so the next tile's first wait overlaps this tile's epilogue, and the epilogue's
 // stores drain while the next tile's MFMAs run.  Twice the MFMAs per barrier and
 // 0.375 fragment reads per MFMA (vs 0.5 at 64 x 64 per wave).
-// nk0 > 0: split-bf16 operands (MLG_VIT_SPLIT).  A rows are [A_hi | A_lo] (K0 = 64 nk0
-// each), W rows [W_hi | W_lo | W_hi] (K = 3 K0): K-tile t of W pairs with A K-tile t for
-// t < nk0 (hi . hi), t - nk0 for t < 2 nk0 (hi . lo, A_hi again) and t - nk0 beyond (A_lo
-// . W_hi), so the one f32 accumulator sums hi*hi + lo*hi + hi*lo over k in that order.
 template <class Epi>
 __global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
-                                                   int M, int N, int K, int lda, int ldw, Epi epi, int nk0) {
+                                                   int M, int N, int K, int lda, int ldw, Epi epi) {
     constexpr int BK = 64, TM = 256, TN = 256;
     constexpr int A_BYTES = TM * BK * 2, STAGE = (TM + TN) * BK * 2;  // 64 KiB
     constexpr int NA = 4, NB = 4;                                      // DMAs per wave per K-tile
@@ -541,11 +537,10 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A
     const bf16_t* sa = a_base(tile);
     const bf16_t* sb = b_base(tile);
     a_offsets(tile, oa);
-    auto ak = [&](int t) { return (nk0 > 0 && t >= nk0 ? t - nk0 : t) * BK; };  // A column of W K-tile t
 #define D256_DMA(ST, OA, SA, SB, t)                                                                        \
     {                                                                                                      \
         const unsigned b_ = lds_addr(ST);                                                                  \
-        const bf16_t* sa_ = (SA) + ak(t);                                                                  \
+        const bf16_t* sa_ = (SA) + (t) * BK;                                                               \
         const bf16_t* sb_ = (SB) + (t) * BK;                                                               \
         _Pragma("unroll") for (int i = 0; i < NA; ++i) dma16s((OA)[i], sa_, b_ + da + i * 1024);           \
         _Pragma("unroll") for (int i = 0; i < NB; ++i) dma16s(ob[i], sb_, b_ + db + i * 1024);             \
@@ -612,6 +607,139 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A
     __builtin_amdgcn_s_waitcnt(0xF70);
 #undef D256_COMPUTE
 #undef D256_DMA
+}
+
+// Split-bf16 GEMM (MLG_VIT_SPLIT): C = epi(A_hi W_hi^T + A_hi W_lo^T + A_lo W_hi^T), f32
+// accumulation.  A rows are [A_hi | A_lo] (K0 each, lda >= 2 K0), W rows [W_hi | W_lo]
+// (ldw >= 2 K0).  The persistent, XCD-local 256 x 256 tile of k_gemm256 with K-steps of
+// 32: one LDS stage holds the four 256 x 32 planes of a K-step (64 KiB, two stages), each
+// wave reads its W_hi / W_lo / A_hi fragments, issues the hi*hi and lo*hi MFMAs, then
+// reloads its A fragments as A_lo for the hi*lo MFMAs -- 96 MFMAs per 24 fragment reads
+// per wave and K-step, and every operand byte fetched once (a K-concatenated [hi|lo|hi]
+// GEMM re-reads A_hi and W_hi: 3 planes each instead of 2).
+template <class Epi>
+__global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                    int M, int N, int K0, int lda, int ldw, Epi epi) {
+    constexpr int BK = 32, TM = 256, TN = 256;
+    constexpr int PLANE = TM * BK * 2;  // 16 KiB: one 256 x 32 bf16 operand plane
+    constexpr int STAGE = 4 * PLANE;    // A_hi, A_lo, W_hi, W_lo
+    __shared__ __attribute__((aligned(16))) char st0[STAGE];
+    __shared__ __attribute__((aligned(16))) char st1[STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nN = N / TN, nM = (M + TM - 1) / TM, ntiles = nN * nM;
+    const int xcd = blockIdx.x & 7, per_xcd = gridDim.x >> 3;
+    const int tx = (ntiles + 7) >> 3;
+    const int tile_end = min((xcd + 1) * tx, ntiles);
+    int tile = xcd * tx + (blockIdx.x >> 3);
+    if (tile >= tile_end) return;
+
+    const int lr = lane >> 2, lp = lane & 3;  // 16 rows x 4 chunks of 16 B per DMA wave-instruction
+    const int wm = wave & 1, wn = wave >> 1;
+    const int nk = K0 / BK;  // even (checked by the launcher)
+    const int drow = 2 * wave * 1024;  // this wave's 32 rows of every plane
+    unsigned ob[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int row = (2 * wave + i) * 16 + lr;
+        ob[i] = (unsigned)(row * ldw + ((lp ^ ((row >> 1) & 3)) * 8)) * 2u;
+    }
+    auto a_offsets = [&](int t, unsigned* oa) {
+        const int m0 = (t / nN) * TM;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int row = (2 * wave + i) * 16 + lr;
+            oa[i] = (unsigned)((min(m0 + row, M - 1) - m0) * lda + ((lp ^ ((row >> 1) & 3)) * 8)) * 2u;
+        }
+    };
+    auto a_base = [&](int t) { return A + (size_t)((t / nN) * TM) * lda; };
+    auto b_base = [&](int t) { return W + (size_t)((t % nN) * TN) * ldw; };
+    unsigned oa[2];
+    const bf16_t* sa = a_base(tile);
+    const bf16_t* sb = b_base(tile);
+    a_offsets(tile, oa);
+#define S256_DMA(ST, OA, SA, SB, t)                                                                        \
+    {                                                                                                      \
+        const unsigned b_ = lds_addr(ST) + drow;                                                           \
+        const bf16_t* ah_ = (SA) + (t) * BK;                                                               \
+        const bf16_t* wh_ = (SB) + (t) * BK;                                                               \
+        _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                    \
+            dma16s((OA)[i], ah_, b_ + i * 1024);                                                           \
+            dma16s((OA)[i], ah_ + K0, b_ + PLANE + i * 1024);                                              \
+            dma16s(ob[i], wh_, b_ + 2 * PLANE + i * 1024);                                                 \
+            dma16s(ob[i], wh_ + K0, b_ + 3 * PLANE + i * 1024);                                            \
+        }                                                                                                  \
+    }
+#define S256_COMPUTE(ST)                                                                                   \
+    {                                                                                                      \
+        bf16x8 af[8], wh[4], wl[4];                                                                        \
+        const int ch = lane >> 4;                                                                          \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                    \
+            const int row = wn * 64 + i * 16 + (lane & 15);                                                \
+            wh[i] = *reinterpret_cast<const bf16x8*>((ST) + 2 * PLANE + soff<32>(row, ch));                \
+            wl[i] = *reinterpret_cast<const bf16x8*>((ST) + 3 * PLANE + soff<32>(row, ch));                \
+        }                                                                                                  \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                    \
+            const int row = wm * 128 + j * 16 + (lane & 15);                                               \
+            af[j] = *reinterpret_cast<const bf16x8*>((ST) + soff<32>(row, ch));                            \
+        }                                                                                                  \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) _Pragma("unroll") for (int i = 0; i < 4; ++i) {      \
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[i], af[j], acc[i][j], 0, 0, 0);         \
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[i], af[j], acc[i][j], 0, 0, 0);         \
+        }                                                                                                  \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                    \
+            const int row = wm * 128 + j * 16 + (lane & 15);                                               \
+            af[j] = *reinterpret_cast<const bf16x8*>((ST) + PLANE + soff<32>(row, ch));                    \
+        }                                                                                                  \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j) _Pragma("unroll") for (int i = 0; i < 4; ++i)        \
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[i], af[j], acc[i][j], 0, 0, 0);         \
+    }
+
+    S256_DMA(st0, oa, sa, sb, 0);
+    __builtin_amdgcn_s_waitcnt(0xF70);
+    __builtin_amdgcn_s_barrier();
+    for (; tile < tile_end; tile += per_xcd) {
+        const int next = tile + per_xcd < tile_end ? tile + per_xcd : tile;
+        unsigned na[2];
+        a_offsets(next, na);
+        const bf16_t* nsa = a_base(next);
+        const bf16_t* nsb = b_base(next);
+        const int kn = next != tile ? 0 : nk - 1;  // no next tile: harmless re-read
+        f32x4 acc[4][8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < nk; t += 2) {
+            S256_DMA(st1, oa, sa, sb, t + 1);
+            S256_COMPUTE(st0);
+            __builtin_amdgcn_s_waitcnt(0xF70);
+            __builtin_amdgcn_s_barrier();
+            if (t + 2 < nk) {
+                S256_DMA(st0, oa, sa, sb, t + 2);
+            } else {
+                S256_DMA(st0, na, nsa, nsb, kn);  // K-step 0 of the next output tile
+            }
+            S256_COMPUTE(st1);
+            __builtin_amdgcn_s_waitcnt(0xF70);
+            __builtin_amdgcn_s_barrier();
+        }
+        const int mt = tile / nN, m0 = mt * TM, n0 = (tile - mt * nN) * TN;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4;
+                const int m = m0 + wm * 128 + j * 16 + (lane & 15);
+                if (m < M) epi(m, n, acc[i][j]);
+            }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) oa[i] = na[i];
+        sa = nsa;
+        sb = nsb;
+    }
+    __builtin_amdgcn_s_waitcnt(0xF70);
+#undef S256_COMPUTE
+#undef S256_DMA
 }
 
 // Variant 5: the 256 x 256 persistent tile of k_gemm256 with K-tiles of 32 in a 4-deep
@@ -906,7 +1034,7 @@ int launch(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int l
     } else if ((variant == 4 || variant == 5) && N % 256 == 0 && (K / 64) % 2 == 0) {
         const long ntiles = (long)(N / 256) * ((M + 255) / 256);
         const long grid = std::min<long>(g_num_cus, (ntiles + 7) / 8 * 8);  // persistent: <= 1 per CU
-        hipLaunchKernelGGL(dma::k_gemm256<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K, lda, ldw, epi, 0);
+        hipLaunchKernelGGL(dma::k_gemm256<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K, lda, ldw, epi);
     } else if (variant == 3 && N % dma::BN == 0 && (K / 32) % 3 == 0) {
         hipLaunchKernelGGL((dma::k_gemm<Epi, 32>), dim3((unsigned)nwg_dma), dim3(512), 0, s, A, W, M, N, K, lda, ldw,
                            epi);
@@ -923,18 +1051,16 @@ int launch(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int l
 }
 
 // Split-bf16 GEMM (MLG_VIT_SPLIT): A rows [A_hi | A_lo] of K0 each (lda >= 2 K0), W rows
-// [W_hi | W_lo | W_hi] (ldw >= 3 K0); the persistent 256 x 256 tile with the A K-tile remap
+// [W_hi | W_lo] (ldw >= 2 K0); dma::k_gemm256s
 template <class Epi>
 int launch_split(const bf16_t* A, const bf16_t* W, int M, int N, int K0, int lda, int ldw, Epi epi, hipStream_t s) {
     g_num_cus = num_cus();
-    if (M <= 0 || N % 256 || K0 <= 0 || K0 % 64 || ((3 * K0 / 64) % 2) || lda < 2 * K0 || ldw < 3 * K0 ||
-        (lda % 8) || (ldw % 8))
+    if (M <= 0 || N % 256 || K0 <= 0 || K0 % 64 || lda < 2 * K0 || ldw < 2 * K0 || (lda % 8) || (ldw % 8))
         return MLG_EINVAL;
     if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W)) & 15) return MLG_EINVAL;
     const long ntiles = (long)(N / 256) * ((M + 255) / 256);
     const long grid = std::min<long>(g_num_cus, (ntiles + 7) / 8 * 8);
-    hipLaunchKernelGGL(dma::k_gemm256<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, 3 * K0, lda, ldw, epi,
-                       K0 / 64);
+    hipLaunchKernelGGL(dma::k_gemm256s<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K0, lda, ldw, epi);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }
@@ -944,21 +1070,21 @@ int launch_split(const bf16_t* A, const bf16_t* W, int M, int N, int K0, int lda
 int mlg_gemm_qkv_split(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* Q, bf16_t* Kh, bf16_t* V, int M,
                        int T, int Tpad, size_t lo_off, hipStream_t s) {
     if (M % T) return MLG_EINVAL;
-    return launch_split(A, W, M, 3 * 768, 768, 2 * 768, 3 * 768,
+    return launch_split(A, W, M, 3 * 768, 768, 2 * 768, 2 * 768,
                         EpiQKVSplit{Q, Kh, V, bias, T, Tpad, (M / T) * Tpad, lo_off}, s);
 }
 int mlg_gemm_residual_split(const bf16_t* A, const bf16_t* W, const float* bias, const float* gamma, float* X, int M,
                             int N, int K0, hipStream_t s) {
-    return launch_split(A, W, M, N, K0, 2 * K0, 3 * K0, EpiResidual{X, N, bias, gamma}, s);
+    return launch_split(A, W, M, N, K0, 2 * K0, 2 * K0, EpiResidual{X, N, bias, gamma}, s);
 }
 int mlg_gemm_bias_gelu_split(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* C, int M, int N, int K0,
                              hipStream_t s) {
-    return launch_split(A, W, M, N, K0, 2 * K0, 3 * K0, EpiBiasGeluSplit{C, 2 * N, N, bias}, s);
+    return launch_split(A, W, M, N, K0, 2 * K0, 2 * K0, EpiBiasGeluSplit{C, 2 * N, N, bias}, s);
 }
 int mlg_gemm_patch_split(const bf16_t* A, const bf16_t* W, const float* bias, const float* pos, float* X, int M, int P,
                          int Kpad, hipStream_t s) {
     if (M % P) return MLG_EINVAL;
-    return launch_split(A, W, M, 768, Kpad, 2 * Kpad, 3 * Kpad, EpiPatch{X, bias, pos, P}, s);
+    return launch_split(A, W, M, 768, Kpad, 2 * Kpad, 2 * Kpad, EpiPatch{X, bias, pos, P}, s);
 }
 
 int mlg_gemm_f32out(const bf16_t* A, const bf16_t* W, float* C, int M, int N, int K, hipStream_t s) {

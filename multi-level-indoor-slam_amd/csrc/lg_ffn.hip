@@ -63,6 +63,9 @@ __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_ca
 #ifndef MLG_FFN_ROWS
 #define MLG_FFN_ROWS 64
 #endif
+#ifndef MLG_FFN_XR_WAIT
+#define MLG_FFN_XR_WAIT 0
+#endif
 #ifndef MLG_FFN_RING1
 #define MLG_FFN_RING1 2
 #endif
@@ -357,6 +360,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             f32x16 acc[NT1][MT];
             zero(acc);
             gemm_phase<NT1, MT, RING1>(w.Wf2, 256, 32 * NT1 * wave, 8, 0, lds, acc);
+#if MLG_FFN_XR_WAIT
+            __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): the residual rows xr have landed
+#endif
             __syncthreads();  // every wave has read the GELU output
     #pragma unroll
             for (int t = 0; t < NT1; ++t)

@@ -65,10 +65,10 @@ Tensor workspace(size_t bytes, const Tensor& like) {
 constexpr int kVitBlockTensors = 14;
 constexpr int kVitTensors = 4 + MLG_VIT_DEPTH * kVitBlockTensors + 2;
 
-// split: weights packed for MLG_VIT_SPLIT ([W_hi | W_lo | W_hi], 3x the reduction dim)
+// split: weights packed for MLG_VIT_SPLIT ([W_hi | W_lo], 2x the reduction dim)
 mlg_vit_weights vit_weights(const std::vector<Tensor>& w, bool split = false) {
     TORCH_CHECK((int)w.size() == kVitTensors, "vit weights: expected ", kVitTensors, " tensors, got ", w.size());
-    const int64_t m = split ? 3 : 1;
+    const int64_t m = split ? 2 : 1;
     auto want_n = [&](const Tensor& t, int64_t n, const char* what) {
         TORCH_CHECK(t.numel() == n * m && t.scalar_type() == at::kBFloat16, "vit weights: ", what, " must be bf16 with ",
                     n * m, " elements", split ? " (split packing)" : "");

@@ -65,6 +65,11 @@ class RowGather:
         if len(self.sizes) == 1:
             self.out.copy_(local)
             return self.out
+        if len(set(self.sizes)) == 1 and local.is_cuda and dist.get_backend(self.group) == "nccl":
+            # equal shards (N % W == 0, e.g. 5000 over 1 / 2 / 4 / 8 ranks): one RCCL
+            # all-gather straight into the [N, D] database, no staging copy
+            dist.all_gather_into_tensor(self.out, local.contiguous(), group=self.group)
+            return self.out
         self.send[:local.shape[0]].copy_(local)
         all_gather_into(self.bufs, self.send, group=self.group)
         torch.cat([b[:s] for b, s in zip(self.bufs, self.sizes)], out=self.out)
@@ -78,8 +83,8 @@ def balanced_pairs(pa, pb, world, rank, group=None, group_reverse=False):
     verifying them where they were found leaves ranks idle.  All ranks all-gather the
     lists (8 B per pair) and take the rank-th contiguous slice of the global,
     rank-ordered list: the union of the slices is exactly the global list and slice
-    sizes differ by at most one.  Every keyframe's features are all-gathered before this
-    step, so any rank can verify any pair.
+    sizes differ by at most one.  FeatureExchange then delivers each rank the features
+    (or frames) of exactly the keyframes its slice touches.
     With ``group_reverse`` the slices are cut over the UNORDERED pairs instead: (a, b) and
     (b, a) land on the same rank, which matches them once (LightGlue is symmetric in its
     two images; mlg_lg_orient_matches); the unordered pairs are split evenly, in

@@ -161,7 +161,7 @@ class DeviceGate:
                  similarity_threshold=0.5, min_time_gap=10.0, strict_mode=True, retrieval_floor_gating=True,
                  verifier_floor_gating=True, verify=True, K=None, min_inliers=20, min_inlier_ratio=0.25,
                  vit_batch=123, sp_batch=64, lg_chunk=1024, max_keypoints=2048, vit_state_dict=None, record=False,
-                 vit_precise=True):
+                 vit_precise=True, matcher='lightglue', loftr_chunk=256, max_pairs=None):
         import torch
         from . import distributed as mdist
         from .lightglue import LightGlueGPU
@@ -204,7 +204,20 @@ class DeviceGate:
         self.local_feats = torch.empty(self.n_local, self.eng.n_local, EMBED, dtype=torch.float32, device=self.dev)
         self.totals = torch.zeros(2, dtype=torch.int64, device=self.dev)
         self.verify = verify
-        if verify:
+        # matcher: 'lightglue' (SuperPoint + LightGlue, the reference default) or 'loftr'
+        # (GeometricVerifier('loftr'), geometric_verification.py:424-526; BASELINE configs[4])
+        if matcher not in ('lightglue', 'loftr'):
+            raise ValueError(f"Unknown matcher: {matcher}")
+        self.matcher = matcher
+        self.loftr_chunk = int(loftr_chunk)
+        self.max_pairs = max_pairs  # verify only the first max_pairs pairs of the global list (bench sub-runs)
+        if verify and matcher == 'loftr':
+            from .loftr import LoFTRGPU
+            self.lf = LoFTRGPU(device=self.dev, feature_batch=16)
+            self.fx = mdist.FeatureExchange(N, world, rank) if world > 1 else None
+            Kc = np.asarray(K if K is not None else np.eye(3), np.float64)
+            self.K = torch.from_numpy(Kc.reshape(9).copy()).to(self.dev) if K is not None else None
+        elif verify:
             KP = max_keypoints
             self.sp = SuperPointGPU(device=self.dev, max_num_keypoints=KP)
             self.lg = LightGlueGPU(device=self.dev)
@@ -261,7 +274,7 @@ class DeviceGate:
         if not self.verify:
             return out
         # SuperPoint once per keyframe (the reference re-extracts per pair), cached in HBM
-        for b0 in range(0, self.n_local, self.sp_batch):
+        for b0 in range(0, self.n_local if self.matcher == 'lightglue' else 0, self.sp_batch):
             b1 = min(self.n_local, b0 + self.sp_batch)
             kp, _, ds, _, cnt = self.sp.extract_device(self.frames[b0:b1])
             self.kp_loc[b0:b1].copy_(kp.view(b1 - b0, -1))
@@ -277,6 +290,8 @@ class DeviceGate:
             same = (ha & hb & (self.f_all[pa_t.long()] == self.f_all[pb_t.long()])) | (~ha & ~hb)
             out["skipped_floor_mismatch"] = int((~same).sum())
             pa_t, pb_t = pa_t[same], pb_t[same]
+        if self.matcher == 'loftr':
+            return self._verify_loftr(pa_t, pb_t, out)
         # pair-level load balance across ranks: the pairs are re-balanced first (the union
         # of the slices is the global pair list), then FeatureExchange delivers each rank
         # exactly the SuperPoint features its own slice touches
@@ -380,3 +395,111 @@ class DeviceGate:
         out["gate_rejected_cross_floor"] = gate_rej
         out["accepted"] = n_valid - gate_rej
         return out
+
+    def _verify_loftr(self, pa_t, pb_t, out):
+        """verify_with_semantics with GeometricVerifier('loftr') on this rank's slice of the
+        pairs (geometric_verification.py:469-526 matches, :104-153 RANSAC, :602-620 rule).
+        LoFTR is not symmetric in its images (the fine stage refines in image 1), so every
+        ordered pair is matched.  Each rank receives the raw frames its slice touches
+        (0.9 MB per keyframe; FeatureExchange over uint8 rows) and runs the backbone on
+        them: cheaper to move than the 44 MB of coarse + fine features per keyframe.  Pairs
+        go in chunks of loftr_chunk, ordered by (query, match); the backbone features of a
+        chunk's keyframes are kept across chunks in a buffer of 2 x 2 x loftr_chunk rows
+        and recomputed only for keyframes not already held."""
+        torch = self.torch
+        from . import geometry
+        import time
+        torch.cuda.synchronize(self.dev)
+        t_start = time.perf_counter()
+        if self.max_pairs is not None:
+            pa_t, pb_t = self._first_pairs(pa_t, pb_t, self.max_pairs)
+        pa_t, pb_t = self.mdist.balanced_pairs(pa_t, pb_t, self.world, self.rank)
+        pa, pb = pa_t.cpu().numpy().astype(np.int64), pb_t.cpu().numpy().astype(np.int64)
+        self.last_pairs = (pa, pb)
+        need = np.unique(np.concatenate([pa, pb])) if len(pa) else np.zeros(0, np.int64)
+        if self.world > 1:
+            fl = self.frames.reshape(self.n_local, -1)
+            frames = self.fx(need, [fl])[0].view((len(need),) + tuple(self.frames.shape[1:]))
+            out["features_exchanged_bytes"] = self.fx.last_bytes
+            row_of = {int(f): i for i, f in enumerate(need)}
+        else:
+            frames = self.frames
+            row_of = None
+        H, W = int(frames.shape[1]) // 8 * 8, int(frames.shape[2]) // 8 * 8
+        order = np.lexsort((pb, pa))
+        C = self.loftr_chunk
+        cap = 4 * C
+        slot_of, free = {}, list(range(cap))
+        coarse = fine = None
+        n_valid_t = torch.zeros((), dtype=torch.int64, device=self.dev)
+        gate_rej_t = torch.zeros((), dtype=torch.int64, device=self.dev)
+        rec = [] if self.record else None
+        for c0 in range(0, len(order), C):
+            sel = order[c0:c0 + C]
+            ca, cb = pa[sel], pb[sel]
+            frs = np.unique(np.concatenate([ca, cb]))
+            keep = set(int(f) for f in frs)
+            for f in [f for f in slot_of if f not in keep] if len(free) < len(frs) else []:
+                free.append(slot_of.pop(f))
+            todo = [int(f) for f in frs if int(f) not in slot_of]
+            if todo:
+                rows = [f if row_of is None else row_of[f] for f in todo]
+                if row_of is None:
+                    rows = [f - self.lo for f in rows]
+                cf_, ff_ = self.lf.features(frames[torch.as_tensor(rows, device=self.dev)].contiguous())
+                if coarse is None:
+                    coarse = torch.empty((cap,) + tuple(cf_.shape[1:]), dtype=cf_.dtype, device=self.dev)
+                    fine = torch.empty((cap,) + tuple(ff_.shape[1:]), dtype=ff_.dtype, device=self.dev)
+                slots = [free.pop() for _ in todo]
+                st = torch.as_tensor(slots, device=self.dev)
+                coarse.index_copy_(0, st, cf_)
+                fine.index_copy_(0, st, ff_)
+                slot_of.update(zip(todo, slots))
+            n, k0, k1, _ = self.lf.match_device(coarse, fine, H, W, [slot_of[int(a)] for a in ca],
+                                                [slot_of[int(b)] for b in cb])
+            n = n.to(self.dev).long()
+            P = len(sel)
+            lv = torch.arange(k0.shape[1], device=self.dev)[None, :] < n[:, None]
+            pi, si = torch.nonzero(lv, as_tuple=True)
+            offs = torch.zeros(P + 1, dtype=torch.int32, device=self.dev)
+            offs[1:] = torch.cumsum(n, 0)
+            _, _, inl, _, _ = geometry.epipolar_ransac_device(k0[pi, si].contiguous(), k1[pi, si].contiguous(),
+                                                              offs, self.K, 0, 3.0)
+            ratio = inl.double() / n.clamp(min=1).double()
+            ok = (n >= 5) & (inl >= self.min_inliers) & (ratio >= self.min_inlier_ratio)
+            n_valid_t += ok.sum()
+            ta = torch.from_numpy(ca).to(self.dev)
+            tb = torch.from_numpy(cb).to(self.dev)
+            gate_rej_t += (ok & ((self.f_num[ta] - self.f_num[tb]).abs() > self.limit)).sum()
+            if rec is not None:
+                rec.append((sel, n, inl, ok))
+        n_valid, gate_rej = int(n_valid_t), int(gate_rej_t)
+        self.last_verify_s = time.perf_counter() - t_start  # this rank's LoFTR verification wall time
+        if rec is not None:
+            r = {"a": pa, "b": pb, "matches": np.zeros(len(pa), np.int32), "inliers": np.zeros(len(pa), np.int32),
+                 "is_valid": np.zeros(len(pa), bool)}
+            for sel, n, inl, ok in rec:
+                r["matches"][sel] = n.cpu().numpy()
+                r["inliers"][sel] = inl.cpu().numpy()
+                r["is_valid"][sel] = ok.cpu().numpy()
+            self.last_pair_results = r
+        out["pairs_verified"] = len(pa)
+        out["pairs_matched_loftr"] = len(pa)
+        out["verified_valid"] = n_valid
+        out["verifier_invalid"] = len(pa) - n_valid
+        out["gate_rejected_cross_floor"] = gate_rej
+        out["accepted"] = n_valid - gate_rej
+        return out
+
+    def _first_pairs(self, pa_t, pb_t, limit):
+        """The first `limit` pairs of the global (rank-ordered) pair list, as this rank's part."""
+        if self.world == 1:
+            return pa_t[:limit], pb_t[:limit]
+        torch = self.torch
+        n = torch.tensor([pa_t.numel()], dtype=torch.int64, device=self.dev)
+        sizes = [torch.zeros_like(n) for _ in range(self.world)]
+        self.mdist.all_gather_into(sizes, n)
+        before = sum(int(x.item()) for x in sizes[:self.rank])
+        take = max(0, min(pa_t.numel(), limit - before))
+        return pa_t[:take], pb_t[:take]
+

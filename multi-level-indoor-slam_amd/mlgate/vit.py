@@ -40,13 +40,12 @@ MLG_VIT_SPLIT = 4  # include/mlgate.h
 
 
 def split_weight(w):
-    """[out, in] float32 -> bf16 [out, 3 in] = [W_hi | W_lo | W_hi] (MLG_VIT_SPLIT packing:
-    hi = bf16(W), lo = bf16(W - hi); the kernel pairs the three K-blocks with A_hi, A_hi,
-    A_lo)."""
+    """[out, in] float32 -> bf16 [out, 2 in] = [W_hi | W_lo] (MLG_VIT_SPLIT packing:
+    hi = bf16(W), lo = bf16(W - hi), so W = hi + lo to 2^-17)."""
     w = w.to(torch.float32)
     hi = w.to(torch.bfloat16)
     lo = (w - hi.to(torch.float32)).to(torch.bfloat16)
-    return torch.cat([hi, lo, hi], dim=1).contiguous()
+    return torch.cat([hi, lo], dim=1).contiguous()
 
 
 class VitB14:

@@ -8,7 +8,10 @@ the keyframes each rank's pairs touch exchanged (FeatureExchange).
 Bar (the reference's per-query loop is row-independent,
 place_recognition.py:873-909): the all-reduced counts and rejection terms, and every
 ordered pair's (matches, inliers, is_valid) gathered to rank 0, equal the world-1 run
-exactly."""
+exactly.  The "loftr" case runs the same sharded gate with LoFTR as the matcher: pairs
+split evenly over the ranks, the raw frames of the keyframes a rank's pairs touch
+exchanged instead of SuperPoint features, every ordered pair matched (LoFTR is not
+symmetric)."""
 import json
 import os
 import socket
@@ -41,6 +44,10 @@ def _case(name):
         thr, gap = (float(x) for x in g["thr_gap"])
         kw = dict(k=k, similarity_threshold=thr, min_time_gap=gap, vit_batch=64, lg_chunk=64)
         return seq, np.asarray(g["labels"]), kw, ogeo.ISEC_K
+    if name == "loftr":  # GeometricVerifier('loftr') as the matcher (BASELINE configs[4])
+        seq = synthetic.make_sequence(160, 24, 5)
+        labels, _ = floor_labels_from_imu(seq.t, synthetic.imu_log(seq), start_floor=5)
+        return seq, labels, dict(k=8, vit_batch=64, matcher="loftr", loftr_chunk=48), ogeo.ISEC_K
     seq = synthetic.make_sequence(1000, 120, 3)
     labels, _ = floor_labels_from_imu(seq.t, synthetic.imu_log(seq), start_floor=5)
     return seq, labels, dict(k=20, vit_batch=123, lg_chunk=512), ogeo.ISEC_K
@@ -88,7 +95,7 @@ def _worker(rank, world, port, case, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", ["chain", "seq1000"])
+@pytest.mark.parametrize("case", ["chain", "seq1000", "loftr"])
 def test_sharded_gate_equals_single_rank(tmp_path, case):
     out = str(tmp_path / "res.json")
     mp.spawn(_worker, args=(2, _free_port(), case, out), nprocs=2, join=True)
