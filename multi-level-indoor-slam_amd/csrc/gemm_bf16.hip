@@ -91,16 +91,26 @@ struct EpiBiasGeluBF16 {
 };
 
 // y = gelu(acc + b) as the split pair: hi = bf16(y) at column n, lo = bf16(y - hi) at
-// column n + lo_col of the same row (the [hi | lo] A rows of the split fc2 GEMM).  The
-// exact erf form torch's nn.GELU() computes: gelu_poly2's 1e-6 absolute error would be
-// the largest error term of the split forward.
+// column n + lo_col of the same row (the [hi | lo] A rows of the split fc2 GEMM).  GELU as
+// common.h gelu_poly2 (|error| <= 1e-6, below the pair's 2^-17 relative representation
+// error for |y| > 0.13; erff here made fc1 epilogue-bound: MLG_SPLIT_GELU_ERF=1 keeps it
+// for A/B)
+#ifndef MLG_SPLIT_GELU_ERF
+#define MLG_SPLIT_GELU_ERF 0
+#endif
 struct EpiBiasGeluSplit {
     bf16_t* C; int ldc; int lo_col; const float* bias;
     __device__ static float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f)); }
     __device__ void operator()(int m, int n, const f32x4& v) const {
         const float4 b = *reinterpret_cast<const float4*>(bias + n);
         uint2 h, l;
+#if MLG_SPLIT_GELU_ERF
         split_bf16x4(gelu(v[0] + b.x), gelu(v[1] + b.y), gelu(v[2] + b.z), gelu(v[3] + b.w), h, l);
+#else
+        const f32x2 g01 = gelu_poly2(f32x2{v[0] + b.x, v[1] + b.y});
+        const f32x2 g23 = gelu_poly2(f32x2{v[2] + b.z, v[3] + b.w});
+        split_bf16x4(g01.x, g01.y, g23.x, g23.y, h, l);
+#endif
         *reinterpret_cast<uint2*>(C + (size_t)m * ldc + n) = h;
         *reinterpret_cast<uint2*>(C + (size_t)m * ldc + lo_col + n) = l;
     }

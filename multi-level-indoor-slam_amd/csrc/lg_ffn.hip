@@ -66,6 +66,13 @@ __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_ca
 #ifndef MLG_FFN_XR_WAIT
 #define MLG_FFN_XR_WAIT 0
 #endif
+// LayerNorm rstd: 1 = the bare v_rsq_f32 (product), 0 = rsqrtf with its denormal fix-up,
+// 2 = bare + 5 wait states (probe arm).  Under hipcc's SLP pass form 0 packed the two
+// m-tiles' fix-ups into one v_pk_mul_f32 reading both v_rsq_f32 results one wait state
+// later, which gave co-scheduling dependent rstd (DESIGN.md §5, round-4 FFN probe).
+#ifndef MLG_FFN_RSQ
+#define MLG_FFN_RSQ 1
+#endif
 #ifndef MLG_FFN_RING1
 #define MLG_FFN_RING1 2
 #endif
@@ -309,7 +316,17 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                 float q = 0.f;
     #pragma unroll
                 for (int v = 0; v < NW; ++v) q += red[1][v][32 * mt + col];
+#if MLG_FFN_RSQ == 0
                 rstd[mt] = rsqrtf(q * (1.0f / 512.0f) + 1e-5f);
+#else
+                // the bare v_rsq_f32: the argument is >= 1e-5, never in the range rsqrtf's
+                // denormal fix-up handles, so the bits are the same (probe arm 2: followed by
+                // 5 wait states before any consumer)
+                rstd[mt] = __builtin_amdgcn_rsqf(q * (1.0f / 512.0f) + 1e-5f);
+#if MLG_FFN_RSQ == 2
+                asm volatile("s_nop 4" : "+v"(rstd[mt]));
+#endif
+#endif
             }
     #pragma unroll
             for (int t = 0; t < NT2; ++t)

@@ -1018,7 +1018,9 @@ __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict_
         b1[i][4] = -a5[6];
     }
     if (!ok) {
-        if (act && r == 0) nsol[(size_t)p * H + h] = 0;
+        // inactive hypotheses too (5-point direct pairs beyond h = 0, RANSAC pairs beyond
+        // nsub): k_ransac_score and the argmax in k_ransac_select read every slot h < H
+        if (h < H && r == 0) nsol[(size_t)p * H + h] = 0;
         return;
     }
 #if defined(RS_ABLATE) && RS_ABLATE == 2
