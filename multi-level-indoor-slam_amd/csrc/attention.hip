@@ -457,18 +457,20 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
             __builtin_amdgcn_wave_barrier();
             bf16_t* dst = orow + (part ? lo_col : 0);
-            uint4 rows[8];
+            // a vector type, not uint4: copies of the HIP struct are memcpys, which kept this
+            // array out of registers (hipcc then placed it in LDS: 32 KiB per workgroup)
+            u32x4 rows[8];
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
                 const int r = p * 8 + (lane >> 3), c = lane & 7;
-                rows[p] = *reinterpret_cast<const uint4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
+                rows[p] = *reinterpret_cast<const u32x4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);  // staging read before the next part overwrites it
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
                 const int r = p * 8 + (lane >> 3), c = lane & 7, qrow = qbase + r;
-                if (qrow < nq) *reinterpret_cast<uint4*>(dst + (size_t)qrow * ldo + c * 8) = rows[p];
+                if (qrow < nq) *reinterpret_cast<u32x4*>(dst + (size_t)qrow * ldo + c * 8) = rows[p];
             }
         }
     }

@@ -219,6 +219,7 @@ struct EpiBiasAddRelu {
 // (X, ldx) and / or bf16 (C, ldc), either may be null.
 struct EpiConv {
     const float* bias; const float* R; int ldr; float* X; int ldx; bf16_t* C; int ldc; int act; int act_cols;
+    float vdiv = 0.f;  // != 0: columns >= act_cols divided by it (LoFTR's values / v_length)
     __device__ void operator()(int m, int n, const f32x4& v) const {
         float y[4] = {v[0], v[1], v[2], v[3]};
         if (bias) {
@@ -236,6 +237,10 @@ struct EpiConv {
                 else if (act == 2) y[i] = y[i] > 0.f ? y[i] : 0.01f * y[i];
                 else y[i] = (y[i] > 0.f ? y[i] : expf(y[i]) - 1.f) + 1.f;  // elu(y) + 1, as torch
             }
+        }
+        if (vdiv != 0.f && n >= act_cols) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) y[i] = y[i] / vdiv;
         }
         if (X) *reinterpret_cast<float4*>(X + (size_t)m * ldx + n) = make_float4(y[0], y[1], y[2], y[3]);
         if (C) *reinterpret_cast<uint2*>(C + (size_t)m * ldc + n) =
@@ -752,6 +757,127 @@ __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ 
 #undef S256_DMA
 }
 
+// Split-bf16 GEMM, 192 x 192 form (MLG_SPLIT_TILE=192): the same three products per
+// K-step of 32 as k_gemm256s on a 192 x 192 tile, whose four operand planes (48 KiB) fit a
+// THREE-stage LDS-DMA ring (144 KiB): each K-step's planes are fetched two compute steps
+// ahead instead of one.  The ring runs on across the workgroup's output tiles (flat step
+// index over its tiles; steps past the last re-fetch the last one into a slot already
+// consumed).  Same per-output MFMA order as k_gemm256s, so the same bits.
+template <class Epi>
+__global__ __launch_bounds__(512, 1) void k_gemm192s(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+                                                    int M, int N, int K0, int lda, int ldw, Epi epi) {
+    constexpr int BK = 32, TM = 192, TN = 192;
+    constexpr int PLANE = TM * BK * 2;  // 12 KiB
+    constexpr int STAGE = 4 * PLANE;    // A_hi, A_lo, W_hi, W_lo
+    constexpr int PIECES = 6;           // 1 KiB DMA wave-instructions per wave and stage (48 / 8 waves)
+    __shared__ __attribute__((aligned(16))) char ring[3 * STAGE];
+    // wave index through readfirstlane: the DMA bases derived from it stay in SGPRs
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nN = N / TN, nM = (M + TM - 1) / TM, ntiles = nN * nM;
+    const int xcd = blockIdx.x & 7, per_xcd = gridDim.x >> 3;
+    const int tx = (ntiles + 7) >> 3;
+    const int tile_end = min((xcd + 1) * tx, ntiles);
+    const int tile0 = xcd * tx + (blockIdx.x >> 3);
+    if (tile0 >= tile_end) return;
+    const int ntl = (tile_end - tile0 + per_xcd - 1) / per_xcd;
+    const int nk = K0 / BK;
+    const int S = ntl * nk;
+
+    const int lr = lane >> 2, lp = lane & 3;
+    const int wm = wave & 1, wn = wave >> 1;
+    // piece i of this wave: plane pl = p / 12 (0 A_hi, 1 A_lo, 2 W_hi, 3 W_lo), rows 16 (p % 12) ..
+    int prow[PIECES], pplane[PIECES];
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+        const int p = wave * PIECES + i;
+        pplane[i] = p / 12;
+        prow[i] = (p % 12) * 16 + lr;
+    }
+    auto issue = [&](int st, int slot) {  // DMA of flat step st into ring slot `slot`
+        const int q = st / nk, k = st - q * nk;
+        const int tile = tile0 + q * per_xcd;
+        const int m0 = (tile / nN) * TM, n0 = (tile - (tile / nN) * nN) * TN;
+        const unsigned b = lds_addr(ring + slot * STAGE);
+#pragma unroll
+        for (int i = 0; i < PIECES; ++i) {
+            const int row = prow[i], pl = pplane[i];
+            const int sw = (lp ^ ((row >> 1) & 3)) * 8;
+            const unsigned dst = b + pl * PLANE + (row - lr) * 64;
+            if (pl < 2) {
+                const unsigned off = (unsigned)((min(m0 + row, M - 1) - m0) * lda + sw) * 2u;
+                dma16s(off, A + (size_t)m0 * lda + k * BK + (pl ? K0 : 0), dst);
+            } else {
+                const unsigned off = (unsigned)(row * ldw + sw) * 2u;
+                dma16s(off, W + (size_t)n0 * ldw + k * BK + (pl == 3 ? K0 : 0), dst);
+            }
+        }
+    };
+    f32x4 acc[3][6];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    issue(0, 0);
+    issue(min(1, S - 1), 1);
+    __builtin_amdgcn_s_waitcnt(0xF70 | PIECES);  // vmcnt(6): step 0 has landed
+    __builtin_amdgcn_s_barrier();
+    const int ch = lane >> 4;
+    for (int st = 0; st < S; ++st) {
+        issue(min(st + 2, S - 1), (st + 2) % 3);  // into the slot step st - 1 used (all waves are past it)
+        const char* P = ring + (st % 3) * STAGE;
+        {
+            bf16x8 af[6], wh[3], wl[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const int row = wn * 48 + i * 16 + (lane & 15);
+                wh[i] = *reinterpret_cast<const bf16x8*>(P + 2 * PLANE + soff<32>(row, ch));
+                wl[i] = *reinterpret_cast<const bf16x8*>(P + 3 * PLANE + soff<32>(row, ch));
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int row = wm * 96 + j * 16 + (lane & 15);
+                af[j] = *reinterpret_cast<const bf16x8*>(P + soff<32>(row, ch));
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j)
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[i], af[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[i], af[j], acc[i][j], 0, 0, 0);
+                }
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                const int row = wm * 96 + j * 16 + (lane & 15);
+                af[j] = *reinterpret_cast<const bf16x8*>(P + PLANE + soff<32>(row, ch));
+            }
+#pragma unroll
+            for (int j = 0; j < 6; ++j)
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[i], af[j], acc[i][j], 0, 0, 0);
+        }
+        const int q = st / nk;
+        if (st - q * nk == nk - 1) {  // the tile's last K-step: epilogue
+            const int tile = tile0 + q * per_xcd;
+            const int mt = tile / nN, m0 = mt * TM, n0 = (tile - mt * nN) * TN;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 6; ++j) {
+                    const int n = n0 + wn * 48 + i * 16 + (lane >> 4) * 4;
+                    const int m = m0 + wm * 96 + j * 16 + (lane & 15);
+                    if (m < M) epi(m, n, acc[i][j]);
+                    acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+            __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): stores counted there too
+        } else {
+            __builtin_amdgcn_s_waitcnt(0xF70 | PIECES);  // vmcnt(6): step st + 1 has landed
+        }
+        __builtin_amdgcn_s_barrier();
+    }
+    __builtin_amdgcn_s_waitcnt(0xF70);
+}
+
 // Variant 5: the 256 x 256 persistent tile of k_gemm256 with K-tiles of 32 in a 4-deep
 // LDS ring (4 x 32 KiB): the DMA of K-tile t + 3 is issued when t is computed, so three
 // compute steps (not one) hide each tile's fetch; the ring runs on across output tiles
@@ -1063,11 +1189,21 @@ int launch(const bf16_t* A, const bf16_t* W, int M, int N, int K, int lda, int l
 // Split-bf16 GEMM (MLG_VIT_SPLIT): A rows [A_hi | A_lo] of K0 each (lda >= 2 K0), W rows
 // [W_hi | W_lo] (ldw >= 2 K0); dma::k_gemm256s
 template <class Epi>
+#ifndef MLG_SPLIT_TILE
+#define MLG_SPLIT_TILE 256
+#endif
 int launch_split(const bf16_t* A, const bf16_t* W, int M, int N, int K0, int lda, int ldw, Epi epi, hipStream_t s) {
     g_num_cus = num_cus();
-    if (M <= 0 || N % 256 || K0 <= 0 || K0 % 64 || lda < 2 * K0 || ldw < 2 * K0 || (lda % 8) || (ldw % 8))
-        return MLG_EINVAL;
+    if (M <= 0 || K0 <= 0 || K0 % 64 || lda < 2 * K0 || ldw < 2 * K0 || (lda % 8) || (ldw % 8)) return MLG_EINVAL;
     if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W)) & 15) return MLG_EINVAL;
+    if (MLG_SPLIT_TILE == 192 && N % 192 == 0) {
+        const long nt = (long)(N / 192) * ((M + 191) / 192);
+        const long g = std::min<long>(g_num_cus, (nt + 7) / 8 * 8);
+        hipLaunchKernelGGL(dma::k_gemm192s<Epi>, dim3((unsigned)g), dim3(512), 0, s, A, W, M, N, K0, lda, ldw, epi);
+        MLG_LAUNCH_CHECK();
+        return MLG_OK;
+    }
+    if (N % 256) return MLG_EINVAL;
     const long ntiles = (long)(N / 256) * ((M + 255) / 256);
     const long grid = std::min<long>(g_num_cus, (ntiles + 7) / 8 * 8);
     hipLaunchKernelGGL(dma::k_gemm256s<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K0, lda, ldw, epi);
@@ -1122,9 +1258,9 @@ int mlg_gemm_bias_add_relu(const bf16_t* A, int lda, const bf16_t* W, const floa
     return launch(A, W, M, N, K_, lda, K_, EpiBiasAddRelu{R, X, ldx, C, bias}, s);
 }
 int mlg_gemm_conv(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, int ldr, float* X,
-                  int ldx, bf16_t* C, int ldc, int act, int act_cols, int M, int N, int K_, hipStream_t s) {
+                  int ldx, bf16_t* C, int ldc, int act, int act_cols, int M, int N, int K_, hipStream_t s, float vdiv) {
     if ((!X && !C) || act < 0 || act > 3) return MLG_EINVAL;
-    return launch(A, W, M, N, K_, lda, K_, EpiConv{bias, R, ldr, X, ldx, C, ldc, act, act_cols}, s);
+    return launch(A, W, M, N, K_, lda, K_, EpiConv{bias, R, ldr, X, ldx, C, ldc, act, act_cols, vdiv}, s);
 }
 int mlg_gemm_set_variant(int variant) {
     if (variant < 1 || variant > 5) return MLG_EINVAL;

@@ -41,9 +41,11 @@ int mlg_gemm_bias_relu_bf16(const bf16_t* A, int lda, const bf16_t* W, const flo
 int mlg_gemm_bias_add_relu(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, float* X,
                            int ldx, bf16_t* C, int M, int N, int K_, hipStream_t s);
 // y = A . W^T (+ bias) (+ R) -> act (1 relu, 2 leaky 0.01, 3 elu + 1 on cols < act_cols)
-// -> f32 X and / or bf16 C (LoFTR convs on im2col rows and its transformer linears)
+// (vdiv != 0: cols >= act_cols / vdiv) -> f32 X and / or bf16 C (LoFTR convs on im2col rows
+// and its transformer linears)
 int mlg_gemm_conv(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, int ldr, float* X,
-                  int ldx, bf16_t* C, int ldc, int act, int act_cols, int M, int N, int K_, hipStream_t s);
+                  int ldx, bf16_t* C, int ldc, int act, int act_cols, int M, int N, int K_, hipStream_t s,
+                  float vdiv = 0.f);
 // implicit-GEMM k x k (k = 1 or 3, pad k / 2) stride-s convolution over NHWC bf16 [B, H, W, C]
 // (C % 64 == 0), weights [N][tap * C + c], EpiConv epilogue; `zero` = 16 zero bytes
 int mlg_conv_implicit(const bf16_t* in, const bf16_t* zero, int B, int H, int W, int C, int k, int s,
@@ -96,6 +98,8 @@ int mlg_salad_head(const bf16_t* xn, const float* Y, int B, int T, const float* 
 // knn.hip
 int mlg_row_normalize(const float* X, float* Xn, int N, int D, float* norms, hipStream_t s);
 int mlg_similarity_f32(const float* A, int Q, const float* B, int N, int D, float* S, int lds, hipStream_t s);
+// the same product stored as LoFTR's coarse similarity (S / 256) / 0.1
+int mlg_similarity_f32_loftr(const float* A, int Q, const float* B, int N, int D, float* S, int lds, hipStream_t s);
 int mlg_similarity_f32_t(const float* A, int Q, const float* B, int N, int D, float* S, int lds, float* St, int ldt,
                          hipStream_t s);
 int mlg_topk_gate(const float* S, int lds, int N, int Q, const double* tq, const double* tdb, const int64_t* fq,
@@ -175,7 +179,9 @@ struct mlg_lg_conf_i {
     float thr, width;
     float* lz; uint8_t* flags;
 };
-// relu != 0: ReLU without LayerNorm (SuperGlue's MLP with BatchNorm folded into Wf1)
+// relu == 1: ReLU without LayerNorm (SuperGlue's MLP with BatchNorm folded into Wf1);
+// relu == 2: a LoFTREncoderLayer tail (no biases; Wout = merge, then norm1; ReLU MLP; norm2
+// before the residual; ln_g / ln_b = [norm1 | norm2], 256 each)
 int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s,
                const mlg_lg_conf_i* conf = nullptr, int relu = 0);
 // lg_proj.hip -- LightGlue q/k/v projections (+ rotary for the self block) straight into

@@ -168,6 +168,10 @@ __device__ __forceinline__ void sim_tile(const float* __restrict__ A, int Q, con
 }
 
 // St (optional): the transpose, St[j][i] = S[i][j] (SuperGlue's column passes)
+// LFSIM: the stored value is LoFTR's coarse similarity (S / 256) / 0.1 (the reference
+// scales each side by 1/16 and divides the product by the temperature 0.1), computed
+// once here instead of in each dual-softmax pass over S (loftr.hip)
+template <bool LFSIM = false>
 __global__ __launch_bounds__(256, 2) void k_sim_f32(const float* __restrict__ A, int Q, const float* __restrict__ B,
                                                     int N, int D, float* __restrict__ S, int lds,
                                                     float* __restrict__ St, int ldt) {
@@ -178,6 +182,13 @@ __global__ __launch_bounds__(256, 2) void k_sim_f32(const float* __restrict__ A,
     const int wm = wave >> 1, wn = wave & 1;
     f32x16 acc[2][2];
     sim_tile(A, Q, B, N, D, m0, n0, As, Bs, acc);
+    if (LFSIM)
+#pragma unroll
+        for (int ta = 0; ta < 2; ++ta)
+#pragma unroll
+            for (int tb = 0; tb < 2; ++tb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[ta][tb][r] = (acc[ta][tb][r] * (1.0f / 256.0f)) / 0.1f;
     // D[i][j]: col j = lane & 31, row i = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
 #pragma unroll
     for (int ta = 0; ta < 2; ++ta)
@@ -880,7 +891,16 @@ int mlg_similarity_f32_t(const float* A, int Q, const float* B, int N, int D, fl
     if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return MLG_EINVAL;
     if (St && (ldt < Q || (ldt % 4) || (reinterpret_cast<uintptr_t>(St) & 15))) return MLG_EINVAL;
     dim3 grid((N + SBN - 1) / SBN, (Q + SBM - 1) / SBM);
-    hipLaunchKernelGGL(k_sim_f32, grid, dim3(256), 0, s, A, Q, B, N, D, S, lds, St, ldt);
+    hipLaunchKernelGGL(k_sim_f32<false>, grid, dim3(256), 0, s, A, Q, B, N, D, S, lds, St, ldt);
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}
+
+int mlg_similarity_f32_loftr(const float* A, int Q, const float* B, int N, int D, float* S, int lds, hipStream_t s) {
+    if (N <= 0 || D <= 0 || Q <= 0 || (D % 4) || lds < N) return MLG_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return MLG_EINVAL;
+    dim3 grid((N + SBN - 1) / SBN, (Q + SBM - 1) / SBM);
+    hipLaunchKernelGGL(k_sim_f32<true>, grid, dim3(256), 0, s, A, Q, B, N, D, S, lds, (float*)nullptr, 0);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }

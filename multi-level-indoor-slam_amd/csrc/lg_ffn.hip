@@ -180,10 +180,17 @@ __device__ __forceinline__ void zero(f32x16 (&acc)[NT][MT]) {
 // bench step on one box (tools/gpu_ab_ffn_proj.sh), so it is off.
 // R token rows per workgroup of NW waves: <64, 4> (two workgroups per CU) or <128, 8>
 // (one per CU: every weight fragment fetched from L2 feeds twice the MFMAs).
-template <bool PERSIST, int R, int NW>
+//
+// LOFTR: the tail of a LoFTREncoderLayer (kornia loftr/loftr_module/transformer.py, the
+// reference's LoFTR matcher, geometric_verification.py:458-526) on the same three GEMMs:
+//   msg = norm1(merge(attn));  x += norm2(mlp(cat[x, msg]))   (mlp: Linear, ReLU, Linear)
+// no biases; norm1 (LayerNorm 256) in the msg epilogue, norm2 in the final row pass;
+// LayerNorm affine from ln_g / ln_b = [norm1 (256) | norm2 (256)].
+template <bool PERSIST, int R, int NW, bool LOFTR = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_t* __restrict__ ctx, float* __restrict__ X,
                                                   bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w,
                                                   mlg_lg_conf_i cf, int relu) {
+    if (LOFTR) relu = 1;
     constexpr int MT = R / 32, NT1 = 256 / NW / 32, NT2 = 512 / NW / 32, NTH = 64 * NW;
     constexpr int RING = NW == 8 ? 8 : MLG_FFN_RING2;  // weight k-steps in flight per wave (ffn1)
     // ring of the msg / ffn2 phases (NT1 column tiles, half the MFMAs per k-step of ffn1).
@@ -204,12 +211,12 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
     float* s_bf2 = prm + 1792;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
     for (int i = tid; i < 512; i += NTH) {
-        s_bf1[i] = w.bf1[i];
-        s_lng[i] = relu ? 1.f : w.ln_g[i];
-        s_lnb[i] = relu ? 0.f : w.ln_b[i];
+        s_bf1[i] = LOFTR ? 0.f : w.bf1[i];
+        s_lng[i] = (relu && !LOFTR) ? 1.f : w.ln_g[i];
+        s_lnb[i] = (relu && !LOFTR) ? 0.f : w.ln_b[i];
         if (i < 256) {
-            s_bout[i] = w.bout[i];
-            s_bf2[i] = w.bf2[i];
+            s_bout[i] = LOFTR ? 0.f : w.bout[i];
+            s_bf2[i] = LOFTR ? 0.f : w.bf2[i];
         }
     }
     const int ntiles = (M + R - 1) / R;
@@ -244,6 +251,47 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             zero(acc);
             gemm_phase<NT1, MT, RING1>(w.Wout, 256, 32 * NT1 * wave, 4, 32, lds, acc);
             __syncthreads();  // every wave has read the ctx half
+            float mean1[MT], rstd1[MT];
+            if constexpr (LOFTR) {
+                // norm1 over the 256 msg columns of each row: lane -> half-wave -> waves
+                // through LDS, two passes (mean, then centred variance) as torch
+    #pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    float sum = 0.f;
+    #pragma unroll
+                    for (int t = 0; t < NT1; ++t)
+    #pragma unroll
+                        for (int i = 0; i < 16; ++i) sum += acc[t][mt][i];
+                    sum += __shfl_xor(sum, 32, 64);
+                    if (hh == 0) red[0][wave][32 * mt + col] = sum;
+                }
+                __syncthreads();
+    #pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    float sum = 0.f;
+    #pragma unroll
+                    for (int v = 0; v < NW; ++v) sum += red[0][v][32 * mt + col];
+                    mean1[mt] = sum * (1.0f / 256.0f);
+                    float q = 0.f;
+    #pragma unroll
+                    for (int t = 0; t < NT1; ++t)
+    #pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const float d = acc[t][mt][i] - mean1[mt];
+                            q += d * d;
+                        }
+                    q += __shfl_xor(q, 32, 64);
+                    if (hh == 0) red[1][wave][32 * mt + col] = q;
+                }
+                __syncthreads();
+    #pragma unroll
+                for (int mt = 0; mt < MT; ++mt) {
+                    float q = 0.f;
+    #pragma unroll
+                    for (int v = 0; v < NW; ++v) q += red[1][v][32 * mt + col];
+                    rstd1[mt] = 1.0f / sqrtf(q * (1.0f / 256.0f) + 1e-5f);
+                }
+            }
     #pragma unroll
             for (int t = 0; t < NT1; ++t)
     #pragma unroll
@@ -253,9 +301,22 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
     #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) {
                         const f32x16& a = acc[t][mt];
+                        float y0, y1, y2, y3;
+                        if constexpr (LOFTR) {
+                            const float4 lg = *reinterpret_cast<const float4*>(s_lng + n);
+                            const float4 lb = *reinterpret_cast<const float4*>(s_lnb + n);
+                            y0 = (a[4 * g] - mean1[mt]) * rstd1[mt] * lg.x + lb.x;
+                            y1 = (a[4 * g + 1] - mean1[mt]) * rstd1[mt] * lg.y + lb.y;
+                            y2 = (a[4 * g + 2] - mean1[mt]) * rstd1[mt] * lg.z + lb.z;
+                            y3 = (a[4 * g + 3] - mean1[mt]) * rstd1[mt] * lg.w + lb.w;
+                        } else {
+                            y0 = a[4 * g] + b.x;
+                            y1 = a[4 * g + 1] + b.y;
+                            y2 = a[4 * g + 2] + b.z;
+                            y3 = a[4 * g + 3] + b.w;
+                        }
                         *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, 32 + n / 8) + 8 * hh) =
-                            make_uint2(pack_bf16x2(a[4 * g] + b.x, a[4 * g + 1] + b.y),
-                                       pack_bf16x2(a[4 * g + 2] + b.z, a[4 * g + 3] + b.w));
+                            make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
                     }
                 }
         }
@@ -412,10 +473,23 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                 const float4 y = *reinterpret_cast<const float4*>(lds + r * 1024 + ((lane ^ (r & 15)) << 4));
                 float4* px = reinterpret_cast<float4*>(X + (size_t)m * 256) + lane;
                 float4 x = xr[i];
-                x.x += y.x;
-                x.y += y.y;
-                x.z += y.z;
-                x.w += y.w;
+                if constexpr (LOFTR) {  // norm2 over the row (one wave = one 256-wide row)
+                    const float mean = wave_sum(y.x + y.y + y.z + y.w) * (1.0f / 256.0f);
+                    const float d0 = y.x - mean, d1 = y.y - mean, d2 = y.z - mean, d3 = y.w - mean;
+                    const float q = wave_sum(fmaf(d3, d3, fmaf(d2, d2, fmaf(d1, d1, d0 * d0))));
+                    const float rstd = 1.0f / sqrtf(q * (1.0f / 256.0f) + 1e-5f);
+                    const float4 lg = *reinterpret_cast<const float4*>(s_lng + 256 + 4 * lane);
+                    const float4 lb = *reinterpret_cast<const float4*>(s_lnb + 256 + 4 * lane);
+                    x.x += d0 * rstd * lg.x + lb.x;
+                    x.y += d1 * rstd * lg.y + lb.y;
+                    x.z += d2 * rstd * lg.z + lb.z;
+                    x.w += d3 * rstd * lg.w + lb.w;
+                } else {
+                    x.x += y.x;
+                    x.y += y.y;
+                    x.z += y.z;
+                    x.w += y.w;
+                }
                 stream_st(px, x);
                 *reinterpret_cast<uint2*>(xcopy + (size_t)m * ldc + 4 * lane) =
                     make_uint2(pack_bf16x2(x.x, x.y), pack_bf16x2(x.z, x.w));
@@ -482,7 +556,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
 int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s,
                const mlg_lg_conf_i* conf, int relu) {
     if (M <= 0) return MLG_OK;
-    if (ldc < 256 || (ldc % 8)) return MLG_EINVAL;
+    if (ldc < 256 || (ldc % 8) || relu < 0 || relu > 2) return MLG_EINVAL;
+    if (relu == 2 && (MLG_FFN_ROWS != 64 || MLG_FFN_GRID > 0)) return MLG_EINVAL;  // LoFTR form: default launch only
     mlg_lg_conf_i cf{};
     if (conf) cf = *conf;
 #if MLG_FFN_ROWS == 128
@@ -495,8 +570,12 @@ int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const
                        relu);
 #else
     const long ntiles = (M + 63) / 64;
-    hipLaunchKernelGGL((k_lg_ffn<false, 64, 4>), dim3((unsigned)ntiles), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf,
-                       relu);
+    if (relu == 2)
+        hipLaunchKernelGGL((k_lg_ffn<false, 64, 4, true>), dim3((unsigned)ntiles), dim3(256), 0, s, ctx, X, xcopy, ldc,
+                           M, w, cf, relu);
+    else
+        hipLaunchKernelGGL((k_lg_ffn<false, 64, 4>), dim3((unsigned)ntiles), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w,
+                           cf, relu);
 #endif
     MLG_LAUNCH_CHECK();
     return MLG_OK;

@@ -195,8 +195,8 @@ __global__ void k_lf_tokens(const float* __restrict__ coarse, const int32_t* __r
 }
 
 // ------------------------------------------------------ linear attention ----
-// per (segment, head): KV[dk][dv] = sum_s phik[s][dk] * (v[s][dv] / L), ksum[dk] = sum_s
-// phik[s][dk]; phik / v rows of segment g start at (g * L + s) * ld + col offset.  Thread
+// per (segment, head): KV[dk][dv] = sum_s phik[s][dk] * (v[s][dv] / L) (v arrives divided by
+// L from the qkv GEMM epilogue), ksum[dk] = sum_s phik[s][dk]; phik / v rows of segment g start at (g * L + s) * ld + col offset.  Thread
 // (dk, dv-quad) of a 256-thread group; tokens staged 64 at a time through LDS.
 template <int DH>
 __global__ __launch_bounds__(256) void k_lf_kv(const float* __restrict__ k, const float* __restrict__ v, int ldk,
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void k_lf_kv(const float* __restrict__ k, cons
             if (s < n) {
                 const size_t row = (size_t)src * L + s0 + s;
                 a = k[row * ldk + h * DH + d];
-                b = v[row * ldv + h * DH + d] / (float)L;
+                b = v[row * ldv + h * DH + d];  // already v / L (qkv GEMM epilogue)
             }
             sk[s][d] = a;
             sv[s][d] = b;
@@ -270,7 +270,6 @@ __global__ __launch_bounds__(256) void k_lf_kv_part(const float* __restrict__ k,
     const int s0 = c * LF_KV_CHUNK, s1 = min(L, s0 + LF_KV_CHUNK);
     float acc[B][B] = {};
     float ks[B] = {};
-    const float fL = (float)L;
     // 8 tokens' k / v loads in flight before their FMAs (tokens still summed in order)
     int s = s0;
     for (; s + 8 <= s1; s += 8) {
@@ -283,7 +282,7 @@ __global__ __launch_bounds__(256) void k_lf_kv_part(const float* __restrict__ k,
 #pragma unroll
             for (int i = 0; i < B; ++i) {
                 a[u][i] = kr[i];
-                b[u][i] = vr[i] / fL;
+                b[u][i] = vr[i];
             }
         }
 #pragma unroll
@@ -303,7 +302,7 @@ __global__ __launch_bounds__(256) void k_lf_kv_part(const float* __restrict__ k,
 #pragma unroll
         for (int i = 0; i < B; ++i) {
             a[i] = kr[i];
-            b[i] = vr[i] / fL;
+            b[i] = vr[i];
         }
 #pragma unroll
         for (int i = 0; i < B; ++i) {
@@ -426,97 +425,161 @@ __global__ __launch_bounds__(256) void k_lf_ln(const float* __restrict__ in, con
 }
 
 // ------------------------------------------------------- dual softmax -------
-// sim = (S / 256) / 0.1 (the reference divides each side by 16 and the product by the
-// temperature); per row i: max_j sim, sum_j exp(sim - max); per column likewise.
-__device__ __forceinline__ float lf_sim(float s) { return (s * (1.0f / 256.0f)) / 0.1f; }
+// S holds the similarity x = (f0 . f1 / 256) / 0.1 (mlg_similarity_f32_loftr: the
+// reference divides each side by 16 and the product by the temperature); per row i:
+// max_j x, sum_j exp(x - max); per column likewise; conf = softmax over dim 1 (column-
+// wise) * softmax over dim 2 (row-wise), as torch.  Softmax sums are two-pass (max, then
+// sum of exp(x - max)), with the row / column held in registers (one HBM read each).
+// Row-best / column-best of conf: conf_ij is proportional to exp(2 x_ij - rkey_i - ckey_j)
+// with rkey = rmax + log rsum, ckey = cmax + log csum, so a pass keeps the best key and
+// evaluates the exact conf only where the key is within LF_KEY_BAND of it (f32 conf
+// rounding moves the key by ~1e-6): the same argmax / max as the exact conf everywhere,
+// two exponentials per candidate instead of per cell.
+constexpr int LF_ROWREG = 24;        // float4 per lane: rows of up to 6144 cells in registers
+constexpr float LF_KEY_BAND = 1e-3f;  // + 1e-5 |key|
+constexpr int LF_RCH = 64;           // rows per column chunk
 
+__device__ __forceinline__ float lf_band(float k) { return LF_KEY_BAND + 1e-5f * fabsf(k); }
+
+// conf as the reference computes it: softmax(sim, 1) * softmax(sim, 2)
+__device__ __forceinline__ float lf_conf(float x, float rm, float rz, float cm, float cz) {
+    return (expf(x - cm) / cz) * (expf(x - rm) / rz);
+}
+
+// one wave per row; the row lives in v[] (lane l: float4 l + 64 k); rows longer than
+// 256 LF_ROWREG cells take the two-pass loop over memory
 __global__ __launch_bounds__(256) void k_lf_rowstats(const float* __restrict__ S, int L, float* __restrict__ rmax,
-                                                     float* __restrict__ rsum) {
+                                                     float* __restrict__ rsum, float* __restrict__ rkey) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= L) return;
     const float* s = S + (size_t)row * L;
-    float m = -INFINITY, z = 0.f;  // online per lane, merged across the wave
-    auto add = [&](float v) {
-        const float x = lf_sim(v), mn = fmaxf(m, x);
-        z = z * expf(m - mn) + expf(x - mn);
-        m = mn;
-    };
-    if ((L & 3) == 0) {
+    float m = -INFINITY, z = 0.f;
+    if ((L & 3) == 0 && L <= 256 * LF_ROWREG) {
         const float4* s4 = reinterpret_cast<const float4*>(s);
-        for (int j = lane; j < L / 4; j += 64) {
-            const float4 v = s4[j];
-            add(v.x);
-            add(v.y);
-            add(v.z);
-            add(v.w);
+        float4 v[LF_ROWREG];
+#pragma unroll
+        for (int k = 0; k < LF_ROWREG; ++k) {
+            const int j = lane + 64 * k;
+            v[k] = j < L / 4 ? s4[j] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+            m = fmaxf(m, fmaxf(fmaxf(v[k].x, v[k].y), fmaxf(v[k].z, v[k].w)));
         }
+        m = wave_max(m);
+#pragma unroll
+        for (int k = 0; k < LF_ROWREG; ++k)
+            if (lane + 64 * k < L / 4) z += expf(v[k].x - m) + expf(v[k].y - m) + expf(v[k].z - m) + expf(v[k].w - m);
     } else {
-        for (int j = lane; j < L; j += 64) add(s[j]);
+        for (int j = lane; j < L; j += 64) m = fmaxf(m, s[j]);
+        m = wave_max(m);
+        for (int j = lane; j < L; j += 64) z += expf(s[j] - m);
     }
-    const float mw = wave_max(m);
-    z = wave_sum(m == -INFINITY ? 0.f : z * expf(m - mw));
-    m = mw;
+    z = wave_sum(z);
     if (lane == 0) {
         rmax[row] = m;
         rsum[row] = z;
+        rkey[row] = m + logf(z);
     }
 }
 
 // Column statistics in two steps so that the whole chip reads S: grid (column blocks of
-// 256, row chunks of LF_RCH); thread = column, coalesced 1 KiB row reads.  Chunk c's
-// (max, sum exp(x - max)) -> pm / pz [c][L]; k_lf_colfin merges the chunks in order
-// (max, then sum_c pz_c exp(pm_c - max)).
-constexpr int LF_RCH = 64;
+// 256, row chunks of LF_RCH); thread = column, coalesced 1 KiB row reads, the chunk's 64
+// values in registers.  Chunk c's (max, sum exp(x - max)) -> pm / pz [c][L]; k_lf_colfin
+// merges the chunks (max, then sum_c pz_c exp(pm_c - max)).
 __global__ __launch_bounds__(256) void k_lf_colpart(const float* __restrict__ S, int L, float* __restrict__ pm,
                                                     float* __restrict__ pz) {
     const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
     if (col >= L) return;
-    const int r0 = c * LF_RCH, r1 = min(L, r0 + LF_RCH);
-    float m = -INFINITY, z = 0.f;  // online: one read of S
-#pragma unroll 8
-    for (int i = r0; i < r1; ++i) {
-        const float x = lf_sim(S[(size_t)i * L + col]), mn = fmaxf(m, x);
-        z = z * expf(m - mn) + expf(x - mn);
-        m = mn;
+    const int r0 = c * LF_RCH, n = min(L - r0, LF_RCH);
+    float v[LF_RCH], m = -INFINITY, z = 0.f;
+#pragma unroll
+    for (int i = 0; i < LF_RCH; ++i) {
+        v[i] = i < n ? S[(size_t)(r0 + i) * L + col] : -INFINITY;
+        m = fmaxf(m, v[i]);
     }
+#pragma unroll
+    for (int i = 0; i < LF_RCH; ++i)
+        if (i < n) z += expf(v[i] - m);
     pm[(size_t)c * L + col] = m;
     pz[(size_t)c * L + col] = z;
 }
 
+// 64 columns x 4 chunk groups per workgroup (group g: chunks g, g + 4, ..): the chunk
+// loads of a column run in parallel; the four partials combine in group order
 __global__ __launch_bounds__(256) void k_lf_colfin(const float* __restrict__ pm, const float* __restrict__ pz, int L,
-                                                   int nch, float* __restrict__ cmax, float* __restrict__ csum) {
-    const int col = blockIdx.x * 256 + threadIdx.x;
-    if (col >= L) return;
-    float m = -INFINITY, z = 0.f;  // chunks merged in order
-#pragma unroll 8
-    for (int c = 0; c < nch; ++c) {
-        const float pmc = pm[(size_t)c * L + col], mn = fmaxf(m, pmc);
-        z = z * expf(m - mn) + pz[(size_t)c * L + col] * expf(pmc - mn);
-        m = mn;
+                                                   int nch, float* __restrict__ cmax, float* __restrict__ csum,
+                                                   float* __restrict__ ckey) {
+    __shared__ float part[4][64];
+    const int cl = threadIdx.x & 63, g = threadIdx.x >> 6, col = blockIdx.x * 64 + cl;
+    const bool ok = col < L;
+    float m = -INFINITY;
+    if (ok)
+#pragma unroll 4
+        for (int c = g; c < nch; c += 4) m = fmaxf(m, pm[(size_t)c * L + col]);
+    part[g][cl] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(part[0][cl], part[1][cl]), fmaxf(part[2][cl], part[3][cl]));
+    __syncthreads();
+    float z = 0.f;
+    if (ok)
+#pragma unroll 4
+        for (int c = g; c < nch; c += 4) z += pz[(size_t)c * L + col] * expf(pm[(size_t)c * L + col] - m);
+    part[g][cl] = z;
+    __syncthreads();
+    if (g == 0 && ok) {
+        z = ((part[0][cl] + part[1][cl]) + part[2][cl]) + part[3][cl];
+        cmax[col] = m;
+        csum[col] = z;
+        ckey[col] = m + logf(z);
     }
-    cmax[col] = m;
-    csum[col] = z;
-}
-
-// conf = softmax over dim 1 (column-wise) * softmax over dim 2 (row-wise), as torch
-__device__ __forceinline__ float lf_conf(float s, float rm, float rz, float cm, float cz) {
-    const float x = lf_sim(s);
-    return (expf(x - cm) / cz) * (expf(x - rm) / rz);
 }
 
 __global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S, int L, const float* __restrict__ rmax,
                                                     const float* __restrict__ rsum, const float* __restrict__ cmax,
-                                                    const float* __restrict__ csum, float* __restrict__ bval,
-                                                    int32_t* __restrict__ bidx) {
+                                                    const float* __restrict__ csum, const float* __restrict__ ckey,
+                                                    float* __restrict__ bval, int32_t* __restrict__ bidx) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= L) return;
     const float* s = S + (size_t)row * L;
     const float rm = rmax[row], rz = rsum[row];
     float bv = -1.f;
     int bi = 0x7fffffff;
-    for (int j = lane; j < L; j += 64) {
-        const float c = lf_conf(s[j], rm, rz, cmax[j], csum[j]);
-        if (c > bv) { bv = c; bi = j; }
+    auto take = [&](float x, int j) {
+        const float c = lf_conf(x, rm, rz, cmax[j], csum[j]);
+        if (c > bv || (c == bv && j < bi)) { bv = c; bi = j; }
+    };
+    float kb = -INFINITY;
+    if ((L & 3) == 0 && L <= 256 * LF_ROWREG) {
+        const float4* s4 = reinterpret_cast<const float4*>(s);
+        const float4* k4 = reinterpret_cast<const float4*>(ckey);
+        float4 v[LF_ROWREG];
+#pragma unroll
+        for (int k = 0; k < LF_ROWREG; ++k) {
+            const int j = lane + 64 * k;
+            if (j < L / 4) {
+                v[k] = s4[j];
+                const float4 ck = k4[j];
+                kb = fmaxf(kb, fmaxf(fmaxf(2.f * v[k].x - ck.x, 2.f * v[k].y - ck.y),
+                                     fmaxf(2.f * v[k].z - ck.z, 2.f * v[k].w - ck.w)));
+            }
+        }
+        kb = wave_max(kb);
+        const float lim = kb - lf_band(kb);
+#pragma unroll
+        for (int k = 0; k < LF_ROWREG; ++k) {
+            const int j = lane + 64 * k;
+            if (j < L / 4) {
+                const float4 ck = k4[j];
+                if (2.f * v[k].x - ck.x >= lim) take(v[k].x, 4 * j);
+                if (2.f * v[k].y - ck.y >= lim) take(v[k].y, 4 * j + 1);
+                if (2.f * v[k].z - ck.z >= lim) take(v[k].z, 4 * j + 2);
+                if (2.f * v[k].w - ck.w >= lim) take(v[k].w, 4 * j + 3);
+            }
+        }
+    } else {
+        for (int j = lane; j < L; j += 64) kb = fmaxf(kb, 2.f * s[j] - ckey[j]);
+        kb = wave_max(kb);
+        const float lim = kb - lf_band(kb);
+        for (int j = lane; j < L; j += 64)
+            if (2.f * s[j] - ckey[j] >= lim) take(s[j], j);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {  // max value, first index on ties
@@ -530,17 +593,29 @@ __global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S,
     }
 }
 
-// column max of conf, chunked like k_lf_colpart (max is exact in any order)
+// column max of conf per row chunk (max is exact in any order)
 __global__ __launch_bounds__(256) void k_lf_colmaxpart(const float* __restrict__ S, int L,
                                                        const float* __restrict__ rmax, const float* __restrict__ rsum,
-                                                       const float* __restrict__ cmax, const float* __restrict__ csum,
-                                                       float* __restrict__ pb) {
+                                                       const float* __restrict__ rkey, const float* __restrict__ cmax,
+                                                       const float* __restrict__ csum, float* __restrict__ pb) {
+    __shared__ float rk[LF_RCH];
     const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
+    const int r0 = c * LF_RCH, n = min(L - r0, LF_RCH);
+    if (threadIdx.x < LF_RCH) rk[threadIdx.x] = threadIdx.x < n ? rkey[r0 + threadIdx.x] : INFINITY;
+    __syncthreads();
     if (col >= L) return;
-    const int r0 = c * LF_RCH, r1 = min(L, r0 + LF_RCH);
     const float cm = cmax[col], cz = csum[col];
+    float v[LF_RCH], kb = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < LF_RCH; ++i) {
+        v[i] = i < n ? S[(size_t)(r0 + i) * L + col] : 0.f;
+        kb = fmaxf(kb, 2.f * v[i] - rk[i]);
+    }
+    const float lim = kb - lf_band(kb);
     float m = -1.f;
-    for (int i = r0; i < r1; ++i) m = fmaxf(m, lf_conf(S[(size_t)i * L + col], rmax[i], rsum[i], cm, cz));
+#pragma unroll
+    for (int i = 0; i < LF_RCH; ++i)
+        if (i < n && 2.f * v[i] - rk[i] >= lim) m = fmaxf(m, lf_conf(v[i], rmax[r0 + i], rsum[r0 + i], cm, cz));
     pb[(size_t)c * L + col] = m;
 }
 
@@ -855,6 +930,28 @@ int mlg_loftr_features(const mlg_loftr_weights* wp, const uint8_t* frames_in, in
 // ------------------------------------------------------------- matching -----
 namespace {
 
+// Coarse layers' block tail (merge, norm1, MLP, norm2, residual) as ONE fused kernel per
+// 64-token tile (lg_ffn.hip, LoFTR form): the merge output, the MLP hidden and the
+// pre-norm2 message never leave LDS (per token 3.5 KB of HBM instead of ~11 KB through
+// five launches).  0 builds the unfused GEMM + LayerNorm sequence (A/B arm).
+#ifndef MLG_LF_FUSED_TAIL
+#define MLG_LF_FUSED_TAIL 1
+#endif
+
+// nn.Linear weight [N][K] bf16 -> k-step-major [K / 16][N][16] (lg_ffn.hip's layout)
+__global__ void k_lf_pack_kstep(const bf16_t* __restrict__ w, int N, int K, bf16_t* __restrict__ out) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)N * K) return;
+    const int n = (int)(i / K), k = (int)(i % K);
+    out[((size_t)(k >> 4) * N + n) * 16 + (k & 15)] = w[i];
+}
+
+struct TailW {  // one coarse layer's packed block-tail weights (workspace)
+    bf16_t *wmerge, *w1, *w2;
+    float *ln_g, *ln_b;  // [norm1 | norm2]
+};
+constexpr size_t TAIL_ELEMS = 256 * 256 + 512 * 512 + 256 * 512;  // bf16 per layer
+
 struct LayerBufs {
     float* x;     // [rows][d] residual stream
     bf16_t* cat;  // [rows][2d]: bf16(x) | norm1(msg)
@@ -870,18 +967,21 @@ struct LayerBufs {
 // One LoFTREncoderLayer over `nseg` segments of L tokens (rows x0 .. of the buffers);
 // source rows src0 (== x0 for self).  d = 256 (coarse) or 128 (fine).
 int encoder_layer(const mlg_loftr_layer& lw, const LayerBufs& b, int d, long x0, long src0, int nseg, int L,
-                  hipStream_t s) {
+                  hipStream_t s, const TailW* tw = nullptr) {
     const long rows = (long)nseg * L;
     const int dh = d / 8;
     float* qkv = b.qkv + x0 * 3 * d;
-    if (x0 == src0) {  // q | k | v in one GEMM, elu + 1 on q and k
+    // q | k | v, elu + 1 on q and k, v stored as v / L (the reference's values / v_length,
+    // divided once here rather than per (k, v) product in k_lf_kv*)
+    const float vl = (float)L;
+    if (x0 == src0) {
         LF_TRY(mlg_gemm_conv(b.cat + x0 * 2 * d, 2 * d, (const bf16_t*)lw.w, nullptr, nullptr, 0, qkv, 3 * d, nullptr,
-                             0, 3, 2 * d, (int)rows, 3 * d, d, s));
+                             0, 3, 2 * d, (int)rows, 3 * d, d, s, vl));
     } else {
         LF_TRY(mlg_gemm_conv(b.cat + x0 * 2 * d, 2 * d, (const bf16_t*)lw.w, nullptr, nullptr, 0, qkv, 3 * d, nullptr,
                              0, 3, d, (int)rows, d, d, s));
         LF_TRY(mlg_gemm_conv(b.cat + src0 * 2 * d, 2 * d, (const bf16_t*)lw.w + (size_t)d * d, nullptr, nullptr, 0,
-                             qkv + d, 3 * d, nullptr, 0, 3, d, (int)rows, 2 * d, d, s));
+                             qkv + d, 3 * d, nullptr, 0, 3, d, (int)rows, 2 * d, d, s, vl));
     }
     float* kv = b.kv + (size_t)(x0 / L) * 8 * dh * dh;
     float* ks = b.ks + (size_t)(x0 / L) * 8 * dh;
@@ -919,6 +1019,15 @@ int encoder_layer(const mlg_loftr_layer& lw, const LayerBufs& b, int d, long x0,
                            b.msg + x0 * d);
     }
     MLG_LAUNCH_CHECK();
+    if (tw) {  // d == 256: merge -> norm1 -> MLP -> norm2 -> residual, fused
+        mlg_lg_block_i bw{};
+        bw.Wout = tw->wmerge;
+        bw.Wf1 = tw->w1;
+        bw.Wf2 = tw->w2;
+        bw.ln_g = tw->ln_g;
+        bw.ln_b = tw->ln_b;
+        return mlg_lg_ffn(b.msg + x0 * d, b.x + x0 * d, b.cat + x0 * 2 * d, 2 * d, (int)rows, bw, s, nullptr, 2);
+    }
     // merge -> norm1 -> bf16 into cat[:, d:]
     LF_TRY(mlg_gemm_conv(b.msg + x0 * d, d, (const bf16_t*)lw.wmerge, nullptr, nullptr, 0, b.t + x0 * d, d, nullptr,
                          0, 0, 0, (int)rows, d, d, s));
@@ -948,15 +1057,46 @@ int encoder_layer(const mlg_loftr_layer& lw, const LayerBufs& b, int d, long x0,
 // the reference's layer order: self on both sides; cross updates side 0 from side 1,
 // then side 1 from the updated side 0.  Side-major rows: side s, segment g at
 // (s * nseg + g) * L.
-int transformer(const mlg_loftr_layer* layers, int nl, const LayerBufs& b, int d, int nseg, int L, hipStream_t s) {
+int transformer(const mlg_loftr_layer* layers, int nl, const LayerBufs& b, int d, int nseg, int L, hipStream_t s,
+                const TailW* tails = nullptr) {
     const long half = (long)nseg * L;
     for (int i = 0; i < nl; ++i) {
+        const TailW* tw = tails ? tails + i : nullptr;
         if (i % 2 == 0) {
-            LF_TRY(encoder_layer(layers[i], b, d, 0, 0, 2 * nseg, L, s));
+            LF_TRY(encoder_layer(layers[i], b, d, 0, 0, 2 * nseg, L, s, tw));
         } else {
-            LF_TRY(encoder_layer(layers[i], b, d, 0, half, nseg, L, s));
-            LF_TRY(encoder_layer(layers[i], b, d, half, 0, nseg, L, s));
+            LF_TRY(encoder_layer(layers[i], b, d, 0, half, nseg, L, s, tw));
+            LF_TRY(encoder_layer(layers[i], b, d, half, 0, nseg, L, s, tw));
         }
+    }
+    return MLG_OK;
+}
+
+// the coarse layers' tail weights packed for the fused kernel (a few microseconds per call)
+int pack_tails(const mlg_loftr_weights& w, char* base, TailW (&tw)[8], hipStream_t s) {
+    bf16_t* p = (bf16_t*)base;
+    float* f = (float*)(base + 8 * TAIL_ELEMS * 2);
+    for (int l = 0; l < 8; ++l) {
+        const mlg_loftr_layer& lw = w.coarse[l];
+        tw[l].wmerge = p;
+        tw[l].w1 = p + 256 * 256;
+        tw[l].w2 = p + 256 * 256 + 512 * 512;
+        tw[l].ln_g = f + l * 1024;
+        tw[l].ln_b = f + l * 1024 + 512;
+        p += TAIL_ELEMS;
+        const struct { const uint16_t* src; bf16_t* dst; int n, k; } m[3] = {
+            {lw.wmerge, tw[l].wmerge, 256, 256}, {lw.w1, tw[l].w1, 512, 512}, {lw.w2, tw[l].w2, 256, 512}};
+        for (const auto& e : m) {
+            const long n = (long)e.n * e.k;
+            hipLaunchKernelGGL(k_lf_pack_kstep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                               (const bf16_t*)e.src, e.n, e.k, e.dst);
+            MLG_LAUNCH_CHECK();
+        }
+        if (hipMemcpyAsync(tw[l].ln_g, lw.ln1_g, 1024, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(tw[l].ln_g + 256, lw.ln2_g, 1024, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(tw[l].ln_b, lw.ln1_b, 1024, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(tw[l].ln_b + 256, lw.ln2_b, 1024, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return MLG_EHIP;
     }
     return MLG_OK;
 }
@@ -964,8 +1104,8 @@ int transformer(const mlg_loftr_layer* layers, int nl, const LayerBufs& b, int d
 struct MatchLayout {
     size_t cx, ccat, cqkv, cmsg, ct, ch, ckv, cks, ckvp;  // coarse transformer (rows 2 P L, d 256)
     size_t fx, fcat, fqkv, fmsg, ft, fh, fkv, fks;  // fine transformer (rows 2 C 25, d 128)
-    size_t win, crow, cd, cm, S, rmax, rsum, cmax, csum, pm, pz, bval, bidx, cbest, mi, mj, mconf, cnt, frm, mp, ms,
-        total;
+    size_t win, crow, cd, cm, S, rmax, rsum, rkey, cmax, csum, ckey, pm, pz, bval, bidx, cbest, mi, mj, mconf, cnt,
+        frm, mp, ms, tails, total;
 };
 
 constexpr int FINE_CHUNK = 4096;  // matches per fine-stage pass
@@ -1003,8 +1143,10 @@ MatchLayout match_layout(int P, int L) {
     M.S = take((size_t)L * L * 4);
     M.rmax = take((size_t)L * 4);
     M.rsum = take((size_t)L * 4);
+    M.rkey = take((size_t)L * 4);
     M.cmax = take((size_t)L * 4);
     M.csum = take((size_t)L * 4);
+    M.ckey = take((size_t)L * 4);
     const size_t nrch = (size_t)(L + LF_RCH - 1) / LF_RCH;
     M.pm = take(nrch * L * 4);
     M.pz = take(nrch * L * 4);
@@ -1018,6 +1160,7 @@ MatchLayout match_layout(int P, int L) {
     M.frm = take((size_t)2 * P * 4);
     M.mp = take((size_t)FINE_CHUNK * 4);
     M.ms = take((size_t)FINE_CHUNK * 4);
+    M.tails = take((size_t)8 * TAIL_ELEMS * 2 + (size_t)8 * 1024 * 4);
     M.total = o;
     return M;
 }
@@ -1055,6 +1198,8 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
     float* rsum = (float*)at(ML.rsum);
     float* cmax = (float*)at(ML.cmax);
     float* csum = (float*)at(ML.csum);
+    float* rkey = (float*)at(ML.rkey);
+    float* ckey = (float*)at(ML.ckey);
     float* pm = (float*)at(ML.pm);
     float* pz = (float*)at(ML.pz);
     const int nrch = (L + LF_RCH - 1) / LF_RCH;
@@ -1081,18 +1226,21 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
     hipLaunchKernelGGL(k_lf_tokens, dim3((unsigned)((crows * 64 + 255) / 256)), dim3(256), 0, s, coarse, frm, L, pe,
                        bc.x, bc.cat, (int)crows);
     MLG_LAUNCH_CHECK();
-    LF_TRY(transformer(w.coarse, 8, bc, 256, P, L, s));
+    TailW tails[8];
+    if (MLG_LF_FUSED_TAIL) LF_TRY(pack_tails(w, (char*)at(ML.tails), tails, s));
+    LF_TRY(transformer(w.coarse, 8, bc, 256, P, L, s, MLG_LF_FUSED_TAIL ? tails : nullptr));
     // dual softmax + mutual nearest, pair by pair over one [L, L] similarity buffer
     for (int p = 0; p < P; ++p) {
         const float* f0 = bc.x + (size_t)p * L * 256;
         const float* f1 = bc.x + ((size_t)P + p) * L * 256;
-        LF_TRY(mlg_similarity_f32(f0, L, f1, L, 256, S, L, s));
-        hipLaunchKernelGGL(k_lf_rowstats, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum);
+        LF_TRY(mlg_similarity_f32_loftr(f0, L, f1, L, 256, S, L, s));
+        hipLaunchKernelGGL(k_lf_rowstats, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, rkey);
         hipLaunchKernelGGL(k_lf_colpart, dim3((L + 255) / 256, nrch), dim3(256), 0, s, S, L, pm, pz);
-        hipLaunchKernelGGL(k_lf_colfin, dim3((L + 255) / 256), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum);
-        hipLaunchKernelGGL(k_lf_rowbest, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, cmax, csum, bval, bidx);
-        hipLaunchKernelGGL(k_lf_colmaxpart, dim3((L + 255) / 256, nrch), dim3(256), 0, s, S, L, rmax, rsum, cmax, csum,
-                           pm);
+        hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum, ckey);
+        hipLaunchKernelGGL(k_lf_rowbest, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, cmax, csum, ckey, bval,
+                           bidx);
+        hipLaunchKernelGGL(k_lf_colmaxpart, dim3((L + 255) / 256, nrch), dim3(256), 0, s, S, L, rmax, rsum, rkey, cmax,
+                           csum, pm);
         hipLaunchKernelGGL(k_lf_colmaxfin, dim3((L + 255) / 256), dim3(256), 0, s, pm, L, nrch, cbest);
         hipLaunchKernelGGL(k_lf_select, dim3(1), dim3(1024), 0, s, bval, bidx, cbest, L, hc, wc, 0.2f, 2,
                            mi + (size_t)p * L, mj + (size_t)p * L, mconf + (size_t)p * L, cnt + p);

@@ -128,7 +128,10 @@ __global__ __launch_bounds__(512) void k_conv3x3(const bf16_t* __restrict__ in, 
     // weights of one K-step: COUT_T rows x 64 channels (8 chunks per row)
     constexpr int WCH = COUT_T * 8;
     constexpr int WPT = (WCH + 511) / 512;
-    uint4 wreg[WPT];
+    // a vector type, not uint4: HIP struct copies are memcpys, which kept this array out of
+    // registers (hipcc placed it in LDS, 16 KiB per workgroup, on the load path)
+    typedef __attribute__((ext_vector_type(4))) unsigned int wvec;
+    wvec wreg[WPT];
     auto wload = [&](int step) {
         const int tap = step / (CIN / KC), cc = step % (CIN / KC);
 #pragma unroll
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(512) void k_conv3x3(const bf16_t* __restrict__ in, 
             const int i = tid + j * 512;
             if (i < WCH) {
                 const int r = i >> 3, ch = i & 7;
-                wreg[j] = *reinterpret_cast<const uint4*>(wt + ((size_t)(n0 + r) * 9 + tap) * CIN + cc * KC + ch * 8);
+                wreg[j] = *reinterpret_cast<const wvec*>(wt + ((size_t)(n0 + r) * 9 + tap) * CIN + cc * KC + ch * 8);
             }
         }
     };
@@ -144,7 +147,7 @@ __global__ __launch_bounds__(512) void k_conv3x3(const bf16_t* __restrict__ in, 
 #pragma unroll
         for (int j = 0; j < WPT; ++j) {
             const int i = tid + j * 512;
-            if (i < WCH) *reinterpret_cast<uint4*>(sb + buf * B_BYTES + (i >> 3) * BS + (i & 7) * 16) = wreg[j];
+            if (i < WCH) *reinterpret_cast<wvec*>(sb + buf * B_BYTES + (i >> 3) * BS + (i & 7) * 16) = wreg[j];
         }
     };
     wload(0);

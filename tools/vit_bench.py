@@ -28,11 +28,13 @@ def main():
     ap.add_argument("--frames", type=int, default=246)
     ap.add_argument("--batch", type=int, default=123)
     ap.add_argument("--iters", type=int, default=2)
+    ap.add_argument("--vit", choices=("split", "bf16"), default="split",
+                    help="split: the gate's split-bf16 forward (MLG_VIT_SPLIT, default); bf16: one bf16 pass")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     seq = synthetic.make_sequence(a.frames, max(2, a.frames // 4), 0)
     frames = synthetic.frames_device(seq, np.arange(a.frames), dev)
-    eng = VitB14(synthetic_state_dict(0), device=dev, max_batch=a.batch)
+    eng = VitB14(synthetic_state_dict(0), device=dev, max_batch=a.batch, precise=a.vit == "split")
     desc = torch.empty(a.frames, 768, device=dev)
     local = torch.empty(a.frames, eng.n_local, 768, device=dev)
     eng.forward_into(frames, desc, local)
@@ -47,7 +49,9 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     L.mlg_prof_enable(0)
-    res = {"frames": a.frames, "batch": a.batch, "ms_per_keyframe": round(e0.elapsed_time(e1) / a.iters / a.frames, 4)}
+    import hashlib
+    res = {"frames": a.frames, "batch": a.batch, "vit": a.vit,
+           "desc_sha1": hashlib.sha1(desc.cpu().numpy().tobytes() + local.cpu().numpy().tobytes()).hexdigest()[:16], "ms_per_keyframe": round(e0.elapsed_time(e1) / a.iters / a.frames, 4)}
     for slot, name in ((0, "fc1"), (1, "fc2"), (2, "qkv"), (3, "proj"), (4, "attention")):
         ms, cnt, work = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
         L.mlg_prof_read(slot, ctypes.byref(ms), ctypes.byref(cnt))
