@@ -355,6 +355,9 @@ def main():
     # (profiles/r02t_chunk_sweep.txt); 5120 (164 GB, 5 calls per step instead of 6) another
     # +0.3-0.5 % and 6144 (196 GB) no more (profiles/r03as_chunk_sweep.txt); 8192 would need 260 GB
     ap.add_argument("--lg-chunk", type=int, default=5120)
+    ap.add_argument("--lg-tail", type=int, default=0,
+                    help="last LightGlue chunk = 1/N of the remainder (its RANSAC runs alone); 0 = off "
+                         "(same-box A/B: no gain, profiles/r04p_ab_lg_tail.txt)")
     ap.add_argument("--k", type=int, default=20)  # configs[2]: top-20 candidates per query
     ap.add_argument("--places", type=int, default=600)
     ap.add_argument("--verify", choices=["all", "none"], default="all")
@@ -377,7 +380,7 @@ def main():
     lo, hi = mdist.shard(args.keyframes, world, rank)
     frames = synthetic.frames_device(seq, np.arange(lo, hi), dev)
     gate = DeviceGate(frames, seq.t, labels, world, rank, dev, k=args.k, verify=args.verify == "all", K=ISEC_K,
-                      vit_batch=args.batch, sp_batch=args.sp_batch, lg_chunk=args.lg_chunk,
+                      vit_batch=args.batch, sp_batch=args.sp_batch, lg_chunk=args.lg_chunk, lg_tail=args.lg_tail,
                       vit_state_dict=synthetic_state_dict(0), vit_precise=args.vit == "split")
     ops = _native.ops()  # torch.ops.mlgate (HIP-event profiling slots of the C ABI)
     all_slots = (1 << len(SLOTS)) - 1

@@ -111,6 +111,29 @@ __device__ __forceinline__ void block_max2(f32x16 (&v)[2], float (&m)[2]) {
     m[1] = b;
 }
 
+// One query tile (the 8-wave form, 32 queries per wave): the same chain, one column.
+__device__ __forceinline__ void block_max1(f32x16 (&v)[1], float (&m)[1]) {
+    float a, t0;
+    asm volatile("s_nop 11" : "+v"(v[0][15]));
+    asm("v_max3_f32 %0, %2, %3, %4\n\t"
+        "v_max3_f32 %0, %0, %5, %6\n\t"
+        "v_max3_f32 %0, %0, %7, %8\n\t"
+        "v_max3_f32 %0, %0, %9, %10\n\t"
+        "v_max3_f32 %0, %0, %11, %12\n\t"
+        "v_max3_f32 %0, %0, %13, %14\n\t"
+        "v_max3_f32 %0, %0, %15, %16\n\t"
+        "v_max3_f32 %0, %0, %17, %17\n\t"
+        "v_mov_b32 %1, %0\n\t"
+        "s_nop 1\n\t"
+        "v_permlane32_swap_b32 %0, %1\n\t"
+        "v_max_f32 %0, %0, %1"
+        : "=&v"(a), "=&v"(t0)
+        : "v"(v[0][0]), "v"(v[0][1]), "v"(v[0][2]), "v"(v[0][3]), "v"(v[0][4]), "v"(v[0][5]), "v"(v[0][6]),
+          "v"(v[0][7]), "v"(v[0][8]), "v"(v[0][9]), "v"(v[0][10]), "v"(v[0][11]), "v"(v[0][12]), "v"(v[0][13]),
+          "v"(v[0][14]), "v"(v[0][15]));
+    m[0] = a;
+}
+
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 
@@ -143,33 +166,49 @@ struct PipeCtx {
 // tied to element [15]).  Changing this MFMA's shape (e.g. 16x16x32, 4 passes) or
 // splitting the accumulator requires re-deriving the pad; tests/test_kernels_gpu.py's
 // attention bit-identity test is the run-time guard.
-template <bool SPLIT>
-__device__ __forceinline__ void qk_half(const char* kb, const PipeCtx& c, const bf16x8 (&qf)[2][4],
-                                        const bf16x8 (&qfl)[2][4], int kt, f32x16 (&s)[2]) {
+template <bool SPLIT, int QT>
+__device__ __forceinline__ void qk_half(const char* kb, const PipeCtx& c, const bf16x8 (&qf)[QT][4],
+                                        const bf16x8 (&qfl)[QT][4], int kt, f32x16 (&s)[QT]) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { s[0][i] = 0.f; s[1][i] = 0.f; }
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) s[qt][i] = 0.f;
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
         const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + kt * 4096 + c.koff[st]);
-        s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[0][st], s[0], 0, 0, 0);
-        s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[1][st], s[1], 0, 0, 0);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) s[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[qt][st], s[qt], 0, 0, 0);
         if (SPLIT) {
             const bf16x8 kl = *reinterpret_cast<const bf16x8*>(kb + KTILE_BYTES + kt * 4096 + c.koff[st]);
-            s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qf[0][st], s[0], 0, 0, 0);
-            s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qf[1][st], s[1], 0, 0, 0);
-            s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qfl[0][st], s[0], 0, 0, 0);
-            s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qfl[1][st], s[1], 0, 0, 0);
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+                s[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl, qf[qt][st], s[qt], 0, 0, 0);
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+                s[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qfl[qt][st], s[qt], 0, 0, 0);
         }
     }
 }
 
+template <int QT>
+__device__ __forceinline__ void block_max(f32x16 (&v)[QT], float (&m)[QT]) {
+    if constexpr (QT == 2) block_max2(v, m);
+    else block_max1(v, m);
+}
+
 // half-step H of stage j: consume `cur` (keys 64 j + 32 H ..), produce `nxt`.  kcur /
 // knext: K ring slots of stages j / j + 1; kw: slot for K_{j+2}.
-template <int H, bool LASTSTAGE, int R, bool SPLIT>
-__device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)[2], const PipeCtx& c,
-                                          const bf16x8 (&qf)[2][4], const bf16x8 (&qfl)[2][4], f32x16 (&o)[2][2],
-                                          float (&mrun)[2], float (&lsum)[2][2], uint4 (&stage)[8], int rr = 0) {
+// QT query tiles of 32 per wave (2: the 4-wave form, 64 queries per wave; 1: the 8-wave
+// form, 32 per wave -- two waves per SIMD where the tile's registers allow only one wave
+// of the 4-wave form); SP = K / V staging rows per thread per plane (2 for 256 threads, 1
+// for 512)
+template <int H, bool LASTSTAGE, int R, bool SPLIT, int QT>
+__device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[QT], f32x16 (&nxt)[QT], const PipeCtx& c,
+                                          const bf16x8 (&qf)[QT][4], const bf16x8 (&qfl)[QT][4], f32x16 (&o)[QT][2],
+                                          float (&mrun)[QT], float (&lsum)[QT][2], uint4 (&stage)[4 * QT],
+                                          int rr = 0) {
     constexpr int KS = Slots<SPLIT>::K, VS = Slots<SPLIT>::V;
+    constexpr int SP = QT;  // 256 threads (QT 2): rows srow and srow + 32; 512 threads: row srow
     // ring slots are compile-time constants (stage j uses K slot j % 3 = R, V slot R), so
     // every LDS fragment address is a lane offset plus an immediate; R < 0: slot rr at run
     // time (the last stage only)
@@ -180,17 +219,17 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
     if (!LASTSTAGE && H == 0) {  // K_{j+2} (clamped), V_{j+1} -> registers, into LDS at the stage end
         const bf16_t* pk = c.Kh + (size_t)min(j + 2, c.nkb - 1) * (KB * 64) + c.gk_off;
         stage[0] = *reinterpret_cast<const uint4*>(pk);
-        stage[1] = *reinterpret_cast<const uint4*>(pk + 32 * 64);
+        if (SP == 2) stage[1] = *reinterpret_cast<const uint4*>(pk + 32 * 64);
         const bf16_t* pv = c.Vh + (size_t)(j + 1) * 4096 + c.gv_off;
-        stage[2] = *reinterpret_cast<const uint4*>(pv);
-        stage[3] = *reinterpret_cast<const uint4*>(pv + 32 * 64);
+        stage[SP] = *reinterpret_cast<const uint4*>(pv);
+        if (SP == 2) stage[3] = *reinterpret_cast<const uint4*>(pv + 32 * 64);
         if (SPLIT) {
             const bf16_t* pkl = c.Kl + (size_t)min(j + 2, c.nkb - 1) * (KB * 64) + c.gk_off;
-            stage[4] = *reinterpret_cast<const uint4*>(pkl);
-            stage[5] = *reinterpret_cast<const uint4*>(pkl + 32 * 64);
+            stage[2 * SP] = *reinterpret_cast<const uint4*>(pkl);
+            if (SP == 2) stage[5] = *reinterpret_cast<const uint4*>(pkl + 32 * 64);
             const bf16_t* pvl = c.Vl + (size_t)(j + 1) * 4096 + c.gv_off;
-            stage[6] = *reinterpret_cast<const uint4*>(pvl);
-            stage[7] = *reinterpret_cast<const uint4*>(pvl + 32 * 64);
+            stage[3 * SP] = *reinterpret_cast<const uint4*>(pvl);
+            if (SP == 2) stage[7] = *reinterpret_cast<const uint4*>(pvl + 32 * 64);
         }
     }
     if (LASTSTAGE && (c.T & (KB - 1))) {  // partial last stage: mask keys >= T
@@ -198,21 +237,23 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (key >= c.T) { cur[0][r] = -INFINITY; cur[1][r] = -INFINITY; }
+            if (key >= c.T)
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt) cur[qt][r] = -INFINITY;
         }
     }
-    float mnew[2];
+    float mnew[QT];
     bool grow = false;
-    float bm[2];
-    block_max2(cur, bm);  // both lane halves
+    float bm[QT];
+    block_max<QT>(cur, bm);  // both lane halves
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
         mnew[qt] = fmaxf(mrun[qt], bm[qt]);
         grow |= (mnew[qt] - mrun[qt]) * C > 8.0f;
     }
     if (__any(grow)) {
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
+        for (int qt = 0; qt < QT; ++qt) {
             const float alpha = __builtin_amdgcn_exp2f((mrun[qt] - mnew[qt]) * C);
             lsum[qt][0] *= alpha;
             lsum[qt][1] *= alpha;
@@ -221,23 +262,24 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
             mrun[qt] = mnew[qt];
         }
     }
-    const float mc0 = mrun[0] * C, mc1 = mrun[1] * C;
+    float mc[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) mc[qt] = mrun[qt] * C;
     // next half-block's scores on the MFMA pipe
     const char* kring = c.smem;
-    if (!(LASTSTAGE && H == 1)) qk_half<SPLIT>(kring + (H == 0 ? kcur : knext), c, qf, qfl, H ^ 1, nxt);
+    if (!(LASTSTAGE && H == 1)) qk_half<SPLIT, QT>(kring + (H == 0 ? kcur : knext), c, qf, qfl, H ^ 1, nxt);
     // P of this half-block [st][qt]: keys 16 st + 8 hh .. + 7, then O^T += V^T . P^T
     const char* vb = c.smem + 3 * KS + rs * VS;
-    bf16x8 pf[2][2], pfl[2][2];
+    bf16x8 pf[2][QT], pfl[2][QT];
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-            const float mc = qt ? mc1 : mc0;
+        for (int qt = 0; qt < QT; ++qt) {
             u32x4 w, wl;
 #pragma unroll
             for (int jj = 0; jj < 4; ++jj) {
-                const float p0 = __builtin_amdgcn_exp2f(fmaf(cur[qt][8 * st + 2 * jj], C, -mc));
-                const float p1 = __builtin_amdgcn_exp2f(fmaf(cur[qt][8 * st + 2 * jj + 1], C, -mc));
+                const float p0 = __builtin_amdgcn_exp2f(fmaf(cur[qt][8 * st + 2 * jj], C, -mc[qt]));
+                const float p1 = __builtin_amdgcn_exp2f(fmaf(cur[qt][8 * st + 2 * jj + 1], C, -mc[qt]));
                 lsum[qt][0] += p0;
                 lsum[qt][1] += p1;
                 w[jj] = pack_bf16x2(p0, p1);
@@ -252,16 +294,19 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
             const s16x4 lo = *reinterpret_cast<const s16x4*>(vb + c.voff[H][st][2 * dt]);
             const s16x4 hi = *reinterpret_cast<const s16x4*>(vb + c.voff[H][st][2 * dt + 1]);
             const bf16x8 vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-            o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st][0], o[0][dt], 0, 0, 0);
-            o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st][1], o[1][dt], 0, 0, 0);
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+                o[qt][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st][qt], o[qt][dt], 0, 0, 0);
             if (SPLIT) {
                 const s16x4 llo = *reinterpret_cast<const s16x4*>(vb + VTILE_BYTES + c.voff[H][st][2 * dt]);
                 const s16x4 lhi = *reinterpret_cast<const s16x4*>(vb + VTILE_BYTES + c.voff[H][st][2 * dt + 1]);
                 const bf16x8 vl = __builtin_shufflevector(llo, lhi, 0, 1, 2, 3, 4, 5, 6, 7);
-                o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, pf[st][0], o[0][dt], 0, 0, 0);
-                o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, pf[st][1], o[1][dt], 0, 0, 0);
-                o[0][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pfl[st][0], o[0][dt], 0, 0, 0);
-                o[1][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pfl[st][1], o[1][dt], 0, 0, 0);
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+                    o[qt][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vl, pf[st][qt], o[qt][dt], 0, 0, 0);
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+                    o[qt][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pfl[st][qt], o[qt][dt], 0, 0, 0);
             }
         }
     }
@@ -269,35 +314,41 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[2], f32x16 (&nxt)
         char* kwp = c.smem + kw;
         char* vw = c.smem + 3 * KS + ((rs + 1) % 3) * VS;
         *reinterpret_cast<uint4*>(kwp + c.sk0) = stage[0];
-        *reinterpret_cast<uint4*>(kwp + c.sk1) = stage[1];
-        *reinterpret_cast<uint2*>(vw + c.sv0a) = make_uint2(stage[2].x, stage[2].y);
-        *reinterpret_cast<uint2*>(vw + c.sv0b) = make_uint2(stage[2].z, stage[2].w);
-        *reinterpret_cast<uint2*>(vw + c.sv1a) = make_uint2(stage[3].x, stage[3].y);
-        *reinterpret_cast<uint2*>(vw + c.sv1b) = make_uint2(stage[3].z, stage[3].w);
+        if (SP == 2) *reinterpret_cast<uint4*>(kwp + c.sk1) = stage[1];
+        *reinterpret_cast<uint2*>(vw + c.sv0a) = make_uint2(stage[SP].x, stage[SP].y);
+        *reinterpret_cast<uint2*>(vw + c.sv0b) = make_uint2(stage[SP].z, stage[SP].w);
+        if (SP == 2) {
+            *reinterpret_cast<uint2*>(vw + c.sv1a) = make_uint2(stage[3].x, stage[3].y);
+            *reinterpret_cast<uint2*>(vw + c.sv1b) = make_uint2(stage[3].z, stage[3].w);
+        }
         if (SPLIT) {
-            *reinterpret_cast<uint4*>(kwp + KTILE_BYTES + c.sk0) = stage[4];
-            *reinterpret_cast<uint4*>(kwp + KTILE_BYTES + c.sk1) = stage[5];
+            *reinterpret_cast<uint4*>(kwp + KTILE_BYTES + c.sk0) = stage[2 * SP];
+            if (SP == 2) *reinterpret_cast<uint4*>(kwp + KTILE_BYTES + c.sk1) = stage[5];
             char* vl = vw + VTILE_BYTES;
-            *reinterpret_cast<uint2*>(vl + c.sv0a) = make_uint2(stage[6].x, stage[6].y);
-            *reinterpret_cast<uint2*>(vl + c.sv0b) = make_uint2(stage[6].z, stage[6].w);
-            *reinterpret_cast<uint2*>(vl + c.sv1a) = make_uint2(stage[7].x, stage[7].y);
-            *reinterpret_cast<uint2*>(vl + c.sv1b) = make_uint2(stage[7].z, stage[7].w);
+            *reinterpret_cast<uint2*>(vl + c.sv0a) = make_uint2(stage[3 * SP].x, stage[3 * SP].y);
+            *reinterpret_cast<uint2*>(vl + c.sv0b) = make_uint2(stage[3 * SP].z, stage[3 * SP].w);
+            if (SP == 2) {
+                *reinterpret_cast<uint2*>(vl + c.sv1a) = make_uint2(stage[7].x, stage[7].y);
+                *reinterpret_cast<uint2*>(vl + c.sv1b) = make_uint2(stage[7].z, stage[7].w);
+            }
         }
         __syncthreads();
     }
 }
 
-template <bool SPLIT>
+template <bool SPLIT, int NW = 4>
 __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __restrict__ Qh,
                                                     const bf16_t* __restrict__ Kh, const bf16_t* __restrict__ Vh,
                                                     int T, int nq, int qmax, int qblock, bf16_t* __restrict__ orow,
                                                     int ldo, size_t lo_off, int lo_col) {
     constexpr int KS = Slots<SPLIT>::K;
+    constexpr int QT = NW == 4 ? 2 : 1;  // query tiles of 32 per wave: 256 queries per workgroup
+    constexpr int SP = QT;               // K / V staging rows per thread per plane
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hh = lane >> 5, col = lane & 31;
-    const int qbase = qblock * 256 + wave * 64;
-    bf16x8 qf[2][4], qfl[2][4];
+    const int qbase = qblock * 256 + wave * 32 * QT;
+    bf16x8 qf[QT][4], qfl[QT][4];
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int qt = 0; qt < QT; ++qt) {
         const int qld = min(qbase + qt * 32 + col, qmax - 1);
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
@@ -313,7 +364,7 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
     c.smem = smem;
     c.T = T;
     c.nkb = (T + KB - 1) / KB;
-    const int srow = tid >> 3, sch = tid & 7;
+    const int srow = tid >> 3, sch = tid & 7;  // rows srow (+ 32 when 256 threads) of each 64-row tile
     c.gk_off = srow * 64 + sch * 8;
     c.gv_off = srow * 64 + sch * 8;
     c.sk0 = k_off(srow, sch);
@@ -334,57 +385,67 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
                 c.voff[h][st][2 * dt + 1] = v_off(dt * 32 + col, h * 8 + st * 4 + hh + 2);
             }
     {
+        // (rows srow + 32 only with 256 threads; the same statement order as the 4-wave tile)
         const uint4 k0 = *reinterpret_cast<const uint4*>(Kh + c.gk_off);
-        const uint4 k1 = *reinterpret_cast<const uint4*>(Kh + c.gk_off + 32 * 64);
+        const uint4 k1 = SP == 2 ? *reinterpret_cast<const uint4*>(Kh + c.gk_off + 32 * 64) : k0;
         const uint4 v0 = *reinterpret_cast<const uint4*>(Vh + c.gv_off);
-        const uint4 v1 = *reinterpret_cast<const uint4*>(Vh + c.gv_off + 32 * 64);
+        const uint4 v1 = SP == 2 ? *reinterpret_cast<const uint4*>(Vh + c.gv_off + 32 * 64) : v0;
         const bf16_t* pk = Kh + (size_t)min(1, c.nkb - 1) * (KB * 64) + c.gk_off;
         const uint4 k2 = *reinterpret_cast<const uint4*>(pk);
-        const uint4 k3 = *reinterpret_cast<const uint4*>(pk + 32 * 64);
+        const uint4 k3 = SP == 2 ? *reinterpret_cast<const uint4*>(pk + 32 * 64) : k2;
         *reinterpret_cast<uint4*>(smem + c.sk0) = k0;
-        *reinterpret_cast<uint4*>(smem + c.sk1) = k1;
+        if (SP == 2) *reinterpret_cast<uint4*>(smem + c.sk1) = k1;
         *reinterpret_cast<uint4*>(smem + KS + c.sk0) = k2;
-        *reinterpret_cast<uint4*>(smem + KS + c.sk1) = k3;
+        if (SP == 2) *reinterpret_cast<uint4*>(smem + KS + c.sk1) = k3;
         char* vw = smem + 3 * KS;
         *reinterpret_cast<uint2*>(vw + c.sv0a) = make_uint2(v0.x, v0.y);
         *reinterpret_cast<uint2*>(vw + c.sv0b) = make_uint2(v0.z, v0.w);
-        *reinterpret_cast<uint2*>(vw + c.sv1a) = make_uint2(v1.x, v1.y);
-        *reinterpret_cast<uint2*>(vw + c.sv1b) = make_uint2(v1.z, v1.w);
+        if (SP == 2) {
+            *reinterpret_cast<uint2*>(vw + c.sv1a) = make_uint2(v1.x, v1.y);
+            *reinterpret_cast<uint2*>(vw + c.sv1b) = make_uint2(v1.z, v1.w);
+        }
         if (SPLIT) {
             const bf16_t* Kl = c.Kl;
             const bf16_t* Vl = c.Vl;
             const uint4 l0 = *reinterpret_cast<const uint4*>(Kl + c.gk_off);
-            const uint4 l1 = *reinterpret_cast<const uint4*>(Kl + c.gk_off + 32 * 64);
+            const uint4 l1 = SP == 2 ? *reinterpret_cast<const uint4*>(Kl + c.gk_off + 32 * 64) : l0;
             const uint4 w0 = *reinterpret_cast<const uint4*>(Vl + c.gv_off);
-            const uint4 w1 = *reinterpret_cast<const uint4*>(Vl + c.gv_off + 32 * 64);
+            const uint4 w1 = SP == 2 ? *reinterpret_cast<const uint4*>(Vl + c.gv_off + 32 * 64) : w0;
             const bf16_t* pl = Kl + (size_t)min(1, c.nkb - 1) * (KB * 64) + c.gk_off;
             const uint4 l2 = *reinterpret_cast<const uint4*>(pl);
-            const uint4 l3 = *reinterpret_cast<const uint4*>(pl + 32 * 64);
+            const uint4 l3 = SP == 2 ? *reinterpret_cast<const uint4*>(pl + 32 * 64) : l2;
             *reinterpret_cast<uint4*>(smem + KTILE_BYTES + c.sk0) = l0;
-            *reinterpret_cast<uint4*>(smem + KTILE_BYTES + c.sk1) = l1;
+            if (SP == 2) *reinterpret_cast<uint4*>(smem + KTILE_BYTES + c.sk1) = l1;
             *reinterpret_cast<uint4*>(smem + KS + KTILE_BYTES + c.sk0) = l2;
-            *reinterpret_cast<uint4*>(smem + KS + KTILE_BYTES + c.sk1) = l3;
+            if (SP == 2) *reinterpret_cast<uint4*>(smem + KS + KTILE_BYTES + c.sk1) = l3;
             char* vl = vw + VTILE_BYTES;
             *reinterpret_cast<uint2*>(vl + c.sv0a) = make_uint2(w0.x, w0.y);
             *reinterpret_cast<uint2*>(vl + c.sv0b) = make_uint2(w0.z, w0.w);
-            *reinterpret_cast<uint2*>(vl + c.sv1a) = make_uint2(w1.x, w1.y);
-            *reinterpret_cast<uint2*>(vl + c.sv1b) = make_uint2(w1.z, w1.w);
+            if (SP == 2) {
+                *reinterpret_cast<uint2*>(vl + c.sv1a) = make_uint2(w1.x, w1.y);
+                *reinterpret_cast<uint2*>(vl + c.sv1b) = make_uint2(w1.z, w1.w);
+            }
         }
     }
     __syncthreads();
-    f32x16 sA[2], sB[2];
-    qk_half<SPLIT>(smem, c, qf, qfl, 0, sA);
-    f32x16 o[2][2];
+    f32x16 sA[QT], sB[QT];
+    qk_half<SPLIT, QT>(smem, c, qf, qfl, 0, sA);
+    f32x16 o[QT][2];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { o[0][0][i] = 0.f; o[0][1][i] = 0.f; o[1][0][i] = 0.f; o[1][1][i] = 0.f; }
-    float mrun[2] = {-INFINITY, -INFINITY};
-    float lsum[2][2] = {{0.f, 0.f}, {0.f, 0.f}};  // per lane half, two partial sums each
-    uint4 stage[8];
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) { o[qt][0][i] = 0.f; o[qt][1][i] = 0.f; }
+    float mrun[QT], lsum[QT][2];  // per lane half, two partial sums each
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) mrun[qt] = -INFINITY;
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) { lsum[qt][0] = 0.f; lsum[qt][1] = 0.f; }
+    uint4 stage[4 * QT];
     // stages unrolled by 3 (K and V ring slot of stage j = j % 3, compile-time)
 #define PIPE_STAGE(J, R, LAST)                                                                 \
     {                                                                                          \
-        pipe_half<0, LAST, R, SPLIT>(J, sA, sB, c, qf, qfl, o, mrun, lsum, stage, (J) % 3);    \
-        pipe_half<1, LAST, R, SPLIT>(J, sB, sA, c, qf, qfl, o, mrun, lsum, stage, (J) % 3);    \
+        pipe_half<0, LAST, R, SPLIT, QT>(J, sA, sB, c, qf, qfl, o, mrun, lsum, stage, (J) % 3); \
+        pipe_half<1, LAST, R, SPLIT, QT>(J, sB, sA, c, qf, qfl, o, mrun, lsum, stage, (J) % 3); \
     }
     const int last = c.nkb - 1;
     int j = 0;
@@ -405,14 +466,14 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
 #undef PIPE_STAGE
 
     // O staged through LDS (the K / V rings are dead once every wave is past its last
-    // stage) as this wave's [64 queries][64 d] bf16, 16-B chunk c of row r at c ^ (r & 7),
+    // stage) as this wave's [32 QT queries][64 d] bf16, 16-B chunk c of row r at c ^ (r & 7),
     // then written as whole 128-B row pieces: 8 rows per wave-instruction instead of 32
     // rows x 16 B (the store tail of a row-per-lane epilogue is issue-bound)
     __syncthreads();
-    char* st = smem + wave * (64 * 128);
+    char* st = smem + wave * (32 * QT * 128);
     if constexpr (!SPLIT) {
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
+        for (int qt = 0; qt < QT; ++qt) {
             const float inv = 1.0f / swap_sum(lsum[qt][0] + lsum[qt][1]);
             const int r = qt * 32 + col;
 #pragma unroll
@@ -428,20 +489,20 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int p = 0; p < 8; ++p) {
+        for (int p = 0; p < 4 * QT; ++p) {
             const int r = p * 8 + (lane >> 3), c = lane & 7, qrow = qbase + r;
             if (qrow < nq)
                 *reinterpret_cast<uint4*>(orow + (size_t)qrow * ldo + c * 8) =
                     *reinterpret_cast<const uint4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
         }
     } else {  // two passes through the staging image: hi rows, then lo rows at column lo_col
-        float inv[2];
+        float inv[QT];
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) inv[qt] = 1.0f / swap_sum(lsum[qt][0] + lsum[qt][1]);
+        for (int qt = 0; qt < QT; ++qt) inv[qt] = 1.0f / swap_sum(lsum[qt][0] + lsum[qt][1]);
 #pragma unroll
         for (int part = 0; part < 2; ++part) {
 #pragma unroll
-            for (int qt = 0; qt < 2; ++qt) {
+            for (int qt = 0; qt < QT; ++qt) {
                 const int r = qt * 32 + col;
 #pragma unroll
                 for (int dt = 0; dt < 2; ++dt)
@@ -459,16 +520,16 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
             bf16_t* dst = orow + (part ? lo_col : 0);
             // a vector type, not uint4: copies of the HIP struct are memcpys, which kept this
             // array out of registers (hipcc then placed it in LDS: 32 KiB per workgroup)
-            u32x4 rows[8];
+            u32x4 rows[4 * QT];
 #pragma unroll
-            for (int p = 0; p < 8; ++p) {
+            for (int p = 0; p < 4 * QT; ++p) {
                 const int r = p * 8 + (lane >> 3), c = lane & 7;
                 rows[p] = *reinterpret_cast<const u32x4*>(st + r * 128 + ((c ^ (r & 7)) << 4));
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);  // staging read before the next part overwrites it
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int p = 0; p < 8; ++p) {
+            for (int p = 0; p < 4 * QT; ++p) {
                 const int r = p * 8 + (lane >> 3), c = lane & 7, qrow = qbase + r;
                 if (qrow < nq) *reinterpret_cast<u32x4*>(dst + (size_t)qrow * ldo + c * 8) = rows[p];
             }
@@ -487,8 +548,8 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
 // XCD (hardware deals linear block b to XCD b % 8) and share its L2.
 // VIT: the same tile under a second symbol, so rocprof's per-kernel rows (and their
 // average durations) keep the ViT's ~70 us launches apart from LightGlue's
-template <bool VIT, bool SPLIT = false>
-__global__ __launch_bounds__(256, 1) void k_attention_varlen(const bf16_t* __restrict__ Q,
+template <bool VIT, bool SPLIT = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 1) void k_attention_varlen(const bf16_t* __restrict__ Q,
                                                              const bf16_t* __restrict__ K,
                                                              const bf16_t* __restrict__ Vt, bf16_t* __restrict__ O,
                                                              int ldo, int Npad, const int4* __restrict__ tasks,
@@ -504,7 +565,7 @@ __global__ __launch_bounds__(256, 1) void k_attention_varlen(const bf16_t* __res
     const int4 tk = tasks[t];  // q_off, q_len, kv_off, kv_len
     if (qb * 256 >= tk.y || tk.w <= 0) return;
     const int qpad = (tk.y + 63) & ~63;
-    attention_tile_pipe<SPLIT>(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
+    attention_tile_pipe<SPLIT, NW>(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
                                Vt + ((size_t)h * Npad + tk.z) * 64, tk.w, tk.y, qpad, qb,
                                O + (size_t)out_off[t] * ldo + h * 64, ldo, lo_off, lo_col);
 }
@@ -518,7 +579,7 @@ __global__ void k_vit_tasks(int4* __restrict__ tasks, int* __restrict__ out_off,
     }
 }
 
-template <bool VIT, bool SPLIT = false>
+template <bool VIT, bool SPLIT = false, int NW = 4>
 int varlen_launch(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,
                   const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s, size_t lo_off = 0,
                   int lo_col = 0) {
@@ -528,7 +589,7 @@ int varlen_launch(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O,
     const long total = (long)nqb * heads * ntasks;
     if (total > (1L << 30)) return MLG_EINVAL;
     const int grid = (int)((total + 7) & ~7L);
-    hipLaunchKernelGGL((k_attention_varlen<VIT, SPLIT>), dim3(grid), dim3(256), 0, s, Q, K, Vt, O, ldo, Npad, tasks,
+    hipLaunchKernelGGL((k_attention_varlen<VIT, SPLIT, NW>), dim3(grid), dim3(64 * NW), 0, s, Q, K, Vt, O, ldo, Npad, tasks,
                        out_off, nqb, heads, (int)total, lo_off, lo_col);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
@@ -547,7 +608,11 @@ int mlg_attention(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O,
 }
 
 // Split-bf16 ViT attention (MLG_VIT_SPLIT): Q, K, Vt hi planes with the lo planes
-// lo_off elements further; O rows of 1536 = [hi | lo]
+// lo_off elements further; O rows of 1536 = [hi | lo].  MLG_ATTN_SPLIT_WAVES: 4 (64 queries
+// per wave, one wave per SIMD: 288 registers) or 8 (32 per wave, two per SIMD).
+#ifndef MLG_ATTN_SPLIT_WAVES
+#define MLG_ATTN_SPLIT_WAVES 8
+#endif
 int mlg_attention_split(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int B, int T, int Tpad,
                         size_t lo_off, int32_t* task_ws, hipStream_t s) {
     if (B <= 0 || T <= 0 || Tpad % 64 || Tpad < T || !task_ws || (long)B * Tpad * 64 >= (1L << 31)) return MLG_EINVAL;
@@ -555,10 +620,17 @@ int mlg_attention_split(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16
     int* out_off = task_ws + 4 * B;
     hipLaunchKernelGGL(k_vit_tasks, dim3(1), dim3(256), 0, s, tasks, out_off, B, T, Tpad);
     MLG_LAUNCH_CHECK();
-    return varlen_launch<true, true>(Q, K, Vt, O, 1536, B * Tpad, 12, tasks, out_off, B, T, s, lo_off, 768);
+    return varlen_launch<true, true, MLG_ATTN_SPLIT_WAVES>(Q, K, Vt, O, 1536, B * Tpad, 12, tasks, out_off, B, T, s,
+                                                          lo_off, 768);
 }
 
+// LightGlue: MLG_ATTN_LG_WAVES = 4 (64 queries per wave; two workgroups per CU give two
+// waves per SIMD) or 8 (build-time A/B arm)
+#ifndef MLG_ATTN_LG_WAVES
+#define MLG_ATTN_LG_WAVES 4
+#endif
 int mlg_attention_varlen(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int ldo, int Npad, int heads,
                          const int4* tasks, const int* out_off, int ntasks, int max_q, hipStream_t s) {
-    return varlen_launch<false>(Q, K, Vt, O, ldo, Npad, heads, tasks, out_off, ntasks, max_q, s);
+    return varlen_launch<false, false, MLG_ATTN_LG_WAVES>(Q, K, Vt, O, ldo, Npad, heads, tasks, out_off, ntasks, max_q,
+                                                          s);
 }

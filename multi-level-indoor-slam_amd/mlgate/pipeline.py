@@ -161,7 +161,7 @@ class DeviceGate:
                  similarity_threshold=0.5, min_time_gap=10.0, strict_mode=True, retrieval_floor_gating=True,
                  verifier_floor_gating=True, verify=True, K=None, min_inliers=20, min_inlier_ratio=0.25,
                  vit_batch=123, sp_batch=64, lg_chunk=1024, max_keypoints=2048, vit_state_dict=None, record=False,
-                 vit_precise=True, matcher='lightglue', loftr_chunk=256, max_pairs=None):
+                 vit_precise=True, matcher='lightglue', loftr_chunk=256, max_pairs=None, lg_tail=0):
         import torch
         from . import distributed as mdist
         from .lightglue import LightGlueGPU
@@ -182,6 +182,7 @@ class DeviceGate:
         self.retrieval_floor_gating, self.verifier_floor_gating = retrieval_floor_gating, verifier_floor_gating
         self.min_inliers, self.min_inlier_ratio = min_inliers, min_inlier_ratio
         self.sp_batch, self.lg_chunk, self.kp = sp_batch, lg_chunk, max_keypoints
+        self.lg_tail = int(lg_tail)
         self.t_all = torch.as_tensor(np.asarray(timestamps, np.float64), device=self.dev)
         from .vpr import floor_codes
         self.labels = np.asarray(floor_labels)
@@ -327,20 +328,50 @@ class DeviceGate:
         else:
             ua, ub, inv, swap_all = pa, pb, np.arange(len(pa)), np.zeros(len(pa), np.uint8)
         order = np.argsort(inv, kind="stable")
-        bounds = np.searchsorted(inv[order], np.arange(0, len(ua) + self.lg_chunk, self.lg_chunk))
+        # chunk starts: full chunks, then (lg_tail > 0) the remainder cut so the LAST chunk
+        # is 1 / lg_tail of it -- that chunk's RANSAC is the only one with no LightGlue to
+        # overlap (per-pair results do not depend on the chunking)
+        starts = list(range(0, len(ua), self.lg_chunk))
+        rem = len(ua) - starts[-1] if starts else 0
+        if self.lg_tail > 0 and rem >= 1024:
+            starts.append(len(ua) - max(256, rem // self.lg_tail))
+        starts.append(len(ua))
+        bounds = np.searchsorted(inv[order], np.asarray(starts))
         out["pairs_matched_lightglue"] = len(ua)
         ua, ub = local(ua), local(ub)  # LightGlue indexes the feature tables
         # RANSAC of chunk c runs on a side stream while LightGlue matches chunk c + 1 on
         # this one (mlg_lightglue waits on its stream once per layer; the side stream
         # fills those gaps and the CUs the small RANSAC / assignment grids leave idle)
+        n_valid_t, gate_rej_t, rec = self._verify_chunks(starts, bounds, order, inv, ua, ub, pa, pb, swap_all, dedup,
+                                                         kp_all, ds_all, counts, local)
+        n_valid, gate_rej = int(n_valid_t), int(gate_rej_t)
+        if rec is not None:
+            r = {"a": pa, "b": pb, "matches": np.zeros(len(pa), np.int32), "inliers": np.zeros(len(pa), np.int32),
+                 "is_valid": np.zeros(len(pa), bool)}
+            for sel, n, inl, ok in rec:
+                r["matches"][sel] = n.cpu().numpy()
+                r["inliers"][sel] = inl.cpu().numpy()
+                r["is_valid"][sel] = ok.cpu().numpy()
+            self.last_pair_results = r
+        out["pairs_verified"] = len(pa)
+        out["verified_valid"] = n_valid
+        out["verifier_invalid"] = len(pa) - n_valid
+        out["gate_rejected_cross_floor"] = gate_rej
+        out["accepted"] = n_valid - gate_rej
+        return out
+
+    def _verify_chunks(self, starts, bounds, order, inv, ua, ub, pa, pb, swap_all, dedup, kp_all, ds_all, counts,
+                       local):
+        torch = self.torch
+        from . import geometry
         main = torch.cuda.current_stream(self.dev)
         side = self._side_stream()
         n_valid_t = torch.zeros((), dtype=torch.int64, device=self.dev)
         gate_rej_t = torch.zeros((), dtype=torch.int64, device=self.dev)
         rec = [] if self.record else None
-        for ci, c0 in enumerate(range(0, len(ua), self.lg_chunk)):
-            mu, su, nu, _ = self.lg.match_device(kp_all, ds_all, counts, ua[c0:c0 + self.lg_chunk],
-                                                 ub[c0:c0 + self.lg_chunk])
+        for ci in range(len(starts) - 1):
+            c0, c1 = starts[ci], starts[ci + 1]
+            mu, su, nu, _ = self.lg.match_device(kp_all, ds_all, counts, ua[c0:c1], ub[c0:c1])
             sel = order[bounds[ci]:bounds[ci + 1]]  # the ordered pairs of these unordered ones
             ca, cb = pa[sel], pb[sel]
             if dedup:
@@ -380,21 +411,7 @@ class DeviceGate:
                 # tests/test_api_cpu.py::test_gate_none_labels_raise_nan_labels_accept)
                 gate_rej_t += (ok & ((self.f_num[ta] - self.f_num[tb]).abs() > self.limit)).sum()
         main.wait_stream(side)
-        n_valid, gate_rej = int(n_valid_t), int(gate_rej_t)
-        if rec is not None:
-            r = {"a": pa, "b": pb, "matches": np.zeros(len(pa), np.int32), "inliers": np.zeros(len(pa), np.int32),
-                 "is_valid": np.zeros(len(pa), bool)}
-            for sel, n, inl, ok in rec:
-                r["matches"][sel] = n.cpu().numpy()
-                r["inliers"][sel] = inl.cpu().numpy()
-                r["is_valid"][sel] = ok.cpu().numpy()
-            self.last_pair_results = r
-        out["pairs_verified"] = len(pa)
-        out["verified_valid"] = n_valid
-        out["verifier_invalid"] = len(pa) - n_valid
-        out["gate_rejected_cross_floor"] = gate_rej
-        out["accepted"] = n_valid - gate_rej
-        return out
+        return n_valid_t, gate_rej_t, rec
 
     def _verify_loftr(self, pa_t, pb_t, out):
         """verify_with_semantics with GeometricVerifier('loftr') on this rank's slice of the
