@@ -262,6 +262,9 @@ __device__ __forceinline__ size_t part_at(int slot, int dir, int t, int i, int k
 // runs this einsum in float32) at 3 bf16 MFMAs instead of 8 exact-f32 32x32x2 ones per
 // 16-deep k-step.  4 waves of 64 x 64; each wave streams its operand fragments straight
 // from L2 (one contiguous 1 KiB per wave-load), double-buffered one k-step ahead.
+#ifndef ASG_PF
+#define ASG_PF 1
+#endif
 __global__ __launch_bounds__(256, 2) void k_asg_sim(const Asg* __restrict__ tab, const bf16_t* __restrict__ MDH,
                                                     const bf16_t* __restrict__ MDL, int rows,
                                                     float* __restrict__ Sall, float2* __restrict__ part, int kmax) {
@@ -285,19 +288,26 @@ __global__ __launch_bounds__(256, 2) void k_asg_sim(const Asg* __restrict__ tab,
         for (int y = 0; y < 2; ++y)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[x][y][r] = 0.f;
-    bf16x8 ah[2][2], al[2][2], bh[2][2], bl[2][2];  // [buffer][x or y]
+    // ASG_PF k-steps of fragments in flight (2 = double buffer); each step's 8 loads are
+    // L2 round trips that one step of 12 MFMAs does not cover
+    constexpr int NB = ASG_PF + 1;
+    bf16x8 ah[NB][2], al[NB][2], bh[NB][2], bl[NB][2];  // [buffer][x or y]
 #pragma unroll
-    for (int x = 0; x < 2; ++x) {
-        ah[0][x] = *reinterpret_cast<const bf16x8*>(MDH + ao[x]);
-        al[0][x] = *reinterpret_cast<const bf16x8*>(MDL + ao[x]);
-        bh[0][x] = *reinterpret_cast<const bf16x8*>(MDH + bo[x]);
-        bl[0][x] = *reinterpret_cast<const bf16x8*>(MDL + bo[x]);
+    for (int pf = 0; pf < ASG_PF; ++pf) {
+        const size_t o = (size_t)pf * step;
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            ah[pf][x] = *reinterpret_cast<const bf16x8*>(MDH + o + ao[x]);
+            al[pf][x] = *reinterpret_cast<const bf16x8*>(MDL + o + ao[x]);
+            bh[pf][x] = *reinterpret_cast<const bf16x8*>(MDH + o + bo[x]);
+            bl[pf][x] = *reinterpret_cast<const bf16x8*>(MDL + o + bo[x]);
+        }
     }
 #pragma unroll
     for (int ks = 0; ks < LG_D / 16; ++ks) {
-        const int cb = ks & 1, nb = cb ^ 1;
-        if (ks + 1 < LG_D / 16) {
-            const size_t o = (size_t)(ks + 1) * step;
+        const int cb = ks % NB, nb = (ks + ASG_PF) % NB;
+        if (ks + ASG_PF < LG_D / 16) {
+            const size_t o = (size_t)(ks + ASG_PF) * step;
 #pragma unroll
             for (int x = 0; x < 2; ++x) {
                 ah[nb][x] = *reinterpret_cast<const bf16x8*>(MDH + o + ao[x]);
