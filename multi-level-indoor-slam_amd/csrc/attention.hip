@@ -206,7 +206,7 @@ template <int H, bool LASTSTAGE, int R, bool SPLIT, int QT>
 __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[QT], f32x16 (&nxt)[QT], const PipeCtx& c,
                                           const bf16x8 (&qf)[QT][4], const bf16x8 (&qfl)[QT][4], f32x16 (&o)[QT][2],
                                           float (&mrun)[QT], float (&lsum)[QT][2], uint4 (&stage)[4 * QT],
-                                          int rr = 0) {
+                                          int rr = 0, bool busy = true) {
     constexpr int KS = Slots<SPLIT>::K, VS = Slots<SPLIT>::V;
     constexpr int SP = QT;  // 256 threads (QT 2): rows srow and srow + 32; 512 threads: row srow
     // ring slots are compile-time constants (stage j uses K slot j % 3 = R, V slot R), so
@@ -232,6 +232,10 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[QT], f32x16 (&nxt
             if (SP == 2) stage[7] = *reinterpret_cast<const uint4*>(pvl + 32 * 64);
         }
     }
+    // 8-wave split form: a wave whose 32 queries all lie past the segment (the ViT's third
+    // query block: 18 of 256 rows live) only stages K / V and joins the barriers
+    const bool run = !(SPLIT && QT == 1) || busy;
+    if (run) {
     if (LASTSTAGE && (c.T & (KB - 1))) {  // partial last stage: mask keys >= T
         const int key0 = j * KB + H * 32;
 #pragma unroll
@@ -310,6 +314,7 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[QT], f32x16 (&nxt
             }
         }
     }
+    }  // run
     if (!LASTSTAGE && H == 1) {
         char* kwp = c.smem + kw;
         char* vw = c.smem + 3 * KS + ((rs + 1) % 3) * VS;
@@ -428,8 +433,9 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
         }
     }
     __syncthreads();
+    const bool busy = qbase < nq;  // wave-uniform: some of its 32 queries are live
     f32x16 sA[QT], sB[QT];
-    qk_half<SPLIT, QT>(smem, c, qf, qfl, 0, sA);
+    if (!(SPLIT && QT == 1) || busy) qk_half<SPLIT, QT>(smem, c, qf, qfl, 0, sA);
     f32x16 o[QT][2];
 #pragma unroll
     for (int i = 0; i < 16; ++i)
@@ -444,8 +450,8 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
     // stages unrolled by 3 (K and V ring slot of stage j = j % 3, compile-time)
 #define PIPE_STAGE(J, R, LAST)                                                                 \
     {                                                                                          \
-        pipe_half<0, LAST, R, SPLIT, QT>(J, sA, sB, c, qf, qfl, o, mrun, lsum, stage, (J) % 3); \
-        pipe_half<1, LAST, R, SPLIT, QT>(J, sB, sA, c, qf, qfl, o, mrun, lsum, stage, (J) % 3); \
+        pipe_half<0, LAST, R, SPLIT, QT>(J, sA, sB, c, qf, qfl, o, mrun, lsum, stage, (J) % 3, busy); \
+        pipe_half<1, LAST, R, SPLIT, QT>(J, sB, sA, c, qf, qfl, o, mrun, lsum, stage, (J) % 3, busy); \
     }
     const int last = c.nkb - 1;
     int j = 0;
