@@ -66,14 +66,23 @@ __global__ __launch_bounds__(256) void k_lg_kpnorm(const Seg* __restrict__ segs,
     }
 }
 
+#ifndef MLG_LG_INIT_FUSED
+#define MLG_LG_INIT_FUSED 1  // 0: the separate k_lg_gather_rows pass (A/B only)
+#endif
+
 // 64 rows of one segment per workgroup: Fourier positional encoding (cos / sin of
 // Wr . k', 32 frequencies), x = desc, cat[:, :256] = bf16(desc), ind = source index;
-// rows past len zeroed.
+// rows past len zeroed.  With mv (layer 0's self block already run per frame): the live
+// rows' x and bf16 copy come from that block's output instead, mv[seg] = (pair offset,
+// live rows, frame offset, -) -- k_lg_gather_rows folded into this pass.
 __global__ __launch_bounds__(256) void k_lg_init(const Seg* __restrict__ segs, const float4* __restrict__ norm,
                                                  const float* __restrict__ kpts, const float* __restrict__ desc,
                                                  int kmax, const float* __restrict__ Wr, float* __restrict__ x,
                                                  bf16_t* __restrict__ cat, float* __restrict__ ecos,
-                                                 float* __restrict__ esin, int32_t* __restrict__ ind) {
+                                                 float* __restrict__ esin, int32_t* __restrict__ ind,
+                                                 const int4* __restrict__ mv = nullptr,
+                                                 const float* __restrict__ xf = nullptr,
+                                                 const bf16_t* __restrict__ catf = nullptr) {
     const Seg sg = segs[blockIdx.y];
     const int r0 = blockIdx.x * 64;
     if (r0 >= ((sg.len + 63) & ~63)) return;
@@ -94,6 +103,22 @@ __global__ __launch_bounds__(256) void k_lg_init(const Seg* __restrict__ segs, c
         ecos[r * 32 + f] = c;
         esin[r * 32 + f] = sn;
         if (f == 0) ind[r] = live ? i : -1;
+    }
+    if (mv) {
+        const size_t fo = (size_t)mv[blockIdx.y].z;
+        for (int e = threadIdx.x; e < 64 * LG_D / 4; e += 256) {
+            const int i = r0 + e / (LG_D / 4), c4 = (e % (LG_D / 4)) * 4;
+            const size_t r = (size_t)sg.off + i;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            uint2 o = make_uint2(0u, 0u);
+            if (i < sg.len) {
+                v = *reinterpret_cast<const float4*>(xf + (fo + i) * LG_D + c4);
+                o = *reinterpret_cast<const uint2*>(catf + (fo + i) * 512 + c4);
+            }
+            *reinterpret_cast<float4*>(x + r * LG_D + c4) = v;
+            *reinterpret_cast<uint2*>(cat + r * 512 + c4) = o;
+        }
+        return;
     }
     for (int e = threadIdx.x; e < 64 * LG_D / 4; e += 256) {
         const int i = r0 + e / (LG_D / 4), c4 = (e % (LG_D / 4)) * 4;
@@ -639,6 +664,7 @@ __global__ __launch_bounds__(256) void k_lg_orient(const int32_t* __restrict__ m
 }
 
 
+#if !MLG_LG_INIT_FUSED
 // Layer 0's self block on the frame layout -> the pair layout: pair segment k copies the
 // rows of its frame's segment (x f32 and the bf16 x copy in CAT's first 256 columns).
 // mv[k] = (pair offset, live rows, frame offset, -).
@@ -661,6 +687,7 @@ __global__ __launch_bounds__(256) void k_lg_gather_rows(const int4* __restrict__
             reinterpret_cast<const uint4*>(catf + (size_t)(m.z + i) * 512)[c];
     }
 }
+#endif
 
 size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -987,14 +1014,22 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     }
     LG_TRY(upload_layout());
     hipLaunchKernelGGL(k_lg_kpnorm, dim3((unsigned)segs.size()), dim3(256), 0, s, SEGS, kpts, kmax, (float4*)(base + L.norm));
+#if MLG_LG_INIT_FUSED
     hipLaunchKernelGGL(k_lg_init, dim3((unsigned)((kmax + 63) / 64), (unsigned)segs.size()), dim3(256), 0, s, SEGS,
-                       (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X, CAT, EC, ES, IND);
+                       (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X, CAT, EC, ES, IND,
+                       self0_done ? (const int4*)MOVES : nullptr, X2, CAT2);
+    MLG_LAUNCH_CHECK();
+#else
+    hipLaunchKernelGGL(k_lg_init, dim3((unsigned)((kmax + 63) / 64), (unsigned)segs.size()), dim3(256), 0, s, SEGS,
+                       (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X, CAT, EC, ES, IND,
+                       nullptr, nullptr, nullptr);
     MLG_LAUNCH_CHECK();
     if (self0_done) {
         hipLaunchKernelGGL(k_lg_gather_rows, dim3((unsigned)((kmax + 15) / 16), (unsigned)segs.size()), dim3(256), 0, s,
                            MOVES, X2, CAT2, X, CAT);
         MLG_LAUNCH_CHECK();
     }
+#endif
     tr_rows(1, X, LG_D * 4, Npad);
     tr_rows(2, CAT, 512, Npad, 1024);
 
