@@ -34,6 +34,9 @@
 #ifndef MLG_PROJ_PROBE
 #define MLG_PROJ_PROBE 0
 #endif
+#ifndef MLG_PROJ_PIPE
+#define MLG_PROJ_PIPE 1  // the resident form with the epilogue inside the next tile's GEMM
+#endif
 
 namespace {
 
@@ -351,6 +354,212 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------- pipelined resident form
+// The resident form with the epilogue of tile t - 1 issued INSIDE the GEMM of tile t:
+// every wave's bias / rotary / mask / bf16 staging of the previous tile's accumulators is
+// cut into 8 slices (4 column groups x 2 m-tiles), one after every second k-step, so the
+// VALU work fills the MFMA gaps instead of running in a phase of its own (the serial form
+// spends about as long in its epilogue as in its GEMM).  Three LDS buffers: tile t's x
+// rows (GEMM), tile t - 1's staging image over its dead x rows (+ its factors / live
+// bytes), tile t + 1's DMA.  Only the copy-out stays a phase of its own, after the
+// staging barrier.  Results are those of k_lg_proj_res bit for bit (same accumulators,
+// same epilogue arithmetic).
+template <bool SELF>
+__device__ __forceinline__ void slice_qk(int g, int mt, const f32x16& a, char* lds, const float* bias_l,
+                                         const float* fc, const float* fs, const uint8_t* live_l) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 31, hh = lane >> 5;
+    const int n = 32 * wave + 8 * g + 4 * hh, h = n >> 6, d = n & 63;
+    const float4 b = *reinterpret_cast<const float4*>(bias_l + n);
+    const int r = 32 * mt + col;
+    float x0 = a[4 * g] + b.x, x1 = a[4 * g + 1] + b.y, x2 = a[4 * g + 2] + b.z, x3 = a[4 * g + 3] + b.w;
+    if (SELF) {  // as proj_epilogue's resident form
+        const int j = (n & 63) / 2;
+        const int eo = r * 32 + 4 * ((j >> 2) ^ fac_swz(r)) + (j & 3);
+        const float2 rc = *reinterpret_cast<const float2*>(fc + eo);
+        const float2 rs = *reinterpret_cast<const float2*>(fs + eo);
+        const float r0 = __fadd_rn(__fmul_rn(x0, rc.x), __fmul_rn(-x1, rs.x));
+        const float r1 = __fadd_rn(__fmul_rn(x1, rc.x), __fmul_rn(x0, rs.x));
+        const float r2 = __fadd_rn(__fmul_rn(x2, rc.y), __fmul_rn(-x3, rs.y));
+        const float r3 = __fadd_rn(__fmul_rn(x3, rc.y), __fmul_rn(x2, rs.y));
+        x0 = r0; x1 = r1; x2 = r2; x3 = r3;
+    }
+    // branch-free mask: a branch here would end the basic block and with it the
+    // scheduler's freedom to interleave this slice with the GEMM's MFMAs
+    const uint32_t keep = 0u - (uint32_t)(live_l[r] != 0);
+    *reinterpret_cast<uint2*>(lds + stage_off<64>(h, r, d)) =
+        make_uint2(pack_bf16x2(x0, x1) & keep, pack_bf16x2(x2, x3) & keep);
+}
+
+__device__ __forceinline__ void slice_v(int g, int mt, const f32x16& a, char* lds, const float* bias_l,
+                                        const uint8_t* live_l) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 31, hh = lane >> 5;
+    const int n = 32 * wave + col, h = n >> 6, d = n & 63;
+    const float b = bias_l[n];
+    const int r = 32 * mt + 8 * g + 4 * hh;
+    const uint32_t lv = *reinterpret_cast<const uint32_t*>(live_l + r);
+    const float v0 = (lv & 0xff) ? a[4 * g] + b : 0.f;
+    const float v1 = (lv & 0xff00) ? a[4 * g + 1] + b : 0.f;
+    const float v2 = (lv & 0xff0000) ? a[4 * g + 2] + b : 0.f;
+    const float v3 = (lv >> 24) ? a[4 * g + 3] + b : 0.f;
+    *reinterpret_cast<uint2*>(lds + stage_off<64>(h, d, r)) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+}
+
+// acc_new = GEMM of the x tile in `xl`; with STAGE, slice i of the previous tile's
+// staging (acc_old into `sl`) after k-step 2 i.
+template <bool SELF, bool IS_V, bool STAGE>
+__device__ __forceinline__ void pipe_gemm(const bf16x8 (&wf)[16], const char* xl, f32x16 (&acc)[2],
+                                          const f32x16 (&old)[2], char* sl, const float* bias_l, const float* fc,
+                                          const float* fs, const uint8_t* live_l) {
+    const int lane = threadIdx.x & 63, col = lane & 31, hh = lane >> 5;
+    const char* xrow = xl + col * ROWB;
+    const int sw = col & 15;
+    bf16x8 xa[2], xb[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) xa[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + ((hh ^ sw) << 4));
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+        bf16x8(&cur)[2] = (ks & 1) ? xb : xa;
+        bf16x8(&nxt)[2] = (ks & 1) ? xa : xb;
+        if (ks < 15) {
+            const int cn = ((2 * (ks + 1) + hh) ^ sw) << 4;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) nxt[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + cn);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+            acc[mt] = IS_V ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur[mt], wf[ks], acc[mt], 0, 0, 0)
+                           : __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], cur[mt], acc[mt], 0, 0, 0);
+        if (STAGE && !(ks & 1)) {
+            const int g = ks >> 2, mt = (ks >> 1) & 1;
+            if (IS_V) slice_v(g, mt, old[mt], sl, bias_l, live_l);
+            else slice_qk<SELF>(g, mt, old[mt], sl, bias_l, fc, fs, live_l);
+        }
+    }
+}
+
+// copy-out of a staged 64-token tile (proj_epilogue's second half)
+__device__ __forceinline__ void copy_out64(bool is_v, int part, int m0, const char* lds, bf16_t* __restrict__ Q,
+                                           bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad) {
+    bf16_t* dst = is_v ? Vt : (part == 0 ? Q : K);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int L = p * 512 + threadIdx.x, h = L / 512, row = (L >> 3) & 63, c = L & 7;
+        *reinterpret_cast<uint4*>(dst + ((size_t)h * Npad + m0 + row) * 64 + c * 8) =
+            *reinterpret_cast<const uint4*>(lds + stage_off<64>(h, row, 8 * c));
+    }
+}
+
+template <bool SELF, bool IS_V>
+__device__ __forceinline__ void pipe_tiles(const bf16x8 (&wf)[16], char* ring, const float* bias_l,
+                                           const bf16_t* __restrict__ xcopy, int ldx, const float* __restrict__ ecos,
+                                           const float* __restrict__ esin, const uint8_t* __restrict__ live,
+                                           bf16_t* __restrict__ Q, bf16_t* __restrict__ K, bf16_t* __restrict__ Vt,
+                                           int Npad, int part, int t0, int stride, int ntiles) {
+    constexpr int R = 64, XB = R * ROWB, BUF = XB + (SELF ? 2 * R * 32 * 4 : 0), SLOT = BUF + 256;
+    auto bufs = [&](int i) { return ring + i * SLOT; };
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int drow = 8 * wave + (lane >> 5), dslot = lane & 31;
+    auto issue = [&](int tile, char* buf) {
+        const unsigned base = lds_addr(buf) + 4096 * wave;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = drow + 2 * i;
+            dma16(xcopy + (size_t)(tile * R + row) * ldx + ((dslot ^ (row & 15)) * 8), base + 1024 * i);
+        }
+        if (SELF) {
+            const unsigned fb = lds_addr(buf) + XB + 1024 * wave;
+            const int frow = 8 * wave + (lane >> 3);
+            const size_t fo = (size_t)(tile * R + frow) * 32 + 4 * ((lane & 7) ^ fac_swz(frow));
+            dma16(ecos + fo, fb);
+            dma16(esin + fo, fb + R * 32 * 4);
+        }
+        if (wave == 0 && lane < R / 16) dma16(live + (size_t)tile * R + 16 * lane, lds_addr(buf) + BUF);
+    };
+    f32x16 acc0[2], acc1[2];  // the GEMM's and the staged tile's, alternating (compile-time roles)
+    issue(t0, bufs(0));
+    int t = t0, tp = -1, it = 0;  // tile in the GEMM, tile being staged (-1: none)
+    // one iteration; PAR = it & 1 picks the accumulator roles
+    auto step = [&](f32x16 (&an)[2], const f32x16 (&ao)[2]) -> bool {
+        const int bx = it % 3, bp = (it + 2) % 3, bn = (it + 1) % 3;
+        // tile t's DMA has landed (only the previous iteration's 4 copy-out stores per lane
+        // were issued after it; none in the first two iterations)
+        if (it < 2) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        else __builtin_amdgcn_s_waitcnt(0x0F74);         // vmcnt(4)
+        __syncthreads();  // every wave's DMA; every wave's copy-out reads of buffer bn
+        const int tn = t + stride;
+        if (tn < ntiles) issue(tn, bufs(bn));
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) an[mt][i] = 0.f;
+        char* sl = bufs(bp);
+        const float* fc = reinterpret_cast<const float*>(sl + XB);
+        if (tp >= 0) {
+            pipe_gemm<SELF, IS_V, true>(wf, bufs(bx), an, ao, sl, bias_l, fc, fc + R * 32,
+                                        reinterpret_cast<const uint8_t*>(sl + BUF));
+            __syncthreads();  // staging written
+            copy_out64(IS_V, part, tp * R, sl, Q, K, Vt, Npad);
+        } else {
+            pipe_gemm<SELF, IS_V, false>(wf, bufs(bx), an, ao, sl, bias_l, fc, fc + R * 32,
+                                         reinterpret_cast<const uint8_t*>(sl + BUF));
+        }
+        tp = t;
+        ++it;
+        if (tn >= ntiles) {  // the last tile: its staging alone
+            __syncthreads();  // every wave has read its x rows
+            char* sx = bufs(bx);
+            const float* fx = reinterpret_cast<const float*>(sx + XB);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (IS_V) slice_v(i >> 1, i & 1, an[i & 1], sx, bias_l, reinterpret_cast<const uint8_t*>(sx + BUF));
+                else slice_qk<SELF>(i >> 1, i & 1, an[i & 1], sx, bias_l, fx, fx + R * 32,
+                                    reinterpret_cast<const uint8_t*>(sx + BUF));
+            }
+            __syncthreads();
+            copy_out64(IS_V, part, tp * R, sx, Q, K, Vt, Npad);
+            return true;
+        }
+        t = tn;
+        return false;
+    };
+    for (;;) {
+        if (step(acc0, acc1)) return;
+        if (step(acc1, acc0)) return;
+    }
+}
+
+template <bool SELF>
+__global__ __launch_bounds__(512) void k_lg_proj_pipe(const bf16_t* __restrict__ xcopy, int ldx,
+                                                        const bf16_t* __restrict__ W, const float* __restrict__ bias,
+                                                        const float* __restrict__ ecos,
+                                                        const float* __restrict__ esin,
+                                                        const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
+                                                        bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad,
+                                                        int slots) {
+    constexpr int N = SELF ? 768 : 512, NPART = SELF ? 3 : 2, R = 64;
+    constexpr int SLOT = R * ROWB + (SELF ? 2 * R * 32 * 4 : 0) + 256;  // x, factors, live bytes (pipe_tiles)
+    __shared__ __attribute__((aligned(16))) char ring[3 * SLOT];
+    __shared__ __attribute__((aligned(16))) float bias_l[256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 31, hh = lane >> 5;
+    const int xcd = (int)blockIdx.x & 7, j = (int)blockIdx.x >> 3;
+    const int part = j % NPART, slot = j / NPART;
+    const int ntiles = Npad / R, stride = 8 * slots;
+    const int t0 = xcd + 8 * slot;
+    if (slot >= slots || t0 >= ntiles) return;
+    if (threadIdx.x < 256) bias_l[threadIdx.x] = bias[256 * part + threadIdx.x];  // read after the loop-top barrier
+    bf16x8 wf[16];
+    {
+        const bf16_t* wrow = W + (size_t)(256 * part + 32 * wave + col) * 16 + 8 * hh;
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) wf[ks] = ld16(wrow + (size_t)ks * N * 16);
+    }
+    if (part == NPART - 1)
+        pipe_tiles<SELF, true>(wf, ring, bias_l, xcopy, ldx, ecos, esin, live, Q, K, Vt, Npad, part, t0, stride, ntiles);
+    else
+        pipe_tiles<SELF, false>(wf, ring, bias_l, xcopy, ldx, ecos, esin, live, Q, K, Vt, Npad, part, t0, stride,
+                                ntiles);
+}
+
 }  // namespace
 
 int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,
@@ -377,6 +586,17 @@ int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, 
         // one workgroup per CU (256 VGPRs, 64-96 KiB LDS), `slots` part-groups per XCD
         const int slots = std::max(1, std::min((cus / 8) / npart, (ntiles + 7) / 8));
         const unsigned grid = (unsigned)(8 * slots * npart);
+        if (MLG_PROJ_PIPE && !probe) {
+            if (self_block)
+                hipLaunchKernelGGL(k_lg_proj_pipe<true>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin,
+                                   live, Q, K, Vt, Npad, slots);
+            else
+                hipLaunchKernelGGL(k_lg_proj_pipe<false>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias,
+                                   (const float*)nullptr, (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad,
+                                   slots);
+            MLG_LAUNCH_CHECK();
+            return MLG_OK;
+        }
         if (self_block)
             hipLaunchKernelGGL(k_lg_proj_res<true>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin, live,
                                Q, K, Vt, Npad, slots, probe);
