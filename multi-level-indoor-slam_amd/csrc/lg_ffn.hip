@@ -186,11 +186,15 @@ __device__ __forceinline__ void zero(f32x16 (&acc)[NT][MT]) {
 //   msg = norm1(merge(attn));  x += norm2(mlp(cat[x, msg]))   (mlp: Linear, ReLU, Linear)
 // no biases; norm1 (LayerNorm 256) in the msg epilogue, norm2 in the final row pass;
 // LayerNorm affine from ln_g / ln_b = [norm1 (256) | norm2 (256)].
-template <bool PERSIST, int R, int NW, bool LOFTR = false>
+// RELU (SuperGlue's MLP) is a template argument, not a kernel argument: a run-time flag
+// left a uniform branch around every 4-column group of the GELU epilogue, and each
+// basic block held just two dependent 13-step Horner chains (the scheduler cannot
+// interleave groups across blocks).
+template <bool PERSIST, int R, int NW, bool LOFTR = false, bool RELU = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_t* __restrict__ ctx, float* __restrict__ X,
                                                   bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w,
-                                                  mlg_lg_conf_i cf, int relu) {
-    if (LOFTR) relu = 1;
+                                                  mlg_lg_conf_i cf) {
+    constexpr bool relu = LOFTR || RELU;
     constexpr int MT = R / 32, NT1 = 256 / NW / 32, NT2 = 512 / NW / 32, NTH = 64 * NW;
     constexpr int RING = NW == 8 ? 8 : MLG_FFN_RING2;  // weight k-steps in flight per wave (ffn1)
     // ring of the msg / ffn2 phases (NT1 column tiles, half the MFMAs per k-step of ffn1).
@@ -561,21 +565,31 @@ int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const
     mlg_lg_conf_i cf{};
     if (conf) cf = *conf;
 #if MLG_FFN_ROWS == 128
-    hipLaunchKernelGGL((k_lg_ffn<false, 128, 8>), dim3((unsigned)((M + 127) / 128)), dim3(512), 0, s, ctx, X, xcopy, ldc,
-                       M, w, cf, relu);
+    if (relu)
+        hipLaunchKernelGGL((k_lg_ffn<false, 128, 8, false, true>), dim3((unsigned)((M + 127) / 128)), dim3(512), 0, s,
+                           ctx, X, xcopy, ldc, M, w, cf);
+    else
+        hipLaunchKernelGGL((k_lg_ffn<false, 128, 8>), dim3((unsigned)((M + 127) / 128)), dim3(512), 0, s, ctx, X, xcopy,
+                           ldc, M, w, cf);
 #elif MLG_FFN_GRID > 0
     const long ntiles = (M + 63) / 64;
     const long grid = std::min<long>(ntiles, (long)MLG_FFN_GRID * ffn_num_cus());
-    hipLaunchKernelGGL((k_lg_ffn<true, 64, 4>), dim3((unsigned)grid), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf,
-                       relu);
+    if (relu)
+        hipLaunchKernelGGL((k_lg_ffn<true, 64, 4, false, true>), dim3((unsigned)grid), dim3(256), 0, s, ctx, X, xcopy,
+                           ldc, M, w, cf);
+    else
+        hipLaunchKernelGGL((k_lg_ffn<true, 64, 4>), dim3((unsigned)grid), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w, cf);
 #else
     const long ntiles = (M + 63) / 64;
     if (relu == 2)
         hipLaunchKernelGGL((k_lg_ffn<false, 64, 4, true>), dim3((unsigned)ntiles), dim3(256), 0, s, ctx, X, xcopy, ldc,
-                           M, w, cf, relu);
+                           M, w, cf);
+    else if (relu == 1)
+        hipLaunchKernelGGL((k_lg_ffn<false, 64, 4, false, true>), dim3((unsigned)ntiles), dim3(256), 0, s, ctx, X, xcopy,
+                           ldc, M, w, cf);
     else
         hipLaunchKernelGGL((k_lg_ffn<false, 64, 4>), dim3((unsigned)ntiles), dim3(256), 0, s, ctx, X, xcopy, ldc, M, w,
-                           cf, relu);
+                           cf);
 #endif
     MLG_LAUNCH_CHECK();
     return MLG_OK;

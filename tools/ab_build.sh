@@ -1,16 +1,18 @@
 #!/bin/bash
 # Build an A/B arm of the native libraries with extra preprocessor flags on one source:
-#   tools/ab_build.sh OUT_DIR FILE.hip "-DMACRO=V ..."
+#   tools/ab_build.sh OUT_DIR FILE.hip "-DMACRO=V ..." [REPLACEMENT_SOURCE]
 # Copies the package (sources + the tree's objects) to a scratch directory, rebuilds FILE
 # with the flags, relinks, and puts libmlgate.so / libmlgate_torch.so in OUT_DIR for
-# tools/ab_run.py --lib-dir.  The tree's own libraries are not touched.
+# tools/ab_run.py --lib-dir.  The tree's own libraries are not touched.  With a fourth
+# argument FILE is replaced by that source first (e.g. a previous revision from git show).
 set -eu
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
-OUT="$(mkdir -p "$1" && cd "$1" && pwd)"; FILE="$2"; DEFS="$3"
+OUT="$(mkdir -p "$1" && cd "$1" && pwd)"; FILE="$2"; DEFS="$3"; REPL="${4:-}"
 TMP="$(mktemp -d /tmp/abb_XXXX)"
 mkdir -p "$TMP/pkg/mlgate"
 cp -a "$ROOT/include" "$TMP/include"
 cp -a "$ROOT/multi-level-indoor-slam_amd/csrc" "$TMP/pkg/csrc"
+if [ -n "$REPL" ]; then cp "$REPL" "$TMP/pkg/csrc/$FILE"; fi
 touch "$TMP/pkg/csrc/$FILE"
 BASE="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -fno-slp-vectorize"
 make -s -C "$TMP/pkg/csrc" -j8 CXXFLAGS="$BASE $DEFS" > "$TMP/build.log" 2>&1 || { tail -20 "$TMP/build.log"; exit 1; }
