@@ -18,6 +18,8 @@
 // masked on store).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -98,12 +100,25 @@ struct EpiBiasGeluBF16 {
 #ifndef MLG_SPLIT_GELU_ERF
 #define MLG_SPLIT_GELU_ERF 0
 #endif
+#ifndef MLG_EPI_PROBE
+#define MLG_EPI_PROBE 0  // timing-probe builds only (results wrong): 4 no fc1 stores, 8 no GELU
+#endif
 struct EpiBiasGeluSplit {
     bf16_t* C; int ldc; int lo_col; const float* bias;
     __device__ static float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f)); }
-    __device__ void operator()(int m, int n, const f32x4& v) const {
-        const float4 b = *reinterpret_cast<const float4*>(bias + n);
-        uint2 h, l;
+    // batched form (epi_tile): column data, row data, per-fragment prefetch, apply
+    struct Col { float4 b; };
+    struct Row { size_t key = 0; };  // (staged form: unused)
+    struct Pre {};
+    __device__ Col col(int n) const { return {*reinterpret_cast<const float4*>(bias + n)}; }
+    __device__ Row row(int) const { return {}; }
+    __device__ Pre pre(int, int, const Col&, const Row&) const { return {}; }
+    // staged form (k_gemm256s): the pair computed in the fragment layout, written from an
+    // LDS image as whole rows (put)
+    static constexpr int STAGED = 1;
+    __device__ bool staged_wave(int) const { return true; }
+    __device__ void stage2(const f32x4& v, const Col& c, uint2& h, uint2& l) const {
+        const float4 b = c.b;
 #if MLG_SPLIT_GELU_ERF
         split_bf16x4(gelu(v[0] + b.x), gelu(v[1] + b.y), gelu(v[2] + b.z), gelu(v[3] + b.w), h, l);
 #else
@@ -111,23 +126,68 @@ struct EpiBiasGeluSplit {
         const f32x2 g23 = gelu_poly2(f32x2{v[2] + b.z, v[3] + b.w});
         split_bf16x4(g01.x, g01.y, g23.x, g23.y, h, l);
 #endif
+    }
+    __device__ void put(int m, int n, int plane, size_t, const uint4& d) const {
+        *reinterpret_cast<uint4*>(C + (size_t)m * ldc + (plane ? lo_col : 0) + n) = d;
+    }
+    __device__ void apply(int m, int n, const f32x4& v, const Col& c, const Row&, const Pre&) const {
+        const float4 b = c.b;
+        uint2 h, l;
+#if MLG_SPLIT_GELU_ERF
+        split_bf16x4(gelu(v[0] + b.x), gelu(v[1] + b.y), gelu(v[2] + b.z), gelu(v[3] + b.w), h, l);
+#elif MLG_EPI_PROBE & 8  // timing probe only: no GELU
+        split_bf16x4(v[0] + b.x, v[1] + b.y, v[2] + b.z, v[3] + b.w, h, l);
+#else
+        const f32x2 g01 = gelu_poly2(f32x2{v[0] + b.x, v[1] + b.y});
+        const f32x2 g23 = gelu_poly2(f32x2{v[2] + b.z, v[3] + b.w});
+        split_bf16x4(g01.x, g01.y, g23.x, g23.y, h, l);
+#endif
+#if MLG_EPI_PROBE & 4  // timing probe only: stores kept alive by an impossible test
+        if (h.x != 0x7f817f81u) return;
+#endif
         *reinterpret_cast<uint2*>(C + (size_t)m * ldc + n) = h;
         *reinterpret_cast<uint2*>(C + (size_t)m * ldc + lo_col + n) = l;
     }
+    __device__ void operator()(int m, int n, const f32x4& v) const { apply(m, n, v, col(n), Row{}, Pre{}); }
 };
 
 struct EpiResidual {  // X += gamma * (acc + b)   (attn.proj / mlp.fc2 + LayerScale + residual)
     float* X; int ldx; const float* bias; const float* gamma;
-    __device__ void operator()(int m, int n, const f32x4& v) const {
-        float4* p = reinterpret_cast<float4*>(X + (size_t)m * ldx + n);
-        const float4 b = *reinterpret_cast<const float4*>(bias + n);
+    struct Col { float4 b, g; };
+    struct Row {};
+    struct Pre { float4 x; };
+    __device__ Col col(int n) const {
+        return {*reinterpret_cast<const float4*>(bias + n), *reinterpret_cast<const float4*>(gamma + n)};
+    }
+    __device__ Row row(int) const { return {}; }
+    __device__ Pre pre(int m, int n, const Col&, const Row&) const {
+        return {*reinterpret_cast<const float4*>(X + (size_t)m * ldx + n)};
+    }
+    // staged form (k_gemm256s): acc + b staged as f32 rows, then x += gamma * (that) per row
+    static constexpr int STAGED = 2;
+    __device__ float4 stage4(const f32x4& v, const Col& c) const {
+        return make_float4(v[0] + c.b.x, v[1] + c.b.y, v[2] + c.b.z, v[3] + c.b.w);
+    }
+    __device__ float4 load4(int m, int n) const { return *reinterpret_cast<const float4*>(X + (size_t)m * ldx + n); }
+    __device__ void put4(int m, int n, float4 x, const float4& y) const {
         const float4 g = *reinterpret_cast<const float4*>(gamma + n);
-        float4 x = *p;
-        x.x += g.x * (v[0] + b.x);
-        x.y += g.y * (v[1] + b.y);
-        x.z += g.z * (v[2] + b.z);
-        x.w += g.w * (v[3] + b.w);
-        *p = x;
+        x.x += g.x * y.x;
+        x.y += g.y * y.y;
+        x.z += g.z * y.z;
+        x.w += g.w * y.w;
+        *reinterpret_cast<float4*>(X + (size_t)m * ldx + n) = x;
+    }
+    __device__ void apply(int m, int n, const f32x4& v, const Col& c, const Row&, const Pre& p) const {
+        float4 x = p.x;
+        x.x += c.g.x * (v[0] + c.b.x);
+        x.y += c.g.y * (v[1] + c.b.y);
+        x.z += c.g.z * (v[2] + c.b.z);
+        x.w += c.g.w * (v[3] + c.b.w);
+        *reinterpret_cast<float4*>(X + (size_t)m * ldx + n) = x;
+    }
+    __device__ void operator()(int m, int n, const f32x4& v) const {
+        const Col c = col(n);
+        apply(m, n, v, c, Row{}, pre(m, n, c, Row{}));
     }
 };
 
@@ -159,11 +219,31 @@ struct EpiQKV {
 // EpiQKV for the split forward: hi planes as EpiQKV, lo planes lo_off elements further
 struct EpiQKVSplit {
     bf16_t* Q; bf16_t* K; bf16_t* Vt; const float* bias; int T, Tpad, Np; size_t lo_off;
-    __device__ void operator()(int m, int n, const f32x4& v) const {
-        const float4 b = *reinterpret_cast<const float4*>(bias + n);
+    struct Col { float4 b; };
+    struct Row { size_t key; };
+    struct Pre {};
+    __device__ Col col(int n) const { return {*reinterpret_cast<const float4*>(bias + n)}; }
+    __device__ Row row(int m) const {
         const int bi = m / T, t = m - bi * T;
+        return {(size_t)bi * Tpad + t};
+    }
+    __device__ Pre pre(int, int, const Col&, const Row&) const { return {}; }
+    __device__ void operator()(int m, int n, const f32x4& v) const { apply(m, n, v, col(n), row(m), Pre{}); }
+    // staged form (k_gemm256s) for the Q / K waves (a wave's 64 columns are one head of one
+    // of q, k, v): whole 128-B token rows of the head-major planes; V^T keeps apply
+    static constexpr int STAGED = 1;
+    __device__ bool staged_wave(int n) const { return n < 2 * 768; }
+    __device__ void stage2(const f32x4& v, const Col& c, uint2& h, uint2& l) const {
+        split_bf16x4(v[0] + c.b.x, v[1] + c.b.y, v[2] + c.b.z, v[3] + c.b.w, h, l);
+    }
+    __device__ void put(int, int n, int plane, size_t key, const uint4& dd) const {
         const int which = n / 768, c = n - which * 768, h = c >> 6, d = c & 63;
-        const size_t key = (size_t)bi * Tpad + t;
+        *reinterpret_cast<uint4*>((which == 0 ? Q : K) + ((size_t)h * Np + key) * 64 + d + (plane ? lo_off : 0)) = dd;
+    }
+    __device__ void apply(int, int n, const f32x4& v, const Col& cd, const Row& rw, const Pre&) const {
+        const float4 b = cd.b;
+        const int which = n / 768, c = n - which * 768, h = c >> 6, d = c & 63;
+        const size_t key = rw.key;
         uint2 hi, lo;
         split_bf16x4(v[0] + b.x, v[1] + b.y, v[2] + b.z, v[3] + b.w, hi, lo);
         if (which < 2) {
@@ -250,12 +330,26 @@ struct EpiConv {
 
 struct EpiPatch {  // patch tokens: X[b, 1 + p, :] = acc + b + pos[1 + p]
     float* X; const float* bias; const float* pos; int P;  // P = patches per image
-    __device__ void operator()(int m, int n, const f32x4& v) const {
-        const int bi = m / P, p = m - bi * P;
-        const float4 b = *reinterpret_cast<const float4*>(bias + n);
-        const float4 q = *reinterpret_cast<const float4*>(pos + (size_t)(1 + p) * 768 + n);
-        *reinterpret_cast<float4*>(X + ((size_t)bi * (P + 1) + 1 + p) * 768 + n) =
+    struct Col { float4 b; };
+    struct Row { int bi, p; };
+    struct Pre { float4 q; };
+    __device__ Col col(int n) const { return {*reinterpret_cast<const float4*>(bias + n)}; }
+    __device__ Row row(int m) const {
+        const int bi = m / P;
+        return {bi, m - bi * P};
+    }
+    __device__ Pre pre(int, int n, const Col&, const Row& r) const {
+        return {*reinterpret_cast<const float4*>(pos + (size_t)(1 + r.p) * 768 + n)};
+    }
+    __device__ void apply(int, int n, const f32x4& v, const Col& c, const Row& r, const Pre& pq) const {
+        const float4 b = c.b, q = pq.q;
+        *reinterpret_cast<float4*>(X + ((size_t)r.bi * (P + 1) + 1 + r.p) * 768 + n) =
             make_float4(v[0] + b.x + q.x, v[1] + b.y + q.y, v[2] + b.z + q.z, v[3] + b.w + q.w);
+    }
+    __device__ void operator()(int m, int n, const f32x4& v) const {
+        const Col c = col(n);
+        const Row r = row(m);
+        apply(m, n, v, c, r, pre(m, n, c, r));
     }
 };
 
@@ -632,6 +726,13 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A
 // reloads its A fragments as A_lo for the hi*lo MFMAs -- 96 MFMAs per 24 fragment reads
 // per wave and K-step, and every operand byte fetched once (a K-concatenated [hi|lo|hi]
 // GEMM re-reads A_hi and W_hi: 3 planes each instead of 2).
+// Epi::STAGED (k_gemm256s): 1 = a bf16 hi / lo pair per element written from an LDS image
+// as whole rows (stage2 / put), 2 = an f32 row update (stage4 / load4 / put4), 0 = none
+template <class E, class = void>
+struct staged_of { static constexpr int value = 0; };
+template <class E>
+struct staged_of<E, std::void_t<decltype(E::STAGED)>> { static constexpr int value = E::STAGED; };
+
 template <class Epi>
 __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                     int M, int N, int K0, int lda, int ldw, Epi epi) {
@@ -640,6 +741,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ 
     constexpr int STAGE = 4 * PLANE;    // A_hi, A_lo, W_hi, W_lo
     __shared__ __attribute__((aligned(16))) char st0[STAGE];
     __shared__ __attribute__((aligned(16))) char st1[STAGE];
+    constexpr int STG = staged_of<Epi>::value;
+    __shared__ size_t skey[STG == 1 ? 8 : 1][32];  // staged form: the pass's row keys per wave
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nN = N / TN, nM = (M + TM - 1) / TM, ntiles = nN * nM;
     const int xcd = blockIdx.x & 7, per_xcd = gridDim.x >> 3;
@@ -739,14 +842,130 @@ __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ 
             __builtin_amdgcn_s_barrier();
         }
         const int mt = tile / nN, m0 = mt * TM, n0 = (tile - mt * nN) * TN;
+        // batched epilogue: every column's (bias, ...) and every row's index data first, then
+        // per column group the 8 fragments' global reads (the residual) before any of their
+        // stores -- a fragment-at-a-time epilogue waited one L2 / HBM round trip per
+        // fragment (its loads could not pass the previous fragment's stores), 32 per tile
+        // A tile wholly inside M takes a branch-free form: a per-fragment `m < M` test made
+        // every fragment its own basic block (no interleaving of their GELU chains, and a
+        // conservative vmcnt wait at every block entry that serialised the stores).
+        auto epilogue = [&](auto check) {
+            constexpr bool CHECK = decltype(check)::value;
+            typename Epi::Col cols[4];
+            typename Epi::Row rows[8];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i) cols[i] = epi.col(n0 + wn * 64 + i * 16 + (lane >> 4) * 4);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4;
                 const int m = m0 + wm * 128 + j * 16 + (lane & 15);
-                if (m < M) epi(m, n, acc[i][j]);
+                rows[j] = epi.row(CHECK ? min(m, M - 1) : m);
             }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4;
+                typename Epi::Pre pre[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int m = m0 + wm * 128 + j * 16 + (lane & 15);
+                    pre[j] = epi.pre(CHECK ? min(m, M - 1) : m, n, cols[i], rows[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int m = m0 + wm * 128 + j * 16 + (lane & 15);
+                    if (!CHECK || m < M) epi.apply(m, n, acc[i][j], cols[i], rows[j], pre[j]);
+                }
+            }
+        };
+        // Staged form: the wave's 128 x 64 outputs in 4 passes of 32 rows through its 8 KiB
+        // of the dead stage st1 (free until the next tile's second K-step DMA, after the
+        // barrier below), then written as whole 128-B (bf16) / 256-B (f32) row pieces: the
+        // fragment layout stores 16 rows x 32 B per wave-instruction, and those partial-line
+        // stores cost a third of the fc1 GEMM (profiles/r04af_split_gemm_epilogue_probe.txt).
+        if constexpr (STG == 1) {
+            const int nw = n0 + wn * 64;
+            if (epi.staged_wave(nw)) {
+                char* img = st1 + wave * 8192;
+                typename Epi::Col cols[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cols[i] = epi.col(nw + i * 16 + (lane >> 4) * 4);
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj) {
+                        const int j = 2 * p + jj, r = jj * 16 + (lane & 15);
+                        if ((lane >> 4) == 0) {
+                            const int m = m0 + wm * 128 + j * 16 + (lane & 15);
+                            skey[wave][r] = epi.row(min(m, M - 1)).key;
+                        }
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            uint2 h, l;
+                            epi.stage2(acc[i][j], cols[i], h, l);
+                            const int ch = 2 * i + ((lane >> 5) & 1);
+                            const int o = r * 128 + ((ch ^ (r & 7)) << 4) + 8 * ((lane >> 4) & 1);
+                            *reinterpret_cast<uint2*>(img + o) = h;
+                            *reinterpret_cast<uint2*>(img + 4096 + o) = l;
+                        }
+                    }
+                    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's image written
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int it = 0; it < 8; ++it) {
+                        const int L = it * 64 + lane, q = L >> 8, r = (L >> 3) & 31, ch = L & 7;
+                        const int m = m0 + wm * 128 + p * 32 + r;
+                        const uint4 d = *reinterpret_cast<const uint4*>(img + q * 4096 + r * 128 + ((ch ^ (r & 7)) << 4));
+                        if (m < M) epi.put(m, nw + ch * 8, q, skey[wave][r], d);
+                    }
+                    __builtin_amdgcn_s_waitcnt(0xc07f);  // image read before the next pass writes it
+                    __builtin_amdgcn_wave_barrier();
+                }
+            } else if (m0 + TM <= M) {
+                epilogue(std::false_type{});
+            } else {
+                epilogue(std::true_type{});
+            }
+            __syncthreads();  // every wave's image read: the next tile DMAs into st1
+        } else if constexpr (STG == 2) {
+            const int nw = n0 + wn * 64;
+            char* img = st1 + wave * 8192;
+            typename Epi::Col cols[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cols[i] = epi.col(nw + i * 16 + (lane >> 4) * 4);
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    const int j = 2 * p + jj, r = jj * 16 + (lane & 15);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int ch = 4 * i + (lane >> 4);  // 16-B f32 chunk of the 256-B row
+                        *reinterpret_cast<float4*>(img + r * 256 + ((ch ^ (r & 15)) << 4)) =
+                            epi.stage4(acc[i][j], cols[i]);
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                __builtin_amdgcn_wave_barrier();
+                float4 xv[8];
+#pragma unroll
+                for (int it = 0; it < 8; ++it) {
+                    const int L = it * 64 + lane, r = L >> 4, ch = L & 15;
+                    xv[it] = epi.load4(min(m0 + wm * 128 + p * 32 + r, M - 1), nw + ch * 4);
+                }
+#pragma unroll
+                for (int it = 0; it < 8; ++it) {
+                    const int L = it * 64 + lane, r = L >> 4, ch = L & 15;
+                    const int m = m0 + wm * 128 + p * 32 + r;
+                    const float4 y = *reinterpret_cast<const float4*>(img + r * 256 + ((ch ^ (r & 15)) << 4));
+                    if (m < M) epi.put4(m, nw + ch * 4, xv[it], y);
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                __builtin_amdgcn_wave_barrier();
+            }
+            __syncthreads();  // every wave's image read: the next tile DMAs into st1
+        } else {
+            if (m0 + TM <= M) epilogue(std::false_type{});
+            else epilogue(std::true_type{});
+        }
 #pragma unroll
         for (int i = 0; i < 2; ++i) oa[i] = na[i];
         sa = nsa;
