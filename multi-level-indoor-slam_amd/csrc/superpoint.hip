@@ -339,6 +339,10 @@ template <> struct Vec4<uint8_t> { typedef uchar4 type; };
 
 template <typename T>
 __device__ __forceinline__ T vmax_(T a, T b) { return a > b ? a : b; }
+// floats: v_max_f32 / v_max3_f32 instead of a compare + select (+ its VCC wait states) per
+// max -- the same values here: scores are finite or -inf, never NaN or -0
+template <>
+__device__ __forceinline__ float vmax_(float a, float b) { return fmaxf(a, b); }
 
 // (2 R + 1) max filter of the tile, separable, R = 4: each thread produces 4 consecutive
 // outputs from 12 inputs held in registers (one vector read per 4 in x, column reads in

@@ -4,8 +4,8 @@
 #   tools/gpu_ab.sh LIB_DIR TAG [REPEATS] -- command args...
 # e.g. tools/gpu_ab.sh ab_old r05a 2 -- tools/lg_bench.py --pairs 2048 --iters 2
 # Runs `python -u <command>` for the tree, then through tools/ab_run.py --lib-dir LIB_DIR,
-# REPEATS times (default 2), each under its own time limit, and prints the last JSON line
-# of every run; stops at the first failure.
+# REPEATS times (default 2), each under its own time limit, and prints every JSON line of
+# every run; stops at the first failure.
 set -u
 LIB="$1"; TAG="$2"; shift 2
 REP=2
@@ -17,6 +17,6 @@ for ((k = 0; k < REP; ++k)); do
     if [ "$arm" = tree ]; then pre=""; else pre="tools/ab_run.py --lib-dir $LIB"; fi
     log="gpurun_out/${TAG}_$(basename "$arm")_$k.log"
     timeout -k 10 300 python -u $pre "$@" > "$log" 2>&1 || { echo "$arm failed"; tail -5 "$log"; exit 1; }
-    echo "$arm $(grep '^{' "$log" | tail -1 | cut -c1-600)"
+    grep '^{' "$log" | cut -c1-400 | sed "s|^|$arm |"
   done
 done

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "multi-level-indoor-slam_amd"))
 sys.path.insert(0, ROOT)
 
-from bench import make_frames  # noqa: E402
+from mlgate import synthetic  # noqa: E402
 from mlgate import geometry  # noqa: E402
 from mlgate.lightglue import LightGlueGPU  # noqa: E402
 from mlgate.superpoint import SuperPointGPU  # noqa: E402
@@ -45,11 +45,17 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     F = args.frames
-    frames = make_frames(np.arange(F), max(F // 2, 1), dev)  # each place seen about twice
+    seq = synthetic.make_sequence(F, max(F // 2, 1), 0)  # each place seen about twice
+    frames = synthetic.frames_device(seq, np.arange(F), dev)
     sp = SuperPointGPU(device=dev)
     (kp, sc, ds, _, cnt), ms, wall = timed(lambda: sp.extract_device(frames), args.iters)
     counts = cnt.cpu().numpy()
+    import hashlib
+    h = hashlib.sha1()
+    for t in (kp, sc, ds, cnt):
+        h.update(t.float().cpu().numpy().tobytes())
     print(json.dumps({"stage": "superpoint", "frames": F, "ms": round(ms, 3), "wall_ms": round(wall, 3),
+                      "sha1": h.hexdigest()[:16],
                       "frames_per_s": round(F / ms * 1e3, 1), "mean_keypoints": float(counts.mean()),
                       "gflop_per_frame": 52.1}), flush=True)
     rng = np.random.default_rng(0)
