@@ -733,6 +733,16 @@ struct staged_of { static constexpr int value = 0; };
 template <class E>
 struct staged_of<E, std::void_t<decltype(E::STAGED)>> { static constexpr int value = E::STAGED; };
 
+// MLG_S256_PRIO: s_setprio(1) / (0) around each MFMA cluster of k_gemm256s (the guide's
+// T5: hipcc then keeps the cluster between its barriers)
+#ifndef MLG_S256_PRIO
+#define MLG_S256_PRIO 1
+#endif
+#if MLG_S256_PRIO
+#define S256_PRIO(p) __builtin_amdgcn_s_setprio(p)
+#else
+#define S256_PRIO(p) ((void)0)
+#endif
 template <class Epi>
 __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                     int M, int N, int K0, int lda, int ldw, Epi epi) {
@@ -800,16 +810,20 @@ __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ 
             const int row = wm * 128 + j * 16 + (lane & 15);                                               \
             af[j] = *reinterpret_cast<const bf16x8*>((ST) + soff<32>(row, ch));                            \
         }                                                                                                  \
+        S256_PRIO(1);                                                                                      \
         _Pragma("unroll") for (int j = 0; j < 8; ++j) _Pragma("unroll") for (int i = 0; i < 4; ++i) {      \
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[i], af[j], acc[i][j], 0, 0, 0);         \
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[i], af[j], acc[i][j], 0, 0, 0);         \
         }                                                                                                  \
+        S256_PRIO(0);                                                                                      \
         _Pragma("unroll") for (int j = 0; j < 8; ++j) {                                                    \
             const int row = wm * 128 + j * 16 + (lane & 15);                                               \
             af[j] = *reinterpret_cast<const bf16x8*>((ST) + PLANE + soff<32>(row, ch));                    \
         }                                                                                                  \
+        S256_PRIO(1);                                                                                      \
         _Pragma("unroll") for (int j = 0; j < 8; ++j) _Pragma("unroll") for (int i = 0; i < 4; ++i)        \
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[i], af[j], acc[i][j], 0, 0, 0);         \
+        S256_PRIO(0);                                                                                      \
     }
 
     S256_DMA(st0, oa, sa, sb, 0);
