@@ -34,6 +34,7 @@ extern "C" {
 #define MLG_VIT_EMBED 768
 #define MLG_VIT_PATCH_K 768 /* 3*14*14 = 588 patch inputs, zero-padded to 12 K-tiles of 64 */
 
+/* 2: mlg_vit_weights.packing and mlg_loftr_weights.coarse_tails appended (round 5) */
 int mlg_abi_version(void);
 const char* mlg_strerror(int status);
 
@@ -63,6 +64,7 @@ typedef struct mlg_vit_weights {
     const float* pos;        /* [1 + P, 768] */
     mlg_vit_block blocks[MLG_VIT_DEPTH];
     const float *norm_w, *norm_b;
+    int packing; /* 0: plain bf16 GEMM weights; MLG_VIT_SPLIT: [W_hi | W_lo] packing (must match the flag) */
 } mlg_vit_weights;
 
 /* mlg_vit_forward flags */
@@ -72,12 +74,16 @@ typedef struct mlg_vit_weights {
  * bf16 pair hi = bf16(x), lo = bf16(x - hi) (x = hi + lo to ~2^-17) and every product as
  * hi*hi + hi*lo + lo*hi with f32 accumulation (three MFMAs).  The GEMM weights must then
  * be packed [out, 2 * in] = [W_hi | W_lo] along the reduction dimension (the patch weight
- * [768, 2 * MLG_VIT_PATCH_K]).  Descriptor error against the fp32 network
+ * [768, 2 * MLG_VIT_PATCH_K]) and mlg_vit_weights.packing set to MLG_VIT_SPLIT; a flag that
+ * disagrees with the packing returns MLG_EINVAL.  Descriptor error against the fp32 network
  * drops from ~1e-5 to ~1e-11 (1 - cos), so kNN rankings follow the fp32 reference's to
  * its own near-tie level. */
 #define MLG_VIT_SPLIT 4
 
-/* Workspace for a batch of `batch` frames at network input size `image_size` (322). */
+/* Workspace for a batch of `batch` frames at network input size `image_size` (322).  The
+ * size always covers the split forward (MLG_VIT_SPLIT): its [hi | lo] operand rows double
+ * the bf16 activation buffers, so a plain-bf16 caller gets ~2x the operand memory it uses
+ * (about 4.4 GB instead of ~2.4 GB at batch 246), in exchange for one size query for both. */
 size_t mlg_vit_workspace_bytes(int batch, int image_size);
 
 /*
@@ -384,6 +390,12 @@ int mlg_dbg_lg_trace_end(int32_t* tags, int32_t* counts, int max_entries);
  * reads LDS or registers it never wrote then shows pattern-dependent results. */
 int mlg_dbg_fill_lds(uint32_t pattern, void* sink, void* stream);
 int mlg_dbg_fill_regs(uint32_t pattern, void* stream);
+/* Diagnostics (tests/test_ransac_gpu.py): while `on`, every mlg_ransac_epipolar call of
+ * this process overwrites the solution count of each hypothesis slot no pair uses (h > 0
+ * of a 5 / 7-point direct pair, h >= the subset count of a RANSAC pair, every slot of a
+ * pair without a model) with `value` after the solvers ran -- a stand-in for a solver that
+ * leaves a slot unwritten; the readers clamp counts to [0, 10], so results must not change. */
+int mlg_dbg_ransac_poison_nsol(int on, int value);
 
 /* --------------------------------------------------------- SuperGlue --
  * The SuperGlue matcher of the reference's SuperGlue class configuration
@@ -467,7 +479,13 @@ typedef struct {
     const uint16_t* merge_wf;  /* merge_feat weight columns 0..127 (window features) [128][128] */
     const uint16_t* merge_wc;  /* merge_feat weight columns 128..255 (coarse context) [128][128] */
     const float* merge_b;
+    /* optional: the coarse layers' block-tail weights in the fused kernel's layout, written
+     * once by mlg_loftr_pack_tails (mlg_loftr_tails_bytes() bytes of device memory); NULL:
+     * mlg_loftr_match repacks them into its workspace on every call */
+    const void* coarse_tails;
 } mlg_loftr_weights;
+size_t mlg_loftr_tails_bytes(void);
+int mlg_loftr_pack_tails(const mlg_loftr_weights* w, void* out, void* stream);
 /* Backbone for B frames uint8 [B, H, W, C] (C = 3 BGR, 4 BGRA or 1 gray; frame_stride
  * bytes), H, W >= 32.  With H8 = H / 8 * 8, W8 = W / 8 * 8 (frames whose H or W is not a
  * multiple of 8 are converted and resized as the reference does: cv2 BGR2GRAY, then

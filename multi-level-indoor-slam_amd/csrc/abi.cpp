@@ -115,7 +115,7 @@ MlgProfScope::~MlgProfScope() {
 
 extern "C" {
 
-int mlg_abi_version(void) { return 1; }
+int mlg_abi_version(void) { return 2; }
 
 const char* mlg_strerror(int status) {
     switch (status) {
@@ -136,7 +136,7 @@ size_t mlg_vit_workspace_bytes(int batch, int image_size) {
 }  // extern "C"
 
 // Preprocess + patch embedding + the 12 blocks; leaves the residual stream in ws->x.
-// split: the MLG_VIT_SPLIT forward (weights packed [W_hi | W_lo | W_hi]).
+// split: the MLG_VIT_SPLIT forward (weights packed [W_hi | W_lo], 2x the reduction dimension).
 static int vit_trunk(const mlg_vit_weights* w, const uint8_t* frames, const VitGeom& g, int H, int W, int C,
                      long frame_stride, int swap_rb, const VitWorkspace& ws, hipStream_t s, int split = 0) {
     const int M = g.B * g.T;
@@ -213,6 +213,8 @@ int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, 
                     long frame_stride, int image_size, int flags, void* workspace, size_t workspace_bytes,
                     float* desc_out, float* local_out, void* stream) {
     if (!w || !frames || !workspace || !desc_out || batch <= 0 || image_size % PATCH) return MLG_EINVAL;
+    // the split forward reads 2x-wide weight rows: plain weights with the flag would be read out of bounds
+    if (w->packing != ((flags & MLG_VIT_SPLIT) ? MLG_VIT_SPLIT : 0)) return MLG_EINVAL;
     const VitGeom g(batch, image_size);
     VitWorkspace ws;
     if (carve(g, (char*)workspace, &ws) > workspace_bytes) return MLG_ENOMEM;
@@ -234,6 +236,7 @@ int mlg_salad_forward(const mlg_vit_weights* w, const mlg_salad_weights* sw, con
                       int H, int W, int C, long frame_stride, int image_size, void* workspace,
                       size_t workspace_bytes, float* desc_out, void* stream) {
     if (!w || !sw || !frames || !workspace || !desc_out || batch <= 0 || image_size % PATCH) return MLG_EINVAL;
+    if (w->packing != 0) return MLG_EINVAL;  // SALAD's trunk runs the plain bf16 forward
     const VitGeom g(batch, image_size);
     VitWorkspace ws;
     if (carve(g, (char*)workspace, &ws) > workspace_bytes) return MLG_ENOMEM;

@@ -75,7 +75,7 @@ int mlg_preprocess_patches(const uint8_t* img, int B, int H, int W, int C, long 
                            int swap_rb, bf16_t* out, hipStream_t s, int split = 0);
 int mlg_cls_rows(float* X, const float* cls, const float* pos, int B, int T, hipStream_t s);
 int mlg_layernorm_bf16(const float* X, const float* g, const float* b, bf16_t* Y, int M, hipStream_t s);
-// split-bf16 forward (MLG_VIT_SPLIT): [hi | lo] operand rows, weights [W_hi | W_lo | W_hi]
+// split-bf16 forward (MLG_VIT_SPLIT): [hi | lo] operand rows, weights [W_hi | W_lo] (2x the reduction dim)
 int mlg_layernorm_split(const float* X, const float* g, const float* b, bf16_t* Y, int M, hipStream_t s);
 int mlg_gemm_qkv_split(const bf16_t* A, const bf16_t* W, const float* bias, bf16_t* Q, bf16_t* K, bf16_t* Vt, int M,
                        int T, int Tpad, size_t lo_off, hipStream_t s);

@@ -1072,18 +1072,28 @@ int transformer(const mlg_loftr_layer* layers, int nl, const LayerBufs& b, int d
     return MLG_OK;
 }
 
-// the coarse layers' tail weights packed for the fused kernel (a few microseconds per call)
-int pack_tails(const mlg_loftr_weights& w, char* base, TailW (&tw)[8], hipStream_t s) {
+constexpr size_t TAILS_BYTES = (size_t)8 * TAIL_ELEMS * 2 + (size_t)8 * 1024 * 4;
+
+// where each coarse layer's packed tail weights live in a TAILS_BYTES buffer
+void tails_at(char* base, TailW (&tw)[8]) {
     bf16_t* p = (bf16_t*)base;
     float* f = (float*)(base + 8 * TAIL_ELEMS * 2);
     for (int l = 0; l < 8; ++l) {
-        const mlg_loftr_layer& lw = w.coarse[l];
         tw[l].wmerge = p;
         tw[l].w1 = p + 256 * 256;
         tw[l].w2 = p + 256 * 256 + 512 * 512;
         tw[l].ln_g = f + l * 1024;
         tw[l].ln_b = f + l * 1024 + 512;
         p += TAIL_ELEMS;
+    }
+}
+
+// the coarse layers' tail weights packed for the fused kernel (24 small launches + 32
+// copies: once per weights via mlg_loftr_pack_tails, or per call into the workspace)
+int pack_tails(const mlg_loftr_weights& w, char* base, TailW (&tw)[8], hipStream_t s) {
+    tails_at(base, tw);
+    for (int l = 0; l < 8; ++l) {
+        const mlg_loftr_layer& lw = w.coarse[l];
         const struct { const uint16_t* src; bf16_t* dst; int n, k; } m[3] = {
             {lw.wmerge, tw[l].wmerge, 256, 256}, {lw.w1, tw[l].w1, 512, 512}, {lw.w2, tw[l].w2, 256, 512}};
         for (const auto& e : m) {
@@ -1160,7 +1170,7 @@ MatchLayout match_layout(int P, int L) {
     M.frm = take((size_t)2 * P * 4);
     M.mp = take((size_t)FINE_CHUNK * 4);
     M.ms = take((size_t)FINE_CHUNK * 4);
-    M.tails = take((size_t)8 * TAIL_ELEMS * 2 + (size_t)8 * 1024 * 4);
+    M.tails = take(TAILS_BYTES);
     M.total = o;
     return M;
 }
@@ -1227,7 +1237,12 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
                        bc.x, bc.cat, (int)crows);
     MLG_LAUNCH_CHECK();
     TailW tails[8];
-    if (MLG_LF_FUSED_TAIL) LF_TRY(pack_tails(w, (char*)at(ML.tails), tails, s));
+    if (MLG_LF_FUSED_TAIL) {
+        if (w.coarse_tails)
+            tails_at((char*)w.coarse_tails, tails);  // packed once (mlg_loftr_pack_tails)
+        else
+            LF_TRY(pack_tails(w, (char*)at(ML.tails), tails, s));
+    }
     LF_TRY(transformer(w.coarse, 8, bc, 256, P, L, s, MLG_LF_FUSED_TAIL ? tails : nullptr));
     // dual softmax + mutual nearest, pair by pair over one [L, L] similarity buffer
     for (int p = 0; p < P; ++p) {
@@ -1287,4 +1302,12 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
     }
     if (hipStreamSynchronize(s) != hipSuccess) return MLG_EHIP;  // pageable uploads complete
     return MLG_OK;
+}
+
+extern "C" size_t mlg_loftr_tails_bytes(void) { return TAILS_BYTES; }
+
+extern "C" int mlg_loftr_pack_tails(const mlg_loftr_weights* w, void* out, void* stream) {
+    if (!w || !out) return MLG_EINVAL;
+    TailW tw[8];
+    return pack_tails(*w, (char*)out, tw, (hipStream_t)stream);
 }

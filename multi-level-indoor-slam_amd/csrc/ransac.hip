@@ -52,6 +52,13 @@ constexpr int MAXSOL = 10;
 constexpr int RS_CHUNK = 1024;  // points per LDS stage in scoring (4 doubles each = 32 KB)
 constexpr int RS_ROUND1 = 256;  // hypotheses of the first round (inlier ratio >= 0.5 stops inside it)
 
+// A hypothesis' solution count as the readers use it, clamped to [0, MAXSOL]: the solver
+// kernels write every slot they own, but a slot left unwritten by a future bug (round 4:
+// 5-point direct pairs) must not index past the pair's MAXSOL models and scores.
+__device__ __forceinline__ int nsol_at(const int8_t* __restrict__ nsol, size_t i) {
+    return min(max((int)nsol[i], 0), MAXSOL);
+}
+
 // ------------------------------------------------------------------ small linear algebra
 
 // Null space of an m x 9 matrix (m = 5 or 7) by Gauss-Jordan elimination with partial
@@ -1226,7 +1233,7 @@ __global__ __launch_bounds__(256) void k_ransac_score(const PairInfo* __restrict
     }
     const bool ess = pi.mode == 1 || pi.mode == 5;
     const double4* src = (ess ? ptsn : ptsr) + pi.start;
-    const int ns = h < H ? nsol[(size_t)p * H + h] : 0;
+    const int ns = h < H ? nsol_at(nsol, (size_t)p * H + h) : 0;
     // waves skip the loads of absent hypotheses but keep the barrier count uniform
     int cnt[MAXSOL];
     for (int s = 0; s < MAXSOL; ++s) cnt[s] = 0;
@@ -1458,7 +1465,7 @@ __global__ __launch_bounds__(256) void k_ransac_probe(const PairInfo* __restrict
         const int ns_it = nsub[p], total = H * MAXSOL;
         int niters = H, max_good = 0;
         for (int it = 0; it < niters && it < ns_it && it < H1; ++it) {
-            const int ns = nsol[(size_t)p * H + it];
+            const int ns = nsol_at(nsol, (size_t)p * H + it);
             for (int s = 0; s < ns; ++s) {
                 const int g = (int)score[(size_t)p * total + it * MAXSOL + s];
                 if (g > max(max_good, mp - 1)) {
@@ -1495,7 +1502,7 @@ __global__ __launch_bounds__(256) void k_ransac_select(const PairInfo* __restric
             const int ns_it = nsub[p];
             int niters = H, max_good = 0, bidx = -1;
             for (int it = 0; it < niters && it < ns_it; ++it) {
-                const int ns = nsol[(size_t)p * H + it];
+                const int ns = nsol_at(nsol, (size_t)p * H + it);
                 for (int s = 0; s < ns; ++s) {
                     const int g = (int)score[(size_t)p * total + it * MAXSOL + s];
                     if (g > max(max_good, mp - 1)) {
@@ -1639,6 +1646,21 @@ __global__ __launch_bounds__(256) void k_recover_pose(const float* __restrict__ 
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// mlg_dbg_ransac_poison_nsol: overwrite the counts of the slots no scan uses
+bool g_poison_nsol = false;
+int g_poison_value = 0;
+
+__global__ __launch_bounds__(64) void k_ransac_poison_nsol(const PairInfo* __restrict__ info, int H,
+                                                           const int32_t* __restrict__ nsub, int8_t* __restrict__ nsol,
+                                                           int h0, int hn, const uint8_t* __restrict__ done, int value) {
+    const int p = blockIdx.y;
+    const int h = h0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= h0 + hn || h >= H || (done && done[p])) return;
+    const int mode = info[p].mode;
+    const bool unused = mode == 0 || ((mode == 4 || mode == 5) && h > 0) || ((mode == 1 || mode == 2) && h >= nsub[p]);
+    if (unused) nsol[(size_t)p * H + h] = (int8_t)value;
+}
+
 struct RsLayout {
     size_t info, ptsn, ptsr, models, nsol, score, subsets, nsub, done, total;
 };
@@ -1698,6 +1720,11 @@ int mlg_ransac_run(const float* kp1, const float* kp2, const int32_t* offs, int 
         hipLaunchKernelGGL(k_ransac_hyp5, dim3((hn + 15) / 16, P), dim3(256), 0, s, info, ptsn, H, subsets, nsub,
                            models, nsol, h0, skip);
         MLG_LAUNCH_CHECK();
+        if (g_poison_nsol) {
+            hipLaunchKernelGGL(k_ransac_poison_nsol, dim3((hn + 63) / 64, P), dim3(64), 0, s, info, H, nsub, nsol, h0,
+                               hn, skip, g_poison_value);
+            MLG_LAUNCH_CHECK();
+        }
         hipLaunchKernelGGL(k_ransac_score, dim3((hn + 255) / 256, P), dim3(256), 0, s, info, ptsn, ptsr, H, models,
                            nsol, score, h0, skip);
         MLG_LAUNCH_CHECK();
@@ -1724,5 +1751,11 @@ int mlg_recover_pose_run(const float* kp1, const float* kp2, const int32_t* offs
     hipLaunchKernelGGL(k_recover_pose, dim3(P), dim3(256), 0, s, kp1, kp2, offs, K, k_stride, E, mask, pose,
                        (int32_t*)nullptr);
     MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}
+
+extern "C" int mlg_dbg_ransac_poison_nsol(int on, int value) {
+    g_poison_nsol = on != 0;
+    g_poison_value = value;
     return MLG_OK;
 }

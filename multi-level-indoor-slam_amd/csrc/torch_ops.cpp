@@ -99,6 +99,7 @@ mlg_vit_weights vit_weights(const std::vector<Tensor>& w, bool split = false) {
     }
     s.norm_w = cp<float>(w[kVitTensors - 2]);
     s.norm_b = cp<float>(w[kVitTensors - 1]);
+    s.packing = split ? MLG_VIT_SPLIT : 0;
     return s;
 }
 
@@ -296,11 +297,13 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> superpoint(const Tensor& fram
 // ------------------------------------------------------------------ LoFTR
 // weights: stem_w, stem_b, conv_w[21], conv_b[21] (empty = none), 8 coarse + 2 fine
 // layers x (w, wmerge, w1, w2, ln1_g, ln1_b, ln2_g, ln2_b), down_w, down_b, merge_wf,
-// merge_wc, merge_b (mlgate/loftr.py builds the list)
+// merge_wc, merge_b (mlgate/loftr.py builds the list), optionally followed by the packed
+// coarse tails (uint8 [mlg_loftr_tails_bytes()], loftr_pack_tails)
 constexpr int kLoftrTensors = 2 + 2 * MLG_LOFTR_NCONV + 10 * 8 + 5;
 
 mlg_loftr_weights loftr_weights(at::TensorList w) {
-    TORCH_CHECK((int)w.size() == kLoftrTensors, "loftr weights: expected ", kLoftrTensors, " tensors, got ", w.size());
+    TORCH_CHECK((int)w.size() == kLoftrTensors || (int)w.size() == kLoftrTensors + 1, "loftr weights: expected ",
+                kLoftrTensors, " (+ 1 packed tails) tensors, got ", w.size());
     mlg_loftr_weights s;
     std::memset(&s, 0, sizeof(s));
     int i = 0;
@@ -324,7 +327,23 @@ mlg_loftr_weights loftr_weights(at::TensorList w) {
     s.merge_wf = cp<uint16_t>(w[i++]);
     s.merge_wc = cp<uint16_t>(w[i++]);
     s.merge_b = cp<float>(w[i++]);
+    if ((int)w.size() > kLoftrTensors) {
+        const Tensor& t = w[i];
+        TORCH_CHECK(t.scalar_type() == at::kByte && (size_t)t.numel() == mlg_loftr_tails_bytes() && t.is_contiguous(),
+                    "loftr packed tails must be uint8 [", mlg_loftr_tails_bytes(), "] (loftr_pack_tails)");
+        s.coarse_tails = t.data_ptr();
+    }
     return s;
+}
+
+// the coarse block-tail weights packed once for the fused kernel (mlg_loftr_pack_tails)
+Tensor loftr_pack_tails(at::TensorList w) {
+    TORCH_CHECK((int)w.size() == kLoftrTensors, "loftr weights: expected ", kLoftrTensors, " tensors");
+    const mlg_loftr_weights s = loftr_weights(w);
+    c10::DeviceGuard g(w[0].device());
+    Tensor out = at::empty({(int64_t)mlg_loftr_tails_bytes()}, w[0].options().dtype(at::kByte));
+    check_rc(mlg_loftr_pack_tails(&s, out.data_ptr(), stream_of(w[0])), "mlg_loftr_pack_tails");
+    return out;
 }
 
 std::tuple<Tensor, Tensor> loftr_features(const Tensor& frames, at::TensorList w) {
@@ -809,6 +828,7 @@ TORCH_LIBRARY(mlgate, m) {
     m.def("recover_pose(Tensor k1, Tensor k2, Tensor offsets, Tensor K, int k_stride, Tensor E, Tensor mask) -> Tensor");
     m.def("resnet50(Tensor frames, Tensor[] weights, int descriptor_dim) -> Tensor");
     m.def("loftr_features(Tensor frames, Tensor[] weights) -> (Tensor, Tensor)");
+    m.def("loftr_pack_tails(Tensor[] weights) -> Tensor");
     m.def("superglue(Tensor kpts, Tensor scores, Tensor desc, Tensor counts, Tensor pair_a, Tensor pair_b, "
           "Tensor[] weights, float bin_score, int W, int H, int iters, float threshold) -> (Tensor, Tensor, Tensor)");
     m.def("loftr_match(Tensor coarse, Tensor fine, Tensor pair_a, Tensor pair_b, Tensor pe, Tensor[] weights, int H, "
@@ -844,6 +864,7 @@ TORCH_LIBRARY_IMPL(mlgate, CUDA, m) {
     m.impl("recover_pose", &recover_pose);
     m.impl("resnet50", &resnet50);
     m.impl("loftr_features", &loftr_features);
+    m.impl("loftr_pack_tails", &loftr_pack_tails);
     m.impl("superglue", &superglue);
     m.impl("loftr_match", &loftr_match);
     m.impl("pillow_resize_224", &pillow_resize_224);

@@ -123,9 +123,13 @@ class LoFTRGPU:
             state_dict, self.weights_source = resolve_loftr_state_dict(seed=seed)
         else:
             self.weights_source = "caller"
-        self.weights = weight_list(state_dict, self.device)
-        self.feature_batch = feature_batch
         self.ops = _native.ops()
+        self.weights = weight_list(state_dict, self.device)
+        # the fused coarse layer tails read their weights k-step packed: pack once here
+        # (mlg_loftr_pack_tails), not on every mlg_loftr_match call
+        self.weights.append(self.ops.loftr_pack_tails(self.weights))
+        self.feature_batch = feature_batch
+        self._pe = {}
 
     def features(self, frames):
         """uint8 [F, H, W, C] device frames -> (coarse [F, H8/8 W8/8, 256], fine [F, H8/2 W8/2, 128])
@@ -140,7 +144,9 @@ class LoFTRGPU:
         [P, L, 2], conf [P, L]); pair p's matches are the first counts[p] rows."""
         pa = torch.as_tensor(np.asarray(pair_a, np.int32))
         pb = torch.as_tensor(np.asarray(pair_b, np.int32))
-        pe = torch.from_numpy(position_encoding(H // 8, W // 8)).to(self.device)
+        pe = self._pe.get((H, W))
+        if pe is None:
+            pe = self._pe[(H, W)] = torch.from_numpy(position_encoding(H // 8, W // 8)).to(self.device)
         return self.ops.loftr_match(coarse, fine, pa, pb, pe, self.weights, int(H), int(W))
 
     def match_frames(self, frames, pairs):

@@ -23,6 +23,18 @@ on CUDA (scaled_dot_product_attention), point pruning while a side has more than
 ``emulate_bf16`` rounds every GEMM input (weights and activations) and the attention
 operands to bfloat16 as the GPU kernels consume them, so GPU-vs-oracle differences
 reduce to summation order.
+
+Precision probes (tools/lg_precision_probe.py) take finer switches:
+  * ``sites``: the subset of SITES whose operands are bf16-rounded (emulate_bf16 = all):
+    'proj' (Wqkv / to_qk / to_v inputs + weights), 'attn' (q, k, v and P), 'out'
+    (out_proj / to_out), 'ffn1' (ffn.0), 'ffn2' (ffn.3), 'asg' (final_proj);
+  * ``attn_fp16``: the reference's own CUDA attention -- cvg/LightGlue's Attention.forward
+    with flash enabled runs ``F.scaled_dot_product_attention`` on ``x.half()`` q, k, v and
+    casts the fp16 output back (the FlashAttention kernel: fp32 scores and softmax, P
+    rounded to fp16 for P.V, fp16 output);
+  * ``dtype``: torch.float64 for an (almost) exact realisation;
+  * ``perm_seed``: every GEMM / attention reduction taken in a seeded permuted order -- a
+    second fp32 realisation with the same operands and different rounding sequence.
 """
 import numpy as np
 import torch
@@ -30,6 +42,16 @@ import torch.nn.functional as F
 
 D, H, L = 256, 4, 9
 HD = D // H
+SITES = ("proj", "attn", "out", "ffn1", "ffn2", "asg")
+_SITE_OF = {"Wqkv": "proj", "to_qk": "proj", "to_v": "proj", "out_proj": "out", "to_out": "out", "ffn.0": "ffn1",
+            "ffn.3": "ffn2", "final_proj": "asg"}
+
+
+def _site(name):
+    for key, site in _SITE_OF.items():
+        if name.endswith(key):
+            return site
+    raise KeyError(name)
 
 
 def conf_threshold(i, n_layers=L):
@@ -53,17 +75,35 @@ def rotate_half(x):
     return torch.stack((-x2, x1), dim=-1).flatten(start_dim=-2)
 
 
+def _h(t):
+    return t.to(torch.float16).to(t.dtype)
+
+
 class Oracle:
-    def __init__(self, sd, emulate_bf16=True, device=None):
+    def __init__(self, sd, emulate_bf16=True, device=None, sites=None, attn_fp16=False, dtype=torch.float32,
+                 perm_seed=None):
         # device: the CPU by default; a bench-scale checker tool may place the fp32
         # restatement on the GPU box's device (same ops, fp32 throughout)
         self.dev = torch.device(device or "cpu")
-        self.sd = {k: torch.as_tensor(np.asarray(v, np.float32)).to(self.dev) for k, v in sd.items()}
-        self.bf = emulate_bf16
+        self.dt = dtype
+        self.sd = {k: torch.as_tensor(np.asarray(v, np.float32)).to(self.dev).to(dtype) for k, v in sd.items()}
+        self.sites = frozenset(SITES if (sites is None and emulate_bf16) else (sites or ()))
+        self.bf = bool(self.sites)
+        self.fp16 = bool(attn_fp16)
+        self.rng = None if perm_seed is None else torch.Generator().manual_seed(int(perm_seed))
+
+    def _perm(self, n):
+        return None if self.rng is None else torch.randperm(n, generator=self.rng).to(self.dev)
+
+    def _mm(self, a, b):
+        """a @ b, the reduction in a permuted order when perm_seed is set."""
+        p = self._perm(a.shape[-1])
+        return a @ b if p is None else a[..., p] @ b[..., p, :]
 
     def lin(self, x, name):
         w, b = self.sd[name + ".weight"], self.sd[name + ".bias"]
-        return _q(x, self.bf) @ _q(w, self.bf).T + b
+        on = _site(name) in self.sites
+        return self._mm(_q(x, on), _q(w, on).T) + b
 
     def ffn(self, x, msg, p):
         h = self.lin(torch.cat([x, msg], -1), p + ".ffn.0")
@@ -72,10 +112,15 @@ class Oracle:
         return x + self.lin(h, p + ".ffn.3")
 
     def attn(self, q, k, v):
-        q, k, v = (_q(t, self.bf) for t in (q, k, v))
-        s = (q @ k.transpose(-1, -2)) / HD ** 0.5
+        on = "attn" in self.sites
+        if self.fp16:  # FlashAttention on x.half(): fp32 scores / softmax, fp16 P and output
+            q, k, v = (_h(t) for t in (q, k, v))
+            s = self._mm(q, k.transpose(-1, -2)) / HD ** 0.5
+            return _h(self._mm(_h(torch.softmax(s, -1)), v))
+        q, k, v = (_q(t, on) for t in (q, k, v))
+        s = self._mm(q, k.transpose(-1, -2)) / HD ** 0.5
         p = torch.softmax(s, -1)
-        return _q(p, self.bf) @ v if self.bf else p @ v
+        return self._mm(_q(p, on), v)
 
     def self_block(self, x, enc, i):
         p = f"transformers.{i}.self_attn"
@@ -113,7 +158,7 @@ class Oracle:
         p = f"log_assignment.{i}"
         m0, m1 = self.lin(x0, p + ".final_proj"), self.lin(x1, p + ".final_proj")
         m0, m1 = m0 / D ** 0.25, m1 / D ** 0.25
-        sim = m0 @ m1.T
+        sim = self._mm(m0, m1.T)
         z0, z1 = self.matchability(x0, i), self.matchability(x1, i)
         cert = F.logsigmoid(z0) + F.logsigmoid(z1).T
         s0 = F.log_softmax(sim, 1)
@@ -149,10 +194,10 @@ class Oracle:
         replaces the early-stop test by "stop after layer s" (to compare matches when a
         bf16 kernel took the other side of an ambiguous decision)."""
         dev = self.dev
-        k0 = normalize_keypoints(torch.as_tensor(kpts0, dtype=torch.float32, device=dev))
-        k1 = normalize_keypoints(torch.as_tensor(kpts1, dtype=torch.float32, device=dev))
-        x0 = torch.as_tensor(desc0, dtype=torch.float32, device=dev).clone()
-        x1 = torch.as_tensor(desc1, dtype=torch.float32, device=dev).clone()
+        k0 = normalize_keypoints(torch.as_tensor(kpts0, device=dev).to(self.dt))
+        k1 = normalize_keypoints(torch.as_tensor(kpts1, device=dev).to(self.dt))
+        x0 = torch.as_tensor(desc0, device=dev).to(self.dt).clone()
+        x1 = torch.as_tensor(desc1, device=dev).to(self.dt).clone()
         m, n = len(x0), len(x1)
         e0, e1 = self.posenc(k0), self.posenc(k1)
         ind0, ind1 = torch.arange(m, device=dev), torch.arange(n, device=dev)

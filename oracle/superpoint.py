@@ -20,6 +20,12 @@ trained model).  Semantics restated:
 Weights come from the caller (the product's seeded generator,
 mlgate.weights.superpoint_state_dict, or a checkpoint).  ``emulate_bf16`` rounds weights and every stored activation to bfloat16 the way the
 GPU kernels store them, so GPU-vs-oracle differences reduce to summation order.
+Precision probes (tools/lg_precision_probe.py) split it: ``sites`` = {'w'} rounds only the
+weights, {'act'} only the stored activations; ``tf32`` rounds every conv's input and
+weights to TF32 (10-bit mantissa, round to nearest) -- what cuDNN does by default on
+Ampere and later NVIDIA GPUs (torch.backends.cudnn.allow_tf32 defaults to True), the
+reference's SuperPoint on CUDA; ``dtype`` float64 gives an (almost) exact realisation;
+``perm_seed`` permutes every conv's input channels (same sums, another rounding order).
 """
 import numpy as np
 import torch
@@ -34,7 +40,14 @@ def bgr_to_gray_u8(img):
 
 
 def _bf16(t):
-    return t.to(torch.bfloat16).to(torch.float32)
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+def _tf32(t):
+    """Round float32 to TF32 (10 explicit mantissa bits), to nearest, ties away from zero."""
+    b = t.to(torch.float32).contiguous().view(torch.int32)
+    b = (b + 0x1000) & ~0x1FFF
+    return b.view(torch.float32).to(t.dtype)
 
 
 def simple_nms(scores, r):
@@ -59,16 +72,26 @@ def sample_descriptors(kp, desc, s=8):
     return F.normalize(d.reshape(b, c, -1), p=2, dim=1)
 
 
-def dense_maps(sd, gray_f, emulate_bf16=True):
+def dense_maps(sd, gray_f, emulate_bf16=True, sites=None, tf32=False, perm_seed=None):
     """gray_f float32 [B, 1, H, W] in [0, 1] -> (scores [B, H, W], descriptor map [B, 256, H/8, W/8]).
     Runs on gray_f's device (the CPU, or the GPU box's device when a tool uses this
-    restatement as a bench-scale checker)."""
-    q = _bf16 if emulate_bf16 else (lambda t: t)
-    sd = {k: torch.as_tensor(np.asarray(v, np.float32)).to(gray_f.device) for k, v in sd.items()}
-    W = {k: (q(v) if k.endswith("weight") and not k.startswith("conv1a") else v) for k, v in sd.items()}
+    restatement as a bench-scale checker) and in gray_f's dtype."""
+    sites = frozenset(("w", "act") if (sites is None and emulate_bf16) else (sites or ()))
+    ident = lambda t: t  # noqa: E731
+    q = _bf16 if "act" in sites else ident
+    qw = _bf16 if "w" in sites else ident
+    sd = {k: torch.as_tensor(np.asarray(v, np.float32)).to(gray_f.device).to(gray_f.dtype) for k, v in sd.items()}
+    W = {k: (qw(v) if k.endswith("weight") and not k.startswith("conv1a") else v) for k, v in sd.items()}
+    rng = None if perm_seed is None else torch.Generator().manual_seed(int(perm_seed))
 
     def conv(x, name, relu=True, pad=1):
-        y = F.conv2d(x, W[f"{name}.weight"], W[f"{name}.bias"], padding=pad)
+        w = W[f"{name}.weight"]
+        if tf32:
+            x, w = _tf32(x), _tf32(w)
+        if rng is not None and x.shape[1] > 1:
+            p = torch.randperm(x.shape[1], generator=rng).to(x.device)
+            x, w = x[:, p], w[:, p]
+        y = F.conv2d(x, w, W[f"{name}.bias"], padding=pad)
         return torch.relu(y) if relu else y
 
     x = q(conv(gray_f, "conv1a"))
@@ -109,13 +132,15 @@ def detect(scores, desc, max_kp=2048, det_thr=0.001, nms_radius=4, border=4):
         if max_kp is not None and max_kp < len(k):
             s, idx = torch.topk(s, max_kp, dim=0, sorted=True)
             k = k[idx]
-        k = torch.flip(k, [1]).float()
+        k = torch.flip(k, [1]).to(desc.dtype)
         d = sample_descriptors(k[None], desc[i:i + 1], 8)[0].T
         out.append({"keypoints": k, "keypoint_scores": s, "descriptors": d})
     return out
 
 
-def superpoint(sd, images_bgr, max_kp=2048, det_thr=0.001, emulate_bf16=True, nms_radius=4, device=None):
+def superpoint(sd, images_bgr, max_kp=2048, det_thr=0.001, emulate_bf16=True, nms_radius=4, device=None, sites=None,
+               tf32=False, dtype=torch.float32, perm_seed=None):
     gray = np.stack([bgr_to_gray_u8(im) for im in images_bgr]).astype(np.float32) / 255.0
-    sc, desc = dense_maps(sd, torch.from_numpy(gray)[:, None].to(device or "cpu"), emulate_bf16)
+    sc, desc = dense_maps(sd, torch.from_numpy(gray)[:, None].to(device or "cpu").to(dtype), emulate_bf16, sites, tf32,
+                          perm_seed)
     return detect(sc, desc, max_kp, det_thr, nms_radius)

@@ -182,7 +182,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, name), name
     assert set(_native.EXPORTS) <= declared
     L = _native.lib()
-    assert L.mlg_abi_version() == 1
+    assert L.mlg_abi_version() == 2
     assert L.mlg_vit_workspace_bytes(64, 322) > 0
     assert L.mlg_vit_workspace_bytes(64, 300) == 0
     assert L.mlg_strerror(-1).decode().startswith("invalid")

@@ -192,3 +192,34 @@ def test_mixed_small_pairs_over_poisoned_workspace(dev):
             assert res_.max() < 1e-9 and sv[2] < 1e-3 and abs(sv[0] - sv[1]) < 1e-2 * sv[0], (res_.max(), sv)
         else:
             assert np.array_equal(r.mask, G.inlier_mask(r.model, k1, k2, K, 3.0))
+
+
+@pytest.mark.parametrize("use_k", [True, False])
+@pytest.mark.parametrize("value", [127, -128])
+def test_poisoned_solution_counts_change_nothing(dev, use_k, value):
+    """the score / probe / select kernels clamp each hypothesis'
+    solution count to [0, MAXSOL].  mlg_dbg_ransac_poison_nsol overwrites the count of
+    every slot no scan uses (h > 0 of a direct pair, h >= the subset count, pairs without
+    a model) with an out-of-range value after the solvers ran, as a solver that left its
+    slot unwritten would; every pair's result must equal the clean run's."""
+    import torch
+    from mlgate import _native
+    rng = np.random.default_rng(23)
+    specs = ([(5, 0), (3, 0), (7, 0), (40, 10), (6, 0), (10, 2), (200, 50), (4, 0), (60, 30), (12, 0)] * 3
+             + [(900, 300)])
+    pairs = [G.synthetic_pair(rng, n_in, n_out, 0.3) for n_in, n_out in specs]
+    k1s, k2s = [p[0] for p in pairs], [p[1] for p in pairs]
+    Kx = K if use_k else None
+    clean = geometry.epipolar_ransac(k1s, k2s, Kx, 3.0, device=str(dev))
+    L = _native.lib()
+    assert L.mlg_dbg_ransac_poison_nsol(1, value) == 0
+    try:
+        dirty = geometry.epipolar_ransac(k1s, k2s, Kx, 3.0, device=str(dev))
+        torch.cuda.synchronize()
+    finally:
+        L.mlg_dbg_ransac_poison_nsol(0, 0)
+    for a, b in zip(clean, dirty):
+        assert a.status == b.status and a.inliers == b.inliers and np.array_equal(a.mask, b.mask)
+        assert (a.model is None) == (b.model is None)
+        if a.model is not None:
+            assert np.array_equal(a.model, b.model)
