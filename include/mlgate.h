@@ -486,6 +486,13 @@ typedef struct {
 } mlg_loftr_weights;
 size_t mlg_loftr_tails_bytes(void);
 int mlg_loftr_pack_tails(const mlg_loftr_weights* w, void* out, void* stream);
+/* Op-level check (tests/test_loftr_gpu.py): one coarse encoder layer (even: self on both
+ * sides; odd: cross, side 0 then side 1) over x f32 [2 nseg L, 256] and cat bf16
+ * [2 nseg L, 512] (cat[:, :256] = bf16(x)), in place; fused != 0 runs the block tail as
+ * the one fused kernel the product uses, 0 as the unfused GEMM + LayerNorm sequence. */
+size_t mlg_op_loftr_coarse_layer_ws_bytes(int nseg, int L);
+int mlg_op_loftr_coarse_layer(const mlg_loftr_weights* w, int layer, int fused, float* x, uint16_t* cat, int nseg,
+                              int L, void* workspace, size_t workspace_bytes, void* stream);
 /* Backbone for B frames uint8 [B, H, W, C] (C = 3 BGR, 4 BGRA or 1 gray; frame_stride
  * bytes), H, W >= 32.  With H8 = H / 8 * 8, W8 = W / 8 * 8 (frames whose H or W is not a
  * multiple of 8 are converted and resized as the reference does: cv2 BGR2GRAY, then

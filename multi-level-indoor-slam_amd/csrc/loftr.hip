@@ -1311,3 +1311,57 @@ extern "C" int mlg_loftr_pack_tails(const mlg_loftr_weights* w, void* out, void*
     TailW tw[8];
     return pack_tails(*w, (char*)out, tw, (hipStream_t)stream);
 }
+
+// ------------------------------------------------ op-level check of one coarse layer
+namespace {
+struct CoarseLayerLayout {
+    size_t qkv, msg, t, h, kv, ks, kvp, tails, total;
+};
+CoarseLayerLayout coarse_layer_layout(int nseg, int L) {
+    CoarseLayerLayout M;
+    size_t o = 0;
+    auto take = [&](size_t b) { const size_t at = o; o += (b + 255) & ~(size_t)255; return at; };
+    const size_t rows = (size_t)2 * nseg * L;
+    M.qkv = take(rows * 768 * 4);
+    M.msg = take(rows * 256 * 2);
+    M.t = take(rows * 256 * 4);
+    M.h = take(rows * 512 * 2);
+    M.kv = take((size_t)2 * nseg * 8 * 32 * 32 * 4);
+    M.ks = take((size_t)2 * nseg * 8 * 32 * 4);
+    M.kvp = take((size_t)2 * nseg * 8 * ((L + LF_KV_CHUNK - 1) / LF_KV_CHUNK) * (32 * 32 + 32) * 4);
+    M.tails = take(TAILS_BYTES);
+    M.total = o;
+    return M;
+}
+}  // namespace
+
+extern "C" size_t mlg_op_loftr_coarse_layer_ws_bytes(int nseg, int L) {
+    return (nseg > 0 && L > 0) ? coarse_layer_layout(nseg, L).total : 0;
+}
+
+// One coarse LoFTREncoderLayer `layer` (even: self on both sides; odd: cross, side 0 then
+// side 1) over x f32 [2 nseg L, 256] / cat bf16 [2 nseg L, 512] (cat[:, :256] = bf16(x)),
+// with the block tail fused (lg_ffn.hip, LoFTR form) or as the unfused GEMM + LayerNorm
+// sequence -- the two arms of the fused-tail parity test (tests/test_loftr_gpu.py).
+extern "C" int mlg_op_loftr_coarse_layer(const mlg_loftr_weights* w, int layer, int fused, float* x, uint16_t* cat,
+                                         int nseg, int L, void* ws, size_t ws_bytes, void* stream) {
+    if (!w || !x || !cat || !ws || layer < 0 || layer >= 8 || nseg <= 0 || L <= 0) return MLG_EINVAL;
+    const CoarseLayerLayout M = coarse_layer_layout(nseg, L);
+    if (ws_bytes < M.total) return MLG_ENOMEM;
+    char* base = (char*)ws;
+    hipStream_t s = (hipStream_t)stream;
+    const LayerBufs b{x, (bf16_t*)cat, (float*)(base + M.qkv), (bf16_t*)(base + M.msg), (float*)(base + M.t),
+                      (bf16_t*)(base + M.h), (float*)(base + M.kv), (float*)(base + M.ks), (float*)(base + M.kvp)};
+    TailW tails[8];
+    if (fused) {
+        if (w->coarse_tails)
+            tails_at((char*)w->coarse_tails, tails);
+        else
+            LF_TRY(pack_tails(*w, base + M.tails, tails, s));
+    }
+    const TailW* tw = fused ? tails + layer : nullptr;
+    const long half = (long)nseg * L;
+    if (layer % 2 == 0) return encoder_layer(w->coarse[layer], b, 256, 0, 0, 2 * nseg, L, s, tw);
+    LF_TRY(encoder_layer(w->coarse[layer], b, 256, 0, half, nseg, L, s, tw));
+    return encoder_layer(w->coarse[layer], b, 256, half, 0, nseg, L, s, tw);
+}

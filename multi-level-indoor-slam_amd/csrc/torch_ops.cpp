@@ -336,6 +336,21 @@ mlg_loftr_weights loftr_weights(at::TensorList w) {
     return s;
 }
 
+// one coarse encoder layer in place, fused or unfused tail (mlg_op_loftr_coarse_layer)
+void loftr_coarse_layer(const Tensor& x, const Tensor& cat, at::TensorList w, int64_t layer, int64_t fused,
+                        int64_t nseg, int64_t L) {
+    want(x, at::kFloat, "x");
+    want(cat, at::kBFloat16, "cat");
+    TORCH_CHECK(x.numel() == 2 * nseg * L * 256 && cat.numel() == 2 * nseg * L * 512,
+                "x must be [2 nseg L, 256], cat [2 nseg L, 512]");
+    const mlg_loftr_weights s = loftr_weights(w);
+    c10::DeviceGuard g(x.device());
+    Tensor ws = workspace(mlg_op_loftr_coarse_layer_ws_bytes((int)nseg, (int)L), x);
+    check_rc(mlg_op_loftr_coarse_layer(&s, (int)layer, (int)fused, mp<float>(x), mp<uint16_t>(cat), (int)nseg, (int)L,
+                                       ws.data_ptr(), (size_t)ws.numel(), stream_of(x)),
+             "mlg_op_loftr_coarse_layer");
+}
+
 // the coarse block-tail weights packed once for the fused kernel (mlg_loftr_pack_tails)
 Tensor loftr_pack_tails(at::TensorList w) {
     TORCH_CHECK((int)w.size() == kLoftrTensors, "loftr weights: expected ", kLoftrTensors, " tensors");
@@ -829,6 +844,7 @@ TORCH_LIBRARY(mlgate, m) {
     m.def("resnet50(Tensor frames, Tensor[] weights, int descriptor_dim) -> Tensor");
     m.def("loftr_features(Tensor frames, Tensor[] weights) -> (Tensor, Tensor)");
     m.def("loftr_pack_tails(Tensor[] weights) -> Tensor");
+    m.def("loftr_coarse_layer(Tensor(a!) x, Tensor(b!) cat, Tensor[] weights, int layer, int fused, int nseg, int L) -> ()");
     m.def("superglue(Tensor kpts, Tensor scores, Tensor desc, Tensor counts, Tensor pair_a, Tensor pair_b, "
           "Tensor[] weights, float bin_score, int W, int H, int iters, float threshold) -> (Tensor, Tensor, Tensor)");
     m.def("loftr_match(Tensor coarse, Tensor fine, Tensor pair_a, Tensor pair_b, Tensor pe, Tensor[] weights, int H, "
@@ -865,6 +881,7 @@ TORCH_LIBRARY_IMPL(mlgate, CUDA, m) {
     m.impl("resnet50", &resnet50);
     m.impl("loftr_features", &loftr_features);
     m.impl("loftr_pack_tails", &loftr_pack_tails);
+    m.impl("loftr_coarse_layer", &loftr_coarse_layer);
     m.impl("superglue", &superglue);
     m.impl("loftr_match", &loftr_match);
     m.impl("pillow_resize_224", &pillow_resize_224);

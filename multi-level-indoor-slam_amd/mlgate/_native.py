@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(_HERE, "libmlgate.so")
 TORCH_LIB_PATH = os.path.join(_HERE, "libmlgate_torch.so")
 OPS = ("vit_forward_into", "salad_forward", "knn_gate", "knn_query", "row_normalize", "similarity", "xcorr_score", "xcorr_batch",
        "superpoint",
-       "lightglue", "ransac_epipolar", "recover_pose", "resnet50", "loftr_features", "loftr_pack_tails", "loftr_match", "superglue", "pillow_resize_224", "plane_ransac", "proximity",
+       "lightglue", "ransac_epipolar", "recover_pose", "resnet50", "loftr_features", "loftr_pack_tails", "loftr_coarse_layer", "loftr_match", "superglue", "pillow_resize_224", "plane_ransac", "proximity",
        "prof_enable", "prof_reset", "prof_read")
 
 
@@ -102,6 +102,9 @@ EXPORTS = {
     "mlg_dbg_ransac_poison_nsol": (c_int, [c_int, c_int]),
     "mlg_loftr_tails_bytes": (c_size_t, []),
     "mlg_loftr_pack_tails": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "mlg_op_loftr_coarse_layer_ws_bytes": (c_size_t, [c_int, c_int]),
+    "mlg_op_loftr_coarse_layer": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_size_t,
+                                          c_void_p]),
     "mlg_png_info": (c_int, [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mlg_png_decode_bgr": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_png_load_bgr": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),

@@ -191,6 +191,7 @@ class DeviceGate:
         # gate's |floor_i - floor_j| > limit (loop_closure_gate.py:91-98; NaN never rejects)
         lab = list(self.labels.tolist()) if self.labels.dtype != object else list(self.labels)
         codes, has = floor_codes(lab)
+        self.h_codes, self.h_has = np.asarray(codes), np.asarray(has, np.uint8)
         self.f_all = torch.as_tensor(codes, device=self.dev)
         self.hf_all = torch.as_tensor(has, dtype=torch.uint8, device=self.dev)
         num = np.array([np.nan if v is None else float(v) for v in lab], np.float64)
@@ -234,6 +235,10 @@ class DeviceGate:
         # record=True: step() keeps every verified ordered pair's (a, b, matches, inliers,
         # is_valid) in self.last_pair_results (host arrays in verification order)
         self.record = record
+        # time_verify=True: _verify_loftr brackets its work with device syncs and leaves the
+        # wall time in last_verify_s (bench.py's LoFTR sub-run); off, the gate never syncs for it
+        self.time_verify = False
+        self.last_verify_s = None
         self.last_pair_results = None
         self.last_retrieval = None
 
@@ -263,15 +268,18 @@ class DeviceGate:
         idx, sim, valid, count = retrieval.knn_gate(self.gather.out, self.t_all, self.f_all, self.hf_all, self.gap,
                                                     self.thr, self.k, self.retrieval_floor_gating, q0=self.lo,
                                                     Q=self.n_local, totals=self.totals)
+        # the retrieval lists come to the host once (Q x k entries): the pair list that
+        # drives the verifier's chunks is built there, with no further device syncs
+        h_idx, h_valid, h_count = (x.cpu().numpy() for x in (idx, valid, count))
         if self.record:  # this rank's query rows: idx / sim / valid [Q, k], count [Q] (host)
-            self.last_retrieval = tuple(x.cpu().numpy() for x in (idx, sim, valid, count))
+            self.last_retrieval = (h_idx, sim.cpu().numpy(), h_valid, h_count)
         k = idx.shape[1]
-        live = torch.arange(k, device=self.dev)[None, :] < count[:, None].long()
-        out = {"matches": int(count.sum()), "retrieval_floor_rejected": 0, "skipped_floor_mismatch": 0,
+        live = np.arange(k)[None, :] < h_count[:, None]
+        out = {"matches": int(h_count.sum()), "retrieval_floor_rejected": 0, "skipped_floor_mismatch": 0,
                "verifier_invalid": 0, "gate_rejected_cross_floor": 0, "pairs_verified": 0, "verified_valid": 0,
                "accepted": 0}
         # PlaceMatch.is_valid == False: emitted but floor-rejected
-        out["retrieval_floor_rejected"] = int((live & (valid == 0)).sum())
+        out["retrieval_floor_rejected"] = int((live & (h_valid == 0)).sum())
         if not self.verify:
             return out
         # SuperPoint once per keyframe (the reference re-extracts per pair), cached in HBM
@@ -282,23 +290,33 @@ class DeviceGate:
             self.ds_loc[b0:b1].copy_(ds.view(b1 - b0, -1))
             self.cnt_loc[b0:b1, 0].copy_(cnt)
         # matches handed to verify_with_semantics (is_valid ones), skip rule on floors
-        qs, js = torch.nonzero(live & (valid != 0), as_tuple=True)
-        pa_t, pb_t = (qs + self.lo).to(torch.int32), idx[qs, js].to(torch.int32)
+        qs, js = np.nonzero(live & (h_valid != 0))
+        pa_h, pb_h = (qs + self.lo).astype(np.int32), h_idx[qs, js].astype(np.int32)
         if self.verifier_floor_gating:
             # verify_with_semantics skips when floor1 != floor2 in Python
             # (geometric_verification.py:709-710): None == None only, NaN != NaN
-            ha, hb = self.hf_all[pa_t.long()] != 0, self.hf_all[pb_t.long()] != 0
-            same = (ha & hb & (self.f_all[pa_t.long()] == self.f_all[pb_t.long()])) | (~ha & ~hb)
+            ha, hb = self.h_has[pa_h] != 0, self.h_has[pb_h] != 0
+            same = (ha & hb & (self.h_codes[pa_h] == self.h_codes[pb_h])) | (~ha & ~hb)
             out["skipped_floor_mismatch"] = int((~same).sum())
-            pa_t, pb_t = pa_t[same], pb_t[same]
+            pa_h, pb_h = pa_h[same], pb_h[same]
+        pa_t, pb_t = torch.from_numpy(pa_h).to(self.dev), torch.from_numpy(pb_h).to(self.dev)
         if self.matcher == 'loftr':
             return self._verify_loftr(pa_t, pb_t, out)
         # pair-level load balance across ranks: the pairs are re-balanced first (the union
         # of the slices is the global pair list), then FeatureExchange delivers each rank
         # exactly the SuperPoint features its own slice touches
         dedup = self._dedup()
-        pa_t, pb_t = self.mdist.balanced_pairs(pa_t, pb_t, self.world, self.rank, group_reverse=dedup)
-        pa, pb = pa_t.cpu().numpy(), pb_t.cpu().numpy()
+        if self.world > 1:
+            pa_t, pb_t = self.mdist.balanced_pairs(pa_t, pb_t, self.world, self.rank, group_reverse=dedup)
+            pa, pb = pa_t.cpu().numpy(), pb_t.cpu().numpy()
+        else:
+            pa, pb = pa_h, pb_h
+        return self._verify_lightglue(pa, pb, dedup, out)
+
+    def _verify_lightglue(self, pa, pb, dedup, out):
+        """SuperPoint features (local table or need-driven exchange) -> LightGlue (once per
+        unordered pair when dedup) -> RANSAC + decision + floor gate per ordered pair, for
+        this rank's slice (pa, pb) of the pair list (host int32 arrays); fills `out`."""
         self.last_pairs = (pa, pb)
         # features of the keyframes the pairs touch: the local table (world 1), or the
         # need-driven exchange (row k of the compact tables = keyframe need[k])
@@ -386,19 +404,29 @@ class DeviceGate:
                 side.wait_event(ready)
                 m.record_stream(side)
                 n.record_stream(side)
-                # matched keypoints -> one batched RANSAC (+ recoverPose when K is given)
+                # matched keypoints -> one batched RANSAC (+ recoverPose when K is given).
+                # The flat match arrays are laid out on the device without a host sync (no
+                # nonzero): pair p's matches go to [offs[p], offs[p] + n[p]) of a buffer of
+                # P * kmax rows (RANSAC reads each pair's own range only), the padding of
+                # the match lists to one dummy row past the end.
                 P = len(ca)
-                lv = torch.arange(self.kp, device=self.dev)[None, :] < n[:, None]
-                pi, si = torch.nonzero(lv, as_tuple=True)
+                KP = self.kp
+                sidx = torch.arange(KP, device=self.dev)
+                lv = sidx[None, :] < n[:, None]
                 ta = torch.from_numpy(ca).to(self.dev).long()  # global keyframe indices
                 tb = torch.from_numpy(cb).to(self.dev).long()
                 la = torch.from_numpy(local(ca)).to(self.dev).long()  # feature-table rows
                 lb = torch.from_numpy(local(cb)).to(self.dev).long()
-                k1 = kp_all[la[pi], m[pi, si, 0].long()].contiguous()
-                k2 = kp_all[lb[pi], m[pi, si, 1].long()].contiguous()
                 offs = torch.zeros(P + 1, dtype=torch.int32, device=self.dev)
                 offs[1:] = torch.cumsum(n, 0)
-                _, _, inl, _, _ = geometry.epipolar_ransac_device(k1, k2, offs, self.K, 0, 3.0)
+                dest = torch.where(lv, offs[:-1, None].long() + sidx[None, :], P * KP).view(-1)
+                m0 = torch.where(lv, m[:, :, 0].long(), 0)
+                m1 = torch.where(lv, m[:, :, 1].long(), 0)
+                k1 = kp_all.new_zeros(P * KP + 1, 2)
+                k2 = kp_all.new_zeros(P * KP + 1, 2)
+                k1.index_copy_(0, dest, kp_all[la[:, None], m0].view(-1, 2))
+                k2.index_copy_(0, dest, kp_all[lb[:, None], m1].view(-1, 2))
+                _, _, inl, _, _ = geometry.epipolar_ransac_device(k1[:P * KP], k2[:P * KP], offs, self.K, 0, 3.0)
                 ratio = inl.double() / n.clamp(min=1).double()
                 ok = (n >= 5) & (inl >= self.min_inliers) & (ratio >= self.min_inlier_ratio)
                 n_valid_t += ok.sum()
@@ -426,7 +454,8 @@ class DeviceGate:
         torch = self.torch
         from . import geometry
         import time
-        torch.cuda.synchronize(self.dev)
+        if self.time_verify:
+            torch.cuda.synchronize(self.dev)
         t_start = time.perf_counter()
         if self.max_pairs is not None:
             pa_t, pb_t = self._first_pairs(pa_t, pb_t, self.max_pairs)
@@ -490,8 +519,9 @@ class DeviceGate:
             gate_rej_t += (ok & ((self.f_num[ta] - self.f_num[tb]).abs() > self.limit)).sum()
             if rec is not None:
                 rec.append((sel, n, inl, ok))
-        n_valid, gate_rej = int(n_valid_t), int(gate_rej_t)
-        self.last_verify_s = time.perf_counter() - t_start  # this rank's LoFTR verification wall time
+        n_valid, gate_rej = int(n_valid_t), int(gate_rej_t)  # (a device sync)
+        if self.time_verify:
+            self.last_verify_s = time.perf_counter() - t_start  # this rank's LoFTR verification wall time
         if rec is not None:
             r = {"a": pa, "b": pb, "matches": np.zeros(len(pa), np.int32), "inliers": np.zeros(len(pa), np.int32),
                  "is_valid": np.zeros(len(pa), bool)}

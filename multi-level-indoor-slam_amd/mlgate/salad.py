@@ -52,7 +52,7 @@ class SaladGPU:
             self.weights_source = "given"
         backbone = {k[len("backbone.model."):]: v for k, v in state_dict.items() if k.startswith("backbone.model.")}
         self._vit = VitB14(backbone, device=device, image_size=IMAGE_SIZE, max_batch=max_batch, pool="gem",
-                           swap_rb=False)
+                           swap_rb=False, precise=False)  # mlg_salad_forward runs the plain bf16 trunk
         self.device = self._vit.device
         self.max_batch = max_batch
         agg, self.dust_bin = pack_aggregator(state_dict)

@@ -55,10 +55,12 @@ class VitB14:
     GEMM and attention operand carried as a hi + lo bf16 pair, three MFMA products each.
     Descriptors then agree with the fp32 network to ~1e-11 (1 - cos) instead of ~1e-5, and
     kNN rankings over near-identical descriptors follow the fp32 reference's
-    (tests/test_bench_parity_gpu.py)."""
+    (tests/test_bench_parity_gpu.py).  It is the default everywhere the descriptors feed
+    retrieval (DeviceGate, the CricaVPR / AnyLoc drop-ins); precise=False keeps the plain
+    bf16 forward (3x fewer MFMA products; SALAD's trunk, A/B tools)."""
 
     def __init__(self, state_dict, device="cuda", image_size=322, max_batch=64, pool="gem", swap_rb=True,
-                 precise=False):
+                 precise=True):
         self.device = _native.require_device(device)
         if image_size % PATCH:
             raise ValueError("image_size must be a multiple of 14")

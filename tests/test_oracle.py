@@ -119,3 +119,17 @@ def test_oracle_resize_identity_and_ramps():
     const = np.full((480, 640, 3), 173, np.uint8)
     assert np.all(_lib.resize_linear_u8(const, 322, 322) == 173)
     assert _lib.lib().orc_resize_vec_end(966) == 960
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "knn_*.npz")))[:4], ids=os.path.basename)
+def test_oracle_python_loop_restatement(path):
+    """retrieval.find_loop_closures_loop (the reference's per-row Python loop, timed as the
+    reference CPU path by bench.py's cpu_baseline) equals the reference's golden output."""
+    g = dict(np.load(path, allow_pickle=False))
+    k, thr, gap, gating = g["params"]
+    labels = [int(f) if h else None for f, h in zip(g["floor"], g["has_floor"])]
+    out = retrieval.find_loop_closures_loop(g["desc"].astype(np.float32), g["t"], labels, gap, thr, int(k),
+                                            bool(gating))
+    assert [o[0] for o in out] == g["q"].tolist() and [o[1] for o in out] == g["m"].tolist()
+    assert [o[3] for o in out] == g["valid"].astype(bool).tolist()
+    assert np.array_equal(np.array([o[2] for o in out]), g["sim"])

@@ -37,7 +37,7 @@ def frames():
 def test_descriptor_cosine(dev, sd, frames):
     from oracle import vit as ovit
     torch.set_num_threads(8)
-    eng = VitB14(sd, device="cuda", max_batch=4)
+    eng = VitB14(sd, device="cuda", max_batch=4, precise=False)
     desc, local = eng.forward(torch.from_numpy(frames).to(dev), with_local=True)
     torch.cuda.synchronize()
     desc, local = desc.cpu(), local.cpu()
@@ -55,8 +55,8 @@ def test_descriptor_cosine(dev, sd, frames):
 
 def test_batch_split_consistent(dev, sd, frames):
     """Descriptors do not depend on how frames are batched (max_batch split)."""
-    eng2 = VitB14(sd, device="cuda", max_batch=2)
-    eng4 = VitB14(sd, device="cuda", max_batch=4)
+    eng2 = VitB14(sd, device="cuda", max_batch=2, precise=False)
+    eng4 = VitB14(sd, device="cuda", max_batch=4, precise=False)
     x = torch.from_numpy(frames).to(dev)
     d2, d4 = eng2.forward(x), eng4.forward(x)
     torch.cuda.synchronize()
@@ -66,7 +66,7 @@ def test_batch_split_consistent(dev, sd, frames):
 def test_gray_and_bgra_inputs(dev, sd, frames):
     from oracle import vit as ovit
     osd = {k: torch.from_numpy(v) for k, v in sd.items()}
-    eng = VitB14(sd, device="cuda", max_batch=2)
+    eng = VitB14(sd, device="cuda", max_batch=2, precise=False)
     gray = frames[:1, :, :, 1].copy()
     bgra = np.concatenate([frames[:1], np.full(frames[:1].shape[:3] + (1,), 255, np.uint8)], axis=-1)
     for f in (gray, bgra):

@@ -158,6 +158,14 @@ def ransac(feats, ia, ib, matches, dev):
     return inl.cpu().numpy().astype(np.int64)
 
 
+def _c_twin(job):
+    """(i, k1, k2) -> (i, inliers) with oracle/csrc/ransac_cv.c (pool worker)."""
+    from oracle import _lib
+    from oracle import geometry as ogeo
+    i, k1, k2 = job
+    return i, (_lib.essential_ransac(k1, k2, ogeo.ISEC_K, 3.0)[2] if len(k1) >= 5 else 0)
+
+
 def decide(n, inl):
     return (n >= 5) & (inl >= 20) & (inl / np.maximum(n, 1) >= 0.25)
 
@@ -198,7 +206,15 @@ def main():
     ap.add_argument("--pairs", type=int, default=2000)
     ap.add_argument("--chains", default="", help="comma list of sp/lg to run instead of the set")
     ap.add_argument("--out", default="gpurun_out")
+    ap.add_argument("--c-twin", default="", help="comma list of chains whose lists also go through the C twin "
+                                                   "of findEssentialMat (oracle/csrc/ransac_cv.c) on a host pool")
+    ap.add_argument("--save-xy", default="", help="comma list of chains whose match coordinates are saved")
+    ap.add_argument("--workers", type=int, default=16)
     a = ap.parse_args()
+    pool = None
+    if a.c_twin:
+        import multiprocessing as mp
+        pool = mp.get_context("fork").Pool(a.workers)  # forked before the process touches the GPU
     torch.backends.cuda.matmul.allow_tf32 = False
     torch.backends.cudnn.allow_tf32 = False
     dev = torch.device("cuda:0")
@@ -270,10 +286,29 @@ def main():
         r = compare("hip/hip vs tf32/fp16attn", res["tf32/fp16attn"], res["hip/hip"], n_near)
         log(**r)
         rows.append(r)
+    xy_out = {}
+    for key in [c for c in a.save_xy.split(",") if c in res]:
+        xy = res[key]["xy"]
+        xy_out[f"{key}|xy"] = np.concatenate(xy).astype(np.float32)
+        xy_out[f"{key}|offs"] = np.concatenate([[0], np.cumsum([len(x) for x in xy])]).astype(np.int64)
+    for key in [c for c in a.c_twin.split(",") if c in res]:
+        # the same lists through the C twin: GPU RANSAC == OpenCV's loop restated, pair by pair
+        jobs = [pool.apply_async(_c_twin, ((i, x[:, :2], x[:, 2:]),)) for i, x in enumerate(res[key]["xy"])]
+        inl_c = np.zeros(len(jobs), np.int64)
+        for j in jobs:
+            i, g = j.get()
+            inl_c[i] = g
+        eq = inl_c == res[key]["inl"]
+        r = {"chain": f"{key}: GPU RANSAC vs C twin on the same lists", "inliers_equal": float(eq.mean()),
+             "differ": [(int(i), int(res[key]["inl"][i]), int(inl_c[i]), int(res[key]["n"][i]))
+                        for i in np.flatnonzero(~eq)[:20]]}
+        log(**r)
+        rows.append(r)
+        xy_out[f"{key}|inl_c"] = inl_c
     os.makedirs(a.out, exist_ok=True)
     np.savez_compressed(os.path.join(a.out, f"lgp_{a.set}.npz"), a=pa, b=pb, near=n_near,
                         **{f"{k}|{f}": v[f] for k, v in res.items() for f in ("n", "inl", "ok")},
-                        report=json.dumps(rows))
+                        report=json.dumps(rows), **xy_out)
     log(phase="done", s=round(time.time() - t0, 1))
 
 
