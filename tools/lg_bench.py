@@ -9,6 +9,7 @@ with achieved TFLOP/s (TB/s for the HBM-bound FFN), and a histogram of the layer
 """
 import argparse
 import ctypes
+import hashlib
 import json
 import os
 import sys
@@ -59,7 +60,10 @@ def main():
     L.mlg_prof_enable(0)
     res = {"pairs": args.pairs, "mean_keypoints": float(counts.mean()), "no_prune": args.no_prune,
            "ms_per_call": round(e0.elapsed_time(e1) / args.iters, 2),
-           "stop_hist": np.bincount(stop, minlength=10).tolist(), "matches_mean": float(n.float().mean())}
+           "stop_hist": np.bincount(stop, minlength=10).tolist(), "matches_mean": float(n.float().mean()),
+           # bit-identity check across builds: a digest of every pair's matches and scores
+           "digest": hashlib.sha1(m.cpu().numpy().tobytes() + s.cpu().numpy().tobytes()
+                                  + n.cpu().numpy().tobytes()).hexdigest()[:16]}
     for slot, name in ((5, "attention"), (6, "qkv_proj"), (8, "ffn_fused")):
         ms, cnt_, work = ctypes.c_double(), ctypes.c_long(), ctypes.c_double()
         L.mlg_prof_read(slot, ctypes.byref(ms), ctypes.byref(cnt_))
