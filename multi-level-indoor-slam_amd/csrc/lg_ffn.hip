@@ -33,7 +33,6 @@
 #include <stdlib.h>
 
 #include <algorithm>
-#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -118,9 +117,6 @@ __device__ __forceinline__ float logsigmoid_f(float x) { return fminf(x, 0.f) - 
 // fragments are read one k-step ahead into the other half of a double buffer.  Loads
 // past the last step re-read the last step (no branches, so the waitcnt pass counts
 // the in-flight loads exactly); addresses are recomputed per call, not hoisted.
-// The accumulators need no zeroing: k-step 0 (peeled) issues its MFMAs with the inline
-// constant 0 as C (acc = W . T + 0, the same bits as a zeroed accumulator), which saves
-// the 16 v_mov_b32 per accumulator tile a zero fill costs (192 per tile and wave).
 template <int NT, int MT, int RING = 4>
 __device__ __forceinline__ void gemm_phase(const bf16_t* __restrict__ W, int N, int n0, int nkb, int chunk0,
                                            const char* lds, f32x16 (&acc)[NT][MT]) {
@@ -140,8 +136,8 @@ __device__ __forceinline__ void gemm_phase(const bf16_t* __restrict__ W, int N, 
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
         xa[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + (((chunk0 + hh) ^ sw) << 4));
-    const f32x16 zero16 = {};
-    auto block = [&](int kb, auto first) {
+#pragma unroll 1
+    for (int kb = 0; kb < 4 * nkb / RING; ++kb) {
 #pragma unroll
         for (int s = 0; s < RING; ++s) {
             const int ks = RING * kb + s;
@@ -154,20 +150,14 @@ __device__ __forceinline__ void gemm_phase(const bf16_t* __restrict__ W, int N, 
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
                 for (int t = 0; t < NT; ++t)
-                    acc[t][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[t][s], cur[mt],
-                                                                         (decltype(first)::value && s == 0) ? zero16
-                                                                                                            : acc[t][mt],
-                                                                         0, 0, 0);
+                    acc[t][mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[t][s], cur[mt], acc[t][mt], 0, 0, 0);
 #pragma unroll
             for (int t = 0; t < NT; ++t) wf[t][s] = ld16(wrow[t] + min(ks + RING, last) * step);
             // pin the refill here: left alone, the scheduler sinks it next to its use
             // (minimising live ranges) and every step waits on a fresh L2 round trip
             __builtin_amdgcn_sched_barrier(0);
         }
-    };
-    block(0, std::true_type{});
-#pragma unroll 1
-    for (int kb = 1; kb < 4 * nkb / RING; ++kb) block(kb, std::false_type{});
+    }
 }
 
 template <int NT, int MT>
@@ -262,6 +252,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
         // 1. msg = ctx . Wout^T + bout  -> bf16 over the ctx half
         {
             f32x16 acc[NT1][MT];
+            zero(acc);
             gemm_phase<NT1, MT, RING1>(w.Wout, 256, 32 * NT1 * wave, 4, 32, lds, acc);
             __syncthreads();  // every wave has read the ctx half
             float mean1[MT], rstd1[MT];
@@ -338,6 +329,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
         // 2. h = [x | msg] . W1^T + b1; LayerNorm; GELU -> bf16 over [x | msg]
         {
             f32x16 acc[NT2][MT];
+            zero(acc);
             gemm_phase<NT2, MT, RING>(w.Wf1, 512, 32 * NT2 * wave, 8, 0, lds, acc);
     #pragma unroll
             for (int t = 0; t < NT2; ++t)
@@ -448,6 +440,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                 xr[i] = stream_ld(reinterpret_cast<const float4*>(X + (size_t)min(m0 + wave * (R / NW) + i, M - 1) * 256) + lane);
             __builtin_amdgcn_sched_barrier(0);
             f32x16 acc[NT1][MT];
+            zero(acc);
             gemm_phase<NT1, MT, RING1>(w.Wf2, 256, 32 * NT1 * wave, 8, 0, lds, acc);
 #if MLG_FFN_XR_WAIT
             __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): the residual rows xr have landed

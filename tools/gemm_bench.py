@@ -94,7 +94,7 @@ def main():
         print(json.dumps(row), flush=True)
         del A, W, C
 
-    eng = VitB14(synthetic_state_dict(0), device=dev, max_batch=args.batch)
+    eng = VitB14(synthetic_state_dict(0), device=dev, max_batch=args.batch, precise=False)
     frames = torch.randint(0, 256, (args.batch, 480, 640, 3), dtype=torch.uint8, device=dev)
     desc = {}
     for v in (int(x) for x in args.variants.split(",")):

@@ -102,6 +102,25 @@ __device__ __forceinline__ int p_ffn_y_read(const Lane& l, int it) {  // residua
     return r * 1024 + ((l.lane ^ (r & 15)) << 4);
 }
 
+// write-rule calibration (b64): which lane groups share a cycle, what conflicts
+__device__ __forceinline__ int p_w_swap8(const Lane& l, int) { return (l.lane * 8) ^ 8; }
+__device__ __forceinline__ int p_w_stride16(const Lane& l, int) { return l.lane * 16; }
+__device__ __forceinline__ int p_w_gap64(const Lane& l, int) { return l.lane * 8 + (l.lane >> 3) * 64; }
+__device__ __forceinline__ int p_w_swap16(const Lane& l, int) { return (l.lane * 8) ^ (((l.lane >> 3) & 1) * 16); }
+__device__ __forceinline__ int p_w_it(const Lane& l, int it) { return l.lane * 8 + (it & 1) * 512; }
+__device__ __forceinline__ int p_w_rev(const Lane& l, int) { return (63 - l.lane) * 8; }
+__device__ __forceinline__ int p_w_half(const Lane& l, int) { return (l.lane & 31) * 8 + (l.lane >> 5) * 4096; }
+__device__ __forceinline__ int p_w_rows(const Lane& l, int) {  // 8 lanes per 128-B row, rows 128 B apart, in order
+    return (l.lane >> 3) * 128 + (l.lane & 7) * 16;
+}
+__device__ __forceinline__ int p_w_rows8(const Lane& l, int) {  // 16 lanes per 128-B row (contiguous)
+    return (l.lane >> 4) * 128 + (l.lane & 15) * 8;
+}
+__device__ __forceinline__ int p_w_xor(const Lane& l, int) {  // contiguous 8-B granules, XOR-permuted per 128 B
+    const int row = l.lane >> 4, g = l.lane & 15;
+    return row * 128 + ((g ^ (row & 15)) << 3);
+}
+
 template <int PAT>
 __device__ __forceinline__ int addr_of(const Lane& l, int it) {
     switch (PAT) {
@@ -124,6 +143,16 @@ __device__ __forceinline__ int addr_of(const Lane& l, int it) {
         case 16: return p_ffn_cat_write(l, it);
         case 17: return p_ffn_y_write(l, it);
         case 18: return p_ffn_y_read(l, it);
+        case 19: return p_w_swap8(l, it);
+        case 20: return p_w_stride16(l, it);
+        case 21: return p_w_gap64(l, it);
+        case 22: return p_w_swap16(l, it);
+        case 23: return p_w_it(l, it);
+        case 24: return p_w_rev(l, it);
+        case 25: return p_w_half(l, it);
+        case 26: return p_w_rows(l, it);
+        case 27: return p_w_rows8(l, it);
+        case 28: return p_w_xor(l, it);
     }
     return 0;
 }
@@ -200,6 +229,20 @@ int main() {
     run<18, R16>("ffn_y_read", sink);
     run<0, W16>("contig_w128", sink);
     run<1, W8>("contig_w64", sink);
+    run<19, W8>("w_swap8", sink);
+    run<20, W8>("w_stride16", sink);
+    run<21, W8>("w_gap64", sink);
+    run<22, W8>("w_swap16", sink);
+    run<23, W8>("w_it", sink);
+    run<24, W8>("w_rev", sink);
+    run<25, W8>("w_half", sink);
+    run<26, W8>("w_rows(8/row,16B)", sink);
+    run<27, W8>("w_rows8", sink);
+    run<28, W8>("w_xor", sink);
+    run<8, R8>("attn_v_write_as_read", sink);
+    run<12, R8>("proj_stage_qk_as_read", sink);
+    run<20, R8>("r_stride16", sink);
+    run<1, W16>("contig8_as_w128", sink);
     (void)hipFree(sink);
     return 0;
 }

@@ -20,7 +20,7 @@ res = {}
 
 
 def run(batch, x=fr, stream=None):
-    eng = VitB14(sd, device="cuda", max_batch=batch)
+    eng = VitB14(sd, device="cuda", max_batch=batch, precise=False)
     if stream is None:
         d = eng.forward(x)
     else:
