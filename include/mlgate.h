@@ -229,7 +229,11 @@ int mlg_op_lg_ffn(const uint16_t* ctx, float* X, uint16_t* xcopy, int ldc, int M
                   const float* bout, const uint16_t* Wf1, const float* bf1, const float* ln_g, const float* ln_b,
                   const uint16_t* Wf2, const float* bf2, void* stream);
 /* LightGlue block projections (lg_proj.hip): self_block != 0: q, k, v = Wqkv x + b with
- * rotary (ecos / esin f32 [Npad][32]) on q and k; else qk = to_qk x, v = to_v x.  xcopy
+ * rotary on q and k; else qk = to_qk x, v = to_v x.  The rotary factors come interleaved in
+ * `ecos`, f32 [Npad / 64][16][64][4]: for token row r and frequency pair p the four floats
+ * (cos 2p, cos 2p + 1, sin 2p, sin 2p + 1) at ((r / 64) * 16 + p) * 64 + r % 64 (round 5:
+ * one conflict-free 16-B LDS read per lane; mlgate.lightglue.pack_rotary); `esin` is
+ * unused (NULL).  xcopy
  * bf16 [Npad][ldx] (cols 0..255), W k-step-major [16][768 | 512][16] with rows
  * [q|k|v] x (head, 64) (self) or [qk | v]; outputs Q, K bf16 [4][Npad][64], Vt bf16
  * [4][Npad/64][64][64]; rows with live[m] == 0 written as zeros.  Npad % 64 == 0. */

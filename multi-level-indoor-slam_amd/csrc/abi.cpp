@@ -535,7 +535,8 @@ int mlg_op_lg_ffn(const uint16_t* ctx, float* X, uint16_t* xcopy, int ldc, int M
 int mlg_op_lg_proj(int self_block, const uint16_t* xcopy, int ldx, const uint16_t* W, const float* bias,
                    const float* ecos, const float* esin, const uint8_t* live, uint16_t* Q, uint16_t* K, uint16_t* Vt,
                    int Npad, void* stream) {
-    return mlg_lg_proj(self_block != 0, xcopy, ldx, W, bias, ecos, esin, live, Q, K, Vt, Npad, (hipStream_t)stream);
+    (void)esin;  // the factors come interleaved in `ecos` (lg_fac4 layout, include/mlgate.h)
+    return mlg_lg_proj(self_block != 0, xcopy, ldx, W, bias, ecos, live, Q, K, Vt, Npad, (hipStream_t)stream);
 }
 int mlg_op_conv2d_nhwc(const uint16_t* in, const uint16_t* zero16, int B, int H, int W, int C, int k, int s,
                        const uint16_t* Wt, const float* bias, float* out, int N, void* stream) {

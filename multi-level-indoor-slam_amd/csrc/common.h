@@ -58,6 +58,15 @@ __device__ __forceinline__ float wave_max(float v) {
 
 static inline int ceil_div(long a, long b) { return (int)((a + b - 1) / b); }
 
+// LightGlue rotary factors, one float4 per (token row r, frequency pair p):
+// (cos f, cos f + 1, sin f, sin f + 1), f = 2 p, laid out per 64-row tile as
+// [Npad / 64][16 pairs][64 rows] -- a tile's factors are one contiguous 16 KiB block (one
+// LDS-DMA stream), and the 32 rows a projection epilogue lane group reads for one pair
+// are 512 contiguous bytes (a conflict-free ds_read_b128; profiles/r05c_lds_conflict_calibration.txt).
+__host__ __device__ __forceinline__ size_t lg_fac4(size_t r, int p) {
+    return ((r >> 6) * 16 + (size_t)p) * 64 + (r & 63);
+}
+
 // nn.GELU() (exact, erf form) as x * Phi(x) with Phi(x) = 0.5 + xc * P(2 xc^2 / 4.5^2 - 1),
 // xc = clamp(x, -4.5, 4.5), P of degree 12 (a Chebyshev least-squares fit of
 // (Phi(x) - 0.5) / x in the well-conditioned variable, evaluated by Horner in f32):

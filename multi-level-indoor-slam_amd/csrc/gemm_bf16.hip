@@ -65,6 +65,43 @@ struct EpiBiasSplitBF16 {
     }
 };
 
+// LoFTR's coarse similarity from the split-bf16 product: S[m][n] = (acc / 256) / 0.1 as
+// the exact-f32 path scales it (mlg_similarity_f32_loftr), columns n < ncols only (the
+// GEMM's N is padded to the 256-column tile)
+struct EpiSimLoFTR {
+    float* S; int lds; int ncols;
+    struct Col {};
+    struct Row {};
+    struct Pre {};
+    __device__ Col col(int) const { return {}; }
+    __device__ Row row(int) const { return {}; }
+    __device__ Pre pre(int, int, const Col&, const Row&) const { return {}; }
+    __device__ static float sc(float a) { return (a * (1.0f / 256.0f)) / 0.1f; }
+    __device__ void store(int m, int n, float a, float b, float c, float d) const {
+        float* row = S + (size_t)m * lds;
+        if (n + 3 < ncols) {
+            *reinterpret_cast<float4*>(row + n) = make_float4(a, b, c, d);
+        } else {
+            const float v[4] = {a, b, c, d};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (n + e < ncols) row[n + e] = v[e];
+        }
+    }
+    // staged form (k_gemm256s): the scaled products staged as f32 rows, written as whole
+    // 256-B row pieces (no read of S: load4 is a no-op)
+    static constexpr int STAGED = 2;
+    __device__ float4 stage4(const f32x4& v, const Col&) const {
+        return make_float4(sc(v[0]), sc(v[1]), sc(v[2]), sc(v[3]));
+    }
+    __device__ float4 load4(int, int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+    __device__ void put4(int m, int n, float4, const float4& y) const { store(m, n, y.x, y.y, y.z, y.w); }
+    __device__ void apply(int m, int n, const f32x4& v, const Col&, const Row&, const Pre&) const {
+        store(m, n, sc(v[0]), sc(v[1]), sc(v[2]), sc(v[3]));
+    }
+    __device__ void operator()(int m, int n, const f32x4& v) const { apply(m, n, v, Col{}, Row{}, Pre{}); }
+};
+
 struct EpiBiasBF16 {  // y = acc + b  -> bf16
     bf16_t* C; int ldc; const float* bias;
     __device__ void operator()(int m, int n, const f32x4& v) const {
@@ -1464,6 +1501,12 @@ int mlg_gemm_patch_split(const bf16_t* A, const bf16_t* W, const float* bias, co
                          int Kpad, hipStream_t s) {
     if (M % P) return MLG_EINVAL;
     return launch_split(A, W, M, 768, Kpad, 2 * Kpad, 2 * Kpad, EpiPatch{X, bias, pos, P}, s);
+}
+
+int mlg_gemm_sim_split_loftr(const bf16_t* A, const bf16_t* B, int M, int Npad, int K0, float* S, int lds, int ncols,
+                             hipStream_t s) {
+    if (ncols > Npad || (lds % 4)) return MLG_EINVAL;
+    return launch_split(A, B, M, Npad, K0, 2 * K0, 2 * K0, EpiSimLoFTR{S, lds, ncols}, s);
 }
 
 int mlg_gemm_f32out(const bf16_t* A, const bf16_t* W, float* C, int M, int N, int K, hipStream_t s) {

@@ -100,6 +100,10 @@ int mlg_row_normalize(const float* X, float* Xn, int N, int D, float* norms, hip
 int mlg_similarity_f32(const float* A, int Q, const float* B, int N, int D, float* S, int lds, hipStream_t s);
 // the same product stored as LoFTR's coarse similarity (S / 256) / 0.1
 int mlg_similarity_f32_loftr(const float* A, int Q, const float* B, int N, int D, float* S, int lds, hipStream_t s);
+// the same similarity from split-bf16 operands (A / B rows [hi | lo], K0 = 256 each; B
+// readable up to Npad = ncols rounded up to 256 rows): 3 bf16 MFMA products per product
+int mlg_gemm_sim_split_loftr(const bf16_t* A, const bf16_t* B, int M, int Npad, int K0, float* S, int lds, int ncols,
+                             hipStream_t s);
 int mlg_similarity_f32_t(const float* A, int Q, const float* B, int N, int D, float* S, int lds, float* St, int ldt,
                          hipStream_t s);
 int mlg_topk_gate(const float* S, int lds, int N, int Q, const double* tq, const double* tdb, const int64_t* fq,
@@ -186,8 +190,9 @@ int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const
                const mlg_lg_conf_i* conf = nullptr, int relu = 0);
 // lg_proj.hip -- LightGlue q/k/v projections (+ rotary for the self block) straight into
 // the attention operands; W packed k-step-major [16][768 | 512][16]; Npad % 64 == 0.
-int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,
-                const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s);
+// efac: the rotary factors in the lg_fac4 layout (common.h), self block only
+int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* efac,
+                const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s);
 // superglue.hip -- SuperGlue GNN + log-space optimal transport over a ragged batch of pairs
 struct mlg_sg_weights_i {
     const float* kenc_w[3]; const float* kenc_b[3];

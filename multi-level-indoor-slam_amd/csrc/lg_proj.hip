@@ -48,7 +48,13 @@ __device__ __forceinline__ int xoff(int row, int chunk) { return row * ROWB + ((
 
 __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-__device__ __forceinline__ int fac_swz(int row) { return (row >> 1) & 7; }
+// a tile's rotary factors: 16 KiB, [16 pairs][64 rows] float4 (common.h lg_fac4); a lane
+// reads the float4 of its row for one frequency pair: the 32 lanes of a half-wave read 512
+// contiguous bytes, one conflict-free ds_read_b128 (the [64][32] cos / sin images before
+// round 5 took two ds_read_b64 with 2-way conflicts, profiles/r05c_lds_conflict_calibration.txt)
+__device__ __forceinline__ float4 fac_tile(const float* fc, int r, int p) {
+    return *reinterpret_cast<const float4*>(fc + ((p * 64 + r) << 2));
+}
 
 // Output staging image over the dead x tile: [4 heads][64 rows][64] bf16, 16-B chunk c of
 // row r at slot c ^ (r & 7).  Rows are tokens for q / k and head dims for V^T; either way
@@ -97,15 +103,15 @@ __device__ __forceinline__ void proj_gemm(const bf16_t* __restrict__ wrow, size_
 // Bias (+ rotary), live-row mask, staging through the dead x tile `lds` and the
 // coalesced copy-out of one R-token tile of part `part` (the caller has barriered after
 // the GEMM's last LDS read).
-// FAC_LDS (resident form): the tile's rotary factors sit in LDS at `ecos` / `esin` as
-// [R tokens][32] instead of the global [Npad][32] tables, `bias` is this part's 256
+// FAC_LDS (resident form): the tile's rotary factors sit in LDS at `efac` (its 16 KiB
+// lg_fac4 block) instead of the global table, `bias` is this part's 256
 // biases in LDS and `live` the tile's R live bytes in LDS (no global load in the epilogue).
 template <bool SELF, int MT, bool FAC_LDS = false>
 __device__ __forceinline__ void proj_epilogue(const f32x16 (&acc)[MT], bool is_v, int part, int m0, int nrow_,
                                               char* lds, const float* __restrict__ bias,
-                                              const float* __restrict__ ecos, const float* __restrict__ esin,
-                                              const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
-                                              bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad) {
+                                              const float* __restrict__ efac, const uint8_t* __restrict__ live,
+                                              bf16_t* __restrict__ Q, bf16_t* __restrict__ K, bf16_t* __restrict__ Vt,
+                                              int Npad) {
     constexpr int R = 32 * MT;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, col = lane & 31, hh = lane >> 5;
     const int nrow = nrow_ & 0xffff;  // bit 16: timing probe, no copy-out
@@ -121,20 +127,13 @@ __device__ __forceinline__ void proj_epilogue(const f32x16 (&acc)[MT], bool is_v
                 const f32x16& a = acc[mt];
                 float x0 = a[4 * g] + b.x, x1 = a[4 * g + 1] + b.y, x2 = a[4 * g + 2] + b.z, x3 = a[4 * g + 3] + b.w;
                 if (SELF) {  // t * cos + rotate_half(t) * sin, uncontracted as torch
-                    // (cos, sin) of frequencies d/2, d/2 + 1, read after the GEMM (held
-                    // across it they cost 32 VGPRs = one workgroup per CU less) straight
-                    // from global: an LDS-staged copy of the tile's factors gave run-to-run
-                    // different q / k on gfx950 (unexplained; tests/test_kernels_gpu.py::
-                    // test_lightglue_kernels_deterministic)
-                    // resident form: 16-B chunk c of factor row r sits at chunk c ^ ((r >> 1) & 7)
-                    // (fac_swz), so the 32 rows a wave-instruction reads spread over the banks
-                    // (unswizzled, rows 128 B apart: a 16-way bank conflict per read)
-                    const int j = (n & 63) / 2;
-                    const size_t eo = FAC_LDS ? (size_t)r * 32 + 4 * ((j >> 2) ^ fac_swz(r)) + (j & 3)
-                                              : (size_t)m * 32 + j;
-                    const float2 rc = *reinterpret_cast<const float2*>(ecos + eo);
-                    const float2 rs = *reinterpret_cast<const float2*>(esin + eo);
-                    const float2 e0 = make_float2(rc.x, rs.x), e1 = make_float2(rc.y, rs.y);
+                    // (cos, sin) of frequencies d/2, d/2 + 1 (one lg_fac4 float4), read after
+                    // the GEMM (held across it they cost 32 VGPRs = one workgroup per CU
+                    // less): from the tile's LDS block (resident form) or global
+                    const int p = (n & 63) >> 2;
+                    const float4 cs = FAC_LDS ? fac_tile(efac, r, p)
+                                              : reinterpret_cast<const float4*>(efac)[lg_fac4((size_t)m, p)];
+                    const float2 e0 = make_float2(cs.x, cs.z), e1 = make_float2(cs.y, cs.w);
                     const float r0 = __fadd_rn(__fmul_rn(x0, e0.x), __fmul_rn(-x1, e0.y));
                     const float r1 = __fadd_rn(__fmul_rn(x1, e0.x), __fmul_rn(x0, e0.y));
                     const float r2 = __fadd_rn(__fmul_rn(x2, e1.x), __fmul_rn(-x3, e1.y));
@@ -182,9 +181,9 @@ __device__ __forceinline__ void proj_epilogue(const f32x16 (&acc)[MT], bool is_v
 template <bool SELF, int MT>
 __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcopy, int ldx,
                                                 const bf16_t* __restrict__ W, const float* __restrict__ bias,
-                                                const float* __restrict__ ecos, const float* __restrict__ esin,
-                                                const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
-                                                bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad) {
+                                                const float* __restrict__ efac, const uint8_t* __restrict__ live,
+                                                bf16_t* __restrict__ Q, bf16_t* __restrict__ K, bf16_t* __restrict__ Vt,
+                                                int Npad) {
     constexpr int N = SELF ? 768 : 512;
     constexpr int R = 32 * MT;
     __shared__ __attribute__((aligned(16))) char lds[R * ROWB];
@@ -223,7 +222,7 @@ __global__ __launch_bounds__(512) void k_lg_proj(const bf16_t* __restrict__ xcop
         proj_gemm<true, MT>(wrow, (size_t)N * 16, lds, acc);
     }
     __syncthreads();  // every wave has read the x tile
-    proj_epilogue<SELF, MT>(acc, is_v, part, m0, nrow, lds, bias, ecos, esin, live, Q, K, Vt, Npad);
+    proj_epilogue<SELF, MT>(acc, is_v, part, m0, nrow, lds, bias, efac, live, Q, K, Vt, Npad);
 }
 
 // ---------------------------------------------------------------- resident form
@@ -273,8 +272,7 @@ __device__ __forceinline__ void res_gemm(const bf16x8 (&wf)[16], const char* lds
 template <bool SELF>
 __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ xcopy, int ldx,
                                                        const bf16_t* __restrict__ W, const float* __restrict__ bias,
-                                                       const float* __restrict__ ecos,
-                                                       const float* __restrict__ esin,
+                                                       const float* __restrict__ efac,
                                                        const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
                                                        bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad,
                                                        int slots, int probe) {
@@ -312,14 +310,11 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
         if (probe & 4) return;
         // (the v part fetches them too: skipping that measured slower, 1.92 vs 1.71 ms at 2 M
         // tokens; probably the three parts of a tile then drift apart and lose the L2 reuse)
-        if (SELF && !(probe & 8)) {  // 8 KiB of cos and of sin: one 1 KiB piece of each per wave
-            const unsigned fb = lds_addr(buf) + XB + 1024 * wave;
-            // lane -> LDS row 8 w + (lane >> 3), chunk lane & 7, filled from chunk
-            // (lane & 7) ^ fac_swz(row) of the global row
-            const int frow = 8 * wave + (lane >> 3);
-            const size_t fo = (size_t)(tile * R + frow) * 32 + 4 * ((lane & 7) ^ fac_swz(frow));
-            dma16(ecos + fo, fb);
-            dma16(esin + fo, fb + R * 32 * 4);
+        if (SELF && !(probe & 8)) {  // the tile's 16 KiB factor block: two 1 KiB pieces per wave
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                dma16(efac + (size_t)tile * (R * 64) + (2 * wave + i) * 256 + 4 * lane,
+                      lds_addr(buf) + XB + 1024 * (2 * wave + i));
         }
         if (wave == 0 && lane < R / 16) dma16(live + (size_t)tile * R + 16 * lane, lds_addr(buf) + BUF);
     };
@@ -347,7 +342,7 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
         }
         __syncthreads();  // every wave has read the x tile
         const float* fc = reinterpret_cast<const float*>(cur + XB);
-        if (!(probe & 2)) proj_epilogue<SELF, 2, true>(acc, is_v, part, t * R, R | ((probe & 16) << 12), cur, bias_l, fc, fc + R * 32,
+        if (!(probe & 2)) proj_epilogue<SELF, 2, true>(acc, is_v, part, t * R, R | ((probe & 16) << 12), cur, bias_l, fc,
                                      reinterpret_cast<const uint8_t*>(cur + BUF), Q, K, Vt, Npad);
         if (tn >= ntiles) break;
         t = tn;
@@ -366,21 +361,18 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
 // same epilogue arithmetic).
 template <bool SELF>
 __device__ __forceinline__ void slice_qk(int g, int mt, const f32x16& a, char* lds, const float* bias_l,
-                                         const float* fc, const float* fs, const uint8_t* live_l) {
+                                         const float* fc, const uint8_t* live_l) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 31, hh = lane >> 5;
     const int n = 32 * wave + 8 * g + 4 * hh, h = n >> 6, d = n & 63;
     const float4 b = *reinterpret_cast<const float4*>(bias_l + n);
     const int r = 32 * mt + col;
     float x0 = a[4 * g] + b.x, x1 = a[4 * g + 1] + b.y, x2 = a[4 * g + 2] + b.z, x3 = a[4 * g + 3] + b.w;
     if (SELF) {  // as proj_epilogue's resident form
-        const int j = (n & 63) / 2;
-        const int eo = r * 32 + 4 * ((j >> 2) ^ fac_swz(r)) + (j & 3);
-        const float2 rc = *reinterpret_cast<const float2*>(fc + eo);
-        const float2 rs = *reinterpret_cast<const float2*>(fs + eo);
-        const float r0 = __fadd_rn(__fmul_rn(x0, rc.x), __fmul_rn(-x1, rs.x));
-        const float r1 = __fadd_rn(__fmul_rn(x1, rc.x), __fmul_rn(x0, rs.x));
-        const float r2 = __fadd_rn(__fmul_rn(x2, rc.y), __fmul_rn(-x3, rs.y));
-        const float r3 = __fadd_rn(__fmul_rn(x3, rc.y), __fmul_rn(x2, rs.y));
+        const float4 cs = fac_tile(fc, r, (n & 63) >> 2);  // cos j, cos j + 1, sin j, sin j + 1
+        const float r0 = __fadd_rn(__fmul_rn(x0, cs.x), __fmul_rn(-x1, cs.z));
+        const float r1 = __fadd_rn(__fmul_rn(x1, cs.x), __fmul_rn(x0, cs.z));
+        const float r2 = __fadd_rn(__fmul_rn(x2, cs.y), __fmul_rn(-x3, cs.w));
+        const float r3 = __fadd_rn(__fmul_rn(x3, cs.y), __fmul_rn(x2, cs.w));
         x0 = r0; x1 = r1; x2 = r2; x3 = r3;
     }
     // branch-free mask: a branch here would end the basic block and with it the
@@ -409,7 +401,7 @@ __device__ __forceinline__ void slice_v(int g, int mt, const f32x16& a, char* ld
 template <bool SELF, bool IS_V, bool STAGE>
 __device__ __forceinline__ void pipe_gemm(const bf16x8 (&wf)[16], const char* xl, f32x16 (&acc)[2],
                                           const f32x16 (&old)[2], char* sl, const float* bias_l, const float* fc,
-                                          const float* fs, const uint8_t* live_l) {
+                                          const uint8_t* live_l) {
     const int lane = threadIdx.x & 63, col = lane & 31, hh = lane >> 5;
     const char* xrow = xl + col * ROWB;
     const int sw = col & 15;
@@ -432,7 +424,7 @@ __device__ __forceinline__ void pipe_gemm(const bf16x8 (&wf)[16], const char* xl
         if (STAGE && !(ks & 1)) {
             const int g = ks >> 2, mt = (ks >> 1) & 1;
             if (IS_V) slice_v(g, mt, old[mt], sl, bias_l, live_l);
-            else slice_qk<SELF>(g, mt, old[mt], sl, bias_l, fc, fs, live_l);
+            else slice_qk<SELF>(g, mt, old[mt], sl, bias_l, fc, live_l);
         }
     }
 }
@@ -451,8 +443,8 @@ __device__ __forceinline__ void copy_out64(bool is_v, int part, int m0, const ch
 
 template <bool SELF, bool IS_V>
 __device__ __forceinline__ void pipe_tiles(const bf16x8 (&wf)[16], char* ring, const float* bias_l,
-                                           const bf16_t* __restrict__ xcopy, int ldx, const float* __restrict__ ecos,
-                                           const float* __restrict__ esin, const uint8_t* __restrict__ live,
+                                           const bf16_t* __restrict__ xcopy, int ldx, const float* __restrict__ efac,
+                                           const uint8_t* __restrict__ live,
                                            bf16_t* __restrict__ Q, bf16_t* __restrict__ K, bf16_t* __restrict__ Vt,
                                            int Npad, int part, int t0, int stride, int ntiles) {
     constexpr int R = 64, XB = R * ROWB, BUF = XB + (SELF ? 2 * R * 32 * 4 : 0), SLOT = BUF + 256;
@@ -466,12 +458,11 @@ __device__ __forceinline__ void pipe_tiles(const bf16x8 (&wf)[16], char* ring, c
             const int row = drow + 2 * i;
             dma16(xcopy + (size_t)(tile * R + row) * ldx + ((dslot ^ (row & 15)) * 8), base + 1024 * i);
         }
-        if (SELF) {
-            const unsigned fb = lds_addr(buf) + XB + 1024 * wave;
-            const int frow = 8 * wave + (lane >> 3);
-            const size_t fo = (size_t)(tile * R + frow) * 32 + 4 * ((lane & 7) ^ fac_swz(frow));
-            dma16(ecos + fo, fb);
-            dma16(esin + fo, fb + R * 32 * 4);
+        if (SELF) {  // the tile's 16 KiB factor block: two 1 KiB pieces per wave
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                dma16(efac + (size_t)tile * (R * 64) + (2 * wave + i) * 256 + 4 * lane,
+                      lds_addr(buf) + XB + 1024 * (2 * wave + i));
         }
         if (wave == 0 && lane < R / 16) dma16(live + (size_t)tile * R + 16 * lane, lds_addr(buf) + BUF);
     };
@@ -495,12 +486,12 @@ __device__ __forceinline__ void pipe_tiles(const bf16x8 (&wf)[16], char* ring, c
         char* sl = bufs(bp);
         const float* fc = reinterpret_cast<const float*>(sl + XB);
         if (tp >= 0) {
-            pipe_gemm<SELF, IS_V, true>(wf, bufs(bx), an, ao, sl, bias_l, fc, fc + R * 32,
+            pipe_gemm<SELF, IS_V, true>(wf, bufs(bx), an, ao, sl, bias_l, fc,
                                         reinterpret_cast<const uint8_t*>(sl + BUF));
             __syncthreads();  // staging written
             copy_out64(IS_V, part, tp * R, sl, Q, K, Vt, Npad);
         } else {
-            pipe_gemm<SELF, IS_V, false>(wf, bufs(bx), an, ao, sl, bias_l, fc, fc + R * 32,
+            pipe_gemm<SELF, IS_V, false>(wf, bufs(bx), an, ao, sl, bias_l, fc,
                                          reinterpret_cast<const uint8_t*>(sl + BUF));
         }
         tp = t;
@@ -512,8 +503,7 @@ __device__ __forceinline__ void pipe_tiles(const bf16x8 (&wf)[16], char* ring, c
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 if (IS_V) slice_v(i >> 1, i & 1, an[i & 1], sx, bias_l, reinterpret_cast<const uint8_t*>(sx + BUF));
-                else slice_qk<SELF>(i >> 1, i & 1, an[i & 1], sx, bias_l, fx, fx + R * 32,
-                                    reinterpret_cast<const uint8_t*>(sx + BUF));
+                else slice_qk<SELF>(i >> 1, i & 1, an[i & 1], sx, bias_l, fx, reinterpret_cast<const uint8_t*>(sx + BUF));
             }
             __syncthreads();
             copy_out64(IS_V, part, tp * R, sx, Q, K, Vt, Npad);
@@ -531,8 +521,7 @@ __device__ __forceinline__ void pipe_tiles(const bf16x8 (&wf)[16], char* ring, c
 template <bool SELF>
 __global__ __launch_bounds__(512) void k_lg_proj_pipe(const bf16_t* __restrict__ xcopy, int ldx,
                                                         const bf16_t* __restrict__ W, const float* __restrict__ bias,
-                                                        const float* __restrict__ ecos,
-                                                        const float* __restrict__ esin,
+                                                        const float* __restrict__ efac,
                                                         const uint8_t* __restrict__ live, bf16_t* __restrict__ Q,
                                                         bf16_t* __restrict__ K, bf16_t* __restrict__ Vt, int Npad,
                                                         int slots) {
@@ -554,16 +543,16 @@ __global__ __launch_bounds__(512) void k_lg_proj_pipe(const bf16_t* __restrict__
         for (int ks = 0; ks < 16; ++ks) wf[ks] = ld16(wrow + (size_t)ks * N * 16);
     }
     if (part == NPART - 1)
-        pipe_tiles<SELF, true>(wf, ring, bias_l, xcopy, ldx, ecos, esin, live, Q, K, Vt, Npad, part, t0, stride, ntiles);
+        pipe_tiles<SELF, true>(wf, ring, bias_l, xcopy, ldx, efac, live, Q, K, Vt, Npad, part, t0, stride, ntiles);
     else
-        pipe_tiles<SELF, false>(wf, ring, bias_l, xcopy, ldx, ecos, esin, live, Q, K, Vt, Npad, part, t0, stride,
+        pipe_tiles<SELF, false>(wf, ring, bias_l, xcopy, ldx, efac, live, Q, K, Vt, Npad, part, t0, stride,
                                 ntiles);
 }
 
 }  // namespace
 
-int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* ecos,
-                const float* esin, const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s) {
+int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, const float* bias, const float* efac,
+                const uint8_t* live, bf16_t* Q, bf16_t* K, bf16_t* Vt, int Npad, hipStream_t s) {
     if (Npad <= 0 || (Npad % 64) || ldx < 256 || (ldx % 8)) return MLG_EINVAL;
     // Build-time A/B knob: MLG_PROJ_MT = 32-token m-tiles per workgroup (2: 64 tokens, 4: 128).
     // 128-token tiles halve the weight bytes per FLOP but measured 2-7 % slower on one
@@ -588,21 +577,21 @@ int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, 
         const unsigned grid = (unsigned)(8 * slots * npart);
         if (MLG_PROJ_PIPE && !probe) {
             if (self_block)
-                hipLaunchKernelGGL(k_lg_proj_pipe<true>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin,
+                hipLaunchKernelGGL(k_lg_proj_pipe<true>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, efac,
                                    live, Q, K, Vt, Npad, slots);
             else
                 hipLaunchKernelGGL(k_lg_proj_pipe<false>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias,
-                                   (const float*)nullptr, (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad,
+                                   (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad,
                                    slots);
             MLG_LAUNCH_CHECK();
             return MLG_OK;
         }
         if (self_block)
-            hipLaunchKernelGGL(k_lg_proj_res<true>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin, live,
+            hipLaunchKernelGGL(k_lg_proj_res<true>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, efac, live,
                                Q, K, Vt, Npad, slots, probe);
         else
             hipLaunchKernelGGL(k_lg_proj_res<false>, dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias,
-                               (const float*)nullptr, (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad,
+                               (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad,
                                slots, probe);
         MLG_LAUNCH_CHECK();
         return MLG_OK;
@@ -611,18 +600,18 @@ int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, 
     const unsigned grid = (unsigned)((((long)((Npad + R - 1) / R) * (self_block ? 3 : 2)) + 7) & ~7L);
     if (self_block) {
         if (mt == 4)
-            hipLaunchKernelGGL((k_lg_proj<true, 4>), dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin,
+            hipLaunchKernelGGL((k_lg_proj<true, 4>), dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, efac,
                                live, Q, K, Vt, Npad);
         else
-            hipLaunchKernelGGL((k_lg_proj<true, 2>), dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, ecos, esin,
+            hipLaunchKernelGGL((k_lg_proj<true, 2>), dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias, efac,
                                live, Q, K, Vt, Npad);
     } else {
         if (mt == 4)
             hipLaunchKernelGGL((k_lg_proj<false, 4>), dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias,
-                               (const float*)nullptr, (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad);
+                               (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad);
         else
             hipLaunchKernelGGL((k_lg_proj<false, 2>), dim3(grid), dim3(512), 0, s, xcopy, ldx, W, bias,
-                               (const float*)nullptr, (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad);
+                               (const float*)nullptr, live, Q, (bf16_t*)nullptr, Vt, Npad);
     }
     MLG_LAUNCH_CHECK();
     return MLG_OK;

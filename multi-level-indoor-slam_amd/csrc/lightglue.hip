@@ -78,8 +78,8 @@ __global__ __launch_bounds__(256) void k_lg_kpnorm(const Seg* __restrict__ segs,
 __global__ __launch_bounds__(256) void k_lg_init(const Seg* __restrict__ segs, const float4* __restrict__ norm,
                                                  const float* __restrict__ kpts, const float* __restrict__ desc,
                                                  int kmax, const float* __restrict__ Wr, float* __restrict__ x,
-                                                 bf16_t* __restrict__ cat, float* __restrict__ ecos,
-                                                 float* __restrict__ esin, int32_t* __restrict__ ind,
+                                                 bf16_t* __restrict__ cat, float4* __restrict__ efac,
+                                                 int32_t* __restrict__ ind,
                                                  const int4* __restrict__ mv = nullptr,
                                                  const float* __restrict__ xf = nullptr,
                                                  const bf16_t* __restrict__ catf = nullptr) {
@@ -89,20 +89,19 @@ __global__ __launch_bounds__(256) void k_lg_init(const Seg* __restrict__ segs, c
     const float4 nm = norm[blockIdx.y];
     const float* kp = kpts + (size_t)sg.frame * kmax * 2;
     const float* ds = desc + (size_t)sg.frame * kmax * LG_D;
-    for (int e = threadIdx.x; e < 64 * 32; e += 256) {
-        const int i = r0 + e / 32, f = e % 32;
+    for (int e = threadIdx.x; e < 64 * 16; e += 256) {
+        const int i = r0 + e / 16, p = e % 16;
         const size_t r = (size_t)sg.off + i;
         const bool live = i < sg.len;
-        float c = 0.f, sn = 0.f;
+        float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);  // cos f, cos f + 1, sin f, sin f + 1
         if (live) {
             const float kx = (kp[2 * i] - nm.x) / nm.z, ky = (kp[2 * i + 1] - nm.y) / nm.z;
-            const float pr = kx * Wr[2 * f] + ky * Wr[2 * f + 1];
-            c = cosf(pr);
-            sn = sinf(pr);
+            const float p0 = kx * Wr[4 * p] + ky * Wr[4 * p + 1];
+            const float p1 = kx * Wr[4 * p + 2] + ky * Wr[4 * p + 3];
+            cs = make_float4(cosf(p0), cosf(p1), sinf(p0), sinf(p1));
         }
-        ecos[r * 32 + f] = c;
-        esin[r * 32 + f] = sn;
-        if (f == 0) ind[r] = live ? i : -1;
+        efac[lg_fac4(r, p)] = cs;
+        if (p == 0) ind[r] = live ? i : -1;
     }
     if (mv) {
         const size_t fo = (size_t)mv[blockIdx.y].z;
@@ -162,10 +161,10 @@ __global__ __launch_bounds__(256) void k_lg_segstats(const Seg* __restrict__ seg
 // new row dst_off + rank(i) <- old row src_off + i for tokens with keep (or all when
 // keep_all): x, cat[:, :256], enc, ind.  One workgroup per (old) segment.
 __global__ __launch_bounds__(256) void k_lg_compact(const int4* __restrict__ moves, const uint8_t* __restrict__ keep,
-                                                    const float* __restrict__ x, const float* __restrict__ ecos,
-                                                    const float* __restrict__ esin, const int32_t* __restrict__ ind,
+                                                    const float* __restrict__ x, const float4* __restrict__ efac,
+                                                    const int32_t* __restrict__ ind,
                                                     float* __restrict__ x2, bf16_t* __restrict__ cat2,
-                                                    float* __restrict__ ecos2, float* __restrict__ esin2,
+                                                    float4* __restrict__ efac2,
                                                     int32_t* __restrict__ ind2) {
     const int4 mv = moves[blockIdx.x];  // src_off, src_len, dst_off, keep_all
     __shared__ int rank[2048 + 64];
@@ -200,12 +199,11 @@ __global__ __launch_bounds__(256) void k_lg_compact(const int4* __restrict__ mov
         x2[(size_t)(mv.z + rk) * LG_D + cc] = val;
         cat2[(size_t)(mv.z + rk) * 512 + cc] = f32_to_bf16(val);
     }
-    for (int e = tid; e < mv.y * 32; e += 256) {
-        const int i = e / 32, f = e % 32;
+    for (int e = tid; e < mv.y * 16; e += 256) {
+        const int i = e / 16, p = e % 16;
         const int rk = rank[i];
         if (rk < 0) continue;
-        ecos2[(size_t)(mv.z + rk) * 32 + f] = ecos[(size_t)(mv.x + i) * 32 + f];
-        esin2[(size_t)(mv.z + rk) * 32 + f] = esin[(size_t)(mv.x + i) * 32 + f];
+        efac2[lg_fac4((size_t)(mv.z + rk), p)] = efac[lg_fac4((size_t)(mv.x + i), p)];
     }
     for (int i = tid; i < mv.y; i += 256)
         if (rank[i] >= 0) ind2[mv.z + rank[i]] = ind[mv.x + i];
@@ -215,10 +213,9 @@ __global__ __launch_bounds__(256) void k_lg_compact(const int4* __restrict__ mov
         x2[(size_t)(mv.z + i) * LG_D + cc] = 0.f;
         cat2[(size_t)(mv.z + i) * 512 + cc] = 0;
     }
-    for (int e = tid; e < (padded - newlen) * 32; e += 256) {
-        const int i = newlen + e / 32, f = e % 32;
-        ecos2[(size_t)(mv.z + i) * 32 + f] = 0.f;
-        esin2[(size_t)(mv.z + i) * 32 + f] = 0.f;
+    for (int e = tid; e < (padded - newlen) * 16; e += 256) {
+        const int i = newlen + e / 16, p = e % 16;
+        efac2[lg_fac4((size_t)(mv.z + i), p)] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     for (int i = newlen + tid; i < padded; i += 256) ind2[mv.z + i] = -1;
 }
@@ -751,7 +748,7 @@ void trace(int tag, const void* base, int rpt, int row_bytes, size_t row_stride,
 }
 
 struct LgLayout {
-    size_t x, cat, ecos, esin, ind, x2, cat2, ecos2, esin2, ind2, Q, K, Vt, ctx, hf, hb, live, rowseg, lz, keep,
+    size_t x, cat, efac, ind, x2, cat2, efac2, ind2, Q, K, Vt, ctx, hf, hb, live, rowseg, lz, keep,
         stats, segs, tasks, outoff, moves, mdesc, rmax, rlog, cmax, clog, arg, val, part, asg, norm, S, total;
     int asg_cap;
 };
@@ -768,13 +765,11 @@ LgLayout lg_layout(int P, int kmax) {
     };
     L.x = take(N * LG_D * 4);
     L.cat = take(N * 512 * 2);
-    L.ecos = take(N * 32 * 4);
-    L.esin = take(N * 32 * 4);
+    L.efac = take(N * 64 * 4);  // rotary factors, lg_fac4 layout
     L.ind = take(N * 4);
     L.x2 = take(N * LG_D * 4);
     L.cat2 = take(N * 512 * 2);
-    L.ecos2 = take(N * 32 * 4);
-    L.esin2 = take(N * 32 * 4);
+    L.efac2 = take(N * 64 * 4);
     L.ind2 = take(N * 4);
     L.Q = take(N * LG_D * 2);
     L.K = take(N * LG_D * 2);
@@ -832,13 +827,11 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     char* base = (char*)ws;
     float* X = (float*)(base + L.x);
     bf16_t* CAT = (bf16_t*)(base + L.cat);
-    float* EC = (float*)(base + L.ecos);
-    float* ES = (float*)(base + L.esin);
+    float4* EF = (float4*)(base + L.efac);
     int32_t* IND = (int32_t*)(base + L.ind);
     float* X2 = (float*)(base + L.x2);
     bf16_t* CAT2 = (bf16_t*)(base + L.cat2);
-    float* EC2 = (float*)(base + L.ecos2);
-    float* ES2 = (float*)(base + L.esin2);
+    float4* EF2 = (float4*)(base + L.efac2);
     int32_t* IND2 = (int32_t*)(base + L.ind2);
     bf16_t* Q = (bf16_t*)(base + L.Q);
     bf16_t* K = (bf16_t*)(base + L.K);
@@ -985,7 +978,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
             hipLaunchKernelGGL(k_lg_kpnorm, dim3((unsigned)nf), dim3(256), 0, s, SEGS, kpts, kmax,
                                (float4*)(base + L.norm));
             hipLaunchKernelGGL(k_lg_init, dim3((unsigned)((kmax + 63) / 64), (unsigned)nf), dim3(256), 0, s, SEGS,
-                               (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X2, CAT2, EC2, ES2, IND2);
+                               (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X2, CAT2, EF2, IND2);
             MLG_LAUNCH_CHECK();
             tr_tab(9903, SEGS, fsegs.size() * sizeof(Seg));
             tr_tab(9904, TASKS, f_tasks.size() * sizeof(int4));
@@ -993,7 +986,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
             tr_rows(9902, CAT2, 512, NpadF, 1024);
             {
                 MlgProfScope prof(6, s, 2.0 * tok * 768 * 256);
-                LG_TRY(mlg_lg_proj(true, CAT2, 512, w.self[0].Wqkv, w.self[0].bqkv, EC2, ES2, LIVE, Q, K, VT, NpadF, s));
+                LG_TRY(mlg_lg_proj(true, CAT2, 512, w.self[0].Wqkv, w.self[0].bqkv, (const float*)EF2, LIVE, Q, K, VT, NpadF, s));
             }
             tr_heads(9910, Q, NpadF);
             tr_heads(9911, K, NpadF);
@@ -1016,12 +1009,12 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
     hipLaunchKernelGGL(k_lg_kpnorm, dim3((unsigned)segs.size()), dim3(256), 0, s, SEGS, kpts, kmax, (float4*)(base + L.norm));
 #if MLG_LG_INIT_FUSED
     hipLaunchKernelGGL(k_lg_init, dim3((unsigned)((kmax + 63) / 64), (unsigned)segs.size()), dim3(256), 0, s, SEGS,
-                       (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X, CAT, EC, ES, IND,
+                       (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X, CAT, EF, IND,
                        self0_done ? (const int4*)MOVES : nullptr, X2, CAT2);
     MLG_LAUNCH_CHECK();
 #else
     hipLaunchKernelGGL(k_lg_init, dim3((unsigned)((kmax + 63) / 64), (unsigned)segs.size()), dim3(256), 0, s, SEGS,
-                       (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X, CAT, EC, ES, IND,
+                       (const float4*)(base + L.norm), kpts, desc, kmax, w.Wr, X, CAT, EF, IND,
                        nullptr, nullptr, nullptr);
     MLG_LAUNCH_CHECK();
     if (self0_done) {
@@ -1118,7 +1111,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         if (!(i == 0 && self0_done)) {
             {
                 MlgProfScope prof(6, s, 2.0 * live_tokens() * 768 * 256);
-                LG_TRY(mlg_lg_proj(true, CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, EC, ES, LIVE, Q, K, VT, Npad, s));
+                LG_TRY(mlg_lg_proj(true, CAT, 512, w.self[i].Wqkv, w.self[i].bqkv, (const float*)EF, LIVE, Q, K, VT, Npad, s));
             }
             tr_heads(i * 100 + 10, Q, Npad);
             tr_heads(i * 100 + 11, K, Npad);
@@ -1132,7 +1125,7 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
         // cross block
         {
             MlgProfScope prof(6, s, 2.0 * live_tokens() * 512 * 256);
-            LG_TRY(mlg_lg_proj(false, CAT, 512, w.cross[i].Wqkv, w.cross[i].bqkv, nullptr, nullptr, LIVE, Q, nullptr, VT,
+            LG_TRY(mlg_lg_proj(false, CAT, 512, w.cross[i].Wqkv, w.cross[i].bqkv, nullptr, LIVE, Q, nullptr, VT,
                                Npad, s));
         }
         tr_heads(i * 100 + 20, Q, Npad);
@@ -1209,13 +1202,12 @@ int mlg_lightglue_run(const mlg_lg_weights_i& w, const float* kpts, const float*
             if (hipMemcpyAsync(MOVES, h_moves.data(), h_moves.size() * sizeof(int4), hipMemcpyHostToDevice, s) !=
                 hipSuccess)
                 return MLG_EHIP;
-            hipLaunchKernelGGL(k_lg_compact, dim3((unsigned)h_moves.size()), dim3(256), 0, s, MOVES, KEEP, X, EC, ES,
-                               IND, X2, CAT2, EC2, ES2, IND2);
+            hipLaunchKernelGGL(k_lg_compact, dim3((unsigned)h_moves.size()), dim3(256), 0, s, MOVES, KEEP, X, EF,
+                               IND, X2, CAT2, EF2, IND2);
             MLG_LAUNCH_CHECK();
             std::swap(X, X2);
             std::swap(CAT, CAT2);
-            std::swap(EC, EC2);
-            std::swap(ES, ES2);
+            std::swap(EF, EF2);
             std::swap(IND, IND2);
         }
         // an empty side after pruning ends that pair with no matches (reference loop break)

@@ -424,6 +424,21 @@ __global__ __launch_bounds__(256) void k_lf_ln(const float* __restrict__ in, con
     }
 }
 
+// f32 [rows][256] -> bf16 [rows][512] = [hi | lo] (x = hi + lo to 2^-17; the LoFTR
+// coarse similarity's split operands, MLG_LF_SIM_SPLIT)
+__global__ __launch_bounds__(256) void k_lf_split_rows(const float* __restrict__ x, long rows,
+                                                       bf16_t* __restrict__ out) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one float4 per thread
+    if (e >= rows * 64) return;
+    const long r = e >> 6;
+    const int c = (int)(e & 63) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(x + r * 256 + c);
+    uint2 hi, lo;
+    split_bf16x4(v.x, v.y, v.z, v.w, hi, lo);
+    *reinterpret_cast<uint2*>(out + r * 512 + c) = hi;
+    *reinterpret_cast<uint2*>(out + r * 512 + 256 + c) = lo;
+}
+
 // ------------------------------------------------------- dual softmax -------
 // S holds the similarity x = (f0 . f1 / 256) / 0.1 (mlg_similarity_f32_loftr: the
 // reference divides each side by 16 and the product by the temperature); per row i:
@@ -937,6 +952,12 @@ namespace {
 #ifndef MLG_LF_FUSED_TAIL
 #define MLG_LF_FUSED_TAIL 1
 #endif
+// Coarse similarity f0 . f1^T from split-bf16 operands (hi * hi + hi * lo + lo * hi, f32
+// accumulation: products to ~2^-17 of f32) instead of the exact-f32 MFMA; 0 builds the
+// exact-f32 form (A/B arm)
+#ifndef MLG_LF_SIM_SPLIT
+#define MLG_LF_SIM_SPLIT 1
+#endif
 
 // nn.Linear weight [N][K] bf16 -> k-step-major [K / 16][N][16] (lg_ffn.hip's layout)
 __global__ void k_lf_pack_kstep(const bf16_t* __restrict__ w, int N, int K, bf16_t* __restrict__ out) {
@@ -1114,7 +1135,7 @@ int pack_tails(const mlg_loftr_weights& w, char* base, TailW (&tw)[8], hipStream
 struct MatchLayout {
     size_t cx, ccat, cqkv, cmsg, ct, ch, ckv, cks, ckvp;  // coarse transformer (rows 2 P L, d 256)
     size_t fx, fcat, fqkv, fmsg, ft, fh, fkv, fks;  // fine transformer (rows 2 C 25, d 128)
-    size_t win, crow, cd, cm, S, rmax, rsum, rkey, cmax, csum, ckey, pm, pz, bval, bidx, cbest, mi, mj, mconf, cnt,
+    size_t win, crow, cd, cm, S, csplit, rmax, rsum, rkey, cmax, csum, ckey, pm, pz, bval, bidx, cbest, mi, mj, mconf, cnt,
         frm, mp, ms, tails, total;
 };
 
@@ -1151,6 +1172,9 @@ MatchLayout match_layout(int P, int L) {
     M.cd = take((size_t)2 * FINE_CHUNK * 128 * 2);
     M.cm = take((size_t)2 * FINE_CHUNK * 128 * 4);
     M.S = take((size_t)L * L * 4);
+    // the coarse features as split-bf16 rows [hi | lo] (+ 256 zero rows: the similarity
+    // GEMM reads B rows up to its 256-column tile)
+    M.csplit = take(((size_t)2 * P * L + 256) * 512 * 2);
     M.rmax = take((size_t)L * 4);
     M.rsum = take((size_t)L * 4);
     M.rkey = take((size_t)L * 4);
@@ -1244,11 +1268,25 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
             LF_TRY(pack_tails(w, (char*)at(ML.tails), tails, s));
     }
     LF_TRY(transformer(w.coarse, 8, bc, 256, P, L, s, MLG_LF_FUSED_TAIL ? tails : nullptr));
+    // the coarse similarity: split-bf16 operands (3 bf16 MFMA products at ~6x the exact-f32
+    // MFMA's rate) or the exact-f32 MFMA (MLG_LF_SIM_SPLIT=0)
+    bf16_t* CS = (bf16_t*)at(ML.csplit);
+    const int Lpad = (L + 255) / 256 * 256;
+    if (MLG_LF_SIM_SPLIT) {
+        const long rows = (long)2 * P * L;
+        hipLaunchKernelGGL(k_lf_split_rows, dim3((unsigned)((rows * 64 + 255) / 256)), dim3(256), 0, s, bc.x, rows, CS);
+        MLG_LAUNCH_CHECK();
+        if (hipMemsetAsync(CS + (size_t)rows * 512, 0, (size_t)256 * 512 * 2, s) != hipSuccess) return MLG_EHIP;
+    }
     // dual softmax + mutual nearest, pair by pair over one [L, L] similarity buffer
     for (int p = 0; p < P; ++p) {
         const float* f0 = bc.x + (size_t)p * L * 256;
         const float* f1 = bc.x + ((size_t)P + p) * L * 256;
-        LF_TRY(mlg_similarity_f32_loftr(f0, L, f1, L, 256, S, L, s));
+        if (MLG_LF_SIM_SPLIT)
+            LF_TRY(mlg_gemm_sim_split_loftr(CS + (size_t)p * L * 512, CS + ((size_t)P + p) * L * 512, L, Lpad, 256, S,
+                                            L, L, s));
+        else
+            LF_TRY(mlg_similarity_f32_loftr(f0, L, f1, L, 256, S, L, s));
         hipLaunchKernelGGL(k_lf_rowstats, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, rkey);
         hipLaunchKernelGGL(k_lf_colpart, dim3((L + 255) / 256, nrch), dim3(256), 0, s, S, L, pm, pz);
         hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum, ckey);

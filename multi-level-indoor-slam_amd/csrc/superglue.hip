@@ -100,9 +100,11 @@ __global__ __launch_bounds__(128) void k_sg_gather(const SgSeg* __restrict__ seg
     hr[tid] = f32_to_bf16(fmaxf(a, 0.f));
 }
 
-__global__ void k_sg_fill(float* __restrict__ a, long n, float v) {
+// the identity rotation (cos 1, sin 0) in the projections' lg_fac4 factor layout: every
+// float4 = (cos, cos, sin, sin) = (1, 1, 0, 0) -- the self-block projection with no rotary
+__global__ void k_sg_fill_rot(float4* __restrict__ a, long n) {
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) a[e] = v;
+    if (e < n) a[e] = make_float4(1.f, 1.f, 0.f, 0.f);
 }
 
 // ------------------------------------------------------------- Sinkhorn -----
@@ -287,7 +289,7 @@ inline int sg_chunk(int kmax) {
 }
 
 struct SgLayout {
-    size_t x, cat, Q, K, Vt, ctx, h3, h4, live, ec, es, md, segs, tasks, outoff, S, T, u, v, pairs, rmax, ridx, cidx,
+    size_t x, cat, Q, K, Vt, ctx, h3, h4, live, ef, md, segs, tasks, outoff, S, T, u, v, pairs, rmax, ridx, cidx,
         total;
 };
 
@@ -311,8 +313,7 @@ SgLayout sg_layout(int P, int kmax) {
     L.h3 = take(N * 128 * 2);
     L.h4 = take(N * 256 * 2);
     L.live = take(N);
-    L.ec = take(N * 32 * 4);
-    L.es = take(N * 32 * 4);
+    L.ef = take(N * 64 * 4);
     L.md = take(N * 256 * 4);
     L.segs = take((size_t)2 * P * sizeof(SgSeg));
     L.tasks = take((size_t)4 * P * sizeof(int4));
@@ -378,8 +379,7 @@ int mlg_superglue_run(const mlg_sg_weights_i& w, const float* kpts, const float*
     bf16_t* H3 = (bf16_t*)at(L.h3);
     bf16_t* H4 = (bf16_t*)at(L.h4);
     uint8_t* LIVE = (uint8_t*)at(L.live);
-    float* EC = (float*)at(L.ec);
-    float* ES = (float*)at(L.es);
+    float* EF = (float*)at(L.ef);  // identity rotary factors (lg_fac4 layout)
     float* MD = (float*)at(L.md);
     SgSeg* SEGS = (SgSeg*)at(L.segs);
     int4* TASKS = (int4*)at(L.tasks);
@@ -429,10 +429,8 @@ int mlg_superglue_run(const mlg_sg_weights_i& w, const float* kpts, const float*
         hipMemcpyAsync(OUTOFF, h_out.data(), h_out.size() * sizeof(int), hipMemcpyHostToDevice, s) != hipSuccess)
         return MLG_EHIP;
     hipLaunchKernelGGL(k_sg_live, dim3((Npad + 255) / 256), dim3(256), 0, s, SEGS, nseg, LIVE, Npad);
-    hipLaunchKernelGGL(k_sg_fill, dim3((unsigned)(((long)Npad * 32 + 255) / 256)), dim3(256), 0, s, EC,
-                       (long)Npad * 32, 1.0f);
-    hipLaunchKernelGGL(k_sg_fill, dim3((unsigned)(((long)Npad * 32 + 255) / 256)), dim3(256), 0, s, ES,
-                       (long)Npad * 32, 0.0f);
+    hipLaunchKernelGGL(k_sg_fill_rot, dim3((unsigned)(((long)Npad * 16 + 255) / 256)), dim3(256), 0, s,
+                       (float4*)EF, (long)Npad * 16);
     // keypoint encoder: layers 1-3 on the VALU, 4-5 as GEMMs; x = desc + kenc
     hipLaunchKernelGGL(k_sg_gather, dim3(Npad), dim3(128), 0, s, SEGS, nseg, Npad, kpts, kscores, desc, kmax,
                        (float)W, (float)H, w.kenc_w[0], w.kenc_b[0], w.kenc_w[1], w.kenc_b[1], w.kenc_w[2],
@@ -443,7 +441,7 @@ int mlg_superglue_run(const mlg_sg_weights_i& w, const float* kpts, const float*
     // the GNN: 18 layers, self / cross alternating, every projection from the pre-layer states
     for (int l = 0; l < 18; ++l) {
         const bool cross = (l & 1) != 0;
-        SG_TRY(mlg_lg_proj(true, CAT, 512, w.layer[l].Wqkv, w.layer[l].bqkv, EC, ES, LIVE, Q, K, VT, Npad, s));
+        SG_TRY(mlg_lg_proj(true, CAT, 512, w.layer[l].Wqkv, w.layer[l].bqkv, EF, LIVE, Q, K, VT, Npad, s));
         SG_TRY(mlg_attention_varlen(Q, K, VT, CTX, 256, Npad, 4, TASKS + (cross ? nseg : 0),
                                     OUTOFF + (cross ? nseg : 0), nseg, maxq, s));
         SG_TRY(mlg_lg_ffn(CTX, X, CAT, 512, Npad, w.layer[l], s, nullptr, 1));

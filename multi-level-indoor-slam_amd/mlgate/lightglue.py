@@ -30,6 +30,15 @@ def pack_kstep(w):
     return np.ascontiguousarray(w.reshape(n, k // 16, 16).transpose(1, 0, 2))
 
 
+def pack_rotary(ecos, esin):
+    """Rotary factors cos / sin [Npad, 32] (token row, frequency) -> the projections' tile
+    layout (csrc/common.h lg_fac4, include/mlgate.h mlg_op_lg_proj): [Npad / 64, 16, 64, 4]
+    with (cos 2p, cos 2p + 1, sin 2p, sin 2p + 1) for row r, frequency pair p."""
+    n = ecos.shape[0]
+    cs = torch.stack([ecos.reshape(n // 64, 64, 16, 2), esin.reshape(n // 64, 64, 16, 2)], 3)  # [T, 64, 16, 2, 2]
+    return cs.reshape(n // 64, 64, 16, 4).permute(0, 2, 1, 3).contiguous()
+
+
 class LightGlueGPU:
     """Batched LightGlue(features='superpoint') on the HIP device."""
 

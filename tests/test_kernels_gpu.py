@@ -258,7 +258,7 @@ def test_lg_ffn_fused(dev, M):
 def test_lg_proj(dev, self_block):
     """LightGlue projections (lg_proj.hip) vs float32 torch on the same bf16 operands:
     q / k (+ rotary) in [4][Npad][64], v in the tiled V^T; dead rows zero."""
-    from mlgate.lightglue import pack_kstep
+    from mlgate.lightglue import pack_kstep, pack_rotary
     Npad, H = 192, 4
     N = 768 if self_block else 512
     g = torch.Generator().manual_seed(N)
@@ -270,13 +270,13 @@ def test_lg_proj(dev, self_block):
     live = (torch.rand(Npad, generator=g) > 0.2).to(torch.uint8)
     xc = torch.zeros(Npad, 512, dtype=torch.bfloat16)
     xc[:, :256] = x
-    d = {k: v.to(dev) for k, v in dict(xc=xc, b=b, ec=ec, es=es, live=live).items()}
+    d = {k: v.to(dev) for k, v in dict(xc=xc, b=b, ef=pack_rotary(ec, es), live=live).items()}
     Wd = torch.from_numpy(pack_kstep(W.float().numpy())).to(torch.bfloat16).to(dev)
     Q = torch.full((H, Npad, 64), 7.0, dtype=torch.bfloat16, device=dev)
     K = torch.full((H, Npad, 64), 7.0, dtype=torch.bfloat16, device=dev)
     Vt = torch.full((H, Npad // 64, 64, 64), 7.0, dtype=torch.bfloat16, device=dev)
-    _native.check(_native.lib().mlg_op_lg_proj(int(self_block), P(d["xc"]), 512, P(Wd), P(d["b"]), P(d["ec"]),
-                                               P(d["es"]), P(d["live"]), P(Q), P(K), P(Vt), Npad, S(dev)), "lg_proj")
+    _native.check(_native.lib().mlg_op_lg_proj(int(self_block), P(d["xc"]), 512, P(Wd), P(d["b"]), P(d["ef"]),
+                                               None, P(d["live"]), P(Q), P(K), P(Vt), Npad, S(dev)), "lg_proj")
     torch.cuda.synchronize()
     y = x.float() @ W.float().T + b  # [Npad, N]
     heads = lambda t: t.view(Npad, H, 64).transpose(0, 1)  # noqa: E731
@@ -299,7 +299,7 @@ def test_lg_proj(dev, self_block):
 def test_lightglue_kernels_deterministic(dev):
     """The LightGlue projection, attention and fused block-tail kernels are bit-for-bit
     deterministic run to run on the same inputs (no races, no order-dependent sums)."""
-    from mlgate.lightglue import pack_kstep
+    from mlgate.lightglue import pack_kstep, pack_rotary
     L = _native.lib()
     Npad, H = 8192, 4
     g = torch.Generator().manual_seed(11)
@@ -310,13 +310,14 @@ def test_lightglue_kernels_deterministic(dev):
     b = torch.randn(768, generator=g) * 0.1
     ang = torch.rand(Npad, 32, generator=g) * 6.3
     live = (torch.rand(Npad, generator=g) > 0.1).to(torch.uint8)
-    d = {k: v.to(dev) for k, v in dict(xc=xc, W=W, b=b, ec=torch.cos(ang), es=torch.sin(ang), live=live).items()}
+    d = {k: v.to(dev) for k, v in dict(xc=xc, W=W, b=b, ef=pack_rotary(torch.cos(ang), torch.sin(ang)),
+                                       live=live).items()}
     outs = []
     for _ in range(3):
         Q = torch.zeros(H, Npad, 64, dtype=torch.bfloat16, device=dev)
         K = torch.zeros_like(Q)
         Vt = torch.zeros(H, Npad // 64, 64, 64, dtype=torch.bfloat16, device=dev)
-        _native.check(L.mlg_op_lg_proj(1, P(d["xc"]), 512, P(d["W"]), P(d["b"]), P(d["ec"]), P(d["es"]),
+        _native.check(L.mlg_op_lg_proj(1, P(d["xc"]), 512, P(d["W"]), P(d["b"]), P(d["ef"]), None,
                                        P(d["live"]), P(Q), P(K), P(Vt), Npad, S(dev)), "proj")
         tasks = torch.tensor([[s, 2048, s, 2048] for s in range(0, Npad, 2048)], dtype=torch.int32, device=dev)
         oo = tasks[:, 0].contiguous()

@@ -51,7 +51,8 @@ class Case:
         self.W = bf16(torch.from_numpy(pack_kstep((torch.randn(768, 256, generator=g) / 16).numpy()))).to(dev)
         self.b = (torch.randn(768, generator=g) * 0.1).to(dev)
         ang = torch.rand(rows, 32, generator=g) * 6.3
-        self.ec, self.es = torch.cos(ang).to(dev), torch.sin(ang).to(dev)
+        from mlgate.lightglue import pack_rotary
+        self.ec, self.es = pack_rotary(torch.cos(ang), torch.sin(ang)).to(dev), None
         self.live = (torch.rand(rows, generator=g) > 0.1).to(torch.uint8).to(dev)
         self.Q = torch.zeros(H, rows, 64, dtype=torch.bfloat16, device=dev)
         self.K = torch.zeros_like(self.Q)
@@ -71,7 +72,7 @@ class Case:
         self.L = _native.lib()
 
     def proj(self, s):
-        _native.check(self.L.mlg_op_lg_proj(1, P(self.xc0), 512, P(self.W), P(self.b), P(self.ec), P(self.es),
+        _native.check(self.L.mlg_op_lg_proj(1, P(self.xc0), 512, P(self.W), P(self.b), P(self.ec), None,
                                             P(self.live), P(self.Q), P(self.K), P(self.Vt), self.rows,
                                             torch.cuda.current_stream(self.dev).cuda_stream), "proj")
         return torch.cat([self.Q.view(-1), self.K.view(-1), self.Vt.view(-1)])

@@ -37,7 +37,8 @@ def main():
     W = (torch.randn(768 * 256, device=dev, generator=g) * 0.06).to(torch.bfloat16)
     b = torch.randn(768, device=dev, generator=g) * 0.1
     ang = torch.rand(M, 32, device=dev, generator=g) * 6.283
-    ec, es = torch.cos(ang), torch.sin(ang)
+    from mlgate.lightglue import pack_rotary
+    ec = pack_rotary(torch.cos(ang), torch.sin(ang))
     live = (torch.rand(M, device=dev, generator=g) < 0.85).to(torch.uint8)
     res = {"tokens": M}
     for name, sb in (("self", 1), ("cross", 0)):
@@ -45,7 +46,7 @@ def main():
         K = torch.full_like(Q, 7)
         Vt = torch.full_like(Q, 7)
         fn = lambda: L.mlg_op_lg_proj(sb, p(cat), 512, p(W), p(b), p(ec) if sb else None,  # noqa: E731
-                                      p(es) if sb else None, p(live), p(Q), p(K) if sb else None, p(Vt), M, st)
+                                      None, p(live), p(Q), p(K) if sb else None, p(Vt), M, st)
         assert fn() == 0
         torch.cuda.synchronize()
         h = hashlib.sha1()
