@@ -1272,7 +1272,10 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
     // MFMA's rate) or the exact-f32 MFMA (MLG_LF_SIM_SPLIT=0)
     bf16_t* CS = (bf16_t*)at(ML.csplit);
     const int Lpad = (L + 255) / 256 * 256;
-    if (MLG_LF_SIM_SPLIT) {
+    // (the split GEMM's staged f32 rows are written as 16-B pieces: S rows of L % 4 != 0
+    // cells -- e.g. 720 x 536 frames, L = 6030 -- take the exact-f32 path)
+    const bool split = MLG_LF_SIM_SPLIT && (L % 4) == 0;
+    if (split) {
         const long rows = (long)2 * P * L;
         hipLaunchKernelGGL(k_lf_split_rows, dim3((unsigned)((rows * 64 + 255) / 256)), dim3(256), 0, s, bc.x, rows, CS);
         MLG_LAUNCH_CHECK();
@@ -1282,7 +1285,7 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
     for (int p = 0; p < P; ++p) {
         const float* f0 = bc.x + (size_t)p * L * 256;
         const float* f1 = bc.x + ((size_t)P + p) * L * 256;
-        if (MLG_LF_SIM_SPLIT)
+        if (split)
             LF_TRY(mlg_gemm_sim_split_loftr(CS + (size_t)p * L * 512, CS + ((size_t)P + p) * L * 512, L, Lpad, 256, S,
                                             L, L, s));
         else
