@@ -177,7 +177,7 @@ __device__ __forceinline__ void zero(f32x16 (&acc)[NT][MT]) {
 // PERSIST = true (MLG_FFN_GRID = workgroups per CU): the grid walks the tiles with stride
 // gridDim.x; the compiler hoists lane addresses out of the tile loop and spills 436 B
 // per lane around it: 3.66 vs 2.94 ms per 2 M-token launch and 4.29 vs 3.20 s of FFN per
-// bench step on one box (tools/gpu_ab_ffn_proj.sh), so it is off.
+// bench step on one box (tools/archive/gpu_ab_ffn_proj.sh), so it is off.
 // R token rows per workgroup of NW waves: <64, 4> (two workgroups per CU) or <128, 8>
 // (one per CU: every weight fragment fetched from L2 feeds twice the MFMAs).
 //

@@ -556,7 +556,7 @@ int mlg_lg_proj(bool self_block, const bf16_t* xcopy, int ldx, const bf16_t* W, 
     if (Npad <= 0 || (Npad % 64) || ldx < 256 || (ldx % 8)) return MLG_EINVAL;
     // Build-time A/B knob: MLG_PROJ_MT = 32-token m-tiles per workgroup (2: 64 tokens, 4: 128).
     // 128-token tiles halve the weight bytes per FLOP but measured 2-7 % slower on one
-    // box (tools/gpu_ab_ffn_proj.sh: self 2.39 vs 2.35 ms, cross 1.27 vs 1.19 ms at 2 M
+    // box (tools/archive/gpu_ab_ffn_proj.sh: self 2.39 vs 2.35 ms, cross 1.27 vs 1.19 ms at 2 M
     // tokens): the weight stream is not what bounds this kernel.
     constexpr int mt = MLG_PROJ_MT == 4 ? 4 : 2;
     // default: the weights-resident persistent form; MLG_PROJ_RES=0 builds the tiled form

@@ -13,3 +13,5 @@ tools/gpu_ab.sh ab_base_r05 r05f_lg 2 -- tools/lg_bench.py --pairs 2048 --iters 
 cat "$O/r05f_lg_ab.txt"
 tools/gpu_ab.sh ab_base_r05 r05f_lf 2 -- tools/loftr_bench.py --frames 64 --pairs 64 > "$O/r05f_lf_ab.txt" 2>&1 || { cat "$O/r05f_lf_ab.txt"; exit 1; }
 cat "$O/r05f_lf_ab.txt"
+timeout -k 10 420 python -u bench.py --steps 3 --warmup 2 > "$O/r05f_bench.json" 2> "$O/r05f_bench.err" || { tail -5 "$O/r05f_bench.err"; exit 1; }
+tail -c 1500 "$O/r05f_bench.json"
