@@ -76,6 +76,12 @@ __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_ca
 #ifndef MLG_FFN_RING1
 #define MLG_FFN_RING1 2
 #endif
+// timing-probe builds only (results wrong; 0 in the product), bits drop one phase each:
+// 1 GELU polynomial (the normalised value passes), 2 LayerNorm statistics (mean 0,
+// rstd 1), 4 msg GEMM, 8 ffn1 GEMM, 16 ffn2 GEMM, 32 residual row pass, 64 tile load
+#ifndef MLG_FFN_PROBE
+#define MLG_FFN_PROBE 0
+#endif
 #ifndef MLG_FFN_RING2
 #define MLG_FFN_RING2 4
 #endif
@@ -229,7 +235,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
         // 0. tile -> LDS: the bf16 copy of x (written by the previous block) into chunks
         //    0..31, ctx into chunks 32..63; 32 lanes x 16 B = one 512-B row per half-wave,
         //    rows clamped to M - 1 (never stored)
-        {
+        if (!(MLG_FFN_PROBE & 64)) {
             constexpr int PASSES = R / (2 * NW);
             uint4 rx[PASSES], rc[PASSES];
             const int c = lane & 31;
@@ -253,7 +259,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
         {
             f32x16 acc[NT1][MT];
             zero(acc);
-            gemm_phase<NT1, MT, RING1>(w.Wout, 256, 32 * NT1 * wave, 4, 32, lds, acc);
+            if (!(MLG_FFN_PROBE & 4)) gemm_phase<NT1, MT, RING1>(w.Wout, 256, 32 * NT1 * wave, 4, 32, lds, acc);
             __syncthreads();  // every wave has read the ctx half
             float mean1[MT], rstd1[MT];
             if constexpr (LOFTR) {
@@ -330,7 +336,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
         {
             f32x16 acc[NT2][MT];
             zero(acc);
-            gemm_phase<NT2, MT, RING>(w.Wf1, 512, 32 * NT2 * wave, 8, 0, lds, acc);
+            if (!(MLG_FFN_PROBE & 8)) gemm_phase<NT2, MT, RING>(w.Wf1, 512, 32 * NT2 * wave, 8, 0, lds, acc);
     #pragma unroll
             for (int t = 0; t < NT2; ++t)
     #pragma unroll
@@ -348,7 +354,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
     #pragma unroll
             for (int mt = 0; mt < MT; ++mt) { mean[mt] = 0.f; rstd[mt] = 1.f; }
     #pragma unroll
-            for (int mt = 0; mt < MT && !relu; ++mt) {
+            for (int mt = 0; mt < MT && !relu && !(MLG_FFN_PROBE & 2); ++mt) {
                 float sum = 0.f;
     #pragma unroll
                 for (int t = 0; t < NT2; ++t)
@@ -359,7 +365,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             }
             __syncthreads();  // also: every wave has finished reading [x | msg]
     #pragma unroll
-            for (int mt = 0; mt < MT && !relu; ++mt) {
+            for (int mt = 0; mt < MT && !relu && !(MLG_FFN_PROBE & 2); ++mt) {
                 float sum = 0.f;
     #pragma unroll
                 for (int v = 0; v < NW; ++v) sum += red[0][v][32 * mt + col];
@@ -377,7 +383,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             }
             __syncthreads();
     #pragma unroll
-            for (int mt = 0; mt < MT && !relu; ++mt) {
+            for (int mt = 0; mt < MT && !relu && !(MLG_FFN_PROBE & 2); ++mt) {
                 float q = 0.f;
     #pragma unroll
                 for (int v = 0; v < NW; ++v) q += red[1][v][32 * mt + col];
@@ -404,7 +410,12 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                     for (int mt = 0; mt < MT; ++mt) {
                         const f32x16& a = acc[t][mt];
                         float y0, y1, y2, y3;
-                        if (relu) {
+                        if (MLG_FFN_PROBE & 1) {
+                            y0 = (a[4 * g] - mean[mt]) * rstd[mt] * lg.x + lb.x;
+                            y1 = (a[4 * g + 1] - mean[mt]) * rstd[mt] * lg.y + lb.y;
+                            y2 = (a[4 * g + 2] - mean[mt]) * rstd[mt] * lg.z + lb.z;
+                            y3 = (a[4 * g + 3] - mean[mt]) * rstd[mt] * lg.w + lb.w;
+                        } else if (relu) {
                             y0 = fmaxf(a[4 * g], 0.f);
                             y1 = fmaxf(a[4 * g + 1], 0.f);
                             y2 = fmaxf(a[4 * g + 2], 0.f);
@@ -441,7 +452,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             __builtin_amdgcn_sched_barrier(0);
             f32x16 acc[NT1][MT];
             zero(acc);
-            gemm_phase<NT1, MT, RING1>(w.Wf2, 256, 32 * NT1 * wave, 8, 0, lds, acc);
+            if (!(MLG_FFN_PROBE & 16)) gemm_phase<NT1, MT, RING1>(w.Wf2, 256, 32 * NT1 * wave, 8, 0, lds, acc);
 #if MLG_FFN_XR_WAIT
             __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): the residual rows xr have landed
 #endif
@@ -473,7 +484,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             for (int i = 0; i < R / NW; ++i) {
                 const int r = wave * (R / NW) + i, m = m0 + r;
                 pz[i] = pa[i] = 0.f;
-                if (m >= M) continue;  // wave-uniform
+                if (m >= M || (MLG_FFN_PROBE & 32)) continue;  // wave-uniform
                 const float4 y = *reinterpret_cast<const float4*>(lds + r * 1024 + ((lane ^ (r & 15)) << 4));
                 float4* px = reinterpret_cast<float4*>(X + (size_t)m * 256) + lane;
                 float4 x = xr[i];

@@ -24,9 +24,10 @@
 //                (one wave per segment tile and head: KV, ksum wave-uniform);
 //     merge GEMM -> k_lf_ln (norm1) -> bf16 into CAT's second half; MLP GEMMs
 //     (512 -> 512 ReLU, 512 -> 256); k_lf_ln_res: x += norm2(.), new bf16 copy;
-//   dual softmax: S = f0 . f1^T on the exact-f32 MFMA (knn.hip), sim = S / 256 / 0.1;
-//   k_lf_rowstats / k_lf_colpart + k_lf_colfin (max, sum exp; columns in row chunks merged
-//   in chunk order); k_lf_rowbest (row max of conf, first argmax) / k_lf_colmaxpart +
+//   dual softmax: S = f0 . f1^T from split-bf16 operands (gemm_bf16.hip; exact-f32 MFMA
+//   when L % 4 != 0), sim = S / 256 / 0.1; k_lf_stats (column max, sum exp per row chunk,
+//   row block maxima) + k_lf_colfin (chunks merged in chunk order); k_lf_rowbest (row sum,
+//   then row max of conf, first argmax) / k_lf_colmaxpart +
 //   k_lf_colmaxfin (column max of conf) with conf recomputed identically in both;
 //   k_lf_select: conf > 0.2, 2-cell border, mutual max, compacted in row order;
 //   fine: k_lf_windows gathers the 5x5 windows (stride 4, zero padding) of the 1/2 maps
@@ -517,6 +518,48 @@ __global__ __launch_bounds__(256) void k_lf_colpart(const float* __restrict__ S,
     pz[(size_t)c * L + col] = z;
 }
 
+// k_lf_colpart plus the row maxima of the same tile, so that one read of S yields both
+// (MLG_LF_STATS1): after the column statistics the 64 x 64 (row x lane) values of a wave
+// fold in six butterfly steps -- step b exchanges half of the rows with lane ^ b and keeps
+// the max -- until lane l holds row l's max over the wave's 64 columns; the four waves
+// meet in LDS and prm[column block][row] gets the block's max.  Max is exact in any order,
+// so rmax = max over blocks equals k_lf_rowstats' bit for bit.
+__global__ __launch_bounds__(256) void k_lf_stats(const float* __restrict__ S, int L, float* __restrict__ pm,
+                                                  float* __restrict__ pz, float* __restrict__ prm) {
+    __shared__ float red[4][LF_RCH];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
+    const int r0 = c * LF_RCH, n = min(L - r0, LF_RCH);
+    const bool ok = col < L;
+    float v[LF_RCH], m = -INFINITY, z = 0.f;
+#pragma unroll
+    for (int i = 0; i < LF_RCH; ++i) {
+        v[i] = (ok && i < n) ? S[(size_t)(r0 + i) * L + col] : -INFINITY;
+        m = fmaxf(m, v[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < LF_RCH; ++i)
+        if (i < n) z += expf(v[i] - m);
+    if (ok) {
+        pm[(size_t)c * L + col] = m;
+        pz[(size_t)c * L + col] = z;
+    }
+#pragma unroll
+    for (int h = 32; h >= 1; h >>= 1) {
+        const bool up = (lane & h) != 0;
+#pragma unroll
+        for (int i = 0; i < h; ++i) {
+            const float keep = up ? v[h + i] : v[i], send = up ? v[i] : v[h + i];
+            v[i] = fmaxf(keep, __shfl_xor(send, h, 64));
+        }
+    }
+    red[wave][lane] = v[0];
+    __syncthreads();
+    if (wave == 0 && lane < n)
+        prm[(size_t)blockIdx.x * L + r0 + lane] =
+            fmaxf(fmaxf(red[0][lane], red[1][lane]), fmaxf(red[2][lane], red[3][lane]));
+}
+
 // 64 columns x 4 chunk groups per workgroup (group g: chunks g, g + 4, ..): the chunk
 // loads of a column run in parallel; the four partials combine in group order
 __global__ __launch_bounds__(256) void k_lf_colfin(const float* __restrict__ pm, const float* __restrict__ pz, int L,
@@ -547,14 +590,54 @@ __global__ __launch_bounds__(256) void k_lf_colfin(const float* __restrict__ pm,
     }
 }
 
-__global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S, int L, const float* __restrict__ rmax,
-                                                    const float* __restrict__ rsum, const float* __restrict__ cmax,
-                                                    const float* __restrict__ csum, const float* __restrict__ ckey,
-                                                    float* __restrict__ bval, int32_t* __restrict__ bidx) {
+// SELF (MLG_LF_STATS1): the row max comes from k_lf_stats' block maxima prm[ncb][L] and
+// the row sum is formed here from the registers that hold the row anyway (the same
+// per-lane order and wave sum as k_lf_rowstats, so the same bits); rmax / rsum / rkey are
+// written for k_lf_colmaxpart.  Otherwise they are read (k_lf_rowstats ran before).
+template <bool SELF>
+__global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S, int L, float* __restrict__ rmax,
+                                                    float* __restrict__ rsum, float* __restrict__ rkey,
+                                                    const float* __restrict__ prm, int ncb,
+                                                    const float* __restrict__ cmax, const float* __restrict__ csum,
+                                                    const float* __restrict__ ckey, float* __restrict__ bval,
+                                                    int32_t* __restrict__ bidx) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= L) return;
     const float* s = S + (size_t)row * L;
-    const float rm = rmax[row], rz = rsum[row];
+    float rm, rz;
+    const bool reg = (L & 3) == 0 && L <= 256 * LF_ROWREG;
+    float4 v[LF_ROWREG];
+    if (reg) {
+        const float4* s4 = reinterpret_cast<const float4*>(s);
+#pragma unroll
+        for (int k = 0; k < LF_ROWREG; ++k)
+            if (lane + 64 * k < L / 4) v[k] = s4[lane + 64 * k];
+    }
+    if constexpr (SELF) {
+        float m = -INFINITY;
+        for (int b = lane; b < ncb; b += 64) m = fmaxf(m, prm[(size_t)b * L + row]);
+        m = wave_max(m);
+        float z = 0.f;
+        if (reg) {
+#pragma unroll
+            for (int k = 0; k < LF_ROWREG; ++k)
+                if (lane + 64 * k < L / 4)
+                    z += expf(v[k].x - m) + expf(v[k].y - m) + expf(v[k].z - m) + expf(v[k].w - m);
+        } else {
+            for (int j = lane; j < L; j += 64) z += expf(s[j] - m);
+        }
+        z = wave_sum(z);
+        rm = m;
+        rz = z;
+        if (lane == 0) {
+            rmax[row] = m;
+            rsum[row] = z;
+            rkey[row] = m + logf(z);
+        }
+    } else {
+        rm = rmax[row];
+        rz = rsum[row];
+    }
     float bv = -1.f;
     int bi = 0x7fffffff;
     auto take = [&](float x, int j) {
@@ -562,15 +645,12 @@ __global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S,
         if (c > bv || (c == bv && j < bi)) { bv = c; bi = j; }
     };
     float kb = -INFINITY;
-    if ((L & 3) == 0 && L <= 256 * LF_ROWREG) {
-        const float4* s4 = reinterpret_cast<const float4*>(s);
+    if (reg) {
         const float4* k4 = reinterpret_cast<const float4*>(ckey);
-        float4 v[LF_ROWREG];
 #pragma unroll
         for (int k = 0; k < LF_ROWREG; ++k) {
             const int j = lane + 64 * k;
             if (j < L / 4) {
-                v[k] = s4[j];
                 const float4 ck = k4[j];
                 kb = fmaxf(kb, fmaxf(fmaxf(2.f * v[k].x - ck.x, 2.f * v[k].y - ck.y),
                                      fmaxf(2.f * v[k].z - ck.z, 2.f * v[k].w - ck.w)));
@@ -958,6 +1038,12 @@ namespace {
 #ifndef MLG_LF_SIM_SPLIT
 #define MLG_LF_SIM_SPLIT 1
 #endif
+// Dual softmax in three reads of S: k_lf_stats (column statistics + row block maxima) and
+// a self-normalising k_lf_rowbest replace k_lf_rowstats + k_lf_colpart; 0 builds the
+// four-read sequence (A/B arm).  Both give the same bits.
+#ifndef MLG_LF_STATS1
+#define MLG_LF_STATS1 1
+#endif
 
 // nn.Linear weight [N][K] bf16 -> k-step-major [K / 16][N][16] (lg_ffn.hip's layout)
 __global__ void k_lf_pack_kstep(const bf16_t* __restrict__ w, int N, int K, bf16_t* __restrict__ out) {
@@ -1135,7 +1221,7 @@ int pack_tails(const mlg_loftr_weights& w, char* base, TailW (&tw)[8], hipStream
 struct MatchLayout {
     size_t cx, ccat, cqkv, cmsg, ct, ch, ckv, cks, ckvp;  // coarse transformer (rows 2 P L, d 256)
     size_t fx, fcat, fqkv, fmsg, ft, fh, fkv, fks;  // fine transformer (rows 2 C 25, d 128)
-    size_t win, crow, cd, cm, S, csplit, rmax, rsum, rkey, cmax, csum, ckey, pm, pz, bval, bidx, cbest, mi, mj, mconf, cnt,
+    size_t win, crow, cd, cm, S, csplit, rmax, rsum, rkey, cmax, csum, ckey, pm, pz, prm, bval, bidx, cbest, mi, mj, mconf, cnt,
         frm, mp, ms, tails, total;
 };
 
@@ -1184,6 +1270,7 @@ MatchLayout match_layout(int P, int L) {
     const size_t nrch = (size_t)(L + LF_RCH - 1) / LF_RCH;
     M.pm = take(nrch * L * 4);
     M.pz = take(nrch * L * 4);
+    M.prm = take((size_t)(L + 255) / 256 * L * 4);
     M.bval = take((size_t)L * 4);
     M.bidx = take((size_t)L * 4);
     M.cbest = take((size_t)L * 4);
@@ -1236,7 +1323,8 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
     float* ckey = (float*)at(ML.ckey);
     float* pm = (float*)at(ML.pm);
     float* pz = (float*)at(ML.pz);
-    const int nrch = (L + LF_RCH - 1) / LF_RCH;
+    float* prm = (float*)at(ML.prm);
+    const int nrch = (L + LF_RCH - 1) / LF_RCH, ncb = (L + 255) / 256;
     float* bval = (float*)at(ML.bval);
     int32_t* bidx = (int32_t*)at(ML.bidx);
     float* cbest = (float*)at(ML.cbest);
@@ -1290,11 +1378,18 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
                                             L, L, s));
         else
             LF_TRY(mlg_similarity_f32_loftr(f0, L, f1, L, 256, S, L, s));
-        hipLaunchKernelGGL(k_lf_rowstats, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, rkey);
-        hipLaunchKernelGGL(k_lf_colpart, dim3((L + 255) / 256, nrch), dim3(256), 0, s, S, L, pm, pz);
-        hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum, ckey);
-        hipLaunchKernelGGL(k_lf_rowbest, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, cmax, csum, ckey, bval,
-                           bidx);
+        if (MLG_LF_STATS1) {  // three reads of S: stats, rowbest, colmaxpart
+            hipLaunchKernelGGL(k_lf_stats, dim3(ncb, nrch), dim3(256), 0, s, S, L, pm, pz, prm);
+            hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum, ckey);
+            hipLaunchKernelGGL(k_lf_rowbest<true>, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, rkey, prm,
+                               ncb, cmax, csum, ckey, bval, bidx);
+        } else {
+            hipLaunchKernelGGL(k_lf_rowstats, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, rkey);
+            hipLaunchKernelGGL(k_lf_colpart, dim3(ncb, nrch), dim3(256), 0, s, S, L, pm, pz);
+            hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum, ckey);
+            hipLaunchKernelGGL(k_lf_rowbest<false>, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, rkey,
+                               nullptr, 0, cmax, csum, ckey, bval, bidx);
+        }
         hipLaunchKernelGGL(k_lf_colmaxpart, dim3((L + 255) / 256, nrch), dim3(256), 0, s, S, L, rmax, rsum, rkey, cmax,
                            csum, pm);
         hipLaunchKernelGGL(k_lf_colmaxfin, dim3((L + 255) / 256), dim3(256), 0, s, pm, L, nrch, cbest);

@@ -1,6 +1,7 @@
 """LoFTR (configs[4]) timing on the GPU box: backbone per keyframe and matching per pair
 at 640x480 on synthetic revisit pairs, HIP-event timed (python tools/loftr_bench.py)."""
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -12,6 +13,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "multi-level-indoor-slam_amd")]
 from mlgate import synthetic  # noqa: E402
 from mlgate.loftr import LoFTRGPU  # noqa: E402
+
+
+def digest(n, k0, k1, cf):
+    """hash of every pair's matches (counts, keypoints, confidences): bit-identity of A/B arms"""
+    h = hashlib.sha256(n.cpu().numpy().tobytes())
+    for p, c in enumerate(n.tolist()):
+        for t in (k0[p, :c], k1[p, :c], cf[p, :c]):
+            h.update(t.contiguous().cpu().numpy().tobytes())
+    return h.hexdigest()[:16]
 
 
 def main():
@@ -35,7 +45,7 @@ def main():
         coarse, fine = lf.features(fr)
     e[1].record()
     for _ in range(a.iters):
-        n, *_ = lf.match_device(coarse, fine, 480, 640, [p for p, _ in pairs], [q for _, q in pairs])
+        n, k0, k1, cf = lf.match_device(coarse, fine, 480, 640, [p for p, _ in pairs], [q for _, q in pairs])
     e[2].record()
     torch.cuda.synchronize()
     feat_ms = e[0].elapsed_time(e[1]) / a.iters
@@ -48,7 +58,7 @@ def main():
                       "backbone_gflop_per_frame": round(gflop_feat, 1),
                       "backbone_tflops": round(gflop_feat * a.frames / feat_ms, 1),
                       "match_ms_per_pair": round(match_ms / len(pairs), 3),
-                      "matches_mean": float(n.float().mean())}), flush=True)
+                      "matches_mean": float(n.float().mean()), "digest": digest(n, k0, k1, cf)}), flush=True)
 
 
 if __name__ == "__main__":
