@@ -82,6 +82,17 @@ __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_ca
 #ifndef MLG_FFN_PROBE
 #define MLG_FFN_PROBE 0
 #endif
+// Phase stagger of the two co-resident workgroups of a CU: every tile runs the same
+// sequence (GEMM, VALU-heavy LayerNorm + GELU, GEMM), so two workgroups that start
+// together stay in step and meet in the same phase.  The second resident set (mode 1:
+// blocks [n_cu, 2 n_cu); mode 2: odd blocks below 2 n_cu) first sleeps MLG_FFN_STAGGER x
+// 127 x 64 cycles; later tiles inherit the offset.  Arithmetic unchanged.
+#ifndef MLG_FFN_STAGGER
+#define MLG_FFN_STAGGER 0
+#endif
+#ifndef MLG_FFN_STAGGER_MODE
+#define MLG_FFN_STAGGER_MODE 1
+#endif
 #ifndef MLG_FFN_RING2
 #define MLG_FFN_RING2 4
 #endif
@@ -228,6 +239,12 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             s_bout[i] = LOFTR ? 0.f : w.bout[i];
             s_bf2[i] = LOFTR ? 0.f : w.bf2[i];
         }
+    }
+    if constexpr (MLG_FFN_STAGGER > 0 && !PERSIST) {
+        const unsigned b = blockIdx.x;
+        const bool late = MLG_FFN_STAGGER_MODE == 1 ? (b >= 256u && b < 512u) : (b < 512u && (b & 1u));
+        if (late)
+            for (int i = 0; i < MLG_FFN_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
     }
     const int ntiles = (M + R - 1) / R;
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {

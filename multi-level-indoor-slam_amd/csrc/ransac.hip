@@ -880,6 +880,55 @@ __device__ int real_roots10(double (&c)[11], double (&roots)[10], int r, int gl)
     return nn;
 }
 
+// The 5-point sample's null space (Householder QR) one hypothesis per lane, ahead of
+// k_ransac_hyp5 (MLG_RS_NULL_SPLIT): inside hyp5's 16-lane groups all 16 lanes ran the
+// same QR, 4 hypotheses per wave.  The basis (36 doubles) and the rank flag (slot 36)
+// go to the hypothesis' own model slot, which hyp5 reads before it writes the models.
+#ifndef MLG_RS_NULL_SPLIT
+#define MLG_RS_NULL_SPLIT 1
+#endif
+__device__ __forceinline__ bool hyp5_active(const PairInfo& pi, int h, int H, const int32_t* __restrict__ nsub, int p) {
+    return h < H && (pi.mode == 5 ? h == 0 : h < nsub[p]);
+}
+
+__device__ __forceinline__ bool hyp5_null(const PairInfo& pi, const double4* __restrict__ ptsn,
+                                          const int32_t* __restrict__ subsets, int p, int H, int h,
+                                          double (&Nb)[4][9]) {
+    double q1[5][2], q2[5][2];
+    for (int i = 0; i < 5; ++i) {
+        const int id = pi.mode == 5 ? i : subsets[((size_t)p * H + h) * 7 + i];
+        const double4 q = ptsn[pi.start + id];
+        q1[i][0] = q.x; q1[i][1] = q.y; q2[i][0] = q.z; q2[i][1] = q.w;
+    }
+    double A[5][9];
+    for (int i = 0; i < 5; ++i) {
+        const double x1 = q1[i][0], y1 = q1[i][1], x2 = q2[i][0], y2 = q2[i][1];
+        A[i][0] = x2 * x1; A[i][1] = x2 * y1; A[i][2] = x2;
+        A[i][3] = y2 * x1; A[i][4] = y2 * y1; A[i][5] = y2;
+        A[i][6] = x1;      A[i][7] = y1;      A[i][8] = 1.0;
+    }
+    return null_space5_reg(A, Nb);
+}
+
+__global__ __launch_bounds__(64) void k_ransac_null5(const PairInfo* __restrict__ info, const double4* __restrict__ ptsn,
+                                                     int H, const int32_t* __restrict__ subsets,
+                                                     const int32_t* __restrict__ nsub, double* __restrict__ models,
+                                                     int h0, int hn, const uint8_t* __restrict__ done) {
+    const int p = blockIdx.y;
+    const int h = h0 + blockIdx.x * 64 + threadIdx.x;
+    if (h >= h0 + hn || (done && done[p])) return;
+    const PairInfo pi = info[p];
+    if (!(pi.mode == 1 || pi.mode == 5) || !hyp5_active(pi, h, H, nsub, p)) return;
+    double Nb[4][9];
+    const bool ok = hyp5_null(pi, ptsn, subsets, p, H, h, Nb);
+    double* o = models + ((size_t)p * H + h) * MAXSOL * 9;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) o[9 * a + k] = Nb[a][k];
+    o[36] = ok ? 1.0 : 0.0;
+}
+
 __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict__ info,
                                                      const double4* __restrict__ ptsn, int H,
                                                      const int32_t* __restrict__ subsets,
@@ -894,30 +943,23 @@ __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict_
     const PairInfo pi = info[p];
     const bool ess = pi.mode == 1 || pi.mode == 5;
     // whole groups are active or not (shuffles stay inside a group)
-    const bool act = ess && h < H && (pi.mode == 5 ? h == 0 : h < nsub[p]);
+    const bool act = ess && hyp5_active(pi, h, H, nsub, p);
     if (!ess) return;  // uniform per block (one pair per blockIdx.y)
     bool ok = act;
     if (act) {
-        double q1[5][2], q2[5][2];
-        for (int i = 0; i < 5; ++i) {
-            const int id = pi.mode == 5 ? i : subsets[((size_t)p * H + h) * 7 + i];
-            const double4 q = ptsn[pi.start + id];
-            q1[i][0] = q.x; q1[i][1] = q.y; q2[i][0] = q.z; q2[i][1] = q.w;
-        }
-        double A[5][9];
-        for (int i = 0; i < 5; ++i) {
-            const double x1 = q1[i][0], y1 = q1[i][1], x2 = q2[i][0], y2 = q2[i][1];
-            A[i][0] = x2 * x1; A[i][1] = x2 * y1; A[i][2] = x2;
-            A[i][3] = y2 * x1; A[i][4] = y2 * y1; A[i][5] = y2;
-            A[i][6] = x1;      A[i][7] = y1;      A[i][8] = 1.0;
-        }
-        double Nb[4][9];
-        ok = null_space5_reg(A, Nb);
-        if (r == 0)
+        if (MLG_RS_NULL_SPLIT) {  // k_ransac_null5 left the basis in this hypothesis' model slot
+            const double* nb = models + ((size_t)p * H + h) * MAXSOL * 9;
+            for (int i = r; i < 36; i += 16) snb[g][i / 9][i % 9] = nb[i];
+            ok = nb[36] != 0.0;
+        } else {
+            double Nb[4][9];
+            ok = hyp5_null(pi, ptsn, subsets, p, H, h, Nb);
+            if (r == 0)
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
+                for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int k = 0; k < 9; ++k) snb[g][a][k] = Nb[a][k];
+                    for (int k = 0; k < 9; ++k) snb[g][a][k] = Nb[a][k];
+        }
     }
     __syncthreads();
 #if defined(RS_ABLATE) && RS_ABLATE == 3
@@ -1717,6 +1759,11 @@ int mlg_ransac_run(const float* kp1, const float* kp2, const int32_t* offs, int 
         hipLaunchKernelGGL(k_ransac_hyp, dim3((hn + 63) / 64, P), dim3(64), 0, s, info, ptsn, H, seed, subsets, nsub,
                            models, nsol, h0, skip);
         MLG_LAUNCH_CHECK();
+        if (MLG_RS_NULL_SPLIT) {
+            hipLaunchKernelGGL(k_ransac_null5, dim3((hn + 63) / 64, P), dim3(64), 0, s, info, ptsn, H, subsets, nsub,
+                               models, h0, hn, skip);
+            MLG_LAUNCH_CHECK();
+        }
         hipLaunchKernelGGL(k_ransac_hyp5, dim3((hn + 15) / 16, P), dim3(256), 0, s, info, ptsn, H, subsets, nsub,
                            models, nsol, h0, skip);
         MLG_LAUNCH_CHECK();

@@ -21,3 +21,10 @@ for rep in 0 1; do
   run rs_tree_$rep tree tools/ransac_bench.py --pairs 5000 --matches 600 --inliers 0.2 --reps 3
   for b in 1 2 3; do run rs_a${b}_$rep ab_rs/a$b tools/ransac_bench.py --pairs 5000 --matches 600 --inliers 0.2 --reps 3; done
 done
+# the per-lane null space (MLG_RS_NULL_SPLIT) against the in-group QR: digest + time
+for rep in 0 1; do
+  run rs_null_tree_$rep tree tools/ransac_bench.py --pairs 5000 --matches 600 --inliers 0.2 --reps 3
+  run rs_null_n0_$rep ab_rs/n0 tools/ransac_bench.py --pairs 5000 --matches 600 --inliers 0.2 --reps 3
+  run rs_null_tree_hi_$rep tree tools/ransac_bench.py --pairs 2000 --matches 1200 --inliers 0.5 --reps 3
+  run rs_null_n0_hi_$rep ab_rs/n0 tools/ransac_bench.py --pairs 2000 --matches 1200 --inliers 0.5 --reps 3
+done
