@@ -400,6 +400,10 @@ int mlg_dbg_fill_regs(uint32_t pattern, void* stream);
  * pair without a model) with `value` after the solvers ran -- a stand-in for a solver that
  * leaves a slot unwritten; the readers clamp counts to [0, 10], so results must not change. */
 int mlg_dbg_ransac_poison_nsol(int on, int value);
+/* Diagnostics (tools/ffn_trace.py): in a build with -DMLG_FFN_TRACE=1, copies the phase
+ * timestamps of the last fused-block-tail launch (per workgroup: 10 s_memtime values, the
+ * wave's HW_ID and XCC_ID; [65536][12] uint64) to host memory; MLG_EINVAL in the product. */
+int mlg_dbg_ffn_trace(void* host, size_t bytes);
 
 /* --------------------------------------------------------- SuperGlue --
  * The SuperGlue matcher of the reference's SuperGlue class configuration

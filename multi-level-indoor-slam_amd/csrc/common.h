@@ -72,7 +72,9 @@ __host__ __device__ __forceinline__ size_t lg_fac4(size_t r, int p) {
 // (Phi(x) - 0.5) / x in the well-conditioned variable, evaluated by Horner in f32):
 // |error| <= 1e-6 on [-4.5, 4.5], <= 3.4e-6 |x| beyond; on N(0, 1.3) inputs its bf16
 // outputs differ from exact GELU's in 0.08 % of elements (A & S 7.1.26: 0.07 %, torch's
-// own f32 GELU: 0.10 %).  No transcendental: pairs of calls pack into v_pk_fma_f32.
+// own f32 GELU: 0.10 %).  No transcendental: pairs of calls pack into v_pk_fma_f32 (two
+// scalar v_fma_f32 chains instead: the LightGlue block tail unchanged, the split ViT fc1
+// epilogue 65 % slower and not bit-identical -- profiles/r05k_ab_gelu_scalar.txt).
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 __device__ __forceinline__ f32x2 gelu_poly2(f32x2 x) {
     f32x2 xc;

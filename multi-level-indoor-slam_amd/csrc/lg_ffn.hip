@@ -96,6 +96,19 @@ __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_ca
 #ifndef MLG_FFN_RING2
 #define MLG_FFN_RING2 4
 #endif
+// Phase timestamps (probe builds, MLG_FFN_TRACE=1): s_memtime at the phase boundaries of
+// every workgroup's tile, with the wave's HW_ID / XCC_ID, read by mlg_dbg_ffn_trace
+// (tools/ffn_trace.py).  0 in the product.
+#ifndef MLG_FFN_TRACE
+#define MLG_FFN_TRACE 0
+#endif
+[[maybe_unused]] constexpr int FFN_TRACE_WGS = 65536, FFN_TRACE_W = 12;
+#if MLG_FFN_TRACE
+__device__ unsigned long long g_ffn_trace[FFN_TRACE_WGS * FFN_TRACE_W];
+#define FFN_T(i) tt[i] = __builtin_amdgcn_s_memtime()
+#else
+#define FFN_T(i) (void)0
+#endif
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 __device__ __forceinline__ uint4 stream_ld(const uint4* p) {
 #if MLG_FFN_NT
@@ -212,6 +225,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                                                   bf16_t* __restrict__ xcopy, int ldc, int M, mlg_lg_block_i w,
                                                   mlg_lg_conf_i cf) {
     constexpr bool relu = LOFTR || RELU;
+#if MLG_FFN_TRACE
+    unsigned long long tt[10] = {};
+#endif
+    FFN_T(0);
     constexpr int MT = R / 32, NT1 = 256 / NW / 32, NT2 = 512 / NW / 32, NTH = 64 * NW;
     constexpr int RING = NW == 8 ? 8 : MLG_FFN_RING2;  // weight k-steps in flight per wave (ffn1)
     // ring of the msg / ffn2 phases (NT1 column tiles, half the MFMAs per k-step of ffn1).
@@ -271,6 +288,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             }
         }
         __syncthreads();
+        FFN_T(1);
 
         // 1. msg = ctx . Wout^T + bout  -> bf16 over the ctx half
         {
@@ -278,6 +296,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             zero(acc);
             if (!(MLG_FFN_PROBE & 4)) gemm_phase<NT1, MT, RING1>(w.Wout, 256, 32 * NT1 * wave, 4, 32, lds, acc);
             __syncthreads();  // every wave has read the ctx half
+            FFN_T(2);
             float mean1[MT], rstd1[MT];
             if constexpr (LOFTR) {
                 // norm1 over the 256 msg columns of each row: lane -> half-wave -> waves
@@ -353,7 +372,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
         {
             f32x16 acc[NT2][MT];
             zero(acc);
+            FFN_T(3);
             if (!(MLG_FFN_PROBE & 8)) gemm_phase<NT2, MT, RING>(w.Wf1, 512, 32 * NT2 * wave, 8, 0, lds, acc);
+            FFN_T(4);
     #pragma unroll
             for (int t = 0; t < NT2; ++t)
     #pragma unroll
@@ -416,6 +437,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
 #endif
 #endif
             }
+            FFN_T(5);
     #pragma unroll
             for (int t = 0; t < NT2; ++t)
     #pragma unroll
@@ -469,7 +491,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
             __builtin_amdgcn_sched_barrier(0);
             f32x16 acc[NT1][MT];
             zero(acc);
+            FFN_T(6);
             if (!(MLG_FFN_PROBE & 16)) gemm_phase<NT1, MT, RING1>(w.Wf2, 256, 32 * NT1 * wave, 8, 0, lds, acc);
+            FFN_T(7);
 #if MLG_FFN_XR_WAIT
             __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): the residual rows xr have landed
 #endif
@@ -489,6 +513,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                     }
                 }
             __syncthreads();
+            FFN_T(8);
             // Heads (cf.wm != nullptr): each lane keeps its 4-column partial dot of each of
             // the wave's 16 rows; one reduce-scatter over the 64 lanes (8 + 4 + 2 + 1 + 1 + 1
             // shuffles per head instead of 16 x 6) leaves every 4-lane group with one row's sum.
@@ -567,6 +592,16 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                 }
             }
         }
+#if MLG_FFN_TRACE
+        FFN_T(9);
+        if (threadIdx.x == 0 && blockIdx.x < FFN_TRACE_WGS) {
+            unsigned long long* o = g_ffn_trace + (size_t)blockIdx.x * FFN_TRACE_W;
+    #pragma unroll
+            for (int i = 0; i < 10; ++i) o[i] = tt[i];
+            o[10] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID
+            o[11] = (unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
+        }
+#endif
         if (!PERSIST) break;  // one tile per workgroup: no loop, no state carried across tiles
         __syncthreads();  // the next tile overwrites the LDS image
     }
@@ -584,6 +619,18 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
 }
 
 }  // namespace
+
+// copies the phase trace of a MLG_FFN_TRACE build ([FFN_TRACE_WGS][12] u64); -1 otherwise
+extern "C" int mlg_dbg_ffn_trace(void* host, size_t bytes) {
+#if MLG_FFN_TRACE
+    const size_t n = std::min(bytes, sizeof(g_ffn_trace));
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ffn_trace), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : MLG_EHIP;
+#else
+    (void)host;
+    (void)bytes;
+    return MLG_EINVAL;
+#endif
+}
 
 int mlg_lg_ffn(const bf16_t* ctx, float* X, bf16_t* xcopy, int ldc, int M, const mlg_lg_block_i& w, hipStream_t s,
                const mlg_lg_conf_i* conf, int relu) {

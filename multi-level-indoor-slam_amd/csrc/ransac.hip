@@ -773,7 +773,13 @@ __device__ __forceinline__ bool null_space5_reg(const double (&A)[5][9], double 
 // solvePoly is the related Durand-Kerner iteration); estimates with a negligible
 // imaginary part are the real roots, polished by two real Newton steps and
 // gathered in lane order, so every lane of the group holds the same list.
-__device__ int real_roots10(double (&c)[11], double (&roots)[10], int r, int gl) {
+// MLG_RS_ROOTS_LDS: each iteration gathers the group's estimates through LDS (one
+// ds_write_b128 of (re, im) per lane, ten broadcast ds_read_b128) instead of twenty
+// 64-bit shuffles (forty ds_bpermute); the same values, so the same roots.
+#ifndef MLG_RS_ROOTS_LDS
+#define MLG_RS_ROOTS_LDS 1
+#endif
+__device__ int real_roots10(double (&c)[11], double (&roots)[10], int r, int gl, double2* __restrict__ zs) {
     double mx = 0.0;
 #pragma unroll
     for (int i = 0; i <= 10; ++i) mx = fmax(mx, fabs(c[i]));
@@ -796,10 +802,22 @@ __device__ int real_roots10(double (&c)[11], double (&roots)[10], int r, int gl)
     for (int it = 0; it < 60; ++it) {
         // every lane of the group takes part in the gathers (converged ones included)
         double xr_[10], xi_[10];
+        if (MLG_RS_ROOTS_LDS) {
+            zs[r] = make_double2(zr, zi);
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int j = 0; j < 10; ++j) {
-            xr_[j] = __shfl(zr, gl + j, 64);
-            xi_[j] = __shfl(zi, gl + j, 64);
+            for (int j = 0; j < 10; ++j) {
+                const double2 z = zs[j];
+                xr_[j] = z.x;
+                xi_[j] = z.y;
+            }
+            __builtin_amdgcn_wave_barrier();  // reads done before the next iteration's write
+        } else {
+#pragma unroll
+            for (int j = 0; j < 10; ++j) {
+                xr_[j] = __shfl(zr, gl + j, 64);
+                xi_[j] = __shfl(zi, gl + j, 64);
+            }
         }
         if (!done) {
             // p(z), p'(z) by Horner (complex)
@@ -929,27 +947,42 @@ __global__ __launch_bounds__(64) void k_ransac_null5(const PairInfo* __restrict_
     o[36] = ok ? 1.0 : 0.0;
 }
 
+// GS lanes per hypothesis group: 16 (4 groups per wave) or 10 (MLG_RS_G10: 6 groups, lanes
+// 60..63 idle) -- the solver's ten constraint rows and ten root estimates each fill one
+// lane, so 10-lane groups put 6 hypotheses on a wave instead of 4.  Same arithmetic per
+// lane; the pivot search (max |a|, ties to the lowest lane) scans the group's lanes in
+// order instead of an xor tree -- the same pivot for every non-NaN column.
+#ifndef MLG_RS_G10
+#define MLG_RS_G10 1
+#endif
+constexpr int HYP5_GS = MLG_RS_G10 ? 10 : 16, HYP5_GPB = 4 * (64 / HYP5_GS);  // lanes per group, groups per block
+
+template <int GS>
 __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict__ info,
                                                      const double4* __restrict__ ptsn, int H,
                                                      const int32_t* __restrict__ subsets,
                                                      const int32_t* __restrict__ nsub, double* __restrict__ models,
                                                      int8_t* __restrict__ nsol, int h0,
                                                      const uint8_t* __restrict__ done) {
-    __shared__ double snb[16][4][9];
-    const int g = threadIdx.x >> 4, r = threadIdx.x & 15, gl = threadIdx.x & 48;  // group, lane in group, base
+    constexpr int GPW = 64 / GS, GPB = 4 * GPW;
+    __shared__ double snb[GPB][4][9];
+    __shared__ double2 szs[GPB][17];  // root estimates per group (17: groups on distinct banks)
+    const int lane = threadIdx.x & 63, gw = lane / GS;
+    const bool valid = gw < GPW;  // GS = 10: lanes 60..63 belong to no group
+    const int g = (threadIdx.x >> 6) * GPW + (valid ? gw : 0), r = lane - gw * GS, gl = gw * GS;  // group, lane in group, base
     const int p = blockIdx.y;
-    const int h = h0 + blockIdx.x * 16 + g;
+    const int h = h0 + blockIdx.x * GPB + g;
     if (done && done[p]) return;  // uniform per block
     const PairInfo pi = info[p];
     const bool ess = pi.mode == 1 || pi.mode == 5;
     // whole groups are active or not (shuffles stay inside a group)
-    const bool act = ess && hyp5_active(pi, h, H, nsub, p);
+    const bool act = valid && ess && hyp5_active(pi, h, H, nsub, p);
     if (!ess) return;  // uniform per block (one pair per blockIdx.y)
     bool ok = act;
     if (act) {
         if (MLG_RS_NULL_SPLIT) {  // k_ransac_null5 left the basis in this hypothesis' model slot
             const double* nb = models + ((size_t)p * H + h) * MAXSOL * 9;
-            for (int i = r; i < 36; i += 16) snb[g][i / 9][i % 9] = nb[i];
+            for (int i = r; i < 36; i += GS) snb[g][i / 9][i % 9] = nb[i];
             ok = nb[36] != 0.0;
         } else {
             double Nb[4][9];
@@ -962,6 +995,7 @@ __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict_
         }
     }
     __syncthreads();
+    if (!valid) return;  // after the barrier: no group reads these lanes
 #if defined(RS_ABLATE) && RS_ABLATE == 3
     if (act && r == 0) nsol[(size_t)p * H + h] = 0;
     return;
@@ -1027,11 +1061,22 @@ __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict_
     for (int c = 0; c < 10; ++c) {
         double best = used ? -1.0 : fabs(row[c]);
         int bl = r;
+        if constexpr (GS == 16) {
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) {
-            const double ob = __shfl_xor(best, o, 64);
-            const int ol = __shfl_xor(bl, o, 64);
-            if (ob > best || (ob == best && ol < bl)) { best = ob; bl = ol; }
+            for (int o = 8; o > 0; o >>= 1) {
+                const double ob = __shfl_xor(best, o, 64);
+                const int ol = __shfl_xor(bl, o, 64);
+                if (ob > best || (ob == best && ol < bl)) { best = ob; bl = ol; }
+            }
+        } else {
+            const double mine = best;
+            best = -2.0;
+            bl = GS;
+#pragma unroll
+            for (int jl = 0; jl < GS; ++jl) {
+                const double ob = __shfl(mine, gl + jl, 64);
+                if (ob > best) { best = ob; bl = jl; }
+            }
         }
         if (!(best > 1e-300)) ok = false;  // singular (uniform in the group)
         piv[c] = bl;
@@ -1104,7 +1149,7 @@ __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict_
     if (r == 0) nsol[(size_t)p * H + h] = (int8_t)(poly[3] > 1e300);
     return;
 #endif
-    const int nz = real_roots10(poly, zr, r, gl);
+    const int nz = real_roots10(poly, zr, r, gl, szs[g]);
     if (r != 0) return;
     double* out = models + ((size_t)p * H + h) * MAXSOL * 9;
     int ns = 0;
@@ -1764,8 +1809,8 @@ int mlg_ransac_run(const float* kp1, const float* kp2, const int32_t* offs, int 
                                models, h0, hn, skip);
             MLG_LAUNCH_CHECK();
         }
-        hipLaunchKernelGGL(k_ransac_hyp5, dim3((hn + 15) / 16, P), dim3(256), 0, s, info, ptsn, H, subsets, nsub,
-                           models, nsol, h0, skip);
+        hipLaunchKernelGGL(k_ransac_hyp5<HYP5_GS>, dim3((hn + HYP5_GPB - 1) / HYP5_GPB, P), dim3(256), 0, s, info,
+                           ptsn, H, subsets, nsub, models, nsol, h0, skip);
         MLG_LAUNCH_CHECK();
         if (g_poison_nsol) {
             hipLaunchKernelGGL(k_ransac_poison_nsol, dim3((hn + 63) / 64, P), dim3(64), 0, s, info, H, nsub, nsol, h0,

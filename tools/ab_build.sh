@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build an A/B arm of the native libraries with extra preprocessor flags on one source:
 #   tools/ab_build.sh OUT_DIR FILE.hip "-DMACRO=V ..." [REPLACEMENT_SOURCE]
+# (FILE may be a quoted list of sources, e.g. "lg_ffn.hip gemm_bf16.hip", without a replacement)
 # Copies the package (sources + the tree's objects) to a scratch directory, rebuilds FILE
 # with the flags, relinks, and puts libmlgate.so / libmlgate_torch.so in OUT_DIR for
 # tools/ab_run.py --lib-dir.  The tree's own libraries are not touched.  With a fourth
@@ -13,7 +14,7 @@ mkdir -p "$TMP/pkg/mlgate"
 cp -a "$ROOT/include" "$TMP/include"
 cp -a "$ROOT/multi-level-indoor-slam_amd/csrc" "$TMP/pkg/csrc"
 if [ -n "$REPL" ]; then cp "$REPL" "$TMP/pkg/csrc/$FILE"; fi
-touch "$TMP/pkg/csrc/$FILE"
+for f in $FILE; do touch "$TMP/pkg/csrc/$f"; done  # FILE may list several sources
 BASE="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -fno-slp-vectorize"
 make -s -C "$TMP/pkg/csrc" -j8 CXXFLAGS="$BASE $DEFS" > "$TMP/build.log" 2>&1 || { tail -20 "$TMP/build.log"; exit 1; }
 cp "$TMP/pkg/mlgate/libmlgate.so" "$TMP/pkg/mlgate/libmlgate_torch.so" "$OUT/"
