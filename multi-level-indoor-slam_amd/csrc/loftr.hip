@@ -259,11 +259,21 @@ __global__ __launch_bounds__(256) void k_lf_kv(const float* __restrict__ k, cons
 // bytes); ksum by the lanes with bv == 0.  Partial sums [seg, head, chunk][DH * DH + DH]
 // (tokens in order inside a chunk); k_lf_kv_combine adds the chunks in chunk order.
 constexpr int LF_KV_CHUNK = 256;
+// MLG_LF_KV_STAGE: the 8 tokens' k / v head slices of a step come in as whole 1-KiB wave
+// loads (lane = 16 B of the 8 x DH k | v block) through a per-wave LDS image, instead of
+// one 16-B load per lane per token and operand (8 lanes sharing each address, 128 B per
+// wave-instruction); the next step's loads are in flight while this step's FMAs run.
+// Same per-lane FMA order, so the same sums.
+#ifndef MLG_LF_KV_STAGE
+#define MLG_LF_KV_STAGE 1
+#endif
 template <int DH>
 __global__ __launch_bounds__(256) void k_lf_kv_part(const float* __restrict__ k, const float* __restrict__ v, int ldk,
                                                     int ldv, int L, int heads, int nseg, int nch,
                                                     float* __restrict__ part) {
     constexpr int B = DH / 8;
+    constexpr int NI = DH / 16;  // float4 per lane per 8-token step (k and v together: 16 DH floats)
+    __shared__ __attribute__((aligned(16))) float stage[4][2 * 8 * DH];
     const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (w >= nseg * heads * nch) return;
     const int c = w % nch, gh = w / nch, h = gh % heads, g = gh / heads;
@@ -271,29 +281,67 @@ __global__ __launch_bounds__(256) void k_lf_kv_part(const float* __restrict__ k,
     const int s0 = c * LF_KV_CHUNK, s1 = min(L, s0 + LF_KV_CHUNK);
     float acc[B][B] = {};
     float ks[B] = {};
-    // 8 tokens' k / v loads in flight before their FMAs (tokens still summed in order)
     int s = s0;
-    for (; s + 8 <= s1; s += 8) {
-        float a[8][B], b[8][B];
+    if (MLG_LF_KV_STAGE) {
+        float* st = stage[threadIdx.x >> 6];
+        // lane's float4 i of a step: flat f = 4 (lane + 64 i) of [k | v][8 tokens][DH]
+        auto fetch = [&](int s_, float4 (&r)[NI]) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const size_t row = (size_t)g * L + s + u;
-            const float* kr = k + row * ldk + h * DH + bk * B;
-            const float* vr = v + row * ldv + h * DH + bv * B;
-#pragma unroll
-            for (int i = 0; i < B; ++i) {
-                a[u][i] = kr[i];
-                b[u][i] = vr[i];
+            for (int i = 0; i < NI; ++i) {
+                const int f = 4 * (lane + 64 * i), kv = f / (8 * DH), u = (f % (8 * DH)) / DH, d = f % DH;
+                const size_t row = (size_t)g * L + s_ + u;
+                r[i] = *reinterpret_cast<const float4*>((kv ? v + row * ldv : k + row * ldk) + h * DH + d);
             }
+        };
+        float4 nxt[NI];
+        if (s + 8 <= s1) fetch(s, nxt);
+        for (; s + 8 <= s1; s += 8) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i) *reinterpret_cast<float4*>(st + 4 * (lane + 64 * i)) = nxt[i];
+            __builtin_amdgcn_wave_barrier();
+            if (s + 16 <= s1) fetch(s + 8, nxt);
+            float a[8][B], b[8][B];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int i = 0; i < B; ++i) {
+                    a[u][i] = st[u * DH + bk * B + i];
+                    b[u][i] = st[8 * DH + u * DH + bv * B + i];
+                }
+            __builtin_amdgcn_wave_barrier();  // reads issued before the next step's writes
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int i = 0; i < B; ++i) {
+                    ks[i] += a[u][i];
+#pragma unroll
+                    for (int j = 0; j < B; ++j) acc[i][j] = fmaf(a[u][i], b[u][j], acc[i][j]);
+                }
         }
+    } else {
+        // 8 tokens' k / v loads in flight before their FMAs (tokens still summed in order)
+        for (; s + 8 <= s1; s += 8) {
+            float a[8][B], b[8][B];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+            for (int u = 0; u < 8; ++u) {
+                const size_t row = (size_t)g * L + s + u;
+                const float* kr = k + row * ldk + h * DH + bk * B;
+                const float* vr = v + row * ldv + h * DH + bv * B;
 #pragma unroll
-            for (int i = 0; i < B; ++i) {
-                ks[i] += a[u][i];
-#pragma unroll
-                for (int j = 0; j < B; ++j) acc[i][j] = fmaf(a[u][i], b[u][j], acc[i][j]);
+                for (int i = 0; i < B; ++i) {
+                    a[u][i] = kr[i];
+                    b[u][i] = vr[i];
+                }
             }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int i = 0; i < B; ++i) {
+                    ks[i] += a[u][i];
+#pragma unroll
+                    for (int j = 0; j < B; ++j) acc[i][j] = fmaf(a[u][i], b[u][j], acc[i][j]);
+                }
+        }
     }
     for (; s < s1; ++s) {
         const size_t row = (size_t)g * L + s;

@@ -956,8 +956,69 @@ __global__ __launch_bounds__(64) void k_ransac_null5(const PairInfo* __restrict_
 #define MLG_RS_G10 1
 #endif
 constexpr int HYP5_GS = MLG_RS_G10 ? 10 : 16, HYP5_GPB = 4 * (64 / HYP5_GS);  // lanes per group, groups per block
+// MLG_RS_ROOTS_SPLIT: k_ransac_hyp5 stops at the degree-10 polynomial and leaves it, with
+// the 3 x 3 polynomial matrix, in the hypothesis' model slot; k_ransac_roots5 then finds
+// the roots and writes the models with a third of the solver's registers, so more waves
+// hide the f64 latency of the root iteration.  Needs MLG_RS_NULL_SPLIT (the slot then
+// holds: [0, 36) null space, [36] stage flag, [37, 48) polynomial, [48, 87) matrix).
+#ifndef MLG_RS_ROOTS_SPLIT
+#define MLG_RS_ROOTS_SPLIT 1
+#endif
+constexpr bool HYP5_ROOTS_SPLIT = MLG_RS_ROOTS_SPLIT && MLG_RS_NULL_SPLIT;
+constexpr int SLOT_FLAG = 36, SLOT_POLY = 37, SLOT_MAT = 48;
+constexpr double FLAG_POLY = 2.0;  // the slot's polynomial and matrix are written
 
-template <int GS>
+// the models of one hypothesis from its real roots z (lane 0 of the group): the null
+// vector of the 3 x 3 matrix at z gives (x, y); E = x X + y Y + z Z + W, normalised
+// bx(i, d), by(i, d), b1(i, d): the matrix's polynomial entries; nb(a, k): the null space
+template <class BX, class BY, class B1, class NB>
+__device__ __forceinline__ int hyp5_models(const double (&zr)[10], int nz, BX bx, BY by, B1 b1, NB nb,
+                                           double* __restrict__ out) {
+    int ns = 0;
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+        if (t >= nz) continue;
+        const double z = zr[t];
+        double M[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            double vx = 0.0, vy = 0.0, v1 = 0.0;
+#pragma unroll
+            for (int d = 3; d >= 0; --d) { vx = vx * z + bx(i, d); vy = vy * z + by(i, d); }
+#pragma unroll
+            for (int d = 4; d >= 0; --d) v1 = v1 * z + b1(i, d);
+            M[i][0] = vx; M[i][1] = vy; M[i][2] = v1;
+        }
+        // null vector of the rank-2 M: the largest cross product of two rows
+        double best[3] = {0.0, 0.0, 0.0}, bn = -1.0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const int b = (a + 1) % 3;
+            const double cx = M[a][1] * M[b][2] - M[a][2] * M[b][1];
+            const double cy = M[a][2] * M[b][0] - M[a][0] * M[b][2];
+            const double cz = M[a][0] * M[b][1] - M[a][1] * M[b][0];
+            const double n2 = cx * cx + cy * cy + cz * cz;
+            if (n2 > bn) { bn = n2; best[0] = cx; best[1] = cy; best[2] = cz; }
+        }
+        if (!(fabs(best[2]) > 1e-300 * sqrt(fmax(bn, 1e-300)))) continue;
+        const double x = best[0] / best[2], y = best[1] / best[2];
+        if (!(fabs(x) < 1e300) || !(fabs(y) < 1e300)) continue;
+        double e[9], nrm = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            e[k] = x * nb(0, k) + y * nb(1, k) + z * nb(2, k) + nb(3, k);
+            nrm += e[k] * e[k];
+        }
+        nrm = 1.0 / sqrt(nrm);
+        double* Eo = out + ns * 9;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) Eo[k] = e[k] * nrm;
+        ++ns;
+    }
+    return ns;
+}
+
+template <int GS, bool SPLIT>
 __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict__ info,
                                                      const double4* __restrict__ ptsn, int H,
                                                      const int32_t* __restrict__ subsets,
@@ -1149,51 +1210,66 @@ __global__ __launch_bounds__(256) void k_ransac_hyp5(const PairInfo* __restrict_
     if (r == 0) nsol[(size_t)p * H + h] = (int8_t)(poly[3] > 1e300);
     return;
 #endif
-    const int nz = real_roots10(poly, zr, r, gl, szs[g]);
-    if (r != 0) return;
-    double* out = models + ((size_t)p * H + h) * MAXSOL * 9;
-    int ns = 0;
+    if constexpr (SPLIT) {  // k_ransac_roots5 continues from the slot
+        if (r == 0) {
+            double* o = models + ((size_t)p * H + h) * MAXSOL * 9;
 #pragma unroll
-    for (int t = 0; t < 10; ++t) {
-        if (t >= nz) continue;
-        const double z = zr[t];
-        double M[3][3];
+            for (int i = 0; i < 11; ++i) o[SLOT_POLY + i] = poly[i];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            double vx = 0.0, vy = 0.0, v1 = 0.0;
+            for (int i = 0; i < 3; ++i) {
 #pragma unroll
-            for (int d = 3; d >= 0; --d) { vx = vx * z + bx[i][d]; vy = vy * z + by[i][d]; }
+                for (int d = 0; d < 4; ++d) {
+                    o[SLOT_MAT + 13 * i + d] = bx[i][d];
+                    o[SLOT_MAT + 13 * i + 4 + d] = by[i][d];
+                }
 #pragma unroll
-            for (int d = 4; d >= 0; --d) v1 = v1 * z + b1[i][d];
-            M[i][0] = vx; M[i][1] = vy; M[i][2] = v1;
+                for (int d = 0; d < 5; ++d) o[SLOT_MAT + 13 * i + 8 + d] = b1[i][d];
+            }
+            o[SLOT_FLAG] = FLAG_POLY;
         }
-        // null vector of the rank-2 M: the largest cross product of two rows
-        double best[3] = {0.0, 0.0, 0.0}, bn = -1.0;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const int b = (a + 1) % 3;
-            const double cx = M[a][1] * M[b][2] - M[a][2] * M[b][1];
-            const double cy = M[a][2] * M[b][0] - M[a][0] * M[b][2];
-            const double cz = M[a][0] * M[b][1] - M[a][1] * M[b][0];
-            const double n2 = cx * cx + cy * cy + cz * cz;
-            if (n2 > bn) { bn = n2; best[0] = cx; best[1] = cy; best[2] = cz; }
-        }
-        if (!(fabs(best[2]) > 1e-300 * sqrt(fmax(bn, 1e-300)))) continue;
-        const double x = best[0] / best[2], y = best[1] / best[2];
-        if (!(fabs(x) < 1e300) || !(fabs(y) < 1e300)) continue;
-        double e[9], nrm = 0.0;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            e[k] = x * snb[g][0][k] + y * snb[g][1][k] + z * snb[g][2][k] + snb[g][3][k];
-            nrm += e[k] * e[k];
-        }
-        nrm = 1.0 / sqrt(nrm);
-        double* Eo = out + ns * 9;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) Eo[k] = e[k] * nrm;
-        ++ns;
+        return;
+    } else {
+        const int nz = real_roots10(poly, zr, r, gl, szs[g]);
+        if (r != 0) return;
+        nsol[(size_t)p * H + h] = (int8_t)hyp5_models(
+            zr, nz, [&](int i, int d) { return bx[i][d]; }, [&](int i, int d) { return by[i][d]; },
+            [&](int i, int d) { return b1[i][d]; }, [&](int a, int k) { return snb[g][a][k]; },
+            models + ((size_t)p * H + h) * MAXSOL * 9);
     }
-    nsol[(size_t)p * H + h] = (int8_t)ns;
+}
+
+// The roots and models of the hypotheses k_ransac_hyp5<.., true> left at the polynomial
+// stage (same group layout; every other slot is left as it is).
+template <int GS>
+__global__ __launch_bounds__(256) void k_ransac_roots5(const PairInfo* __restrict__ info, int H,
+                                                       const int32_t* __restrict__ nsub, double* __restrict__ models,
+                                                       int8_t* __restrict__ nsol, int h0,
+                                                       const uint8_t* __restrict__ done) {
+    constexpr int GPW = 64 / GS, GPB = 4 * GPW;
+    __shared__ double2 szs[GPB][17];
+    __shared__ double scoef[GPB][39 + 36];  // the slot's matrix and null space, read before models overwrite it
+    const int lane = threadIdx.x & 63, gw = lane / GS;
+    const bool valid = gw < GPW;
+    const int g = (threadIdx.x >> 6) * GPW + (valid ? gw : 0), r = lane - gw * GS, gl = gw * GS;
+    const int p = blockIdx.y;
+    const int h = h0 + blockIdx.x * GPB + g;
+    if (done && done[p]) return;
+    const PairInfo pi = info[p];
+    if (!(pi.mode == 1 || pi.mode == 5) || !valid || !hyp5_active(pi, h, H, nsub, p)) return;
+    double* o = models + ((size_t)p * H + h) * MAXSOL * 9;
+    if (o[SLOT_FLAG] != FLAG_POLY) return;  // group-uniform: singular sample, nsol already 0
+    double* sc = scoef[g];
+    for (int i = r; i < 39; i += GS) sc[i] = o[SLOT_MAT + i];
+    for (int i = r; i < 36; i += GS) sc[39 + i] = o[i];
+    double poly[11], zr[10];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) poly[i] = o[SLOT_POLY + i];
+    const int nz = real_roots10(poly, zr, r, gl, szs[g]);  // its LDS waits order the copies above
+    if (r != 0) return;
+    __builtin_amdgcn_wave_barrier();
+    nsol[(size_t)p * H + h] = (int8_t)hyp5_models(
+        zr, nz, [&](int i, int d) { return sc[13 * i + d]; }, [&](int i, int d) { return sc[13 * i + 4 + d]; },
+        [&](int i, int d) { return sc[13 * i + 8 + d]; }, [&](int a, int k) { return sc[39 + 9 * a + k]; }, o);
 }
 
 // OpenCV's sample stream for pair p (modes 1 / 2): subsets of iterations 0..nsub-1.
@@ -1809,8 +1885,13 @@ int mlg_ransac_run(const float* kp1, const float* kp2, const int32_t* offs, int 
                                models, h0, hn, skip);
             MLG_LAUNCH_CHECK();
         }
-        hipLaunchKernelGGL(k_ransac_hyp5<HYP5_GS>, dim3((hn + HYP5_GPB - 1) / HYP5_GPB, P), dim3(256), 0, s, info,
-                           ptsn, H, subsets, nsub, models, nsol, h0, skip);
+        hipLaunchKernelGGL((k_ransac_hyp5<HYP5_GS, HYP5_ROOTS_SPLIT>), dim3((hn + HYP5_GPB - 1) / HYP5_GPB, P),
+                           dim3(256), 0, s, info, ptsn, H, subsets, nsub, models, nsol, h0, skip);
+        if (HYP5_ROOTS_SPLIT) {
+            MLG_LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_ransac_roots5<HYP5_GS>, dim3((hn + HYP5_GPB - 1) / HYP5_GPB, P), dim3(256), 0, s, info,
+                               H, nsub, models, nsol, h0, skip);
+        }
         MLG_LAUNCH_CHECK();
         if (g_poison_nsol) {
             hipLaunchKernelGGL(k_ransac_poison_nsol, dim3((hn + 63) / 64, P), dim3(64), 0, s, info, H, nsub, nsol, h0,
