@@ -26,6 +26,7 @@ Two front ends run the same kernels:
     process per GPU, RCCL all-gathers; bench.py's step).  Its decisions and counts are
     those of FullSemanticGate (tests/test_pipeline_gpu.py).
 """
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -227,7 +228,9 @@ class DeviceGate:
             # features of exactly the keyframes its verification slice touches
             self.kp_loc = torch.empty(self.n_local, KP * 2, device=self.dev)
             self.ds_loc = torch.empty(self.n_local, KP * 256, device=self.dev)
-            self.cnt_loc = torch.empty(self.n_local, 1, dtype=torch.int32, device=self.dev)
+            # zeros: with the SuperPoint overlap the first chunk's call sees rows not yet
+            # extracted this step, and mlg_lightglue range-checks every count
+            self.cnt_loc = torch.zeros(self.n_local, 1, dtype=torch.int32, device=self.dev)
             self.fx = mdist.FeatureExchange(N, world, rank) if world > 1 else None
             Kc = np.asarray(K if K is not None else np.eye(3), np.float64)
             self.K = torch.from_numpy(Kc.reshape(9).copy()).to(self.dev) if K is not None else None
@@ -282,13 +285,14 @@ class DeviceGate:
         out["retrieval_floor_rejected"] = int((live & (h_valid == 0)).sum())
         if not self.verify:
             return out
-        # SuperPoint once per keyframe (the reference re-extracts per pair), cached in HBM
-        for b0 in range(0, self.n_local if self.matcher == 'lightglue' else 0, self.sp_batch):
-            b1 = min(self.n_local, b0 + self.sp_batch)
-            kp, _, ds, _, cnt = self.sp.extract_device(self.frames[b0:b1])
-            self.kp_loc[b0:b1].copy_(kp.view(b1 - b0, -1))
-            self.ds_loc[b0:b1].copy_(ds.view(b1 - b0, -1))
-            self.cnt_loc[b0:b1, 0].copy_(cnt)
+        # SuperPoint once per keyframe (the reference re-extracts per pair), cached in HBM.
+        # One rank: only the keyframes of the first LightGlue chunk are extracted up front;
+        # the rest run on a side stream under that chunk (_verify_lightglue).  Several
+        # ranks: all of them first (FeatureExchange ships rows of the finished table).
+        self._sp_overlap = (self.world == 1 and self.matcher == 'lightglue'
+                            and os.environ.get("MLGATE_SP_OVERLAP", "1") != "0")
+        if self.matcher == 'lightglue' and not self._sp_overlap:
+            self._extract_rows(np.arange(self.n_local))
         # matches handed to verify_with_semantics (is_valid ones), skip rule on floors
         qs, js = np.nonzero(live & (h_valid != 0))
         pa_h, pb_h = (qs + self.lo).astype(np.int32), h_idx[qs, js].astype(np.int32)
@@ -313,6 +317,28 @@ class DeviceGate:
             pa, pb = pa_h, pb_h
         return self._verify_lightglue(pa, pb, dedup, out)
 
+    def _extract_rows(self, rows):
+        """SuperPoint of the local keyframes `rows` (host int array, any order) into the
+        feature tables, in batches of sp_batch on the current stream.  Per-frame results do
+        not depend on which frames share a batch."""
+        torch = self.torch
+        for b0 in range(0, len(rows), self.sp_batch):
+            r = rows[b0:b0 + self.sp_batch]
+            if len(r) == r[-1] - r[0] + 1:  # a contiguous run: a view, no gather
+                fr, dst = self.frames[int(r[0]):int(r[-1]) + 1], slice(int(r[0]), int(r[-1]) + 1)
+            else:
+                dst = torch.from_numpy(np.ascontiguousarray(r, np.int64)).to(self.dev)
+                fr = self.frames.index_select(0, dst)
+            kp, _, ds, _, cnt = self.sp.extract_device(fr)
+            if isinstance(dst, slice):
+                self.kp_loc[dst].copy_(kp.view(len(r), -1))
+                self.ds_loc[dst].copy_(ds.view(len(r), -1))
+                self.cnt_loc[dst, 0].copy_(cnt)
+            else:
+                self.kp_loc.index_copy_(0, dst, kp.view(len(r), -1))
+                self.ds_loc.index_copy_(0, dst, ds.view(len(r), -1))
+                self.cnt_loc.index_copy_(0, dst, cnt.view(-1, 1).to(self.cnt_loc.dtype))
+
     def _verify_lightglue(self, pa, pb, dedup, out):
         """SuperPoint features (local table or need-driven exchange) -> LightGlue (once per
         unordered pair when dedup) -> RANSAC + decision + floor gate per ordered pair, for
@@ -331,7 +357,6 @@ class DeviceGate:
             local = lambda x: np.asarray(x, np.int32)  # noqa: E731
         kp_all = kp_c.view(nf, self.kp, 2)
         ds_all = ds_c.view(nf, self.kp, 256)
-        counts = cnt_c.view(-1).cpu().numpy()
         # LightGlue once per UNORDERED pair: it is symmetric in its two images (shared
         # weights; self / cross blocks, dual-softmax assignment, early stopping and pruning
         # treat both alike), so (b, a) is (a, b) with the image roles exchanged and the
@@ -357,11 +382,20 @@ class DeviceGate:
         bounds = np.searchsorted(inv[order], np.asarray(starts))
         out["pairs_matched_lightglue"] = len(ua)
         ua, ub = local(ua), local(ub)  # LightGlue indexes the feature tables
+        sp_done = None
+        if getattr(self, "_sp_overlap", False):
+            # the first chunk's keyframes now, the rest on a side stream under that chunk
+            first = np.unique(np.concatenate([ua[:starts[1]], ub[:starts[1]]])) if len(starts) > 1 else \
+                np.zeros(0, np.int64)
+            self._extract_rows(first)
+            rest = np.setdiff1d(np.arange(self.n_local), first, assume_unique=True)
+            sp_done = self._extract_side(rest)
+        counts = cnt_c.view(-1).cpu().numpy()  # rows of the first chunk's keyframes final
         # RANSAC of chunk c runs on a side stream while LightGlue matches chunk c + 1 on
         # this one (mlg_lightglue waits on its stream once per layer; the side stream
         # fills those gaps and the CUs the small RANSAC / assignment grids leave idle)
         n_valid_t, gate_rej_t, rec = self._verify_chunks(starts, bounds, order, inv, ua, ub, pa, pb, swap_all, dedup,
-                                                         kp_all, ds_all, counts, local)
+                                                         kp_all, ds_all, counts, local, sp_done, cnt_c)
         n_valid, gate_rej = int(n_valid_t), int(gate_rej_t)
         if rec is not None:
             r = {"a": pa, "b": pb, "matches": np.zeros(len(pa), np.int32), "inliers": np.zeros(len(pa), np.int32),
@@ -378,8 +412,23 @@ class DeviceGate:
         out["accepted"] = n_valid - gate_rej
         return out
 
+    def _extract_side(self, rows):
+        """_extract_rows on the SuperPoint side stream, after everything already queued on
+        the current stream; returns the event the consumers of those rows wait on."""
+        torch = self.torch
+        main = torch.cuda.current_stream(self.dev)
+        if getattr(self, "_sp_stream", None) is None:
+            self._sp_stream = torch.cuda.Stream(device=self.dev)
+        sps = self._sp_stream
+        sps.wait_stream(main)
+        with torch.cuda.stream(sps):
+            self._extract_rows(rows)
+        done = torch.cuda.Event()
+        done.record(sps)
+        return done
+
     def _verify_chunks(self, starts, bounds, order, inv, ua, ub, pa, pb, swap_all, dedup, kp_all, ds_all, counts,
-                       local):
+                       local, sp_done=None, cnt_c=None):
         torch = self.torch
         from . import geometry
         main = torch.cuda.current_stream(self.dev)
@@ -389,6 +438,10 @@ class DeviceGate:
         rec = [] if self.record else None
         for ci in range(len(starts) - 1):
             c0, c1 = starts[ci], starts[ci + 1]
+            if ci == 1 and sp_done is not None:  # the side-stream SuperPoint rows from here on
+                main.wait_event(sp_done)
+                counts = cnt_c.view(-1).cpu().numpy()
+                sp_done = None
             mu, su, nu, _ = self.lg.match_device(kp_all, ds_all, counts, ua[c0:c1], ub[c0:c1])
             sel = order[bounds[ci]:bounds[ci + 1]]  # the ordered pairs of these unordered ones
             ca, cb = pa[sel], pb[sel]
@@ -438,6 +491,8 @@ class DeviceGate:
                 # the drop-in SemanticLoopClosureGate keeps that TypeError,
                 # tests/test_api_cpu.py::test_gate_none_labels_raise_nan_labels_accept)
                 gate_rej_t += (ok & ((self.f_num[ta] - self.f_num[tb]).abs() > self.limit)).sum()
+        if sp_done is not None:  # one chunk only: the tables are complete when step() returns
+            main.wait_event(sp_done)
         main.wait_stream(side)
         return n_valid_t, gate_rej_t, rec
 

@@ -169,6 +169,28 @@ def test_device_gate_unordered_matching_changes_nothing(dev, chain, cfg, monkeyp
     assert len(recs["1"]) == a["pairs_verified"] > 0
 
 
+def test_superpoint_overlap_changes_nothing(dev, chain, monkeypatch):
+    """SuperPoint of the keyframes past the first LightGlue chunk on a side stream under
+    that chunk (MLGATE_SP_OVERLAP, the default) vs every keyframe first: the same counts
+    and, per ordered pair, the same match count, inlier count and decision; several
+    chunks, so the side-stream rows feed later chunks, and two steps, so a step starts
+    from the previous step's tables."""
+    frames = torch.from_numpy(chain["frames"]).to(dev)
+    outs, recs = {}, {}
+    for ov in ("1", "0"):
+        monkeypatch.setenv("MLGATE_SP_OVERLAP", ov)
+        g = DeviceGate(frames, chain["seq"].t, chain["labels"], device=str(dev), k=chain["k"],
+                       similarity_threshold=chain["thr"], min_time_gap=chain["gap"], K=ogeo.ISEC_K,
+                       vit_batch=64, lg_chunk=16, sp_batch=8, record=True)
+        for _ in range(2):
+            outs[ov] = g.step()
+            r = g.last_pair_results
+            recs[ov] = {(int(x), int(y)): (int(n), int(i), bool(v))
+                        for x, y, n, i, v in zip(r["a"], r["b"], r["matches"], r["inliers"], r["is_valid"])}
+    assert outs["1"] == outs["0"]
+    assert recs["1"] == recs["0"] and len(recs["1"]) > 0
+
+
 def test_orient_matches_is_the_swapped_call(dev):
     """mlg_lg_orient_matches: (i0, i1) -> (i1, i0) sorted by the new image0 index, scores
     carried along; unswapped rows copied."""
