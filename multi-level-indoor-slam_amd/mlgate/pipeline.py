@@ -286,11 +286,15 @@ class DeviceGate:
         if not self.verify:
             return out
         # SuperPoint once per keyframe (the reference re-extracts per pair), cached in HBM.
-        # One rank: only the keyframes of the first LightGlue chunk are extracted up front;
-        # the rest run on a side stream under that chunk (_verify_lightglue).  Several
-        # ranks: all of them first (FeatureExchange ships rows of the finished table).
+        # MLGATE_SP_OVERLAP=1 (one rank): only the keyframes of the first LightGlue chunk
+        # are extracted up front, the rest on a side stream under that chunk
+        # (_verify_lightglue).  Same results, +0.2 % on the bench -- the LightGlue tile
+        # leaves SuperPoint's convolutions little room on a CU -- while the bench's
+        # per-stage HIP-event table would then time SuperPoint's launches with the
+        # concurrent LightGlue in them (profiles/r05p_ab_superpoint_overlap.txt): off by
+        # default.  Several ranks: all keyframes first (FeatureExchange ships finished rows).
         self._sp_overlap = (self.world == 1 and self.matcher == 'lightglue'
-                            and os.environ.get("MLGATE_SP_OVERLAP", "1") != "0")
+                            and os.environ.get("MLGATE_SP_OVERLAP", "0") == "1")
         if self.matcher == 'lightglue' and not self._sp_overlap:
             self._extract_rows(np.arange(self.n_local))
         # matches handed to verify_with_semantics (is_valid ones), skip rule on floors

@@ -171,7 +171,7 @@ def test_device_gate_unordered_matching_changes_nothing(dev, chain, cfg, monkeyp
 
 def test_superpoint_overlap_changes_nothing(dev, chain, monkeypatch):
     """SuperPoint of the keyframes past the first LightGlue chunk on a side stream under
-    that chunk (MLGATE_SP_OVERLAP, the default) vs every keyframe first: the same counts
+    that chunk (MLGATE_SP_OVERLAP=1) vs every keyframe first (the default): the same counts
     and, per ordered pair, the same match count, inlier count and decision; several
     chunks, so the side-stream rows feed later chunks, and two steps, so a step starts
     from the previous step's tables."""
