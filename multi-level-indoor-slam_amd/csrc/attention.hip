@@ -19,8 +19,11 @@
 
 namespace {
 
+#ifndef MLG_ATT_LDS_PAD
+#define MLG_ATT_LDS_PAD 0
+#endif
 #ifndef MLG_ATT_QAGPR
-#define MLG_ATT_QAGPR 1
+#define MLG_ATT_QAGPR 0
 #endif
 constexpr int KB = 64;                 // keys per block
 constexpr int KTILE_BYTES = KB * 128;  // 64 rows x 64 bf16
@@ -180,7 +183,7 @@ struct PipeCtx {
 // scores' readers are block_max2's `s_nop 11` pad and, in a partial last stage, the key
 // mask behind its own pad.
 #ifndef MLG_ATT_QK_ASM
-#define MLG_ATT_QK_ASM 1
+#define MLG_ATT_QK_ASM 0
 #endif
 template <bool SPLIT, int QT>
 __device__ __forceinline__ void qk_half(const char* kb, const PipeCtx& c, const bf16x8 (&qf)[QT][4],
@@ -641,7 +644,9 @@ int varlen_launch(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O,
     const long total = (long)nqb * heads * ntasks;
     if (total > (1L << 30)) return MLG_EINVAL;
     const int grid = (int)((total + 7) & ~7L);
-    hipLaunchKernelGGL((k_attention_varlen<VIT, SPLIT, NW>), dim3(grid), dim3(64 * NW), 0, s, Q, K, Vt, O, ldo, Npad, tasks,
+    // probe: MLG_ATT_LDS_PAD extra dynamic LDS bytes per LightGlue workgroup (one workgroup per CU)
+    const size_t pad = (!VIT && !SPLIT && NW == 4) ? (size_t)MLG_ATT_LDS_PAD : 0;
+    hipLaunchKernelGGL((k_attention_varlen<VIT, SPLIT, NW>), dim3(grid), dim3(64 * NW), pad, s, Q, K, Vt, O, ldo, Npad, tasks,
                        out_off, nqb, heads, (int)total, lo_off, lo_col);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
