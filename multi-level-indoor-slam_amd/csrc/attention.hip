@@ -19,12 +19,6 @@
 
 namespace {
 
-#ifndef MLG_ATT_LDS_PAD
-#define MLG_ATT_LDS_PAD 0
-#endif
-#ifndef MLG_ATT_QAGPR
-#define MLG_ATT_QAGPR 0
-#endif
 constexpr int KB = 64;                 // keys per block
 constexpr int KTILE_BYTES = KB * 128;  // 64 rows x 64 bf16
 constexpr int VTILE_BYTES = 64 * KB * 2;
@@ -172,38 +166,9 @@ struct PipeCtx {
 // tied to element [15]).  Changing this MFMA's shape (e.g. 16x16x32, 4 passes) or
 // splitting the accumulator requires re-deriving the pad; tests/test_kernels_gpu.py's
 // attention bit-identity test is the run-time guard.
-// MLG_ATT_QK_ASM (LightGlue's 4-wave tile): the score MFMAs as inline asm with VGPR
-// destinations.  hipcc gives every MFMA of this kernel the accumulator-file form (its
-// register demand needs the AGPRs), so each half-block's 32 scores were copied out with
-// 32 v_accvgpr_read before the VALU could touch them; here they are written where the
-// VALU reads them.  Hazards (the asm is opaque to hipcc's hazard recognizer): the first
-// MFMA of a chain takes C = 0 (no VALU-written C); each later one accumulates the whole
-// previous D (0 wait states); Q comes from the accumulator file, written once before the
-// stage loop (s_nop 1 there); K fragments come from ds_read (hipcc's lgkmcnt wait); the
-// scores' readers are block_max2's `s_nop 11` pad and, in a partial last stage, the key
-// mask behind its own pad.
-#ifndef MLG_ATT_QK_ASM
-#define MLG_ATT_QK_ASM 0
-#endif
 template <bool SPLIT, int QT>
 __device__ __forceinline__ void qk_half(const char* kb, const PipeCtx& c, const bf16x8 (&qf)[QT][4],
                                         const bf16x8 (&qfl)[QT][4], int kt, f32x16 (&s)[QT]) {
-    if constexpr (!SPLIT && QT == 2 && MLG_ATT_QK_ASM && MLG_ATT_QAGPR) {
-        const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kb + kt * 4096 + c.koff[0]);
-        asm("v_mfma_f32_32x32x16_bf16 %0, %2, %3, 0\n\t"
-            "v_mfma_f32_32x32x16_bf16 %1, %2, %4, 0"
-            : "=&v"(s[0]), "=&v"(s[1])
-            : "v"(k0), "a"(qf[0][0]), "a"(qf[1][0]));
-#pragma unroll
-        for (int st = 1; st < 4; ++st) {
-            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + kt * 4096 + c.koff[st]);
-            asm("v_mfma_f32_32x32x16_bf16 %0, %2, %3, %0\n\t"
-                "v_mfma_f32_32x32x16_bf16 %1, %2, %4, %1"
-                : "+v"(s[0]), "+v"(s[1])
-                : "v"(kf), "a"(qf[0][st]), "a"(qf[1][st]));
-        }
-        return;
-    }
 #pragma unroll
     for (int i = 0; i < 16; ++i)
 #pragma unroll
@@ -272,8 +237,6 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[QT], f32x16 (&nxt
     const bool run = !(SPLIT && QT == 1) || busy;
     if (run) {
     if (LASTSTAGE && (c.T & (KB - 1))) {  // partial last stage: mask keys >= T
-        if constexpr (!SPLIT && QT == 2 && MLG_ATT_QK_ASM && MLG_ATT_QAGPR)
-            asm volatile("s_nop 11" : "+v"(cur[0]), "+v"(cur[1]));  // MFMA D -> VALU write
         const int key0 = j * KB + H * 32;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -398,18 +361,6 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
             if (SPLIT) qfl[qt][st] = *reinterpret_cast<const bf16x8*>(Qh + lo_off + (size_t)qld * 64 + st * 16 + hh * 8);
         }
     }
-#if MLG_ATT_QAGPR
-    // the Q fragments are MFMA operands only: pin them in the accumulator half of the
-    // register file, so both 32-key score sets fit in VGPRs (no v_accvgpr_read of a score
-    // set per half-block)
-    if constexpr (!SPLIT)
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-            for (int st = 0; st < 4; ++st) asm volatile("" : "+a"(qf[qt][st]));
-    if constexpr (!SPLIT)
-        asm volatile("s_nop 1" : "+a"(qf[0][0]), "+a"(qf[QT - 1][3]));  // v_accvgpr_write -> MFMA operand
-#endif
     PipeCtx c;
     c.Kh = Kh;
     c.Vh = Vh;
@@ -644,9 +595,7 @@ int varlen_launch(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O,
     const long total = (long)nqb * heads * ntasks;
     if (total > (1L << 30)) return MLG_EINVAL;
     const int grid = (int)((total + 7) & ~7L);
-    // probe: MLG_ATT_LDS_PAD extra dynamic LDS bytes per LightGlue workgroup (one workgroup per CU)
-    const size_t pad = (!VIT && !SPLIT && NW == 4) ? (size_t)MLG_ATT_LDS_PAD : 0;
-    hipLaunchKernelGGL((k_attention_varlen<VIT, SPLIT, NW>), dim3(grid), dim3(64 * NW), pad, s, Q, K, Vt, O, ldo, Npad, tasks,
+    hipLaunchKernelGGL((k_attention_varlen<VIT, SPLIT, NW>), dim3(grid), dim3(64 * NW), 0, s, Q, K, Vt, O, ldo, Npad, tasks,
                        out_off, nqb, heads, (int)total, lo_off, lo_col);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
