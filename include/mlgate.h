@@ -404,6 +404,11 @@ int mlg_dbg_ransac_poison_nsol(int on, int value);
  * timestamps of the last fused-block-tail launch (per workgroup: 10 s_memtime values, the
  * wave's HW_ID and XCC_ID; [65536][12] uint64) to host memory; MLG_EINVAL in the product. */
 int mlg_dbg_ffn_trace(void* host, size_t bytes);
+/* Diagnostics (tools/attn_trace.py): in a build with -DMLG_ATT_TRACE=1, the phase stamps of
+ * the last LightGlue attention launch (per logical workgroup: entry, prologue done, stage
+ * loop done, end, HW_ID, XCC_ID, query count, written flag; [65536][8] uint64); MLG_EINVAL
+ * in the product. */
+int mlg_dbg_att_trace(void* host, size_t bytes);
 
 /* --------------------------------------------------------- SuperGlue --
  * The SuperGlue matcher of the reference's SuperGlue class configuration

@@ -19,6 +19,19 @@
 
 namespace {
 
+// Phase timestamps (probe builds, MLG_ATT_TRACE=1; 0 in the product): per LightGlue
+// workgroup s_memtime at entry, after the prologue barrier, after the stage loop and at
+// the end, with HW_ID / XCC_ID (mlg_dbg_att_trace, tools/attn_trace.py)
+#ifndef MLG_ATT_TRACE
+#define MLG_ATT_TRACE 0
+#endif
+[[maybe_unused]] constexpr int ATT_TRACE_WGS = 1 << 16;
+#if MLG_ATT_TRACE
+__device__ unsigned long long g_att_trace[ATT_TRACE_WGS * 8];
+#define ATT_T(i) att_tt[i] = __builtin_amdgcn_s_memtime()
+#else
+#define ATT_T(i) (void)0
+#endif
 constexpr int KB = 64;                 // keys per block
 constexpr int KTILE_BYTES = KB * 128;  // 64 rows x 64 bf16
 constexpr int VTILE_BYTES = 64 * KB * 2;
@@ -342,7 +355,7 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[QT], f32x16 (&nxt
 }
 
 template <bool SPLIT, int NW = 4>
-__device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __restrict__ Qh,
+__device__ __forceinline__ void attention_tile_pipe(unsigned long long* att_tt, char* smem, const bf16_t* __restrict__ Qh,
                                                     const bf16_t* __restrict__ Kh, const bf16_t* __restrict__ Vh,
                                                     int T, int nq, int qmax, int qblock, bf16_t* __restrict__ orow,
                                                     int ldo, size_t lo_off, int lo_col) {
@@ -433,6 +446,7 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
         }
     }
     __syncthreads();
+    ATT_T(1);
     const bool busy = qbase < nq;  // wave-uniform: some of its 32 queries are live
     f32x16 sA[QT], sB[QT];
     if (!(SPLIT && QT == 1) || busy) qk_half<SPLIT, QT>(smem, c, qf, qfl, 0, sA);
@@ -470,6 +484,7 @@ __device__ __forceinline__ void attention_tile_pipe(char* smem, const bf16_t* __
     }
     PIPE_STAGE(last, -1, true)  // slot last % 3 at run time
 #undef PIPE_STAGE
+    ATT_T(2);
 
     // O staged through LDS (the K / V rings are dead once every wave is past its last
     // stage) as this wave's [32 QT queries][64 d] bf16, 16-B chunk c of row r at c ^ (r & 7),
@@ -571,9 +586,23 @@ __global__ __launch_bounds__(64 * NW, 1) void k_attention_varlen(const bf16_t* _
     const int4 tk = tasks[t];  // q_off, q_len, kv_off, kv_len
     if (qb * 256 >= tk.y || tk.w <= 0) return;
     const int qpad = (tk.y + 63) & ~63;
-    attention_tile_pipe<SPLIT, NW>(smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
+    unsigned long long att_tt[4] = {};
+    ATT_T(0);
+    attention_tile_pipe<SPLIT, NW>(att_tt, smem, Q + ((size_t)h * Npad + tk.x) * 64, K + ((size_t)h * Npad + tk.z) * 64,
                                Vt + ((size_t)h * Npad + tk.z) * 64, tk.w, tk.y, qpad, qb,
                                O + (size_t)out_off[t] * ldo + h * 64, ldo, lo_off, lo_col);
+#if MLG_ATT_TRACE
+    if (!VIT && threadIdx.x == 0 && logical < ATT_TRACE_WGS) {
+        ATT_T(3);
+        unsigned long long* o = g_att_trace + (size_t)logical * 8;
+        for (int i = 0; i < 4; ++i) o[i] = att_tt[i];
+        o[4] = (unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID
+        o[5] = (unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
+        o[6] = (unsigned long long)tk.y;
+        o[7] = 1;
+    }
+#endif
+    (void)att_tt;
 }
 
 // ViT tasks: image b attends its own segment [b * Tpad, b * Tpad + T) in every head;
@@ -602,6 +631,19 @@ int varlen_launch(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O,
 }
 
 }  // namespace
+
+// copies the phase trace of a MLG_ATT_TRACE build ([65536][8] u64, by logical workgroup:
+// 4 stamps, HW_ID, XCC_ID, query count, written flag); -1 otherwise
+extern "C" int mlg_dbg_att_trace(void* host, size_t bytes) {
+#if MLG_ATT_TRACE
+    const size_t n = bytes < sizeof(g_att_trace) ? bytes : sizeof(g_att_trace);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_att_trace), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : MLG_EHIP;
+#else
+    (void)host;
+    (void)bytes;
+    return MLG_EINVAL;
+#endif
+}
 
 int mlg_attention(const bf16_t* Q, const bf16_t* K, const bf16_t* Vt, bf16_t* O, int B, int T, int Tpad,
                   int32_t* task_ws, hipStream_t s) {
