@@ -37,6 +37,9 @@
 #ifndef MLG_PROJ_PIPE
 #define MLG_PROJ_PIPE 1  // the resident form with the epilogue inside the next tile's GEMM
 #endif
+#ifndef MLG_PROJ_SWAP
+#define MLG_PROJ_SWAP 1  // pipelined form: whole 16-B staging chunks (permlane32 swap), b128 writes
+#endif
 
 namespace {
 
@@ -61,7 +64,8 @@ __device__ __forceinline__ float4 fac_tile(const float* fc, int r, int p) {
 // a head's 64 rows are ONE contiguous 8 KiB block of the destination, written as whole
 // 1 KiB pieces (per-lane 8-B stores at a 128-B row stride touched 32 lines each).
 // (A swizzle on r >> 1, 2-way instead of 4-way bank conflicts on the epilogue's writes,
-// measured no faster.)
+// measured no faster.  The pipelined form, the product, stages through stage_pair_off
+// instead: whole 16-B chunks, b128 writes, profiles/r05u_ab_proj_staging.txt.)
 template <int R>
 __device__ __forceinline__ int stage_off(int h, int row, int e) {
     return (h * R + row) * 128 + ((((e >> 3) ^ (row & 7))) << 4) + (e & 7) * 2;
@@ -359,6 +363,69 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
 // bytes), tile t + 1's DMA.  Only the copy-out stays a phase of its own, after the
 // staging barrier.  Results are those of k_lg_proj_res bit for bit (same accumulators,
 // same epilogue arithmetic).
+// Paired staging (MLG_PROJ_SWAP): lanes l and l + 32 hold the two 8-B halves of one 16-B
+// chunk (q / k: head dims 8c..+3 and 8c+4..+7 of token r; v: tokens 8g..+3 and 8g+4..+7 of
+// dim d).  slice_*_val packs a slice's 8 B; stage_pair takes the m-tile 0 and 1 halves,
+// swaps lanes 32-63 of the first with lanes 0-31 of the second (v_permlane32_swap), so
+// lane l < 32 holds m-tile 0's whole chunk and lane l + 32 m-tile 1's, and writes it as
+// ONE ds_write_b128 into an image whose chunk c of row r sits at slot c ^ ((r >> 1) & 7):
+// a 16-lane group's 16 consecutive rows then hit 16 distinct bank quads (conflict-free
+// b128 write, and the copy-out's b128 reads of 2 rows x 8 chunks likewise) -- the b64
+// writes of stage_off paid 4 conflict cycles each (profiles/r05c_lds_conflict_calibration.txt).
+__device__ __forceinline__ int stage_pair_off(int h, int row, int c) {
+    return (h * 64 + row) * 128 + ((c ^ ((row >> 1) & 7)) << 4);
+}
+__device__ __forceinline__ void stage_pair(uint2 m0v, uint2 m1v, char* lds, int h, int row, int c) {
+    const auto s0 = __builtin_amdgcn_permlane32_swap(m0v.x, m1v.x, false, false);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(m0v.y, m1v.y, false, false);
+    *reinterpret_cast<uint4*>(lds + stage_pair_off(h, row, c)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+}
+
+template <bool SELF>
+__device__ __forceinline__ uint2 slice_qk_val(int g, int mt, const f32x16& a, const float* bias_l, const float* fc,
+                                              const uint8_t* live_l) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 31, hh = lane >> 5;
+    const int n = 32 * wave + 8 * g + 4 * hh;
+    const float4 b = *reinterpret_cast<const float4*>(bias_l + n);
+    const int r = 32 * mt + col;
+    float x0 = a[4 * g] + b.x, x1 = a[4 * g + 1] + b.y, x2 = a[4 * g + 2] + b.z, x3 = a[4 * g + 3] + b.w;
+    if (SELF) {  // as slice_qk
+        const float4 cs = fac_tile(fc, r, (n & 63) >> 2);
+        const float r0 = __fadd_rn(__fmul_rn(x0, cs.x), __fmul_rn(-x1, cs.z));
+        const float r1 = __fadd_rn(__fmul_rn(x1, cs.x), __fmul_rn(x0, cs.z));
+        const float r2 = __fadd_rn(__fmul_rn(x2, cs.y), __fmul_rn(-x3, cs.w));
+        const float r3 = __fadd_rn(__fmul_rn(x3, cs.y), __fmul_rn(x2, cs.w));
+        x0 = r0; x1 = r1; x2 = r2; x3 = r3;
+    }
+    const uint32_t keep = 0u - (uint32_t)(live_l[r] != 0);
+    return make_uint2(pack_bf16x2(x0, x1) & keep, pack_bf16x2(x2, x3) & keep);
+}
+// q / k pair write of column group g: row 32 hh + col, chunk (32 wave + 8 g) / 8 of head h
+__device__ __forceinline__ void stage_pair_qk(int g, uint2 m0v, uint2 m1v, char* lds) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 31, hh = lane >> 5;
+    const int n = 32 * wave + 8 * g;
+    stage_pair(m0v, m1v, lds, n >> 6, 32 * hh + col, (n & 63) >> 3);
+}
+
+__device__ __forceinline__ uint2 slice_v_val(int g, int mt, const f32x16& a, const float* bias_l,
+                                             const uint8_t* live_l) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 31, hh = lane >> 5;
+    const float b = bias_l[32 * wave + col];
+    const int r = 32 * mt + 8 * g + 4 * hh;
+    const uint32_t lv = *reinterpret_cast<const uint32_t*>(live_l + r);
+    const float v0 = (lv & 0xff) ? a[4 * g] + b : 0.f;
+    const float v1 = (lv & 0xff00) ? a[4 * g + 1] + b : 0.f;
+    const float v2 = (lv & 0xff0000) ? a[4 * g + 2] + b : 0.f;
+    const float v3 = (lv >> 24) ? a[4 * g + 3] + b : 0.f;
+    return make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+}
+// V^T pair write of token group g: row d, chunk g + 4 hh (tokens 32 hh + 8 g ..) of head h
+__device__ __forceinline__ void stage_pair_v(int g, uint2 m0v, uint2 m1v, char* lds) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, col = lane & 31, hh = lane >> 5;
+    const int n = 32 * wave + col;
+    stage_pair(m0v, m1v, lds, n >> 6, n & 63, g + 4 * hh);
+}
+
 template <bool SELF>
 __device__ __forceinline__ void slice_qk(int g, int mt, const f32x16& a, char* lds, const float* bias_l,
                                          const float* fc, const uint8_t* live_l) {
@@ -406,6 +473,7 @@ __device__ __forceinline__ void pipe_gemm(const bf16x8 (&wf)[16], const char* xl
     const char* xrow = xl + col * ROWB;
     const int sw = col & 15;
     bf16x8 xa[2], xb[2];
+    uint2 pend = make_uint2(0u, 0u);  // MLG_PROJ_SWAP: m-tile 0's half of the pending pair
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) xa[mt] = *reinterpret_cast<const bf16x8*>(xrow + 32 * mt * ROWB + ((hh ^ sw) << 4));
 #pragma unroll
@@ -423,8 +491,21 @@ __device__ __forceinline__ void pipe_gemm(const bf16x8 (&wf)[16], const char* xl
                            : __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[ks], cur[mt], acc[mt], 0, 0, 0);
         if (STAGE && !(ks & 1)) {
             const int g = ks >> 2, mt = (ks >> 1) & 1;
-            if (IS_V) slice_v(g, mt, old[mt], sl, bias_l, live_l);
-            else slice_qk<SELF>(g, mt, old[mt], sl, bias_l, fc, live_l);
+            if (MLG_PROJ_SWAP) {  // m-tile 0's half at ks = 4 g, the pair write at 4 g + 2
+                const uint2 v = IS_V ? slice_v_val(g, mt, old[mt], bias_l, live_l)
+                                     : slice_qk_val<SELF>(g, mt, old[mt], bias_l, fc, live_l);
+                if (mt == 0) {
+                    pend = v;
+                } else if (IS_V) {
+                    stage_pair_v(g, pend, v, sl);
+                } else {
+                    stage_pair_qk(g, pend, v, sl);
+                }
+            } else if (IS_V) {
+                slice_v(g, mt, old[mt], sl, bias_l, live_l);
+            } else {
+                slice_qk<SELF>(g, mt, old[mt], sl, bias_l, fc, live_l);
+            }
         }
     }
 }
@@ -437,7 +518,7 @@ __device__ __forceinline__ void copy_out64(bool is_v, int part, int m0, const ch
     for (int p = 0; p < 4; ++p) {
         const int L = p * 512 + threadIdx.x, h = L / 512, row = (L >> 3) & 63, c = L & 7;
         *reinterpret_cast<uint4*>(dst + ((size_t)h * Npad + m0 + row) * 64 + c * 8) =
-            *reinterpret_cast<const uint4*>(lds + stage_off<64>(h, row, 8 * c));
+            *reinterpret_cast<const uint4*>(lds + (MLG_PROJ_SWAP ? stage_pair_off(h, row, c) : stage_off<64>(h, row, 8 * c)));
     }
 }
 
@@ -500,10 +581,22 @@ __device__ __forceinline__ void pipe_tiles(const bf16x8 (&wf)[16], char* ring, c
             __syncthreads();  // every wave has read its x rows
             char* sx = bufs(bx);
             const float* fx = reinterpret_cast<const float*>(sx + XB);
+            const uint8_t* lx = reinterpret_cast<const uint8_t*>(sx + BUF);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                if (IS_V) slice_v(i >> 1, i & 1, an[i & 1], sx, bias_l, reinterpret_cast<const uint8_t*>(sx + BUF));
-                else slice_qk<SELF>(i >> 1, i & 1, an[i & 1], sx, bias_l, fx, reinterpret_cast<const uint8_t*>(sx + BUF));
+                if (MLG_PROJ_SWAP) {
+                    if (i & 1) continue;
+                    const int g = i >> 1;
+                    if (IS_V)
+                        stage_pair_v(g, slice_v_val(g, 0, an[0], bias_l, lx), slice_v_val(g, 1, an[1], bias_l, lx), sx);
+                    else
+                        stage_pair_qk(g, slice_qk_val<SELF>(g, 0, an[0], bias_l, fx, lx),
+                                      slice_qk_val<SELF>(g, 1, an[1], bias_l, fx, lx), sx);
+                } else if (IS_V) {
+                    slice_v(i >> 1, i & 1, an[i & 1], sx, bias_l, lx);
+                } else {
+                    slice_qk<SELF>(i >> 1, i & 1, an[i & 1], sx, bias_l, fx, lx);
+                }
             }
             __syncthreads();
             copy_out64(IS_V, part, tp * R, sx, Q, K, Vt, Npad);

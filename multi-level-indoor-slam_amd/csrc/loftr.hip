@@ -502,6 +502,15 @@ __global__ __launch_bounds__(256) void k_lf_split_rows(const float* __restrict__
 constexpr int LF_ROWREG = 24;        // float4 per lane: rows of up to 6144 cells in registers
 constexpr float LF_KEY_BAND = 1e-3f;  // + 1e-5 |key|
 constexpr int LF_RCH = 64;           // rows per column chunk
+// Pairs per dual-softmax group: the similarity of up to MLG_LF_PGRP pairs is resident at
+// once ([G][L][L] f32, 92 MB per pair at 480 x 640) and every statistics / selection kernel
+// takes the group in blockIdx.z (pair z: S + z L^2, per-row / per-column arrays + z L, chunk
+// partials + z nch L), so the small per-pair kernels fill the chip and the launch
+// boundaries amortise over the group; per-pair arithmetic unchanged (same bits).
+#ifndef MLG_LF_PGRP
+#define MLG_LF_PGRP 8
+#endif
+#define LF_Z ((size_t)blockIdx.z)
 
 __device__ __forceinline__ float lf_band(float k) { return LF_KEY_BAND + 1e-5f * fabsf(k); }
 
@@ -516,6 +525,10 @@ __global__ __launch_bounds__(256) void k_lf_rowstats(const float* __restrict__ S
                                                      float* __restrict__ rsum, float* __restrict__ rkey) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= L) return;
+    S += LF_Z * L * L;
+    rmax += LF_Z * L;
+    rsum += LF_Z * L;
+    rkey += LF_Z * L;
     const float* s = S + (size_t)row * L;
     float m = -INFINITY, z = 0.f;
     if ((L & 3) == 0 && L <= 256 * LF_ROWREG) {
@@ -552,6 +565,9 @@ __global__ __launch_bounds__(256) void k_lf_colpart(const float* __restrict__ S,
                                                     float* __restrict__ pz) {
     const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
     if (col >= L) return;
+    S += LF_Z * L * L;
+    pm += LF_Z * gridDim.y * L;
+    pz += LF_Z * gridDim.y * L;
     const int r0 = c * LF_RCH, n = min(L - r0, LF_RCH);
     float v[LF_RCH], m = -INFINITY, z = 0.f;
 #pragma unroll
@@ -579,6 +595,10 @@ __global__ __launch_bounds__(256) void k_lf_stats(const float* __restrict__ S, i
     const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
     const int r0 = c * LF_RCH, n = min(L - r0, LF_RCH);
     const bool ok = col < L;
+    S += LF_Z * L * L;
+    pm += LF_Z * gridDim.y * L;
+    pz += LF_Z * gridDim.y * L;
+    prm += LF_Z * gridDim.x * L;
     float v[LF_RCH], m = -INFINITY, z = 0.f;
 #pragma unroll
     for (int i = 0; i < LF_RCH; ++i) {
@@ -616,6 +636,11 @@ __global__ __launch_bounds__(256) void k_lf_colfin(const float* __restrict__ pm,
     __shared__ float part[4][64];
     const int cl = threadIdx.x & 63, g = threadIdx.x >> 6, col = blockIdx.x * 64 + cl;
     const bool ok = col < L;
+    pm += LF_Z * nch * L;
+    pz += LF_Z * nch * L;
+    cmax += LF_Z * L;
+    csum += LF_Z * L;
+    ckey += LF_Z * L;
     float m = -INFINITY;
     if (ok)
 #pragma unroll 4
@@ -651,6 +676,16 @@ __global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S,
                                                     int32_t* __restrict__ bidx) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= L) return;
+    S += LF_Z * L * L;
+    rmax += LF_Z * L;
+    rsum += LF_Z * L;
+    rkey += LF_Z * L;
+    if (SELF) prm += LF_Z * ncb * L;
+    cmax += LF_Z * L;
+    csum += LF_Z * L;
+    ckey += LF_Z * L;
+    bval += LF_Z * L;
+    bidx += LF_Z * L;
     const float* s = S + (size_t)row * L;
     float rm, rz;
     const bool reg = (L & 3) == 0 && L <= 256 * LF_ROWREG;
@@ -744,6 +779,13 @@ __global__ __launch_bounds__(256) void k_lf_colmaxpart(const float* __restrict__
     __shared__ float rk[LF_RCH];
     const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
     const int r0 = c * LF_RCH, n = min(L - r0, LF_RCH);
+    S += LF_Z * L * L;
+    rmax += LF_Z * L;
+    rsum += LF_Z * L;
+    rkey += LF_Z * L;
+    cmax += LF_Z * L;
+    csum += LF_Z * L;
+    pb += LF_Z * gridDim.y * L;
     if (threadIdx.x < LF_RCH) rk[threadIdx.x] = threadIdx.x < n ? rkey[r0 + threadIdx.x] : INFINITY;
     __syncthreads();
     if (col >= L) return;
@@ -766,6 +808,8 @@ __global__ __launch_bounds__(256) void k_lf_colmaxfin(const float* __restrict__ 
                                                       float* __restrict__ cbest) {
     const int col = blockIdx.x * 256 + threadIdx.x;
     if (col >= L) return;
+    pb += LF_Z * nch * L;
+    cbest += LF_Z * L;
     float m = -1.f;
 #pragma unroll 8
     for (int c = 0; c < nch; ++c) m = fmaxf(m, pb[(size_t)c * L + col]);
@@ -782,6 +826,13 @@ __global__ __launch_bounds__(1024) void k_lf_select(const float* __restrict__ bv
     __shared__ int warp_tot[16];
     __shared__ int base;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    bval += LF_Z * L;
+    bidx += LF_Z * L;
+    cbest += LF_Z * L;
+    mi += LF_Z * L;
+    mj += LF_Z * L;
+    mconf += LF_Z * L;
+    count += LF_Z;
     if (tid == 0) base = 0;
     __syncthreads();
     auto inner = [&](int id) {
@@ -1305,23 +1356,24 @@ MatchLayout match_layout(int P, int L) {
     M.crow = take((size_t)2 * FINE_CHUNK * 256 * 2);
     M.cd = take((size_t)2 * FINE_CHUNK * 128 * 2);
     M.cm = take((size_t)2 * FINE_CHUNK * 128 * 4);
-    M.S = take((size_t)L * L * 4);
+    const size_t G = (size_t)std::min(P, MLG_LF_PGRP);  // pairs per dual-softmax group
+    M.S = take(G * L * L * 4);
     // the coarse features as split-bf16 rows [hi | lo] (+ 256 zero rows: the similarity
     // GEMM reads B rows up to its 256-column tile)
     M.csplit = take(((size_t)2 * P * L + 256) * 512 * 2);
-    M.rmax = take((size_t)L * 4);
-    M.rsum = take((size_t)L * 4);
-    M.rkey = take((size_t)L * 4);
-    M.cmax = take((size_t)L * 4);
-    M.csum = take((size_t)L * 4);
-    M.ckey = take((size_t)L * 4);
+    M.rmax = take(G * L * 4);
+    M.rsum = take(G * L * 4);
+    M.rkey = take(G * L * 4);
+    M.cmax = take(G * L * 4);
+    M.csum = take(G * L * 4);
+    M.ckey = take(G * L * 4);
     const size_t nrch = (size_t)(L + LF_RCH - 1) / LF_RCH;
-    M.pm = take(nrch * L * 4);
-    M.pz = take(nrch * L * 4);
-    M.prm = take((size_t)(L + 255) / 256 * L * 4);
-    M.bval = take((size_t)L * 4);
-    M.bidx = take((size_t)L * 4);
-    M.cbest = take((size_t)L * 4);
+    M.pm = take(G * nrch * L * 4);
+    M.pz = take(G * nrch * L * 4);
+    M.prm = take(G * ((L + 255) / 256) * L * 4);
+    M.bval = take(G * L * 4);
+    M.bidx = take(G * L * 4);
+    M.cbest = take(G * L * 4);
     M.mi = take((size_t)P * L * 4);
     M.mj = take((size_t)P * L * 4);
     M.mconf = take((size_t)P * L * 4);
@@ -1417,32 +1469,39 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
         MLG_LAUNCH_CHECK();
         if (hipMemsetAsync(CS + (size_t)rows * 512, 0, (size_t)256 * 512 * 2, s) != hipSuccess) return MLG_EHIP;
     }
-    // dual softmax + mutual nearest, pair by pair over one [L, L] similarity buffer
-    for (int p = 0; p < P; ++p) {
-        const float* f0 = bc.x + (size_t)p * L * 256;
-        const float* f1 = bc.x + ((size_t)P + p) * L * 256;
-        if (split)
-            LF_TRY(mlg_gemm_sim_split_loftr(CS + (size_t)p * L * 512, CS + ((size_t)P + p) * L * 512, L, Lpad, 256, S,
-                                            L, L, s));
-        else
-            LF_TRY(mlg_similarity_f32_loftr(f0, L, f1, L, 256, S, L, s));
+    // dual softmax + mutual nearest, MLG_LF_PGRP pairs at a time over [G][L][L] similarity
+    const int G = std::min(P, MLG_LF_PGRP);
+    for (int p0 = 0; p0 < P; p0 += G) {
+        const unsigned g = (unsigned)std::min(G, P - p0);
+        for (int q = 0; q < (int)g; ++q) {
+            const int p = p0 + q;
+            float* Sq = S + (size_t)q * L * L;
+            if (split)
+                LF_TRY(mlg_gemm_sim_split_loftr(CS + (size_t)p * L * 512, CS + ((size_t)P + p) * L * 512, L, Lpad, 256,
+                                                Sq, L, L, s));
+            else
+                LF_TRY(mlg_similarity_f32_loftr(bc.x + (size_t)p * L * 256, L, bc.x + ((size_t)P + p) * L * 256, L, 256,
+                                                Sq, L, s));
+        }
         if (MLG_LF_STATS1) {  // three reads of S: stats, rowbest, colmaxpart
-            hipLaunchKernelGGL(k_lf_stats, dim3(ncb, nrch), dim3(256), 0, s, S, L, pm, pz, prm);
-            hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum, ckey);
-            hipLaunchKernelGGL(k_lf_rowbest<true>, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, rkey, prm,
-                               ncb, cmax, csum, ckey, bval, bidx);
+            hipLaunchKernelGGL(k_lf_stats, dim3(ncb, nrch, g), dim3(256), 0, s, S, L, pm, pz, prm);
+            hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64, 1, g), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum,
+                               ckey);
+            hipLaunchKernelGGL(k_lf_rowbest<true>, dim3((L + 3) / 4, 1, g), dim3(256), 0, s, S, L, rmax, rsum, rkey,
+                               prm, ncb, cmax, csum, ckey, bval, bidx);
         } else {
-            hipLaunchKernelGGL(k_lf_rowstats, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, rkey);
-            hipLaunchKernelGGL(k_lf_colpart, dim3(ncb, nrch), dim3(256), 0, s, S, L, pm, pz);
-            hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum, ckey);
-            hipLaunchKernelGGL(k_lf_rowbest<false>, dim3((L + 3) / 4), dim3(256), 0, s, S, L, rmax, rsum, rkey,
+            hipLaunchKernelGGL(k_lf_rowstats, dim3((L + 3) / 4, 1, g), dim3(256), 0, s, S, L, rmax, rsum, rkey);
+            hipLaunchKernelGGL(k_lf_colpart, dim3(ncb, nrch, g), dim3(256), 0, s, S, L, pm, pz);
+            hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64, 1, g), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum,
+                               ckey);
+            hipLaunchKernelGGL(k_lf_rowbest<false>, dim3((L + 3) / 4, 1, g), dim3(256), 0, s, S, L, rmax, rsum, rkey,
                                nullptr, 0, cmax, csum, ckey, bval, bidx);
         }
-        hipLaunchKernelGGL(k_lf_colmaxpart, dim3((L + 255) / 256, nrch), dim3(256), 0, s, S, L, rmax, rsum, rkey, cmax,
-                           csum, pm);
-        hipLaunchKernelGGL(k_lf_colmaxfin, dim3((L + 255) / 256), dim3(256), 0, s, pm, L, nrch, cbest);
-        hipLaunchKernelGGL(k_lf_select, dim3(1), dim3(1024), 0, s, bval, bidx, cbest, L, hc, wc, 0.2f, 2,
-                           mi + (size_t)p * L, mj + (size_t)p * L, mconf + (size_t)p * L, cnt + p);
+        hipLaunchKernelGGL(k_lf_colmaxpart, dim3((L + 255) / 256, nrch, g), dim3(256), 0, s, S, L, rmax, rsum, rkey,
+                           cmax, csum, pm);
+        hipLaunchKernelGGL(k_lf_colmaxfin, dim3((L + 255) / 256, 1, g), dim3(256), 0, s, pm, L, nrch, cbest);
+        hipLaunchKernelGGL(k_lf_select, dim3(1, 1, g), dim3(1024), 0, s, bval, bidx, cbest, L, hc, wc, 0.2f, 2,
+                           mi + (size_t)p0 * L, mj + (size_t)p0 * L, mconf + (size_t)p0 * L, cnt + p0);
         MLG_LAUNCH_CHECK();
     }
     std::vector<int32_t> h_cnt(P);
