@@ -368,12 +368,18 @@ __global__ __launch_bounds__(512) void k_lg_proj_res(const bf16_t* __restrict__ 
 // dim d).  slice_*_val packs a slice's 8 B; stage_pair takes the m-tile 0 and 1 halves,
 // swaps lanes 32-63 of the first with lanes 0-31 of the second (v_permlane32_swap), so
 // lane l < 32 holds m-tile 0's whole chunk and lane l + 32 m-tile 1's, and writes it as
-// ONE ds_write_b128 into an image whose chunk c of row r sits at slot c ^ ((r >> 1) & 7):
-// a 16-lane group's 16 consecutive rows then hit 16 distinct bank quads (conflict-free
-// b128 write, and the copy-out's b128 reads of 2 rows x 8 chunks likewise) -- the b64
-// writes of stage_off paid 4 conflict cycles each (profiles/r05c_lds_conflict_calibration.txt).
+// ONE ds_write_b128 into an image whose chunk c of row r sits at slot c ^ (r & 7).  LDS
+// writes retire 128 B per cycle in lane order (b128: 8 lanes, bank = address mod 128 B),
+// reads 256 B (b128: 16 lanes, mod 256 B): the 8 consecutive rows of a write group then
+// hit 8 distinct 16-B slots mod 128, and the copy-out's b128 reads of 2 rows x 8 chunks 16
+// distinct slots mod 256 -- both conflict-free (tools/lds_probe.hip, profiles/
+// r05x_lds_calibration.txt; a (r >> 1) & 7 swizzle paid 2-way on every write, the b64
+// writes of stage_off 4 conflict cycles each).
+#ifndef MLG_PROJ_PAIR_SW
+#define MLG_PROJ_PAIR_SW 0  // 1: the (r >> 1) & 7 swizzle (A/B only)
+#endif
 __device__ __forceinline__ int stage_pair_off(int h, int row, int c) {
-    return (h * 64 + row) * 128 + ((c ^ ((row >> 1) & 7)) << 4);
+    return (h * 64 + row) * 128 + ((c ^ ((MLG_PROJ_PAIR_SW ? row >> 1 : row) & 7)) << 4);
 }
 __device__ __forceinline__ void stage_pair(uint2 m0v, uint2 m1v, char* lds, int h, int row, int c) {
     const auto s0 = __builtin_amdgcn_permlane32_swap(m0v.x, m1v.x, false, false);

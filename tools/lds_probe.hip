@@ -15,7 +15,7 @@ constexpr int ITERS = 4096;
 constexpr int LDS_BYTES = 64 * 1024;
 
 // access widths
-enum { R16 = 0, R8 = 1, W16 = 2, W8 = 3, R4 = 4 };
+enum { R16 = 0, R8 = 1, W16 = 2, W8 = 3, R4 = 4, R1 = 5 };
 
 struct Lane {
     int tid, lane, wave, col, hh;
@@ -80,6 +80,48 @@ __device__ __forceinline__ int p_proj_stage_v(const Lane& l, int it) {  // slice
 __device__ __forceinline__ int p_proj_copyout(const Lane& l, int it) {  // copy_out64 read, b128
     const int L = (it & 3) * 512 + l.tid, h = L / 512, row = (L >> 3) & 63, c = L & 7;
     return stage_off(h, row, 8 * c);
+}
+// lg_proj.hip paired staging (MLG_PROJ_SWAP, round 5): b128 writes of whole chunks, b128 copy-out
+// (pattern 29-31: the (r >> 1) & 7 swizzle first tried, 2-way on the writes; 36-38: r & 7, the product)
+__device__ __forceinline__ int pair_off(int h, int row, int c) { return (h * 64 + row) * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int pair_off7(int h, int row, int c) { return (h * 64 + row) * 128 + ((c ^ (row & 7)) << 4); }
+__device__ __forceinline__ int p_pair7_qk_write(const Lane& l, int it) {
+    const int n = 32 * l.wave + 8 * (it & 3);
+    return pair_off7(n >> 6, 32 * l.hh + l.col, (n & 63) >> 3);
+}
+__device__ __forceinline__ int p_pair7_v_write(const Lane& l, int it) {
+    const int n = 32 * l.wave + l.col;
+    return pair_off7(n >> 6, n & 63, (it & 3) + 4 * l.hh);
+}
+__device__ __forceinline__ int p_pair7_copyout(const Lane& l, int it) {
+    const int L = (it & 3) * 512 + l.tid, h = L / 512, row = (L >> 3) & 63, c = L & 7;
+    return pair_off7(h, row, c);
+}
+__device__ __forceinline__ int p_pair_qk_write(const Lane& l, int it) {  // stage_pair_qk, b128
+    const int n = 32 * l.wave + 8 * (it & 3);
+    return pair_off(n >> 6, 32 * l.hh + l.col, (n & 63) >> 3);
+}
+__device__ __forceinline__ int p_pair_v_write(const Lane& l, int it) {  // stage_pair_v, b128
+    const int n = 32 * l.wave + l.col;
+    return pair_off(n >> 6, n & 63, (it & 3) + 4 * l.hh);
+}
+__device__ __forceinline__ int p_pair_copyout(const Lane& l, int it) {  // copy_out64 read, b128
+    const int L = (it & 3) * 512 + l.tid, h = L / 512, row = (L >> 3) & 63, c = L & 7;
+    return pair_off(h, row, c);
+}
+__device__ __forceinline__ int p_bias_bcast(const Lane& l, int it) {  // slice_qk bias float4 (2 addresses)
+    return 32768 + (32 * l.wave + 8 * (it & 3) + 4 * l.hh) * 4;
+}
+__device__ __forceinline__ int p_live_u8(const Lane& l, int it) {  // slice_qk live byte
+    return 40960 + 32 * ((it >> 2) & 1) + l.col;
+}
+__device__ __forceinline__ int p_live_u32(const Lane& l, int it) {  // slice_v live dword
+    return 40960 + 32 * ((it >> 2) & 1) + 8 * (it & 3) + 4 * l.hh;
+}
+__device__ __forceinline__ int p_fac_tile(const Lane& l, int it) {  // slice_qk rotary float4 (lg_fac4 tile)
+    const int g = it & 3, mt = (it >> 2) & 1;
+    const int n = 32 * l.wave + 8 * g + 4 * l.hh, r = 32 * mt + l.col, p = (n & 63) >> 2;
+    return 16384 + ((p * 64 + r) << 4);
 }
 // lg_ffn.hip
 __device__ __forceinline__ int cat_off(int row, int chunk) { return row * 1024 + ((chunk ^ (row & 15)) << 4); }
@@ -153,6 +195,16 @@ __device__ __forceinline__ int addr_of(const Lane& l, int it) {
         case 26: return p_w_rows(l, it);
         case 27: return p_w_rows8(l, it);
         case 28: return p_w_xor(l, it);
+        case 29: return p_pair_qk_write(l, it);
+        case 30: return p_pair_v_write(l, it);
+        case 31: return p_pair_copyout(l, it);
+        case 32: return p_bias_bcast(l, it);
+        case 33: return p_live_u8(l, it);
+        case 34: return p_live_u32(l, it);
+        case 35: return p_fac_tile(l, it);
+        case 36: return p_pair7_qk_write(l, it);
+        case 37: return p_pair7_v_write(l, it);
+        case 38: return p_pair7_copyout(l, it);
     }
     return 0;
 }
@@ -174,7 +226,7 @@ __global__ __launch_bounds__(256) void k_probe(uint32_t* __restrict__ sink, int 
     uint4 v4 = make_uint4(salt, salt + 1, salt + 2, salt + 3);
 #pragma unroll 8
     for (int it = 0; it < ITERS; ++it) {
-        constexpr int W = (MODE == R16 || MODE == W16) ? 16 : (MODE == R4 ? 4 : 8);
+        constexpr int W = (MODE == R16 || MODE == W16) ? 16 : (MODE == R4 ? 4 : (MODE == R1 ? 1 : 8));
         const int a = addr_of<PAT>(l, it ^ (salt & 0x10000)) & (LDS_BYTES - W);
         if (MODE == R16) {
             const uint4 v = *reinterpret_cast<const uint4*>(lds + a);
@@ -188,6 +240,8 @@ __global__ __launch_bounds__(256) void k_probe(uint32_t* __restrict__ sink, int 
         } else if (MODE == W8) {
             v4.x += it;
             *reinterpret_cast<uint2*>(lds + a) = make_uint2(v4.x, v4.y);
+        } else if (MODE == R1) {
+            acc += (uint32_t)(uint8_t)lds[a];
         } else {
             acc += *reinterpret_cast<const uint32_t*>(lds + a);
         }
@@ -243,6 +297,16 @@ int main() {
     run<12, R8>("proj_stage_qk_as_read", sink);
     run<20, R8>("r_stride16", sink);
     run<1, W16>("contig8_as_w128", sink);
+    run<29, W16>("pair_qk_write", sink);
+    run<30, W16>("pair_v_write", sink);
+    run<31, R16>("pair_copyout_read", sink);
+    run<32, R16>("bias_bcast_read", sink);
+    run<33, R1>("live_u8_read", sink);
+    run<34, R4>("live_u32_read", sink);
+    run<35, R16>("fac_tile_read", sink);
+    run<36, W16>("pair7_qk_write", sink);
+    run<37, W16>("pair7_v_write", sink);
+    run<38, R16>("pair7_copyout_read", sink);
     (void)hipFree(sink);
     return 0;
 }
