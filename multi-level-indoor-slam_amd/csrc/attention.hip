@@ -32,6 +32,16 @@ __device__ unsigned long long g_att_trace[ATT_TRACE_WGS * 8];
 #else
 #define ATT_T(i) (void)0
 #endif
+// Staging writes by the calibrated LDS write rule (writes retire 128 B per cycle in lane
+// order -- b64: 16 lanes, b128: 8 lanes -- and conflict unless those lanes hit distinct
+// banks modulo 128 B; profiles/r05x_lds_calibration.txt): the K / V staging lanes take
+// rows (r, r + 2) per 16-lane group instead of (r, r + 1), whose V^T granule swizzles
+// differ in bit 0, so the two rows' b64 writes fill disjoint halves of the 128-B window;
+// the O epilogue pairs lanes l / l + 32 (v_permlane32_swap) into whole-chunk b128 writes.
+// 0: the round-4 staging (A/B only).
+#ifndef MLG_ATT_STAGE_W
+#define MLG_ATT_STAGE_W 1
+#endif
 constexpr int KB = 64;                 // keys per block
 constexpr int KTILE_BYTES = KB * 128;  // 64 rows x 64 bf16
 constexpr int VTILE_BYTES = 64 * KB * 2;
@@ -382,7 +392,10 @@ __device__ __forceinline__ void attention_tile_pipe(unsigned long long* att_tt, 
     c.smem = smem;
     c.T = T;
     c.nkb = (T + KB - 1) / KB;
-    const int srow = tid >> 3, sch = tid & 7;  // rows srow (+ 32 when 256 threads) of each 64-row tile
+    // rows srow (+ 32 when 256 threads) of each 64-row tile; MLG_ATT_STAGE_W: 16-lane group k
+    // stages rows b, b + 2 with b = 4 (k >> 1) + (k & 1) (a bijection onto the same rows)
+    const int sg = tid >> 4;
+    const int srow = MLG_ATT_STAGE_W ? 4 * (sg >> 1) + (sg & 1) + 2 * ((tid >> 3) & 1) : tid >> 3, sch = tid & 7;
     c.gk_off = srow * 64 + sch * 8;
     c.gv_off = srow * 64 + sch * 8;
     c.sk0 = k_off(srow, sch);
@@ -493,19 +506,43 @@ __device__ __forceinline__ void attention_tile_pipe(unsigned long long* att_tt, 
     __syncthreads();
     char* st = smem + wave * (32 * QT * 128);
     if constexpr (!SPLIT) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt) {
-            const float inv = 1.0f / swap_sum(lsum[qt][0] + lsum[qt][1]);
-            const int r = qt * 32 + col;
+        if (MLG_ATT_STAGE_W && QT == 2) {
+            // lanes l / l + 32 hold the two 8-B halves of chunk (dt, g) of rows col (tile 0) and
+            // 32 + col (tile 1): after the swap lane l < 32 holds row col's whole chunk, lane
+            // l + 32 row 32 + col's -- one b128 write each, 8 consecutive rows per write group
+            const float inv0 = 1.0f / swap_sum(lsum[0][0] + lsum[0][1]);
+            const float inv1 = 1.0f / swap_sum(lsum[QT - 1][0] + lsum[QT - 1][1]);
+            const int r = 32 * hh + col;
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    uint2 w;
-                    w.x = pack_bf16x2(o[qt][dt][4 * g] * inv, o[qt][dt][4 * g + 1] * inv);
-                    w.y = pack_bf16x2(o[qt][dt][4 * g + 2] * inv, o[qt][dt][4 * g + 3] * inv);
-                    *reinterpret_cast<uint2*>(st + r * 128 + (((dt * 4 + g) ^ (r & 7)) << 4) + 8 * hh) = w;
+                    const f32x16& a0 = o[0][dt];
+                    const f32x16& a1 = o[QT - 1][dt];
+                    const auto s0 = __builtin_amdgcn_permlane32_swap(
+                        pack_bf16x2(a0[4 * g] * inv0, a0[4 * g + 1] * inv0),
+                        pack_bf16x2(a1[4 * g] * inv1, a1[4 * g + 1] * inv1), false, false);
+                    const auto s1 = __builtin_amdgcn_permlane32_swap(
+                        pack_bf16x2(a0[4 * g + 2] * inv0, a0[4 * g + 3] * inv0),
+                        pack_bf16x2(a1[4 * g + 2] * inv1, a1[4 * g + 3] * inv1), false, false);
+                    *reinterpret_cast<uint4*>(st + r * 128 + (((dt * 4 + g) ^ (r & 7)) << 4)) =
+                        make_uint4(s0[0], s1[0], s0[1], s1[1]);
                 }
+        } else {
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const float inv = 1.0f / swap_sum(lsum[qt][0] + lsum[qt][1]);
+                const int r = qt * 32 + col;
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        uint2 w;
+                        w.x = pack_bf16x2(o[qt][dt][4 * g] * inv, o[qt][dt][4 * g + 1] * inv);
+                        w.y = pack_bf16x2(o[qt][dt][4 * g + 2] * inv, o[qt][dt][4 * g + 3] * inv);
+                        *reinterpret_cast<uint2*>(st + r * 128 + (((dt * 4 + g) ^ (r & 7)) << 4) + 8 * hh) = w;
+                    }
+            }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
         __builtin_amdgcn_wave_barrier();

@@ -45,6 +45,22 @@ constexpr int ROWB = 1024;  // LDS bytes per token row: 512 bf16
 // group (rows {0-3,12-15,20-27} + 32 k, one chunk) then hit 16 distinct bank quads.
 __device__ __forceinline__ int cat_off(int row, int chunk) { return row * ROWB + ((chunk ^ (row & 15)) << 4); }
 
+// Epilogue writes into [x | msg] / the GELU tile (MLG_FFN_STAGE_W, MT = 2): lanes l and
+// l + 32 hold the two 8-B halves of one 16-B chunk (rows col and 32 + col in m-tiles 0 / 1);
+// a v_permlane32_swap gives lane l < 32 m-tile 0's whole chunk and lane l + 32 m-tile 1's,
+// written as one b128.  LDS writes retire 128 B per cycle in lane order (b128: 8 lanes,
+// banks modulo 128 B; profiles/r05x_lds_calibration.txt): 8 consecutive rows at slots
+// chunk ^ (r & 15) are distinct modulo 128 B -- the per-half b64 writes paid 2-way.
+#ifndef MLG_FFN_STAGE_W
+#define MLG_FFN_STAGE_W 1
+#endif
+__device__ __forceinline__ void cat_pair_write(char* lds, int chunk, uint2 m0v, uint2 m1v) {
+    const int lane = threadIdx.x & 63, col = lane & 31, hh = lane >> 5;
+    const auto s0 = __builtin_amdgcn_permlane32_swap(m0v.x, m1v.x, false, false);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(m0v.y, m1v.y, false, false);
+    *reinterpret_cast<uint4*>(lds + cat_off(32 * hh + col, chunk)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+}
+
 __device__ __forceinline__ bf16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
 // The tile's token rows are read once and the residual written once per block: they go
@@ -344,6 +360,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                 for (int g = 0; g < 4; ++g) {
                     const int n = 32 * NT1 * wave + 32 * t + 8 * g + 4 * hh;
                     const float4 b = *reinterpret_cast<const float4*>(s_bout + n);
+                    uint2 pk[MT];
     #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) {
                         const f32x16& a = acc[t][mt];
@@ -361,8 +378,14 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                             y2 = a[4 * g + 2] + b.z;
                             y3 = a[4 * g + 3] + b.w;
                         }
-                        *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, 32 + n / 8) + 8 * hh) =
-                            make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
+                        pk[mt] = make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
+                    }
+                    if constexpr (MLG_FFN_STAGE_W && MT == 2) {
+                        cat_pair_write(lds, 32 + n / 8, pk[0], pk[MT - 1]);
+                    } else {
+    #pragma unroll
+                        for (int mt = 0; mt < MT; ++mt)
+                            *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, 32 + n / 8) + 8 * hh) = pk[mt];
                     }
                 }
         }
@@ -445,6 +468,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                     const int n = 32 * NT2 * wave + 32 * t + 8 * g + 4 * hh;
                     const float4 lg = *reinterpret_cast<const float4*>(s_lng + n);
                     const float4 lb = *reinterpret_cast<const float4*>(s_lnb + n);
+                    uint2 pk[MT];
     #pragma unroll
                     for (int mt = 0; mt < MT; ++mt) {
                         const f32x16& a = acc[t][mt];
@@ -469,8 +493,14 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void k_lg_ffn(const bf16_
                             y2 = u23.x;
                             y3 = u23.y;
                         }
-                        *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, n / 8) + 8 * hh) =
-                            make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
+                        pk[mt] = make_uint2(pack_bf16x2(y0, y1), pack_bf16x2(y2, y3));
+                    }
+                    if constexpr (MLG_FFN_STAGE_W && MT == 2) {
+                        cat_pair_write(lds, n / 8, pk[0], pk[MT - 1]);
+                    } else {
+    #pragma unroll
+                        for (int mt = 0; mt < MT; ++mt)
+                            *reinterpret_cast<uint2*>(lds + cat_off(32 * mt + col, n / 8) + 8 * hh) = pk[mt];
                     }
                 }
         }
