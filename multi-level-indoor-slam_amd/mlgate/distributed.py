@@ -65,9 +65,11 @@ class RowGather:
         if len(self.sizes) == 1:
             self.out.copy_(local)
             return self.out
-        if len(set(self.sizes)) == 1 and local.is_cuda and dist.get_backend(self.group) == "nccl":
-            # equal shards (N % W == 0, e.g. 5000 over 1 / 2 / 4 / 8 ranks): one RCCL
-            # all-gather straight into the [N, D] database, no staging copy
+        if len(set(self.sizes)) == 1 and not _staged(local, self.group):
+            # equal shards (N % W == 0, e.g. 5000 over 1 / 2 / 4 / 8 ranks): one all-gather
+            # straight into the [N, D] database, no staging copy -- RCCL on device tensors,
+            # and the very same call on host tensors under gloo (the world-size-2 CPU test
+            # with N = 1000 runs this branch, tests/test_distributed.py)
             dist.all_gather_into_tensor(self.out, local.contiguous(), group=self.group)
             return self.out
         self.send[:local.shape[0]].copy_(local)
