@@ -267,6 +267,9 @@ constexpr int SBM = 128;               // k_asg_sim tile (rows = columns)
 constexpr int TSS = SBM + 4;           // its LDS row stride: the 16 lanes of a b128 group (16 rows)
                                        // and the 64 lanes of a b32 column read hit distinct banks
 constexpr int ARM = 64, ARN = 128;     // k_asg_arg tile
+#ifndef MLG_ASG_FULL
+#define MLG_ASG_FULL 1  // k_asg_arg: straight-line scans for full tiles (0: the general loops only, A/B)
+#endif
 constexpr int TSA = ARN + 8;           // its LDS row stride: b128 groups of 8 rows x 2 halves
 
 // per-tile partials: part[((slot * 2 + dir) * tiles + t) * kmax + i]; dir 0 = rows
@@ -388,7 +391,37 @@ __global__ __launch_bounds__(256, 2) void k_asg_sim(const Asg* __restrict__ tab,
     const int q = tid & (SBM - 1);
     if (q >= (colw ? nc : mr)) return;
     float mx = -INFINITY, sm = 0.f;
-    if (colw) {
+    if (MLG_ASG_FULL && (colw ? mr : nc) == SBM) {
+        // full-length line: straight-line scans, no per-element bounds test (same order)
+        if (colw) {
+#pragma unroll 8
+            for (int e = 0; e < SBM; ++e) mx = fmaxf(mx, T[e * TSS + q]);
+            mx *= 0.0625f;
+            const float nm = -mx * L2E;
+#pragma unroll 8
+            for (int e = 0; e < SBM; ++e) sm += __builtin_amdgcn_exp2f(fmaf(T[e * TSS + q], 0.0625f * L2E, nm));
+        } else {
+            const float* p = T + q * TSS;
+#pragma unroll 8
+            for (int e = 0; e < SBM; e += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(p + e);
+                mx = fmaxf(mx, v.x);
+                mx = fmaxf(mx, v.y);
+                mx = fmaxf(mx, v.z);
+                mx = fmaxf(mx, v.w);
+            }
+            mx *= 0.0625f;
+            const float nm = -mx * L2E;
+#pragma unroll 8
+            for (int e = 0; e < SBM; e += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(p + e);
+                sm += __builtin_amdgcn_exp2f(fmaf(v.x, 0.0625f * L2E, nm));
+                sm += __builtin_amdgcn_exp2f(fmaf(v.y, 0.0625f * L2E, nm));
+                sm += __builtin_amdgcn_exp2f(fmaf(v.z, 0.0625f * L2E, nm));
+                sm += __builtin_amdgcn_exp2f(fmaf(v.w, 0.0625f * L2E, nm));
+            }
+        }
+    } else if (colw) {
         for (int e = 0; e < mr; ++e) mx = fmaxf(mx, T[e * TSS + q]);
         mx *= 0.0625f;
         const float nm = -mx * L2E;
@@ -482,7 +515,26 @@ __global__ __launch_bounds__(256, 4) void k_asg_arg(const Asg* __restrict__ tab,
     int bi = 0x7fffffff;
     if (tid < ARN) {
         const int r = tid >> 1, h = tid & 1;
-        if (r < mr) {
+        if (r < mr && MLG_ASG_FULL && nc == ARN) {
+            // full-width tile: straight-line scan, no per-element bounds test (same scores,
+            // same order, same strict > -- the general loop below, branch-free)
+            const float4 me = sr[r];
+            const float* p = T + r * TSA;
+#pragma unroll 4
+            for (int q = 0; q < ARN / 8; ++q) {
+                const int c = 8 * q + 4 * h;
+                const float4 v = *reinterpret_cast<const float4*>(p + c);
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float4 ot = sc[c + k];
+                    const float s = lg_score(vv[k] * 0.0625f, me.x, me.y, ot.x, ot.y, me.z + ot.z);
+                    const bool g = s > best;
+                    best = g ? s : best;
+                    bi = g ? c + k : bi;
+                }
+            }
+        } else if (r < mr) {
             const float4 me = sr[r];
             const float* p = T + r * TSA;
             for (int c = 4 * h; c < nc; c += 8) {
@@ -513,12 +565,23 @@ __global__ __launch_bounds__(256, 4) void k_asg_arg(const Asg* __restrict__ tab,
         const int j = tid - ARN;
         if (j >= nc) return;
         const float4 me = sc[j];
-        for (int e = 0; e < mr; ++e) {
-            const float4 ot = sr[e];
-            const float s = lg_score(T[e * TSA + j] * 0.0625f, ot.x, ot.y, me.x, me.y, ot.z + me.z);
-            if (s > best) {
-                best = s;
-                bi = e;
+        if (MLG_ASG_FULL && mr == ARM) {
+#pragma unroll 8
+            for (int e = 0; e < ARM; ++e) {
+                const float4 ot = sr[e];
+                const float s = lg_score(T[e * TSA + j] * 0.0625f, ot.x, ot.y, me.x, me.y, ot.z + me.z);
+                const bool g = s > best;
+                best = g ? s : best;
+                bi = g ? e : bi;
+            }
+        } else {
+            for (int e = 0; e < mr; ++e) {
+                const float4 ot = sr[e];
+                const float s = lg_score(T[e * TSA + j] * 0.0625f, ot.x, ot.y, me.x, me.y, ot.z + me.z);
+                if (s > best) {
+                    best = s;
+                    bi = e;
+                }
             }
         }
         part[part_at(blockIdx.z, 1, blockIdx.y, n0 + j, kmax)] =
