@@ -347,12 +347,22 @@ __device__ __forceinline__ float vmax_(float a, float b) { return fmaxf(a, b); }
 // (2 R + 1) max filter of the tile, separable, R = 4: each thread produces 4 consecutive
 // outputs from 12 inputs held in registers (one vector read per 4 in x, column reads in
 // y).  Values outside the tile are -inf / 0 (never in a used output: see k_sp_nms).
-template <typename T>
+// M (MLG_SP_NMS_MARGIN): only outputs at least M cells inside the tile border are
+// produced -- pass k of the five needs margin 4 k (its input is valid 4 (k - 1) in, every
+// later pass reads it only there), so the passes shrink instead of each covering the
+// whole 72 x 104 region (47 % of the pooling work; the outputs at margin 20 unchanged).
+#ifndef MLG_SP_NMS_MARGIN
+#define MLG_SP_NMS_MARGIN 1
+#endif
+template <int M0, typename T>
 __device__ __forceinline__ void nms_pool4(const T* in, T* tmp, T* out, T lo) {
     typedef typename Vec4<T>::type V;
+    constexpr int M = MLG_SP_NMS_MARGIN ? M0 : 0;
     constexpr int GX = NMS_LW / 4, GY = NMS_LH / 4;
-    for (int i = threadIdx.x; i < NMS_LH * GX; i += blockDim.x) {  // along x
-        const int y = i / GX, g = i - y * GX;
+    constexpr int XR0 = M > 4 ? M - 4 : 0, XR1 = M > 4 ? NMS_LH - M + 4 : NMS_LH;  // x-pass rows
+    constexpr int XG0 = M / 4, XGN = GX - 2 * (M / 4);                                // x-pass groups
+    for (int i = threadIdx.x; i < (XR1 - XR0) * XGN; i += blockDim.x) {  // along x
+        const int y = XR0 + i / XGN, g = XG0 + i % XGN;
         const V* row = reinterpret_cast<const V*>(in + y * NMS_LW);
         const V c = row[g];
         const V l = g > 0 ? row[g - 1] : V{lo, lo, lo, lo};
@@ -369,8 +379,9 @@ __device__ __forceinline__ void nms_pool4(const T* in, T* tmp, T* out, T lo) {
         reinterpret_cast<V*>(tmp + y * NMS_LW)[g] = V{o[0], o[1], o[2], o[3]};
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < GY * NMS_LW; i += blockDim.x) {  // along y
-        const int g = i / NMS_LW, x = i - g * NMS_LW, y0 = 4 * g;
+    constexpr int YG0 = M / 4, YGN = GY - 2 * (M / 4), YC0 = M, YCN = NMS_LW - 2 * M;  // y-pass
+    for (int i = threadIdx.x; i < YGN * YCN; i += blockDim.x) {  // along y
+        const int g = YG0 + i / YCN, x = YC0 + i % YCN, y0 = 4 * g;
         T v[12];
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
@@ -410,18 +421,21 @@ __global__ __launch_bounds__(512) void k_sp_nms(const float* __restrict__ sc, fl
         S[i] = (y >= 0 && y < H && x >= 0 && x < W) ? img[(size_t)y * W + x] : -INFINITY;
     }
     __syncthreads();
-    nms_pool4(S, Tm, P, -INFINITY);  // max_mask = scores == max_pool(scores)
+    nms_pool4<4>(S, Tm, P, -INFINITY);  // max_mask = scores == max_pool(scores)
     for (int i = threadIdx.x; i < NMS_N; i += blockDim.x) MK[i] = inside(i) && S[i] == P[i];
     __syncthreads();
-    for (int it = 0; it < 2; ++it) {
-        nms_pool4(MK, TU, SP, (uint8_t)0);  // supp_mask = max_pool(max_mask) > 0
+    auto iteration = [&](auto m) {  // margins 4 m + 4 (suppression), 4 m + 8 (new maxima)
+        constexpr int MS = decltype(m)::value;
+        nms_pool4<MS + 4>(MK, TU, SP, (uint8_t)0);  // supp_mask = max_pool(max_mask) > 0
         for (int i = threadIdx.x; i < NMS_N; i += blockDim.x) A[i] = inside(i) ? (SP[i] ? 0.f : S[i]) : -INFINITY;
         __syncthreads();
-        nms_pool4(A, Tm, P, -INFINITY);  // new_max_mask = supp_scores == max_pool(supp_scores)
+        nms_pool4<MS + 8>(A, Tm, P, -INFINITY);  // new_max_mask = supp_scores == max_pool(supp_scores)
         for (int i = threadIdx.x; i < NMS_N; i += blockDim.x)
             MK[i] = MK[i] | (inside(i) && A[i] == P[i] && !SP[i]);
         __syncthreads();
-    }
+    };
+    iteration(std::integral_constant<int, 4>{});
+    iteration(std::integral_constant<int, 12>{});
     for (int i = threadIdx.x; i < NMS_TH * NMS_TW; i += blockDim.x) {
         const int ly = i / NMS_TW + NMS_HALO, lx = i % NMS_TW + NMS_HALO;
         const int y = ly + oy, x = lx + ox;
