@@ -454,6 +454,9 @@ __global__ __launch_bounds__(512) void k_sp_nms(const float* __restrict__ sc, fl
 // are bitonic-sorted in LDS.  Output keypoints are (x, y) floats.
 constexpr int SEL_T = 1024;
 constexpr int SEL_KMAX = 4096;
+#ifndef MLG_SP_SEL_CHUNK
+#define MLG_SP_SEL_CHUNK 1  // coalesced chunked candidate compaction (0: per-thread segments, A/B)
+#endif
 
 __global__ __launch_bounds__(SEL_T) void k_sp_select(const float* __restrict__ scores, int H, int W, float thr, int k,
                                                      uint32_t* __restrict__ cand_key, int32_t* __restrict__ cand_idx,
@@ -471,29 +474,87 @@ __global__ __launch_bounds__(SEL_T) void k_sp_select(const float* __restrict__ s
     __shared__ uint32_t sh_prefix;
 
     // 1) ordered compaction of candidates
-    const long seg = (HW + SEL_T - 1) / SEL_T;
-    const long a0 = tid * seg, a1 = min(HW, a0 + seg);
-    int c = 0;
-    for (long i = a0; i < a1; ++i) c += s[i] > thr;
-    scan[tid] = c;
-    __syncthreads();
-    for (int o = 1; o < SEL_T; o <<= 1) {  // inclusive Hillis-Steele scan
-        const int v = tid >= o ? scan[tid - o] : 0;
-        __syncthreads();
-        scan[tid] += v;
-        __syncthreads();
-    }
-    int off = scan[tid] - c;
-    for (long i = a0; i < a1; ++i) {
-        const float v = s[i];
-        if (v > thr) {
-            ck[off] = __float_as_uint(v);
-            ci[off] = (int32_t)i;
-            ++off;
+    if (MLG_SP_SEL_CHUNK) {
+        // coalesced: chunks of SEL_T x 16 pixels, thread t holding pixels 16 t .. 16 t + 15
+        // of the chunk (four float4 loads, a wave reads 4 KiB contiguous); raster-order
+        // ranks from a wave shuffle scan of the per-thread counts plus the earlier waves'
+        // totals (double-buffered, one barrier per chunk).  The same list, in the same
+        // order, as the per-thread-segment form below (whose 300-pixel segments per lane
+        // made every load touch 64 lines).
+        __shared__ int wsum[2][SEL_T / 64];
+        const int lane = tid & 63, wave = tid >> 6;
+        constexpr int PER = 16, CH = SEL_T * PER;
+        const bool vec = (HW & 3) == 0;
+        int base = 0;
+        for (long c0 = 0, it = 0; c0 < HW; c0 += CH, ++it) {
+            const long p0 = c0 + (long)tid * PER;
+            float v[PER];
+#pragma unroll
+            for (int q = 0; q < PER / 4; ++q) {
+                const long i = p0 + 4 * q;
+                if (vec && i + 3 < HW) {
+                    const float4 f = *reinterpret_cast<const float4*>(s + i);
+                    v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[4 * q + j] = i + j < HW ? s[i + j] : -INFINITY;
+                }
+            }
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) cnt += v[j] > thr;
+            int x = cnt;  // inclusive wave scan
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (lane == 63) wsum[it & 1][wave] = x;
+            __syncthreads();
+            int wbase = 0, tot = 0;
+#pragma unroll
+            for (int w = 0; w < SEL_T / 64; ++w) {
+                const int t = wsum[it & 1][w];
+                wbase += w < wave ? t : 0;
+                tot += t;
+            }
+            int off = base + wbase + x - cnt;
+#pragma unroll
+            for (int j = 0; j < PER; ++j)
+                if (v[j] > thr) {
+                    ck[off] = __float_as_uint(v[j]);
+                    ci[off] = (int32_t)(p0 + j);
+                    ++off;
+                }
+            base += tot;
         }
+        if (tid == 0) sh_n = base;
+        __syncthreads();
+    } else {
+        const long seg = (HW + SEL_T - 1) / SEL_T;
+        const long a0 = tid * seg, a1 = min(HW, a0 + seg);
+        int c = 0;
+        for (long i = a0; i < a1; ++i) c += s[i] > thr;
+        scan[tid] = c;
+        __syncthreads();
+        for (int o = 1; o < SEL_T; o <<= 1) {  // inclusive Hillis-Steele scan
+            const int v = tid >= o ? scan[tid - o] : 0;
+            __syncthreads();
+            scan[tid] += v;
+            __syncthreads();
+        }
+        int off = scan[tid] - c;
+        for (long i = a0; i < a1; ++i) {
+            const float v = s[i];
+            if (v > thr) {
+                ck[off] = __float_as_uint(v);
+                ci[off] = (int32_t)i;
+                ++off;
+            }
+        }
+        if (tid == SEL_T - 1) sh_n = scan[SEL_T - 1];
+        __syncthreads();
     }
-    if (tid == SEL_T - 1) sh_n = scan[SEL_T - 1];
-    __syncthreads();
     const int n = sh_n;
     float* kp = kpts + (size_t)b * k * 2;
     float* ks = kscore + (size_t)b * k;
