@@ -191,13 +191,16 @@ __global__ __launch_bounds__(256) void k_lg_compact(const int4* __restrict__ mov
     const int newlen = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     __syncthreads();
     const int padded = (newlen + 63) & ~63;
-    for (int e = tid; e < mv.y * LG_D; e += 256) {
-        const int i = e / LG_D, cc = e % LG_D;
+    // 16-B x loads / stores and 8-B bf16 stores per lane (the same RNE conversion per
+    // element as f32_to_bf16); a wave moves one whole 1 KiB row of x per instruction
+    for (int e = tid; e < mv.y * (LG_D / 4); e += 256) {
+        const int i = e / (LG_D / 4), c4 = (e % (LG_D / 4)) * 4;
         const int rk = rank[i];
         if (rk < 0) continue;
-        const float val = x[(size_t)(mv.x + i) * LG_D + cc];
-        x2[(size_t)(mv.z + rk) * LG_D + cc] = val;
-        cat2[(size_t)(mv.z + rk) * 512 + cc] = f32_to_bf16(val);
+        const float4 val = *reinterpret_cast<const float4*>(x + (size_t)(mv.x + i) * LG_D + c4);
+        *reinterpret_cast<float4*>(x2 + (size_t)(mv.z + rk) * LG_D + c4) = val;
+        *reinterpret_cast<uint2*>(cat2 + (size_t)(mv.z + rk) * 512 + c4) =
+            make_uint2(pack_bf16x2(val.x, val.y), pack_bf16x2(val.z, val.w));
     }
     for (int e = tid; e < mv.y * 16; e += 256) {
         const int i = e / 16, p = e % 16;
@@ -208,10 +211,10 @@ __global__ __launch_bounds__(256) void k_lg_compact(const int4* __restrict__ mov
     for (int i = tid; i < mv.y; i += 256)
         if (rank[i] >= 0) ind2[mv.z + rank[i]] = ind[mv.x + i];
     // zero the padding rows of the new segment
-    for (int e = tid; e < (padded - newlen) * LG_D; e += 256) {
-        const int i = newlen + e / LG_D, cc = e % LG_D;
-        x2[(size_t)(mv.z + i) * LG_D + cc] = 0.f;
-        cat2[(size_t)(mv.z + i) * 512 + cc] = 0;
+    for (int e = tid; e < (padded - newlen) * (LG_D / 4); e += 256) {
+        const int i = newlen + e / (LG_D / 4), c4 = (e % (LG_D / 4)) * 4;
+        *reinterpret_cast<float4*>(x2 + (size_t)(mv.z + i) * LG_D + c4) = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<uint2*>(cat2 + (size_t)(mv.z + i) * 512 + c4) = make_uint2(0u, 0u);
     }
     for (int e = tid; e < (padded - newlen) * 16; e += 256) {
         const int i = newlen + e / 16, p = e % 16;
