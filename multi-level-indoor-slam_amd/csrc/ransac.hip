@@ -44,6 +44,13 @@
 #include "common.h"
 #include "kernels.h"
 
+// Values that feed a branch, a root or a count come from rs_math.h, the one header the C
+// twin (oracle/csrc/ransac_cv.c) includes too; this file builds with -ffp-contract=off
+// (csrc/Makefile) as the twin does, so both produce the same bits (tests/test_ransac_gpu.py).
+#define RS_FN __host__ __device__ static inline
+#define RS_CONST static __constant__ const
+#include "rs_math.h"
+
 namespace {
 
 #define RS_HD __host__ __device__  // solvers also build for host-side unit checks
@@ -198,217 +205,6 @@ RS_HD int real_roots(const double* cin, int deg, double* roots) {
     return ncrit;
 }
 
-// ------------------------------------------------------------------ 5-point solver
-// E = x X + y Y + z Z + W over the 4-dim null space; the 10 cubic constraints
-// det(E) = 0 and 2 E E^T E - tr(E E^T) E = 0 in monomials x^a y^b z^c (a+b+c <= 3).
-// Hidden variable z (Li & Hartley): C(z) m = 0 with m = [x^3 x^2y xy^2 y^3 x^2 xy y^2 x y 1];
-// det C(z) is a degree-10 polynomial, recovered exactly from its values at the 11th
-// roots of unity; each real root gives m from the null vector of C(z).
-
-// monomial index for exponents (a, b, c), a+b+c <= 3: 20 slots
-RS_HD __forceinline__ int midx(int a, int b, int c) { return (a * 4 + b) * 4 + c; }  // sparse 64-slot map
-
-struct P1 { double v[4]; };    // coefficients of x, y, z, 1
-struct P3 { double v[64]; };   // sparse map over (a, b, c) with a, b, c < 4
-
-RS_HD void p1_mul_p1(const P1& a, const P1& b, double (&out)[64]) {
-    const int ex[4][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}};
-    for (int i = 0; i < 64; ++i) out[i] = 0.0;
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j)
-            out[midx(ex[i][0] + ex[j][0], ex[i][1] + ex[j][1], ex[i][2] + ex[j][2])] += a.v[i] * b.v[j];
-}
-
-RS_HD void p2_mul_p1(const double (&a)[64], const P1& b, double (&out)[64]) {
-    const int ex[4][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}};
-    for (int i = 0; i < 64; ++i) out[i] = 0.0;
-    for (int aa = 0; aa < 3; ++aa)
-        for (int bb = 0; bb + aa < 3; ++bb)
-            for (int cc = 0; cc + aa + bb < 3; ++cc) {
-                const double s = a[midx(aa, bb, cc)];
-                if (s == 0.0) continue;
-                for (int j = 0; j < 4; ++j)
-                    out[midx(aa + ex[j][0], bb + ex[j][1], cc + ex[j][2])] += s * b.v[j];
-            }
-}
-
-struct Cplx { double re, im; };
-RS_HD __forceinline__ Cplx cmul(Cplx a, Cplx b) { return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
-RS_HD __forceinline__ Cplx csub(Cplx a, Cplx b) { return {a.re - b.re, a.im - b.im}; }
-RS_HD __forceinline__ double cabs2(Cplx a) { return a.re * a.re + a.im * a.im; }
-RS_HD __forceinline__ Cplx cdiv(Cplx a, Cplx b) {
-    const double d = cabs2(b);
-    return {(a.re * b.re + a.im * b.im) / d, (a.im * b.re - a.re * b.im) / d};
-}
-
-
-RS_HD int solve_5pt(const double (&q1)[5][2], const double (&q2)[5][2], double* Eout) {
-    // x,y monomial columns of C(z): (a, b) exponents
-    const int kXY[10][2] = {{3, 0}, {2, 1}, {1, 2}, {0, 3}, {2, 0}, {1, 1}, {0, 2}, {1, 0}, {0, 1}, {0, 0}};
-    double A[5][9];
-    for (int i = 0; i < 5; ++i) {
-        const double x1 = q1[i][0], y1 = q1[i][1], x2 = q2[i][0], y2 = q2[i][1];
-        // q2^T E q1 = 0, E row-major
-        A[i][0] = x2 * x1; A[i][1] = x2 * y1; A[i][2] = x2;
-        A[i][3] = y2 * x1; A[i][4] = y2 * y1; A[i][5] = y2;
-        A[i][6] = x1;      A[i][7] = y1;      A[i][8] = 1.0;
-    }
-    double Nb[4][9];
-    if (!null_space9<5>(A, Nb)) return 0;
-    P1 E[9];
-    for (int k = 0; k < 9; ++k) E[k] = P1{{Nb[0][k], Nb[1][k], Nb[2][k], Nb[3][k]}};
-    // equations as sparse 64-slot polynomials
-    double eq[10][64];
-    {
-        // det(E) = E0 (E4 E8 - E5 E7) - E1 (E3 E8 - E5 E6) + E2 (E3 E7 - E4 E6)
-        double t1[64], t2[64], m[64];
-        for (int i = 0; i < 64; ++i) eq[0][i] = 0.0;
-        const int cof[3][5] = {{0, 4, 8, 5, 7}, {1, 3, 8, 5, 6}, {2, 3, 7, 4, 6}};
-        const double sg[3] = {1.0, -1.0, 1.0};
-        for (int r = 0; r < 3; ++r) {
-            p1_mul_p1(E[cof[r][1]], E[cof[r][2]], t1);
-            p1_mul_p1(E[cof[r][3]], E[cof[r][4]], t2);
-            for (int i = 0; i < 64; ++i) t1[i] -= t2[i];
-            p2_mul_p1(t1, E[cof[r][0]], m);
-            for (int i = 0; i < 64; ++i) eq[0][i] += sg[r] * m[i];
-        }
-    }
-    {
-        // EEt[i][j] = sum_k E[i][k] E[j][k]  (quadratics)
-        double EEt[3][3][64];
-        double t[64];
-        for (int i = 0; i < 3; ++i)
-            for (int j = i; j < 3; ++j) {
-                for (int s = 0; s < 64; ++s) EEt[i][j][s] = 0.0;
-                for (int k = 0; k < 3; ++k) {
-                    p1_mul_p1(E[i * 3 + k], E[j * 3 + k], t);
-                    for (int s = 0; s < 64; ++s) EEt[i][j][s] += t[s];
-                }
-                if (j != i)
-                    for (int s = 0; s < 64; ++s) EEt[j][i][s] = EEt[i][j][s];
-            }
-        double tr[64];
-        for (int s = 0; s < 64; ++s) tr[s] = 0.5 * (EEt[0][0][s] + EEt[1][1][s] + EEt[2][2][s]);
-        // (E E^T - 1/2 tr) E  -> 9 cubics
-        for (int i = 0; i < 3; ++i)
-            for (int j = 0; j < 3; ++j) {
-                double* o = eq[1 + i * 3 + j];
-                for (int s = 0; s < 64; ++s) o[s] = 0.0;
-                double m[64];
-                for (int k = 0; k < 3; ++k) {
-                    double a[64];
-                    for (int s = 0; s < 64; ++s) a[s] = EEt[i][k][s] - (i == k ? tr[s] : 0.0);
-                    p2_mul_p1(a, E[k * 3 + j], m);
-                    for (int s = 0; s < 64; ++s) o[s] += m[s];
-                }
-            }
-    }
-    // coefficient of z^c in column (a, b) of row r
-    // det C(z) at the 11th roots of unity
-    Cplx dv[11];
-    for (int k = 0; k < 11; ++k) {
-        const double ang = 2.0 * M_PI * k / 11.0;
-        const Cplx w{cos(ang), sin(ang)};
-        Cplx zp[4] = {{1.0, 0.0}, w, cmul(w, w), cmul(cmul(w, w), w)};
-        Cplx C[10][10];
-        for (int r = 0; r < 10; ++r)
-            for (int col = 0; col < 10; ++col) {
-                const int a = kXY[col][0], b = kXY[col][1];
-                Cplx s{0.0, 0.0};
-                for (int c = 0; a + b + c <= 3; ++c) {
-                    const double co = eq[r][midx(a, b, c)];
-                    s.re += co * zp[c].re;
-                    s.im += co * zp[c].im;
-                }
-                C[r][col] = s;
-            }
-        Cplx det{1.0, 0.0};
-        for (int c = 0; c < 10; ++c) {
-            int p = c;
-            double bv = cabs2(C[c][c]);
-            for (int r = c + 1; r < 10; ++r)
-                if (cabs2(C[r][c]) > bv) { bv = cabs2(C[r][c]); p = r; }
-            if (bv == 0.0) { det = {0.0, 0.0}; break; }
-            if (p != c) {
-                for (int j = 0; j < 10; ++j) { Cplx t = C[c][j]; C[c][j] = C[p][j]; C[p][j] = t; }
-                det = {-det.re, -det.im};
-            }
-            det = cmul(det, C[c][c]);
-            for (int r = c + 1; r < 10; ++r) {
-                const Cplx f = cdiv(C[r][c], C[c][c]);
-                for (int j = c; j < 10; ++j) C[r][j] = csub(C[r][j], cmul(f, C[c][j]));
-            }
-        }
-        dv[k] = det;
-    }
-    double poly[11];
-    for (int j = 0; j <= 10; ++j) {
-        double s = 0.0;
-        for (int k = 0; k < 11; ++k) {
-            const double ang = -2.0 * M_PI * ((j * k) % 11) / 11.0;
-            s += dv[k].re * cos(ang) - dv[k].im * sin(ang);
-        }
-        poly[j] = s / 11.0;
-    }
-    double zr[10];
-    const int nz = real_roots(poly, 10, zr);
-    int nsol = 0;
-    for (int t = 0; t < nz && nsol < MAXSOL; ++t) {
-        const double z = zr[t];
-        double C[10][10];
-        for (int r = 0; r < 10; ++r)
-            for (int col = 0; col < 10; ++col) {
-                const int a = kXY[col][0], b = kXY[col][1];
-                double s = 0.0, zp = 1.0;
-                for (int c = 0; a + b + c <= 3; ++c) { s += eq[r][midx(a, b, c)] * zp; zp *= z; }
-                C[r][col] = s;
-            }
-        // null vector of C: Gaussian elimination with full pivoting, smallest pivot last
-        int colp[10];
-        for (int i = 0; i < 10; ++i) colp[i] = i;
-        for (int c = 0; c < 9; ++c) {
-            int pr = c, pc = c;
-            double bv = 0.0;
-            for (int r = c; r < 10; ++r)
-                for (int q = c; q < 10; ++q)
-                    if (fabs(C[r][q]) > bv) { bv = fabs(C[r][q]); pr = r; pc = q; }
-            if (bv == 0.0) break;
-            if (pr != c)
-                for (int j = 0; j < 10; ++j) { double tt = C[c][j]; C[c][j] = C[pr][j]; C[pr][j] = tt; }
-            if (pc != c) {
-                for (int r = 0; r < 10; ++r) { double tt = C[r][c]; C[r][c] = C[r][pc]; C[r][pc] = tt; }
-                int ti = colp[c]; colp[c] = colp[pc]; colp[pc] = ti;
-            }
-            for (int r = c + 1; r < 10; ++r) {
-                const double f = C[r][c] / C[c][c];
-                for (int j = c; j < 10; ++j) C[r][j] -= f * C[c][j];
-            }
-        }
-        double v[10];
-        v[9] = 1.0;
-        for (int r = 8; r >= 0; --r) {
-            double s = C[r][9] * v[9];
-            for (int j = r + 1; j < 9; ++j) s += C[r][j] * v[j];
-            v[r] = -s / C[r][r];
-        }
-        double m[10];
-        for (int i = 0; i < 10; ++i) m[colp[i]] = v[i];
-        if (fabs(m[9]) < 1e-300) continue;
-        const double x = m[7] / m[9], y = m[8] / m[9];
-        if (!(fabs(x) < 1e300) || !(fabs(y) < 1e300)) continue;  // also rejects NaN
-        double* Eo = Eout + nsol * 9;
-        double nrm = 0.0;
-        for (int k = 0; k < 9; ++k) {
-            Eo[k] = x * Nb[0][k] + y * Nb[1][k] + z * Nb[2][k] + Nb[3][k];
-            nrm += Eo[k] * Eo[k];
-        }
-        nrm = 1.0 / sqrt(nrm);
-        for (int k = 0; k < 9; ++k) Eo[k] *= nrm;
-        ++nsol;
-    }
-    return nsol;
-}
-
 // ------------------------------------------------------------------ 7-point solver
 RS_HD int solve_7pt(const double (&q1)[7][2], const double (&q2)[7][2], double* Fout) {
     double A[7][9];
@@ -525,16 +321,9 @@ struct CvRng {
 constexpr double RANSAC_CONFIDENCE = 0.999;  // findEssentialMat / findFundamentalMat prob
 constexpr int RANSAC_MAX_ATTEMPTS = 10000;   // getSubset(..., maxAttempts) in run()
 
-// RANSACUpdateNumIters (ptsetreg.cpp); cvRound = round half to even
+// RANSACUpdateNumIters (ptsetreg.cpp), rs_math.h
 RS_HD int ransac_update_iters(double p, double ep, int model_points, int max_iters) {
-    p = fmin(fmax(p, 0.0), 1.0);
-    ep = fmin(fmax(ep, 0.0), 1.0);
-    double num = fmax(1.0 - p, 2.2250738585072014e-308);
-    double denom = 1.0 - pow(1.0 - ep, model_points);
-    if (denom < 2.2250738585072014e-308) return 0;
-    num = log(num);
-    denom = log(denom);
-    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
+    return rs_update_iters(p, ep, model_points, max_iters);
 }
 
 // haveCollinearPoints (fundam.cpp) for the last of `count` selected points
@@ -608,8 +397,8 @@ __global__ void k_ransac_prep(const float* __restrict__ kp1, const float* __rest
         __syncthreads();
         double d[2] = {0, 0};
         for (int i = threadIdx.x; i < S; i += blockDim.x) {
-            d[0] += hypot(kp1[2 * (s0 + i)] - m1x, kp1[2 * (s0 + i) + 1] - m1y);
-            d[1] += hypot(kp2[2 * (s0 + i)] - m2x, kp2[2 * (s0 + i) + 1] - m2y);
+            d[0] += rs_hypot(kp1[2 * (s0 + i)] - m1x, kp1[2 * (s0 + i) + 1] - m1y);
+            d[1] += rs_hypot(kp2[2 * (s0 + i)] - m2x, kp2[2 * (s0 + i) + 1] - m2y);
         }
         red[0][threadIdx.x] = d[0];
         red[1][threadIdx.x] = d[1];
@@ -794,10 +583,11 @@ __device__ int real_roots10(double (&c)[11], double (&roots)[10], int r, int gl,
     for (int i = 1; i <= 10; ++i) lead = (i == n) ? c[i] : lead;
 #pragma unroll
     for (int i = 0; i <= 10; ++i) c[i] = i <= n ? c[i] / lead : 0.0;
-    // start on a circle of the roots' geometric-mean modulus |c0|^(1/n)
-    const double R = fmax(pow(fabs(c[0]), 1.0 / n), 1e-6);
-    const double ang = 6.283185307179586 * r / n + 0.4;
-    double zr = R * cos(ang), zi = R * sin(ang);
+    // start on a circle of the roots' geometric-mean modulus |c0|^(1/n), at angles
+    // 2 pi r / n + 0.4 (rs_math.h: the twin's start points, bit for bit)
+    const double R = fmax(rs_root(fabs(c[0]), n), 1e-6);
+    const int rr = r < 10 ? r : 9;  // 16-lane groups: lanes 10..15 hold no root
+    double zr = R * RS_START_RE[n - 1][rr], zi = R * RS_START_IM[n - 1][rr];
     bool done = r >= n;
     for (int it = 0; it < 60; ++it) {
         // every lane of the group takes part in the gathers (converged ones included)
@@ -1326,27 +1116,24 @@ __global__ __launch_bounds__(64) void k_ransac_hyp(const PairInfo* __restrict__ 
     if (h >= H || (done && done[p])) return;
     const PairInfo pi = info[p];
     double* out = models + ((size_t)p * H + h) * MAXSOL * 9;
-    int ns = 0;
-    if (pi.mode == 1 || pi.mode == 5) return;  // essential matrix: k_ransac_hyp5
-    const bool direct = pi.mode == 4 || pi.mode == 5;
+    if (pi.mode == 1 || pi.mode == 5) return;  // essential matrix: k_ransac_null5 / hyp5 / roots5
+    const bool direct = pi.mode == 4;          // 7 points: the 7-point models directly
     if (pi.mode == 0 || (direct && h > 0)) {
         nsol[(size_t)p * H + h] = 0;
         return;
     }
-    const int m = (pi.mode == 1 || pi.mode == 5) ? 5 : 7;
     int idx[7];
-    // the stream depends on (seed, h) only, so a pair's result does not depend on the batch
-    uint64_t st = splitmix(seed ^ (uint64_t)h * 0x632BE59BD9B4E019ull);
     if (direct) {
-        for (int i = 0; i < m; ++i) idx[i] = i;
-    } else if (pi.mode == 1 || pi.mode == 2) {
+        for (int i = 0; i < 7; ++i) idx[i] = i;
+    } else if (pi.mode == 2) {  // RANSAC: OpenCV's sample stream (k_ransac_subsets)
         if (h >= nsub[p]) {
             nsol[(size_t)p * H + h] = 0;
             return;
         }
-        for (int i = 0; i < m; ++i) idx[i] = subsets[((size_t)p * H + h) * 7 + i];
-    } else {
-        for (int i = 0; i < m; ++i) {
+        for (int i = 0; i < 7; ++i) idx[i] = subsets[((size_t)p * H + h) * 7 + i];
+    } else {  // LMedS: the stream depends on (seed, h) only, so a pair's result does not depend on the batch
+        uint64_t st = splitmix(seed ^ (uint64_t)h * 0x632BE59BD9B4E019ull);
+        for (int i = 0; i < 7; ++i) {
             int v;
             bool dup;
             do {
@@ -1358,23 +1145,14 @@ __global__ __launch_bounds__(64) void k_ransac_hyp(const PairInfo* __restrict__ 
             idx[i] = v;
         }
     }
-    if (m == 5) {
-        double q1[5][2], q2[5][2];
-        for (int i = 0; i < 5; ++i) {
-            const double4 q = ptsn[pi.start + idx[i]];
-            q1[i][0] = q.x; q1[i][1] = q.y; q2[i][0] = q.z; q2[i][1] = q.w;
-        }
-        ns = solve_5pt(q1, q2, out);
-    } else {
-        double q1[7][2], q2[7][2];
-        for (int i = 0; i < 7; ++i) {
-            const double4 q = ptsn[pi.start + idx[i]];
-            q1[i][0] = q.x; q1[i][1] = q.y; q2[i][0] = q.z; q2[i][1] = q.w;
-        }
-        double Fn[3 * 9];
-        ns = solve_7pt(q1, q2, Fn);
-        for (int s = 0; s < ns; ++s) denorm_F(Fn + s * 9, pi.T1, pi.T2, out + s * 9);
+    double q1[7][2], q2[7][2];
+    for (int i = 0; i < 7; ++i) {
+        const double4 q = ptsn[pi.start + idx[i]];
+        q1[i][0] = q.x; q1[i][1] = q.y; q2[i][0] = q.z; q2[i][1] = q.w;
     }
+    double Fn[3 * 9];
+    const int ns = solve_7pt(q1, q2, Fn);
+    for (int s = 0; s < ns; ++s) denorm_F(Fn + s * 9, pi.T1, pi.T2, out + s * 9);
     nsol[(size_t)p * H + h] = (int8_t)ns;
 }
 

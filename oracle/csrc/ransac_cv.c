@@ -1,425 +1,906 @@
-/* OpenCV's findEssentialMat(RANSAC) restated in C -- test infrastructure only.
+/* OpenCV's findEssentialMat / findFundamentalMat RANSAC restated in C -- test
+ * infrastructure only.
  *
- * A compiled twin of oracle/geometry.py cv_ransac (K given) and five_point, for checks
- * that need the OpenCV-sequenced RANSAC on tens of thousands of pairs (a whole bench
- * step's verified pairs; the numpy restatement takes seconds per pair).  Same algorithm,
- * same sample stream, same acceptance rule:
- *   * points normalised by K, threshold thr / ((fx + fy) / 2), float32 Sampson error
- *     against float32(t^2) (EMEstimatorCallback::computeError);
- *   * cv::RNG((uint64)-1) multiply-with-carry, getSubset's duplicate redraw;
- *   * a model replaces the best iff its inlier count exceeds max(best, 4), and every
- *     replacement shrinks the budget by RANSACUpdateNumIters (cvRound = rint);
- *   * 5-point solver as geometry.py states it (Li & Hartley hidden-variable resultant):
- *     4-dim null space of the 5x9 epipolar design matrix, the 10 cubic constraints
- *     det(E) = 0 and 2 E E^T E - tr(E E^T) E = 0, det C(z) sampled at the 11th roots of
- *     unity and inverse-DFT'd to its degree-10 coefficients, real roots, (x, y) from the
- *     null vector of C(z), E normalised to unit Frobenius norm.
- * Linear algebra differs from numpy / LAPACK in rounding only (Householder null space
- * instead of an SVD basis, Aberth roots instead of companion eigenvalues, one-sided
- * Jacobi null vectors); tests/test_oracle_geometry.py pins this file against the numpy
- * restatement (identical inlier counts on seeded geometry and on real match sets).
- * Reference call site: scripts/semantic_gating/geometric_verification.py:128-146. */
+ * The serial twin of the GPU path (multi-level-indoor-slam_amd/csrc/ransac.hip), for checks
+ * that need the OpenCV-sequenced RANSAC on tens of thousands of pairs (a whole bench step's
+ * verified pairs; the numpy restatement oracle/geometry.py takes seconds per pair).
+ * Reference call sites: scripts/semantic_gating/geometric_verification.py:128-146
+ * (findEssentialMat when K is given, findFundamentalMat otherwise).
+ *
+ *   * sample stream: cv::RNG((uint64)-1) multiply-with-carry, getSubset's duplicate redraw,
+ *     for F checkSubset's collinearity test (haveCollinearPoints, FLT_EPSILON) with up to
+ *     10000 attempts (calib3d/ptsetreg.cpp, fundam.cpp);
+ *   * a model replaces the best iff its inlier count exceeds max(best, modelPoints - 1);
+ *     every replacement shrinks the budget by RANSACUpdateNumIters (cvRound = rint);
+ *   * E: points normalised by K, threshold thr / ((fx + fy) / 2), float32 Sampson error
+ *     against float32(t^2) (EMEstimatorCallback::computeError); 5 points: the minimal
+ *     solver's models directly;
+ *   * 5-point solver in OpenCV's formulation (calib3d/five-point.cpp runKernel): the 4-dim
+ *     null space of the 5 x 9 epipolar design matrix (Householder QR of its transpose where
+ *     OpenCV takes an SVD), the 10 cubic constraints det(E) = 0 and
+ *     (E E^T - tr(E E^T) / 2) E = 0 as a 10 x 20 coefficient matrix reduced to [I | A] by
+ *     Gauss-Jordan (partial pivoting), the 3 x 3 polynomial matrix in z on (x, y, 1) from
+ *     the pivot pairs (x^2z, x^2), (y^2z, y^2), (xyz, xy), its degree-10 determinant, the
+ *     real roots (Aberth-Ehrlich where OpenCV runs solvePoly's Durand-Kerner), (x, y) from
+ *     the matrix's null vector (largest cross product of two rows), E = x X + y Y + z Z + W
+ *     normalised;
+ *   * F: Hartley-normalised 7-point solver (null space by Gauss-Jordan + modified
+ *     Gram-Schmidt, det(a F1 + (1 - a) F2) interpolated at a = -1, 0, 1, 2, real roots by
+ *     isolation between the derivative's roots), F = T2^T Fn T1; error max(d1^2, d2^2) of
+ *     the point-to-epiline distances in pixels (FMEstimatorCallback); 7 points: the
+ *     solver's models directly; 8..14 points: least median of squares (OpenCV switches
+ *     FM_RANSAC to LMedS below 15) over the GPU's seeded counter-based sample stream.
+ *
+ * Bit-exact twin.  Every sum and product below is evaluated in the operand order
+ * ransac.hip evaluates it -- the GPU's 10 constraint rows sit one per lane and its
+ * Gauss-Jordan moves the pivot row by shuffles; here they are a 10 x 20 array in lane
+ * order; its Aberth iteration updates the ten estimates of a group from one snapshot per
+ * iteration; here likewise --, neither side contracts multiply-adds (oracle/Makefile and
+ * the ransac.hip rule of csrc/Makefile: -ffp-contract=off), and the start points, n-th
+ * root, logarithm and powers come from the one shared header rs_math.h instead of two
+ * math libraries.  So models, inlier counts and masks equal the GPU's bit for bit
+ * (tests/test_ransac_gpu.py).  oracle/geometry.py keeps the independent numpy
+ * restatement (Li & Hartley hidden-variable resultant, SVD null spaces, np.roots), which
+ * this file must agree with on seeded geometry (tests/test_oracle_geometry.py). */
 #define _GNU_SOURCE
-#include <complex.h>
 #include <float.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
-typedef double poly3[4][4][4]; /* coefficient of x^a y^b z^c, a + b + c <= 3 */
+#define RS_FN static inline
+#define RS_CONST static const
+#include "../../multi-level-indoor-slam_amd/csrc/rs_math.h"
 
-static void pmul(poly3 out, poly3 a, poly3 b) {
-    memset(out, 0, sizeof(poly3));
-    for (int a0 = 0; a0 < 4; a0++)
-        for (int a1 = 0; a0 + a1 < 4; a1++)
-            for (int a2 = 0; a0 + a1 + a2 < 4; a2++) {
-                double ca = a[a0][a1][a2];
-                if (ca == 0.0) continue;
-                for (int b0 = 0; a0 + b0 < 4; b0++)
-                    for (int b1 = 0; a0 + a1 + b0 + b1 < 4; b1++)
-                        for (int b2 = 0; a0 + a1 + a2 + b0 + b1 + b2 < 4; b2++)
-                            out[a0 + b0][a1 + b1][a2 + b2] += ca * b[b0][b1][b2];
-            }
-}
+enum { MAXSOL = 10 };
 
-static void padd(poly3 out, poly3 a, double s) { /* out += s * a */
-    for (int i = 0; i < 64; i++) (&out[0][0][0])[i] += s * (&a[0][0][0])[i];
-}
+/* ------------------------------------------------------------------ 5-point solver */
 
-/* null space of the 5x9 design matrix: Householder QR of A^T (9x5), Q's last 4 columns */
-static void null4(const double A[5][9], double N[4][9]) {
-    double M[9][5], Q[9][9];
+/* null space of the 5 x 9 design matrix: Householder QR of A^T (9 x 5), the last 4
+ * columns of Q = H0 ... H4; rank < 5 (a diagonal below 1e-12 of its column) -> 0 */
+static int null5(const double A[5][9], double N[4][9]) {
+    double M[9][5], V[5][9], beta[5];
     for (int i = 0; i < 9; i++)
-        for (int j = 0; j < 5; j++) M[i][j] = A[j][i];
-    for (int i = 0; i < 9; i++)
-        for (int j = 0; j < 9; j++) Q[i][j] = (i == j);
-    for (int j = 0; j < 5; j++) {
-        double nrm = 0.0;
-        for (int i = j; i < 9; i++) nrm += M[i][j] * M[i][j];
-        nrm = sqrt(nrm);
-        if (nrm == 0.0) continue;
-        double v[9] = {0};
-        double alpha = M[j][j] > 0 ? -nrm : nrm;
-        for (int i = j; i < 9; i++) v[i] = M[i][j];
-        v[j] -= alpha;
-        double vv = 0.0;
-        for (int i = j; i < 9; i++) vv += v[i] * v[i];
-        if (vv == 0.0) continue;
-        for (int c = j; c < 5; c++) { /* M = H M */
-            double d = 0.0;
-            for (int i = j; i < 9; i++) d += v[i] * M[i][c];
-            d = 2.0 * d / vv;
-            for (int i = j; i < 9; i++) M[i][c] -= d * v[i];
+        for (int k = 0; k < 5; k++) M[i][k] = A[k][i];
+    int ok = 1;
+    for (int k = 0; k < 5; k++) {
+        double nrm2 = 0.0, scale = 0.0;
+        for (int i = k; i < 9; i++) nrm2 += M[i][k] * M[i][k];
+        for (int i = 0; i < 9; i++) scale += M[i][k] * M[i][k];
+        const double nrm = sqrt(nrm2);
+        ok = ok && nrm > 1e-12 * sqrt(scale) && nrm > 0.0;
+        const double alpha = M[k][k] > 0.0 ? -nrm : nrm;
+        double vn2 = 0.0;
+        for (int i = 0; i < 9; i++) {
+            V[k][i] = i < k ? 0.0 : (i == k ? M[k][k] - alpha : M[i][k]);
+            vn2 += V[k][i] * V[k][i];
         }
-        for (int r = 0; r < 9; r++) { /* Q = Q H */
-            double d = 0.0;
-            for (int i = j; i < 9; i++) d += Q[r][i] * v[i];
-            d = 2.0 * d / vv;
-            for (int i = j; i < 9; i++) Q[r][i] -= d * v[i];
+        beta[k] = vn2 > 0.0 ? 2.0 / vn2 : 0.0;
+        for (int j = k + 1; j < 5; j++) {
+            double s = 0.0;
+            for (int i = k; i < 9; i++) s += V[k][i] * M[i][j];
+            s *= beta[k];
+            for (int i = k; i < 9; i++) M[i][j] -= s * V[k][i];
         }
     }
-    for (int k = 0; k < 4; k++)
-        for (int i = 0; i < 9; i++) N[k][i] = Q[i][5 + k];
+    for (int j = 0; j < 4; j++) {
+        double e[9];
+        for (int i = 0; i < 9; i++) e[i] = (i == 5 + j) ? 1.0 : 0.0;
+        for (int k = 4; k >= 0; k--) {
+            double s = 0.0;
+            for (int i = k; i < 9; i++) s += V[k][i] * e[i];
+            s *= beta[k];
+            for (int i = k; i < 9; i++) e[i] -= s * V[k][i];
+        }
+        for (int i = 0; i < 9; i++) N[j][i] = e[i];
+    }
+    return ok;
 }
 
-static double complex cdet10(double complex A[10][10]) {
-    double complex det = 1.0;
-    for (int c = 0; c < 10; c++) {
-        int p = c;
-        for (int r = c + 1; r < 10; r++)
-            if (fabs(creal(A[r][c])) + fabs(cimag(A[r][c])) > fabs(creal(A[p][c])) + fabs(cimag(A[p][c]))) p = r;
-        if (A[p][c] == 0.0) return 0.0;
-        if (p != c) {
-            for (int j = 0; j < 10; j++) {
-                double complex t = A[c][j];
-                A[c][j] = A[p][j];
-                A[p][j] = t;
-            }
-            det = -det;
-        }
-        det *= A[c][c];
-        for (int r = c + 1; r < 10; r++) {
-            double complex f = A[r][c] / A[c][c];
-            for (int j = c; j < 10; j++) A[r][j] -= f * A[c][j];
-        }
-    }
-    return det;
+/* monomial columns of the 10 x 20 matrix (OpenCV's order):
+ *   x^3 y^3 x^2y xy^2 x^2z x^2 y^2z y^2 xyz xy | xz^2 xz x yz^2 yz y z^3 z^2 z 1 */
+static int mono_col(int a, int b, int c) {
+    return (a == 3) ? 0 : (b == 3) ? 1 : (a == 2 && b == 1) ? 2 : (a == 1 && b == 2) ? 3
+         : (a == 2 && c == 1) ? 4 : (a == 2) ? 5 : (b == 2 && c == 1) ? 6 : (b == 2) ? 7
+         : (a == 1 && b == 1 && c == 1) ? 8 : (a == 1 && b == 1) ? 9 : (a == 1 && c == 2) ? 10
+         : (a == 1 && c == 1) ? 11 : (a == 1) ? 12 : (b == 1 && c == 2) ? 13 : (b == 1 && c == 1) ? 14
+         : (b == 1) ? 15 : (c == 3) ? 16 : (c == 2) ? 17 : (c == 1) ? 18 : 19;
+}
+/* quadratic monomials x^2 xy xz x y^2 yz y z^2 z 1 and the linear ones x y z 1 */
+static const int QA[10] = {2, 1, 1, 1, 0, 0, 0, 0, 0, 0};
+static const int QB[10] = {0, 1, 0, 0, 2, 1, 1, 0, 0, 0};
+static const int QC[10] = {0, 0, 1, 0, 0, 1, 0, 2, 1, 0};
+static const int LA[4] = {1, 0, 0, 0}, LB[4] = {0, 1, 0, 0}, LC[4] = {0, 0, 1, 0};
+static int qidx(int a, int b, int c) {
+    return (a == 2) ? 0 : (a == 1 && b == 1) ? 1 : (a == 1 && c == 1) ? 2 : (a == 1) ? 3 : (b == 2) ? 4
+         : (b == 1 && c == 1) ? 5 : (b == 1) ? 6 : (c == 2) ? 7 : (c == 1) ? 8 : 9;
 }
 
-/* roots of c[0] + c[1] z + ... + c[deg] z^deg (np.roots: leading / trailing exact zeros
- * stripped, trailing ones give roots at 0); Aberth-Ehrlich iteration + Newton polish */
-static int poly_roots(const double *c_in, int deg, double complex *roots) {
-    double c[16];
-    memcpy(c, c_in, sizeof(double) * (deg + 1));
-    while (deg > 0 && c[deg] == 0.0) deg--;
-    int nz = 0, nr = 0;
-    while (nz < deg && c[nz] == 0.0) nz++;
-    for (int i = 0; i < nz; i++) roots[nr++] = 0.0;
-    const double *p = c + nz;
-    int n = deg - nz;
-    if (n <= 0) return nr;
-    /* initial points: a circle of the geometric-mean radius, off the real axis */
-    double rad = pow(fabs(p[0] / p[n]), 1.0 / n);
-    if (!(rad > 0.0) || !isfinite(rad)) rad = 1.0;
-    double complex z[16];
-    for (int i = 0; i < n; i++) z[i] = rad * cexp(I * (2.0 * M_PI * i / n + 0.4));
-    int done[16] = {0}, left = n;
-    for (int it = 0; it < 200 && left > 0; it++) {
-        for (int i = 0; i < n; i++) {
-            if (done[i]) continue;
-            double complex f = p[n], d = 0.0;
-            for (int k = n - 1; k >= 0; k--) {
-                d = d * z[i] + f;
-                f = f * z[i] + p[k];
-            }
-            if (f == 0.0) {
-                done[i] = 1;
-                left--;
-                continue;
-            }
-            double complex ratio = f / d, s = 0.0;
-            for (int j = 0; j < n; j++)
-                if (j != i) s += 1.0 / (z[i] - z[j]);
-            double complex w = ratio / (1.0 - ratio * s);
-            z[i] -= w;
-            if (cabs(w) <= 1e-14 * fmax(1e-300, cabs(z[i]))) {
-                done[i] = 1;
-                left--;
-            }
-        }
-    }
-    for (int i = 0; i < n; i++) { /* Newton polish */
-        for (int it = 0; it < 3; it++) {
-            double complex f = p[n], d = 0.0;
-            for (int k = n - 1; k >= 0; k--) {
-                d = d * z[i] + f;
-                f = f * z[i] + p[k];
-            }
-            if (d == 0.0 || f == 0.0) break;
-            z[i] -= f / d;
-        }
-        roots[nr++] = z[i];
-    }
-    return nr;
+/* q += s * (l1 * l2) over linear polynomials [x, y, z, 1] */
+static void q_fma(double q[10], const double *l1, const double *l2, double s) {
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) q[qidx(LA[i] + LA[j], LB[i] + LB[j], LC[i] + LC[j])] += s * l1[i] * l2[j];
 }
-
-/* null vector of a real 10x10 of rank 9: Householder QR with column pivoting of A^T
- * (the rows of A, largest remaining norm first); the last column of Q is orthogonal to
- * the 9 pivot rows, i.e. spans the null space (geometry.py takes the SVD's last right
- * singular vector: the same direction up to sign and rounding) */
-static void null_vec10(double A[10][10], double out[10]) {
-    double M[10][10], Q[10][10];
+/* c += q * l (quadratic times linear into the 20 cubic columns) */
+static void c_fma(double c[20], const double q[10], const double *l) {
     for (int i = 0; i < 10; i++)
-        for (int j = 0; j < 10; j++) {
-            M[i][j] = A[j][i]; /* column j of M = row j of A */
-            Q[i][j] = (i == j);
-        }
-    for (int j = 0; j < 9; j++) {
-        int piv = j;
-        double best = -1.0;
-        for (int c = j; c < 10; c++) {
-            double nn = 0.0;
-            for (int i = j; i < 10; i++) nn += M[i][c] * M[i][c];
-            if (nn > best) {
-                best = nn;
-                piv = c;
-            }
-        }
-        if (piv != j)
-            for (int i = 0; i < 10; i++) {
-                double t = M[i][j];
-                M[i][j] = M[i][piv];
-                M[i][piv] = t;
-            }
-        double nrm = sqrt(best);
-        if (nrm == 0.0) continue;
-        double v[10] = {0};
-        double alpha = M[j][j] > 0 ? -nrm : nrm;
-        for (int i = j; i < 10; i++) v[i] = M[i][j];
-        v[j] -= alpha;
-        double vv = 0.0;
-        for (int i = j; i < 10; i++) vv += v[i] * v[i];
-        if (vv == 0.0) continue;
-        for (int c = j; c < 10; c++) {
-            double d = 0.0;
-            for (int i = j; i < 10; i++) d += v[i] * M[i][c];
-            d = 2.0 * d / vv;
-            for (int i = j; i < 10; i++) M[i][c] -= d * v[i];
-        }
-        for (int r = 0; r < 10; r++) {
-            double d = 0.0;
-            for (int i = j; i < 10; i++) d += Q[r][i] * v[i];
-            d = 2.0 * d / vv;
-            for (int i = j; i < 10; i++) Q[r][i] -= d * v[i];
-        }
-    }
-    for (int i = 0; i < 10; i++) out[i] = Q[i][9];
+        for (int j = 0; j < 4; j++) c[mono_col(QA[i] + LA[j], QB[i] + LB[j], QC[i] + LC[j])] += q[i] * l[j];
+}
+static void ent(const double Nb[4][9], int k, double *l) {
+    for (int a = 0; a < 4; a++) l[a] = Nb[a][k];
 }
 
-static const int XY[10][2] = {{3, 0}, {2, 1}, {1, 2}, {0, 3}, {2, 0}, {1, 1}, {0, 2}, {1, 0}, {0, 1}, {0, 0}};
+/* the 10 constraint rows: row 0 det(E) = E0 (E4 E8 - E5 E7) - E1 (E3 E8 - E5 E6) +
+ * E2 (E3 E7 - E4 E6); row 1 + 3 i + j entry (i, j) of (E E^T - tr(E E^T) / 2) E */
+static void constraint_rows(const double Nb[4][9], double row[10][20]) {
+    memset(row, 0, sizeof(double) * 200);
+    static const int cof[3][5] = {{0, 4, 8, 5, 7}, {1, 3, 8, 5, 6}, {2, 3, 7, 4, 6}};
+    static const double sg[3] = {1.0, -1.0, 1.0};
+    for (int t = 0; t < 3; t++) {
+        double l0[4], l1[4], l2[4], l3[4], l4[4], q[10] = {0};
+        ent(Nb, cof[t][0], l0);
+        ent(Nb, cof[t][1], l1);
+        ent(Nb, cof[t][2], l2);
+        ent(Nb, cof[t][3], l3);
+        ent(Nb, cof[t][4], l4);
+        q_fma(q, l1, l2, sg[t]);
+        q_fma(q, l3, l4, -sg[t]);
+        c_fma(row[0], q, l0);
+    }
+    for (int r = 1; r < 10; r++) {
+        const int i = (r - 1) / 3, j = (r - 1) % 3;
+        double tr[10] = {0}, eet[3][10] = {{0}};
+        for (int l = 0; l < 3; l++) {
+            double a[4], b[4];
+            for (int kk = 0; kk < 3; kk++) {
+                ent(Nb, l * 3 + kk, a);
+                q_fma(tr, a, a, 0.5);
+            }
+            for (int kk = 0; kk < 3; kk++) {
+                ent(Nb, i * 3 + kk, a);
+                ent(Nb, l * 3 + kk, b);
+                q_fma(eet[l], a, b, 1.0);
+            }
+        }
+        for (int l = 0; l < 3; l++) {
+            double m[10], e[4];
+            for (int s = 0; s < 10; s++) m[s] = eet[l][s] - (l == i ? tr[s] : 0.0);
+            ent(Nb, l * 3 + j, e);
+            c_fma(row[r], m, e);
+        }
+    }
+}
 
-/* all real essential matrices through 5 normalised correspondences (row-major 3x3, unit
- * Frobenius); returns their number (<= 10).  geometry.py five_point. */
+static void pmul_acc(double *out, const double *a, int na, const double *b, int nb, double s) {
+    for (int i = 0; i < na; i++)
+        for (int j = 0; j < nb; j++) out[i + j] += s * a[i] * b[j];
+}
+
+/* real roots of sum c[i] z^i (degree <= 10): Aberth-Ehrlich on all roots at once, each
+ * iteration updating every unconverged estimate from the previous iteration's estimates
+ * (the GPU's ten lanes), at most 60 iterations; estimates with |im| <= 1e-7 max(1, |re|)
+ * polished by two real Newton steps, in estimate order */
+static int real_roots10(const double cin[11], double roots[10]) {
+    double c[11];
+    double mx = 0.0;
+    for (int i = 0; i <= 10; i++) {
+        c[i] = cin[i];
+        mx = fmax(mx, fabs(c[i]));
+    }
+    if (mx == 0.0) return 0;
+    int n = 0;
+    for (int i = 1; i <= 10; i++)
+        if (fabs(c[i]) > 1e-13 * mx) n = i;
+    if (n == 0) return 0;
+    const double lead = c[n];
+    for (int i = 0; i <= 10; i++) c[i] = i <= n ? c[i] / lead : 0.0;
+    const double R = fmax(rs_root(fabs(c[0]), n), 1e-6);
+    double zr[10], zi[10];
+    int done[10];
+    for (int r = 0; r < 10; r++) {
+        zr[r] = R * RS_START_RE[n - 1][r];
+        zi[r] = R * RS_START_IM[n - 1][r];
+        done[r] = r >= n;
+    }
+    for (int it = 0; it < 60; it++) {
+        double xr[10], xi[10];
+        memcpy(xr, zr, sizeof(xr));
+        memcpy(xi, zi, sizeof(xi));
+        int all = 1;
+        for (int r = 0; r < 10; r++) {
+            if (done[r]) continue;
+            double pr = 0.0, pi_ = 0.0, dr = 0.0, di = 0.0;
+            for (int i = 10; i >= 0; i--) {
+                if (i <= n) {
+                    const double ndr = dr * zr[r] - di * zi[r] + pr, ndi = dr * zi[r] + di * zr[r] + pi_;
+                    dr = ndr;
+                    di = ndi;
+                    const double npr = pr * zr[r] - pi_ * zi[r] + c[i], npi = pr * zi[r] + pi_ * zr[r];
+                    pr = npr;
+                    pi_ = npi;
+                }
+            }
+            const double dd = dr * dr + di * di;
+            double wr, wi;
+            if (dd > 0.0) {
+                wr = (pr * dr + pi_ * di) / dd;
+                wi = (pi_ * dr - pr * di) / dd;
+            } else {
+                wr = 1e-3 * R;
+                wi = 1e-3 * R;
+            }
+            double nr_ = 0.0, ni_ = 0.0, er = 1.0, ei = 0.0;
+            for (int j = 0; j < 10; j++) {
+                if (j != r && j < n) {
+                    const double ar = zr[r] - xr[j], ai = zi[r] - xi[j];
+                    const double tr = nr_ * ar - ni_ * ai + er, ti = nr_ * ai + ni_ * ar + ei;
+                    nr_ = tr;
+                    ni_ = ti;
+                    const double ur = er * ar - ei * ai, ui = er * ai + ei * ar;
+                    er = ur;
+                    ei = ui;
+                }
+            }
+            const double qr = er - (wr * nr_ - wi * ni_), qi = ei - (wr * ni_ + wi * nr_);
+            const double mr = wr * er - wi * ei, mi = wr * ei + wi * er;
+            const double qq = qr * qr + qi * qi;
+            double sr = wr, si = wi;
+            if (qq > 0.0 && isfinite(qq)) {
+                sr = (mr * qr + mi * qi) / qq;
+                si = (mi * qr - mr * qi) / qq;
+            }
+            zr[r] -= sr;
+            zi[r] -= si;
+            done[r] = sr * sr + si * si <= 1e-30 * (zr[r] * zr[r] + zi[r] * zi[r]) + 1e-300;
+            all = all && done[r];
+        }
+        if (all) break;
+    }
+    int nn = 0;
+    for (int r = 0; r < n; r++) {
+        if (!(fabs(zi[r]) <= 1e-7 * fmax(1.0, fabs(zr[r])))) continue;
+        double x = zr[r];
+        for (int pass = 0; pass < 2; pass++) {
+            double f = 0.0, df = 0.0;
+            for (int i = 10; i >= 0; i--)
+                if (i <= n) {
+                    df = df * x + f;
+                    f = f * x + c[i];
+                }
+            if (df != 0.0) {
+                const double xn = x - f / df;
+                if (isfinite(xn)) x = xn;
+            }
+        }
+        roots[nn++] = x;
+    }
+    return nn;
+}
+
+/* all real essential matrices through 5 normalised correspondences q1, q2 ([5][2] row
+ * major) into E_out (row-major 3 x 3 each, unit Frobenius); returns their number */
 int orc_five_point(const double *q1, const double *q2, double *E_out) {
-    double A[5][9], N[4][9];
+    double A[5][9], Nb[4][9];
     for (int i = 0; i < 5; i++) {
-        double x1 = q1[2 * i], y1 = q1[2 * i + 1], x2 = q2[2 * i], y2 = q2[2 * i + 1];
-        double row[9] = {x2 * x1, x2 * y1, x2, y2 * x1, y2 * y1, y2, x1, y1, 1.0};
-        memcpy(A[i], row, sizeof(row));
+        const double x1 = q1[2 * i], y1 = q1[2 * i + 1], x2 = q2[2 * i], y2 = q2[2 * i + 1];
+        A[i][0] = x2 * x1; A[i][1] = x2 * y1; A[i][2] = x2;
+        A[i][3] = y2 * x1; A[i][4] = y2 * y1; A[i][5] = y2;
+        A[i][6] = x1;      A[i][7] = y1;      A[i][8] = 1.0;
     }
-    null4(A, N);
-    poly3 E[9];
-    memset(E, 0, sizeof(E));
-    for (int k = 0; k < 9; k++) {
-        E[k][1][0][0] = N[0][k];
-        E[k][0][1][0] = N[1][k];
-        E[k][0][0][1] = N[2][k];
-        E[k][0][0][0] = N[3][k];
+    if (!null5(A, Nb)) return 0;
+    double row[10][20];
+    constraint_rows(Nb, row);
+    /* Gauss-Jordan: pivot = the unused row with the largest |entry| (first on ties); the
+     * pivot row scaled by its reciprocal, every other row (used ones too) eliminated */
+    int piv[10], used[10] = {0};
+    for (int c = 0; c < 10; c++) {
+        double best = -2.0;
+        int bl = 10;
+        for (int l = 0; l < 10; l++) {
+            const double ob = used[l] ? -1.0 : fabs(row[l][c]);
+            if (ob > best) {
+                best = ob;
+                bl = l;
+            }
+        }
+        if (!(best > 1e-300)) return 0;
+        piv[c] = bl;
+        double prow[20];
+        for (int jj = c; jj < 20; jj++) prow[jj] = row[bl][jj];
+        const double inv = 1.0 / prow[c];
+        for (int l = 0; l < 10; l++) {
+            if (l == bl) {
+                for (int jj = c; jj < 20; jj++) row[l][jj] = prow[jj] * inv;
+                used[l] = 1;
+            } else {
+                const double f = row[l][c] * inv;
+                for (int jj = c; jj < 20; jj++) row[l][jj] -= f * prow[jj];
+            }
+        }
     }
-    poly3 eqs[10], t1, t2, t3;
-    memset(eqs, 0, sizeof(eqs));
-    static const int DT[3][6] = {{1, 0, 4, 8, 5, 7}, {-1, 1, 3, 8, 5, 6}, {1, 2, 3, 7, 4, 6}};
-    for (int r = 0; r < 3; r++) {
-        const int *d = DT[r];
-        pmul(t1, E[d[2]], E[d[3]]);
-        pmul(t2, E[d[4]], E[d[5]]);
-        padd(t1, t2, -1.0);
-        pmul(t3, E[d[1]], t1);
-        padd(eqs[0], t3, (double)d[0]);
+    /* the 3 x 3 polynomial matrix on (x, y, 1); non-pivot columns of A:
+     * 0 xz^2, 1 xz, 2 x, 3 yz^2, 4 yz, 5 y, 6 z^3, 7 z^2, 8 z, 9 1 */
+    double bx[3][4], by[3][4], b1[3][5];
+    for (int i = 0; i < 3; i++) {
+        const double *a4 = row[piv[4 + 2 * i]] + 10, *a5 = row[piv[5 + 2 * i]] + 10;
+        bx[i][0] = a4[2]; bx[i][1] = a4[1] - a5[2]; bx[i][2] = a4[0] - a5[1]; bx[i][3] = -a5[0];
+        by[i][0] = a4[5]; by[i][1] = a4[4] - a5[5]; by[i][2] = a4[3] - a5[4]; by[i][3] = -a5[3];
+        b1[i][0] = a4[9]; b1[i][1] = a4[8] - a5[9]; b1[i][2] = a4[7] - a5[8]; b1[i][3] = a4[6] - a5[7];
+        b1[i][4] = -a5[6];
     }
-    static poly3 EEt[3][3];
-    memset(EEt, 0, sizeof(EEt));
+    /* det = bx0 (by1 b12 - b11 by2) - by0 (bx1 b12 - b11 bx2) + b10 (bx1 by2 - by1 bx2) */
+    double poly[11] = {0}, t[8] = {0}, u[7] = {0};
+    pmul_acc(t, by[1], 4, b1[2], 5, 1.0);
+    pmul_acc(t, b1[1], 5, by[2], 4, -1.0);
+    pmul_acc(poly, bx[0], 4, t, 8, 1.0);
+    memset(t, 0, sizeof(t));
+    pmul_acc(t, bx[1], 4, b1[2], 5, 1.0);
+    pmul_acc(t, b1[1], 5, bx[2], 4, -1.0);
+    pmul_acc(poly, by[0], 4, t, 8, -1.0);
+    pmul_acc(u, bx[1], 4, by[2], 4, 1.0);
+    pmul_acc(u, by[1], 4, bx[2], 4, -1.0);
+    pmul_acc(poly, b1[0], 5, u, 7, 1.0);
+    double zr[10];
+    const int nz = real_roots10(poly, zr);
+    int ns = 0;
+    for (int k = 0; k < nz; k++) {
+        const double z = zr[k];
+        double M[3][3];
+        for (int i = 0; i < 3; i++) {
+            double vx = 0.0, vy = 0.0, v1 = 0.0;
+            for (int d = 3; d >= 0; d--) {
+                vx = vx * z + bx[i][d];
+                vy = vy * z + by[i][d];
+            }
+            for (int d = 4; d >= 0; d--) v1 = v1 * z + b1[i][d];
+            M[i][0] = vx;
+            M[i][1] = vy;
+            M[i][2] = v1;
+        }
+        double best[3] = {0.0, 0.0, 0.0}, bn = -1.0;
+        for (int a = 0; a < 3; a++) {
+            const int b = (a + 1) % 3;
+            const double cx = M[a][1] * M[b][2] - M[a][2] * M[b][1];
+            const double cy = M[a][2] * M[b][0] - M[a][0] * M[b][2];
+            const double cz = M[a][0] * M[b][1] - M[a][1] * M[b][0];
+            const double n2 = cx * cx + cy * cy + cz * cz;
+            if (n2 > bn) {
+                bn = n2;
+                best[0] = cx;
+                best[1] = cy;
+                best[2] = cz;
+            }
+        }
+        if (!(fabs(best[2]) > 1e-300 * sqrt(fmax(bn, 1e-300)))) continue;
+        const double x = best[0] / best[2], y = best[1] / best[2];
+        if (!(fabs(x) < 1e300) || !(fabs(y) < 1e300)) continue;
+        double e[9], nrm = 0.0;
+        for (int q = 0; q < 9; q++) {
+            e[q] = x * Nb[0][q] + y * Nb[1][q] + z * Nb[2][q] + Nb[3][q];
+            nrm += e[q] * e[q];
+        }
+        nrm = 1.0 / sqrt(nrm);
+        for (int q = 0; q < 9; q++) E_out[ns * 9 + q] = e[q] * nrm;
+        ns++;
+    }
+    return ns;
+}
+
+/* ------------------------------------------------------------------ 7-point solver */
+
+static double det3(const double *F) {
+    return F[0] * (F[4] * F[8] - F[5] * F[7]) - F[1] * (F[3] * F[8] - F[5] * F[6]) +
+           F[2] * (F[3] * F[7] - F[4] * F[6]);
+}
+
+static double peval(const double *c, int n, double x) {
+    double v = c[n];
+    for (int i = n - 1; i >= 0; i--) v = v * x + c[i];
+    return v;
+}
+
+/* safeguarded regula falsi (Illinois) on a bracket [lo, hi] */
+static double refine_root(const double *c, int n, double lo, double hi, double flo) {
+    double fl = flo, fh = peval(c, n, hi);
+    int side = 0;
+    for (int it = 0; it < 100; it++) {
+        double x = (lo * fh - hi * fl) / (fh - fl);
+        if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
+        const double fx = peval(c, n, x);
+        if (fx == 0.0) return x;
+        if ((fx < 0) == (fl < 0)) {
+            lo = x;
+            fl = fx;
+            if (side == -1) fh *= 0.5;
+            side = -1;
+        } else {
+            hi = x;
+            fh = fx;
+            if (side == 1) fl *= 0.5;
+            side = 1;
+        }
+        if (hi - lo <= 1e-14 * fmax(1.0, fabs(lo))) break;
+    }
+    return 0.5 * (lo + hi);
+}
+
+/* real roots by recursive isolation between the roots of the derivative chain */
+static int real_roots(const double *cin, int deg, double *roots) {
+    double c[11];
+    int n = deg;
+    double mx = 0.0;
+    for (int i = 0; i <= deg; i++) {
+        c[i] = cin[i];
+        mx = fmax(mx, fabs(c[i]));
+    }
+    if (mx == 0.0) return 0;
+    while (n > 0 && fabs(c[n]) <= 1e-13 * mx) n--;
+    if (n == 0) return 0;
+    for (int i = 0; i <= n; i++) c[i] /= c[n];
+    double B = 0.0;
+    for (int i = 0; i < n; i++) B = fmax(B, fabs(c[i]));
+    B += 1.0;
+    double d[11][11];
+    for (int i = 0; i <= n; i++) d[0][i] = c[i];
+    for (int k = 1; k < n; k++)
+        for (int i = 0; i <= n - k; i++) d[k][i] = d[k - 1][i + 1] * (double)(i + 1);
+    double crit[11];
+    int ncrit = 1;
+    crit[0] = -d[n - 1][0] / d[n - 1][1];
+    for (int k = n - 2; k >= 0; k--) {
+        const int dg = n - k;
+        double pts[12], nr[11];
+        int np = 0, nn = 0;
+        pts[np++] = -B;
+        for (int i = 0; i < ncrit; i++)
+            if (crit[i] > -B && crit[i] < B) pts[np++] = crit[i];
+        pts[np++] = B;
+        double fprev = peval(d[k], dg, pts[0]);
+        for (int i = 1; i < np; i++) {
+            const double f = peval(d[k], dg, pts[i]);
+            if (fprev == 0.0) {
+                if (nn == 0 || nr[nn - 1] != pts[i - 1]) nr[nn++] = pts[i - 1];
+            } else if ((fprev < 0) != (f < 0) && f != 0.0) {
+                nr[nn++] = refine_root(d[k], dg, pts[i - 1], pts[i], fprev);
+            }
+            fprev = f;
+        }
+        if (fprev == 0.0 && (nn == 0 || nr[nn - 1] != pts[np - 1])) nr[nn++] = pts[np - 1];
+        ncrit = nn;
+        for (int i = 0; i < nn; i++) crit[i] = nr[i];
+    }
+    for (int i = 0; i < ncrit; i++) roots[i] = crit[i];
+    return ncrit;
+}
+
+/* null space of the 7 x 9 design matrix: Gauss-Jordan with partial pivoting, then two
+ * passes of modified Gram-Schmidt; rank < 7 -> 0 */
+static int null7(double A[7][9], double N[2][9]) {
+    int piv_col[7], r = 0;
+    for (int c = 0; c < 9 && r < 7; c++) {
+        int best = r;
+        double bv = fabs(A[r][c]);
+        for (int i = r + 1; i < 7; i++)
+            if (fabs(A[i][c]) > bv) {
+                bv = fabs(A[i][c]);
+                best = i;
+            }
+        if (bv < 1e-12) continue;
+        if (best != r)
+            for (int j = 0; j < 9; j++) {
+                double t = A[r][j];
+                A[r][j] = A[best][j];
+                A[best][j] = t;
+            }
+        const double inv = 1.0 / A[r][c];
+        for (int j = 0; j < 9; j++) A[r][j] *= inv;
+        for (int i = 0; i < 7; i++)
+            if (i != r) {
+                const double f = A[i][c];
+                if (f != 0.0)
+                    for (int j = 0; j < 9; j++) A[i][j] -= f * A[r][j];
+            }
+        piv_col[r++] = c;
+    }
+    if (r < 7) return 0;
+    int is_piv[9] = {0}, k = 0;
+    for (int i = 0; i < 7; i++) is_piv[piv_col[i]] = 1;
+    for (int f = 0; f < 9; f++) {
+        if (is_piv[f]) continue;
+        for (int j = 0; j < 9; j++) N[k][j] = 0.0;
+        N[k][f] = 1.0;
+        for (int i = 0; i < 7; i++) N[k][piv_col[i]] = -A[i][f];
+        k++;
+    }
+    for (int pass = 0; pass < 2; pass++)
+        for (int a = 0; a < 2; a++) {
+            for (int q = 0; q < a; q++) {
+                double d = 0.0;
+                for (int j = 0; j < 9; j++) d += N[a][j] * N[q][j];
+                for (int j = 0; j < 9; j++) N[a][j] -= d * N[q][j];
+            }
+            double n2 = 0.0;
+            for (int j = 0; j < 9; j++) n2 += N[a][j] * N[a][j];
+            n2 = 1.0 / sqrt(n2);
+            for (int j = 0; j < 9; j++) N[a][j] *= n2;
+        }
+    return 1;
+}
+
+/* fundamental matrices through 7 Hartley-normalised correspondences (unit Frobenius) */
+static int seven_point(const double (*q)[4], double *Fout) {
+    double A[7][9], Nb[2][9];
+    for (int i = 0; i < 7; i++) {
+        const double x1 = q[i][0], y1 = q[i][1], x2 = q[i][2], y2 = q[i][3];
+        A[i][0] = x2 * x1; A[i][1] = x2 * y1; A[i][2] = x2;
+        A[i][3] = y2 * x1; A[i][4] = y2 * y1; A[i][5] = y2;
+        A[i][6] = x1;      A[i][7] = y1;      A[i][8] = 1.0;
+    }
+    if (!null7(A, Nb)) return 0;
+    static const double as[4] = {-1.0, 0.0, 1.0, 2.0};
+    double f[4];
+    for (int i = 0; i < 4; i++) {
+        double F[9];
+        for (int k = 0; k < 9; k++) F[k] = as[i] * Nb[0][k] + (1.0 - as[i]) * Nb[1][k];
+        f[i] = det3(F);
+    }
+    /* Newton divided differences -> monomial coefficients */
+    const double d1 = f[1] - f[0], d2 = f[2] - f[1], d3 = f[3] - f[2];
+    const double e1 = (d2 - d1) / 2.0, e2 = (d3 - d2) / 2.0;
+    const double g = (e2 - e1) / 3.0;
+    double c[4], roots[3];
+    c[3] = g;
+    c[2] = e1;
+    c[1] = d1 + e1 - g;
+    c[0] = f[0] + d1;
+    const int nr = real_roots(c, 3, roots);
+    int ns = 0;
+    for (int t = 0; t < nr; t++) {
+        double *F = Fout + ns * 9, nrm = 0.0;
+        for (int k = 0; k < 9; k++) {
+            F[k] = roots[t] * Nb[0][k] + (1.0 - roots[t]) * Nb[1][k];
+            nrm += F[k] * F[k];
+        }
+        if (!(nrm > 0.0)) continue;
+        nrm = 1.0 / sqrt(nrm);
+        for (int k = 0; k < 9; k++) F[k] *= nrm;
+        ns++;
+    }
+    return ns;
+}
+
+/* F = T2^T Fn T1, unit Frobenius */
+static void denorm_F(const double *Fn, const double *T1, const double *T2, double *F) {
+    const double A[9] = {T1[0], 0, T1[1], 0, T1[0], T1[2], 0, 0, 1};
+    const double B[9] = {T2[0], 0, T2[1], 0, T2[0], T2[2], 0, 0, 1};
+    double t[9], nrm = 0.0;
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++)
-            for (int k = 0; k < 3; k++) {
-                pmul(t1, E[i * 3 + k], E[j * 3 + k]);
-                padd(EEt[i][j], t1, 1.0);
-            }
-    poly3 tr;
-    memset(tr, 0, sizeof(tr));
-    padd(tr, EEt[0][0], 1.0);
-    padd(tr, EEt[1][1], 1.0);
-    padd(tr, EEt[2][2], 1.0);
+            t[i * 3 + j] = Fn[i * 3 + 0] * A[0 * 3 + j] + Fn[i * 3 + 1] * A[1 * 3 + j] + Fn[i * 3 + 2] * A[2 * 3 + j];
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) {
-            poly3 *acc = &eqs[1 + i * 3 + j];
-            for (int k = 0; k < 3; k++) {
-                memcpy(t2, EEt[i][k], sizeof(poly3));
-                if (i == k) padd(t2, tr, -0.5);
-                pmul(t1, t2, E[k * 3 + j]);
-                padd(*acc, t1, 1.0);
-            }
+            F[i * 3 + j] = B[0 * 3 + i] * t[0 * 3 + j] + B[1 * 3 + i] * t[1 * 3 + j] + B[2 * 3 + i] * t[2 * 3 + j];
+            nrm += F[i * 3 + j] * F[i * 3 + j];
         }
-    /* det C(z) at the 11th roots of unity -> degree-10 coefficients */
-    static double complex tw[11];
-    static int tw_ready = 0;
-    if (!tw_ready) {
-        for (int s = 0; s < 11; s++) tw[s] = cexp(2.0 * M_PI * I * s / 11.0);
-        tw_ready = 1;
-    }
-    double complex vals[11];
-    for (int s = 0; s < 11; s++) {
-        double complex w = tw[s], C[10][10];
-        for (int r = 0; r < 10; r++)
-            for (int col = 0; col < 10; col++) {
-                int a = XY[col][0], b = XY[col][1];
-                double complex v = 0.0, zp = 1.0;
-                for (int c = 0; c < 4 - a - b; c++) {
-                    v += eqs[r][a][b][c] * zp;
-                    zp *= w;
-                }
-                C[r][col] = v;
-            }
-        vals[s] = cdet10(C);
-    }
-    double coef[11];
-    for (int j = 0; j < 11; j++) {
-        double complex acc = 0.0;
-        for (int s = 0; s < 11; s++) acc += vals[s] * conj(tw[(j * s) % 11]);
-        coef[j] = creal(acc) / 11.0;
-    }
-    double complex roots[16];
-    int nr = poly_roots(coef, 10, roots);
-    int out = 0;
-    for (int ri = 0; ri < nr; ri++) {
-        double complex zc = roots[ri];
-        if (fabs(cimag(zc)) > 1e-8 * fmax(1.0, cabs(zc))) continue;
-        double z = creal(zc), C[10][10], m[10];
-        for (int r = 0; r < 10; r++)
-            for (int col = 0; col < 10; col++) {
-                int a = XY[col][0], b = XY[col][1];
-                double v = 0.0, zp = 1.0;
-                for (int c = 0; c < 4 - a - b; c++) {
-                    v += eqs[r][a][b][c] * zp;
-                    zp *= z;
-                }
-                C[r][col] = v;
-            }
-        null_vec10(C, m);
-        if (fabs(m[9]) < 1e-300) continue;
-        double x = m[7] / m[9], y = m[8] / m[9], Ev[9], nrm = 0.0;
-        for (int k = 0; k < 9; k++) {
-            Ev[k] = x * N[0][k] + y * N[1][k] + z * N[2][k] + N[3][k];
-            nrm += Ev[k] * Ev[k];
-        }
-        nrm = sqrt(nrm);
-        for (int k = 0; k < 9; k++) E_out[out * 9 + k] = Ev[k] / nrm;
-        out++;
-    }
-    return out;
+    nrm = 1.0 / sqrt(nrm);
+    for (int k = 0; k < 9; k++) F[k] *= nrm;
+}
+
+/* ------------------------------------------------------------------ errors, sampling */
+
+/* float32 Sampson error of E on K-normalised points (EMEstimatorCallback::computeError) */
+static float err_sampson(const double *E, double x1, double y1, double x2, double y2) {
+    const double ex0 = E[0] * x1 + E[1] * y1 + E[2];
+    const double ex1 = E[3] * x1 + E[4] * y1 + E[5];
+    const double ex2 = E[6] * x1 + E[7] * y1 + E[8];
+    const double et0 = E[0] * x2 + E[3] * y2 + E[6];
+    const double et1 = E[1] * x2 + E[4] * y2 + E[7];
+    const double r = x2 * ex0 + y2 * ex1 + ex2;
+    return (float)(r * r / (ex0 * ex0 + ex1 * ex1 + et0 * et0 + et1 * et1));
+}
+
+/* float32 max of the squared point-to-epiline distances in pixels (FMEstimatorCallback) */
+static float err_epiline(const double *F, double x1, double y1, double x2, double y2) {
+    double a = F[0] * x1 + F[1] * y1 + F[2];
+    double b = F[3] * x1 + F[4] * y1 + F[5];
+    double c = F[6] * x1 + F[7] * y1 + F[8];
+    const double s2 = 1.0 / (a * a + b * b);
+    const double d2 = x2 * a + y2 * b + c;
+    a = F[0] * x2 + F[3] * y2 + F[6];
+    b = F[1] * x2 + F[4] * y2 + F[7];
+    c = F[2] * x2 + F[5] * y2 + F[8];
+    const double s1 = 1.0 / (a * a + b * b);
+    const double d1 = x1 * a + y1 * b + c;
+    return (float)fmax(d1 * d1 * s1, d2 * d2 * s2);
 }
 
 typedef struct {
     uint64_t state;
 } cvrng;
 
+/* cv::RNG::next: state' = (uint32)state * 4164903690 + (state >> 32) */
 static uint32_t rng_next(cvrng *r) {
     r->state = (uint64_t)(uint32_t)r->state * 4164903690ULL + (r->state >> 32);
     return (uint32_t)r->state;
 }
 
-static int update_num_iters(double p, double ep, int model_points, int max_iters) {
-    p = fmin(fmax(p, 0.0), 1.0);
-    ep = fmin(fmax(ep, 0.0), 1.0);
-    double num = fmax(1.0 - p, DBL_MIN);
-    double denom = 1.0 - pow(1.0 - ep, model_points);
-    if (denom < DBL_MIN) return 0;
-    num = log(num);
-    denom = log(denom);
-    return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)rint(num / denom);
-}
-
-static int sampson_count(const double *E, const double *p1, const double *p2, int n, float t2, uint8_t *mask) {
-    int g = 0;
-    for (int i = 0; i < n; i++) {
-        double x1 = p1[2 * i], y1 = p1[2 * i + 1], x2 = p2[2 * i], y2 = p2[2 * i + 1];
-        double a0 = E[0] * x1 + E[1] * y1 + E[2], a1 = E[3] * x1 + E[4] * y1 + E[5], a2 = E[6] * x1 + E[7] * y1 + E[8];
-        double b0 = x2 * E[0] + y2 * E[3] + E[6], b1 = x2 * E[1] + y2 * E[4] + E[7];
-        double r = x2 * a0 + y2 * a1 + a2;
-        float err = (float)(r * r / (a0 * a0 + a1 * a1 + b0 * b0 + b1 * b1));
-        int in = err <= t2;
-        if (mask) mask[i] = (uint8_t)in;
-        g += in;
+/* haveCollinearPoints (fundam.cpp) for the last of `count` selected float points */
+static int collinear_last(const float (*pt)[2], int count) {
+    const int i = count - 1;
+    for (int j = 0; j < i; j++) {
+        const double dx1 = (double)(pt[j][0] - pt[i][0]), dy1 = (double)(pt[j][1] - pt[i][1]);
+        for (int k = 0; k < j; k++) {
+            const double dx2 = (double)(pt[k][0] - pt[i][0]), dy2 = (double)(pt[k][1] - pt[i][1]);
+            if (fabs(dx2 * dy1 - dy2 * dx1) <= 1.1920928955078125e-07 * (fabs(dx1) + fabs(dy1) + fabs(dx2) + fabs(dy2)))
+                return 1;
+        }
     }
-    return g;
+    return 0;
 }
 
-/* cv2.findEssentialMat(k1, k2, K, RANSAC, prob, threshold) -> inlier count; mask [n] and
- * the best model (row-major 3x3) when non-null.  geometry.py cv_ransac (K given). */
+/* getSubset: m distinct indices (duplicates redrawn); F (m = 7) redraws the whole subset
+ * while the last point is collinear with two others in either image, <= 10000 attempts */
+static int get_subset(cvrng *rng, int n, int m, const float *k1, const float *k2, int *idx) {
+    for (int iters = 0; iters < 10000; iters++) {
+        float a[7][2], b[7][2];
+        for (int i = 0; i < m; i++) {
+            int v;
+            for (;;) {
+                v = idx[i] = (int)(rng_next(rng) % (uint32_t)n);
+                int j = 0;
+                for (; j < i; j++)
+                    if (v == idx[j]) break;
+                if (j == i) break;
+            }
+            a[i][0] = k1[2 * v];
+            a[i][1] = k1[2 * v + 1];
+            b[i][0] = k2[2 * v];
+            b[i][1] = k2[2 * v + 1];
+        }
+        if (m == 7 && (collinear_last((const float (*)[2])a, 7) || collinear_last((const float (*)[2])b, 7))) continue;
+        return 1;
+    }
+    return 0;
+}
+
+static uint64_t splitmix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+/* ------------------------------------------------------------------ the RANSAC loops */
+
+/* cv2.findEssentialMat(k1, k2, K, RANSAC, conf, thr) -> inlier count; mask [n] and the
+ * best model (row-major 3 x 3) when non-null */
 int orc_essential_ransac(const float *k1, const float *k2, int n, const double *K, double thr, double conf,
                          int max_iters, uint8_t *mask_out, double *E_best) {
     enum { M = 5 };
     if (mask_out) memset(mask_out, 0, (size_t)n);
     if (n < M) return 0;
-    double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
-    double p1[2 * 2048 + 16], p2[2 * 2048 + 16];
-    if (n > 2048 + 8) return -1;
+    const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
+    double(*p)[4] = malloc(sizeof(double[4]) * (size_t)n);
+    uint8_t *cur = malloc((size_t)n);
     for (int i = 0; i < n; i++) {
-        p1[2 * i] = ((double)k1[2 * i] - cx) / fx;
-        p1[2 * i + 1] = ((double)k1[2 * i + 1] - cy) / fy;
-        p2[2 * i] = ((double)k2[2 * i] - cx) / fx;
-        p2[2 * i + 1] = ((double)k2[2 * i + 1] - cy) / fy;
+        p[i][0] = ((double)k1[2 * i] - cx) / fx;
+        p[i][1] = ((double)k1[2 * i + 1] - cy) / fy;
+        p[i][2] = ((double)k2[2 * i] - cx) / fx;
+        p[i][3] = ((double)k2[2 * i + 1] - cy) / fy;
     }
-    double t = thr / ((fx + fy) / 2.0);
-    float t2 = (float)(t * t);
-    double Es[90], q1[10], q2[10];
-    uint8_t cur[2048 + 16];
-    if (n == M) {
-        int ns = orc_five_point(p1, p2, Es);
-        if (!ns) return 0;
-        if (mask_out) memset(mask_out, 1, (size_t)n);
-        if (E_best) memcpy(E_best, Es, sizeof(double) * 9);
-        return n;
+    const double t = thr / ((fx + fy) / 2.0);
+    const float t2 = (float)(t * t);
+    double Es[9 * MAXSOL], q1[10], q2[10];
+    int max_good = 0;
+    if (n == M) { /* the minimal solver's models: the first with the most inliers, mask all ones */
+        for (int i = 0; i < M; i++) {
+            q1[2 * i] = p[i][0]; q1[2 * i + 1] = p[i][1];
+            q2[2 * i] = p[i][2]; q2[2 * i + 1] = p[i][3];
+        }
+        const int ns = orc_five_point(q1, q2, Es);
+        int bs = -1, bg = -1;
+        for (int s = 0; s < ns; s++) {
+            int g = 0;
+            for (int i = 0; i < n; i++) g += err_sampson(Es + 9 * s, p[i][0], p[i][1], p[i][2], p[i][3]) <= t2;
+            if (g > bg) {
+                bg = g;
+                bs = s;
+            }
+        }
+        if (bs >= 0) {
+            max_good = n;
+            if (mask_out) memset(mask_out, 1, (size_t)n);
+            if (E_best) memcpy(E_best, Es + 9 * bs, sizeof(double) * 9);
+        }
+        free(p);
+        free(cur);
+        return max_good;
     }
     cvrng rng = {~0ULL};
-    int niters = max_iters, max_good = 0;
+    int niters = max_iters;
     for (int it = 0; it < niters; it++) {
-        int idx[M];
+        int idx[7];
+        get_subset(&rng, n, M, k1, k2, idx);
         for (int i = 0; i < M; i++) {
-            int v, dup;
-            do {
-                v = (int)(rng_next(&rng) % (uint32_t)n);
-                dup = 0;
-                for (int j = 0; j < i; j++) dup |= idx[j] == v;
-            } while (dup);
-            idx[i] = v;
+            q1[2 * i] = p[idx[i]][0]; q1[2 * i + 1] = p[idx[i]][1];
+            q2[2 * i] = p[idx[i]][2]; q2[2 * i + 1] = p[idx[i]][3];
         }
-        for (int i = 0; i < M; i++) {
-            q1[2 * i] = p1[2 * idx[i]];
-            q1[2 * i + 1] = p1[2 * idx[i] + 1];
-            q2[2 * i] = p2[2 * idx[i]];
-            q2[2 * i + 1] = p2[2 * idx[i] + 1];
-        }
-        int ns = orc_five_point(q1, q2, Es);
+        const int ns = orc_five_point(q1, q2, Es);
         for (int s = 0; s < ns; s++) {
-            int g = sampson_count(Es + 9 * s, p1, p2, n, t2, cur);
+            int g = 0;
+            for (int i = 0; i < n; i++) {
+                cur[i] = err_sampson(Es + 9 * s, p[i][0], p[i][1], p[i][2], p[i][3]) <= t2;
+                g += cur[i];
+            }
             if (g > (max_good > M - 1 ? max_good : M - 1)) {
                 max_good = g;
                 if (mask_out) memcpy(mask_out, cur, (size_t)n);
                 if (E_best) memcpy(E_best, Es + 9 * s, sizeof(double) * 9);
-                niters = update_num_iters(conf, (double)(n - g) / n, M, niters);
+                niters = rs_update_iters(conf, (double)(n - g) / n, M, niters);
             }
         }
     }
+    free(p);
+    free(cur);
     return max_good;
+}
+
+/* cv2.findFundamentalMat(k1, k2, FM_RANSAC, thr, conf) -> inlier count; mask [n] and the
+ * best model (row-major 3 x 3, pixels) when non-null.  n < 7: no model; 7: the solver's
+ * models; 8..14: LMedS over max_iters hypotheses of the stream seeded by `seed` (the
+ * GPU's, not OpenCV's); >= 15: RANSAC. */
+int orc_fundamental_ransac(const float *k1, const float *k2, int n, double thr, double conf, int max_iters,
+                           uint64_t seed, uint8_t *mask_out, double *F_best) {
+    enum { M = 7 };
+    if (mask_out) memset(mask_out, 0, (size_t)n);
+    if (n < M) return 0;
+    /* Hartley normalisation, summed as the GPU's 256-thread block: thread t takes points
+     * t, t + 256, ..., then a pairwise tree over the threads */
+    double red[4][256];
+    memset(red, 0, sizeof(red));
+    for (int t = 0; t < 256; t++)
+        for (int i = t; i < n; i += 256) {
+            red[0][t] += k1[2 * i];
+            red[1][t] += k1[2 * i + 1];
+            red[2][t] += k2[2 * i];
+            red[3][t] += k2[2 * i + 1];
+        }
+    for (int o = 128; o > 0; o >>= 1)
+        for (int t = 0; t < o; t++)
+            for (int j = 0; j < 4; j++) red[j][t] += red[j][t + o];
+    const double inv = 1.0 / n;
+    const double m1x = red[0][0] * inv, m1y = red[1][0] * inv, m2x = red[2][0] * inv, m2y = red[3][0] * inv;
+    memset(red, 0, sizeof(red));
+    for (int t = 0; t < 256; t++)
+        for (int i = t; i < n; i += 256) {
+            red[0][t] += rs_hypot(k1[2 * i] - m1x, k1[2 * i + 1] - m1y);
+            red[1][t] += rs_hypot(k2[2 * i] - m2x, k2[2 * i + 1] - m2y);
+        }
+    for (int o = 128; o > 0; o >>= 1)
+        for (int t = 0; t < o; t++) {
+            red[0][t] += red[0][t + o];
+            red[1][t] += red[1][t + o];
+        }
+    const double md1 = red[0][0] * inv, md2 = red[1][0] * inv;
+    const double sc1 = md1 > 0 ? M_SQRT2 / md1 : 1.0, sc2 = md2 > 0 ? M_SQRT2 / md2 : 1.0;
+    const double T1[3] = {sc1, -sc1 * m1x, -sc1 * m1y}, T2[3] = {sc2, -sc2 * m2x, -sc2 * m2y};
+    double(*q)[4] = malloc(sizeof(double[4]) * (size_t)n);
+    double(*raw)[4] = malloc(sizeof(double[4]) * (size_t)n);
+    uint8_t *cur = malloc((size_t)n);
+    float *e = malloc(sizeof(float) * (size_t)n);
+    for (int i = 0; i < n; i++) {
+        const double x1 = k1[2 * i], y1 = k1[2 * i + 1], x2 = k2[2 * i], y2 = k2[2 * i + 1];
+        q[i][0] = sc1 * x1 + T1[1];
+        q[i][1] = sc1 * y1 + T1[2];
+        q[i][2] = sc2 * x2 + T2[1];
+        q[i][3] = sc2 * y2 + T2[2];
+        raw[i][0] = x1; raw[i][1] = y1; raw[i][2] = x2; raw[i][3] = y2;
+    }
+    const float t2 = (float)(thr * thr);
+    double Fn[3 * 9], Fs[3 * 9], sub[7][4];
+    int max_good = 0;
+    if (n == M || n < 15) {
+        /* n == 7: every model of the one sample; LMedS: max_iters seeded samples.  The best
+         * model: the first with the most inliers (7) / the smallest median error (LMedS) */
+        const int lmeds = n > M;
+        float best = -INFINITY;
+        double Fb[9];
+        int have = 0;
+        for (int h = 0; h < (lmeds ? max_iters : 1); h++) {
+            int idx[7];
+            uint64_t st = splitmix(seed ^ (uint64_t)h * 0x632BE59BD9B4E019ull);
+            for (int i = 0; i < M; i++) {
+                if (!lmeds) {
+                    idx[i] = i;
+                    continue;
+                }
+                int v, dup;
+                do {
+                    st = splitmix(st);
+                    v = (int)((st >> 11) % (uint64_t)n);
+                    dup = 0;
+                    for (int j = 0; j < i; j++) dup |= idx[j] == v;
+                } while (dup);
+                idx[i] = v;
+            }
+            for (int i = 0; i < M; i++) memcpy(sub[i], q[idx[i]], sizeof(sub[i]));
+            const int ns = seven_point((const double (*)[4])sub, Fn);
+            for (int s = 0; s < ns; s++) {
+                denorm_F(Fn + 9 * s, T1, T2, Fs + 9 * s);
+                float sc;
+                if (lmeds) {
+                    for (int i = 0; i < n; i++) { /* insertion sort of the errors */
+                        const float v = err_epiline(Fs + 9 * s, raw[i][0], raw[i][1], raw[i][2], raw[i][3]);
+                        int j = i - 1;
+                        while (j >= 0 && e[j] > v) {
+                            e[j + 1] = e[j];
+                            j--;
+                        }
+                        e[j + 1] = v;
+                    }
+                    sc = -e[n / 2];
+                } else {
+                    int g = 0;
+                    for (int i = 0; i < n; i++) g += err_epiline(Fs + 9 * s, raw[i][0], raw[i][1], raw[i][2], raw[i][3]) <= t2;
+                    sc = (float)g;
+                }
+                if (sc > best) { /* strictly better: ties keep the earlier (hypothesis, solution) */
+                    best = sc;
+                    have = 1;
+                    memcpy(Fb, Fs + 9 * s, sizeof(Fb));
+                }
+            }
+        }
+        if (!have) {
+            free(q); free(raw); free(cur); free(e);
+            return 0;
+        }
+        if (F_best) memcpy(F_best, Fb, sizeof(Fb));
+        float tt = t2;
+        if (lmeds) {
+            const double med = -(double)best;
+            double sigma = 2.5 * 1.4826 * (1.0 + 5.0 / (n - 7)) * sqrt(med);
+            sigma = fmax(sigma, 0.001);
+            tt = (float)(sigma * sigma);
+        }
+        for (int i = 0; i < n; i++) {
+            const int in = lmeds ? err_epiline(Fb, raw[i][0], raw[i][1], raw[i][2], raw[i][3]) <= tt : 1;
+            if (mask_out) mask_out[i] = (uint8_t)in;
+            max_good += in;
+        }
+        free(q); free(raw); free(cur); free(e);
+        return max_good;
+    }
+    cvrng rng = {~0ULL};
+    int niters = max_iters;
+    for (int it = 0; it < niters; it++) {
+        int idx[7];
+        if (!get_subset(&rng, n, M, k1, k2, idx)) break;
+        for (int i = 0; i < M; i++) memcpy(sub[i], q[idx[i]], sizeof(sub[i]));
+        const int ns = seven_point((const double (*)[4])sub, Fn);
+        for (int s = 0; s < ns; s++) {
+            denorm_F(Fn + 9 * s, T1, T2, Fs + 9 * s);
+            int g = 0;
+            for (int i = 0; i < n; i++) {
+                cur[i] = err_epiline(Fs + 9 * s, raw[i][0], raw[i][1], raw[i][2], raw[i][3]) <= t2;
+                g += cur[i];
+            }
+            if (g > (max_good > M - 1 ? max_good : M - 1)) {
+                max_good = g;
+                if (mask_out) memcpy(mask_out, cur, (size_t)n);
+                if (F_best) memcpy(F_best, Fs + 9 * s, sizeof(double) * 9);
+                niters = rs_update_iters(conf, (double)(n - g) / n, M, niters);
+            }
+        }
+    }
+    free(q); free(raw); free(cur); free(e);
+    return max_good;
+}
+
+/* the shared helpers, exported for tests/test_oracle_geometry.py */
+double orc_rs_log(double x) { return rs_log(x); }
+double orc_rs_root(double x, int n) { return rs_root(x, n); }
+int orc_rs_update_iters(double p, double ep, int model_points, int max_iters) {
+    return rs_update_iters(p, ep, model_points, max_iters);
 }

@@ -88,3 +88,60 @@ def test_c_essential_ransac_degenerate_sizes():
     assert _lib.essential_ransac(k1[:4], k2[:4], G.ISEC_K)[2] == 0
     _, mask, g = _lib.essential_ransac(k1, k2, G.ISEC_K)
     assert g == 5 and mask.all()
+
+
+# --- rs_math.h (shared by the GPU RANSAC and the C twin) against the library maths -----
+def test_rs_math_helpers_track_libm():
+    """rs_log / rs_root replace libm inside both RANSACs (so the two agree bit for bit);
+    they must still be the functions they stand for: log within 2 ulp, the Aberth start
+    radius within 4e-15, and RANSACUpdateNumIters identical to the numpy restatement
+    (np.log, **) on a sweep of inlier ratios and budgets."""
+    from oracle import _lib
+    L = _lib.lib()
+    rng = np.random.default_rng(3)
+    xs = np.concatenate([np.exp(rng.uniform(-700, 700, 4000)), rng.uniform(0.5, 2.0, 4000), [1.0, 0.001, 1e-300]])
+    for x in xs:
+        got, want = L.orc_rs_log(float(x)), float(np.log(x))
+        assert abs(got - want) <= 2 * np.spacing(abs(want)) + 1e-300, (x, got, want)
+    for x in np.exp(rng.uniform(-60, 60, 2000)):
+        for n in range(1, 11):
+            got, want = L.orc_rs_root(float(x), n), float(x) ** (1.0 / n)
+            assert abs(got - want) <= 4e-15 * want, (x, n, got, want)
+    assert L.orc_rs_root(0.0, 4) == 0.0
+    for m in (5, 7):
+        for n in (20, 100, 1000, 2048):
+            for g in range(m, n + 1, max(1, n // 300)):
+                ep = (n - g) / n
+                for budget in (1000, 400, 37):
+                    assert L.orc_rs_update_iters(0.999, ep, m, budget) == G.update_num_iters(0.999, ep, m, budget), \
+                        (m, n, g, budget)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_c_fundamental_ransac_equals_numpy_restatement(seed):
+    """>= 15 matches without K: the same sample stream (with the collinearity redraw) and
+    acceptance rule.  The twin solves on Hartley-normalised points as the GPU does, numpy
+    on pixels as OpenCV's run7Point; the inlier counts agree (a point within rounding of
+    the threshold may flip: <= 0.5 %)."""
+    from oracle import _lib
+    rng = np.random.default_rng(300 + seed)
+    n_in = int(rng.integers(40, 300))
+    k1, k2, _, _, _ = G.synthetic_pair(rng, n_in, int(rng.integers(0, n_in // 3 + 1)), noise_px=0.5)
+    _, mask_py, g_py = G.cv_ransac(k1, k2, None, 3.0)
+    F, mask_c, g_c = _lib.fundamental_ransac(k1, k2, 3.0)
+    assert abs(g_c - g_py) <= max(1, 0.005 * len(k1)), (g_c, g_py)
+    assert np.array_equal(mask_c, G.inlier_mask(F, k1, k2, None, 3.0))
+
+
+def test_c_fundamental_small_sizes():
+    from oracle import _lib
+    rng = np.random.default_rng(8)
+    k1, k2, _, _, _ = G.synthetic_pair(rng, 12, 0, noise_px=0.2)
+    assert _lib.fundamental_ransac(k1[:6], k2[:6])[2] == 0
+    F, mask, g = _lib.fundamental_ransac(k1[:7], k2[:7])
+    assert g == 7 and mask.all() and F is not None
+    F, mask, g = _lib.fundamental_ransac(k1, k2)  # LMedS: mask = the sigma test of the model
+    e = G.epiline_error(F, k1, k2)
+    med = np.sort(e)[len(e) // 2]
+    sigma = max(2.5 * 1.4826 * (1 + 5.0 / (len(e) - 7)) * np.sqrt(np.float64(med)), 0.001)
+    assert np.array_equal(mask, e <= np.float32(sigma * sigma)) and g == int(mask.sum())

@@ -145,17 +145,62 @@ def test_verifier_decisions_batched_vs_single(dev):
 @pytest.mark.parametrize("use_k", [True, False])
 def test_ransac_follows_opencv_loop(dev, use_k):
     """The GPU runs OpenCV's RANSACPointSetRegistrator::run: cv::RNG((uint64)-1) sample
-    stream, strict-improvement updates, RANSACUpdateNumIters stop.  The numpy
-    restatement of that loop (oracle.geometry.cv_ransac) must reach the same inlier count
-    -- up to points within rounding of the threshold under the two solvers' slightly
-    different minimal-sample models (<= 0.3 %)."""
+    stream, strict-improvement updates, RANSACUpdateNumIters stop.  Its C twin
+    (oracle/csrc/ransac_cv.c: the same loop, the same solver formulation evaluated in the
+    same operand order, no FP contraction on either side, shared rs_math.h) must give the
+    same inlier count, mask and model bit for bit.  The independent numpy restatement
+    (oracle.geometry.cv_ransac: another 5-point formulation, SVD null spaces, np.roots; F on
+    pixels) reaches the same count up to points within rounding of the threshold."""
+    from oracle import _lib
     specs = [(300, 100), (150, 150), (800, 200), (60, 40), (1000, 30), (30, 300)]
     pairs = _pairs(31 if use_k else 32, specs)
     res = geometry.epipolar_ransac([p[0] for p in pairs], [p[1] for p in pairs], K if use_k else None, 3.0,
                                    device=str(dev))
     for (k1, k2, *_), r in zip(pairs, res):
-        _, mask, n_in = G.cv_ransac(k1, k2, K if use_k else None, 3.0)
-        assert abs(r.inliers - n_in) <= max(1, 0.003 * len(k1)), (len(k1), r.inliers, n_in)
+        M, mask, n_in = _lib.essential_ransac(k1, k2, K, 3.0) if use_k else _lib.fundamental_ransac(k1, k2, 3.0)
+        assert r.inliers == n_in and np.array_equal(r.mask, mask), (len(k1), r.inliers, n_in)
+        assert np.array_equal(r.model, M)
+        _, _, n_np = G.cv_ransac(k1, k2, K if use_k else None, 3.0)
+        assert abs(r.inliers - n_np) <= max(1, 0.003 * len(k1)), (len(k1), r.inliers, n_np)
+
+
+def _twin_pairs(seed, n_pairs):
+    """Seeded pairs across the regimes RANSAC meets in the gate: every size class (below 5,
+    5, 6, 7, 8..14, 15.., up to 2048 matches), inlier ratios from 0.1 to 1 (the near-
+    identical views of a revisit: ratio >= 0.99, sub-pixel noise, where the last bits of E
+    decide boundary points), tiny baselines and rotations (near-degenerate E)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    sizes = [3, 5, 6, 7, 9, 12, 14, 15, 20, 50, 200, 700, 1500, 2048]
+    for i in range(n_pairs):
+        n = int(sizes[i % len(sizes)]) if i < len(sizes) else int(rng.integers(15, 2049))
+        ratio = float(rng.choice([0.1, 0.3, 0.5, 0.8, 0.95, 0.99, 1.0]))
+        n_in = max(min(n, int(round(n * ratio))), min(n, 5))
+        noise = float(rng.choice([0.05, 0.3, 1.0, 2.0]))
+        rot = float(rng.choice([0.5, 3.0, 10.0]))
+        base = float(rng.choice([0.02, 0.2, 0.6]))
+        k1, k2, *_ = G.synthetic_pair(rng, n_in, n - n_in, noise, rot_deg=rot, baseline=base)
+        out.append((k1, k2))
+    return out
+
+
+@pytest.mark.parametrize("use_k", [True, False])
+def test_ransac_bit_exact_to_c_twin_many_pairs(dev, use_k):
+    """on identical match lists the GPU RANSAC's inlier count, mask
+    and model equal the C twin's, pair by pair -- 240 seeded pairs over every size class
+    and regime in one batched launch sequence (the bench's way of calling it)."""
+    from oracle import _lib
+    pairs = _twin_pairs(41 if use_k else 42, 240)
+    res = geometry.epipolar_ransac([p[0] for p in pairs], [p[1] for p in pairs], K if use_k else None, 3.0,
+                                   device=str(dev))
+    bad = []
+    for i, ((k1, k2), r) in enumerate(zip(pairs, res)):
+        M, mask, n_in = _lib.essential_ransac(k1, k2, K, 3.0) if use_k else _lib.fundamental_ransac(k1, k2, 3.0)
+        same = r.inliers == n_in and np.array_equal(r.mask, mask) and (
+            (M is None and r.model is None) or (M is not None and r.model is not None and np.array_equal(r.model, M)))
+        if not same:
+            bad.append((i, len(k1), r.inliers, n_in))
+    assert not bad, bad
 
 
 def test_mixed_small_pairs_over_poisoned_workspace(dev):

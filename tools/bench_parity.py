@@ -163,11 +163,49 @@ def probe(a):
 
 
 def _ransac_job(job):
-    """(key, k1, k2) -> (key, inliers) with the C restatement of findEssentialMat (pool worker)."""
+    """(key, k1, k2) -> (key, inliers, mask) with the C twin of findEssentialMat (pool worker)."""
     from oracle import _lib
     from oracle import geometry as ogeo
     key, k1, k2 = job
-    return key, (_lib.essential_ransac(k1, k2, ogeo.ISEC_K, 3.0)[2] if len(k1) >= 5 else 0)
+    _, mask, g = _lib.essential_ransac(k1, k2, ogeo.ISEC_K, 3.0)
+    return key, g, np.packbits(mask)
+
+
+def _capture_product_ransac(store):
+    """Wrap mlgate.geometry.epipolar_ransac_device so every RANSAC call of the product gate
+    also leaves its inputs and outputs (host copies) in `store`: the product's own match
+    lists, for the GPU-vs-C-twin check on identical lists."""
+    from mlgate import geometry as mgeo
+    orig = mgeo.epipolar_ransac_device
+
+    def hook(k1, k2, offs, K=None, k_stride=0, threshold=3.0, **kw):
+        out = orig(k1, k2, offs, K, k_stride, threshold, **kw)
+        o = offs.cpu().numpy()  # on the current (RANSAC side) stream: ordered after the launch
+        store.append((k1[:int(o[-1])].cpu().numpy(), k2[:int(o[-1])].cpu().numpy(), o, out[2].cpu().numpy(),
+                      out[1][:int(o[-1])].cpu().numpy()))
+        return out
+    mgeo.epipolar_ransac_device = hook
+    return orig
+
+
+def _twin_report(pool, lists, gpu_inl, gpu_masks, label):
+    """GPU RANSAC vs the C twin on the same lists: counts and masks, pair by pair."""
+    jobs = [pool.apply_async(_ransac_job, ((i, k1, k2),)) for i, (k1, k2) in enumerate(lists)]
+    eq_n = eq_m = 0
+    bad = []
+    for job in jobs:
+        i, g, pm = job.get()
+        same_n = int(gpu_inl[i]) == int(g)
+        same_m = np.array_equal(np.packbits(gpu_masks[i].astype(bool)), pm)
+        eq_n += same_n
+        eq_m += same_m
+        if not (same_n and same_m) and len(bad) < 20:
+            bad.append({"pair": i, "matches": len(lists[i][0]), "gpu": int(gpu_inl[i]), "twin": int(g)})
+    n = max(len(lists), 1)
+    rep = {"check": label, "pairs": len(lists), "inliers_equal_c_twin": eq_n / n, "masks_equal_c_twin": eq_m / n,
+           "differ": bad}
+    log(**rep)
+    return rep
 
 
 def chain(a):
@@ -188,8 +226,22 @@ def chain(a):
     sd = synthetic_state_dict(0)
     gate = DeviceGate(frames, seq.t, labels, 1, 0, dev, k=k, verify=True, K=bench.ISEC_K, vit_batch=246, sp_batch=64,
                       lg_chunk=a.lg_chunk, vit_state_dict=sd, record=True)
+    captured = []
+    orig_ransac = _capture_product_ransac(captured)
     counts_gpu = gate.step()
     torch.cuda.synchronize()
+    from mlgate import geometry as mgeo
+    mgeo.epipolar_ransac_device = orig_ransac
+    # (1) the product's own match lists: its GPU RANSAC vs the C twin, every ordered pair
+    p_lists, p_inl, p_masks = [], [], []
+    for k1c, k2c, o, inl_c, mask_c in captured:
+        for p_ in range(len(o) - 1):
+            p_lists.append((k1c[o[p_]:o[p_ + 1]], k2c[o[p_]:o[p_ + 1]]))
+            p_inl.append(inl_c[p_])
+            p_masks.append(mask_c[o[p_]:o[p_ + 1]])
+    del captured
+    twin_product = _twin_report(pool, p_lists, p_inl, p_masks, "product lists: GPU RANSAC vs C twin")
+    del p_lists, p_inl, p_masks
     gr = gate.last_pair_results
     g_idx, g_sim, g_valid, g_count = gate.last_retrieval
     del gate
@@ -228,18 +280,39 @@ def chain(a):
     lg = olg.Oracle(lightglue_state_dict(0), emulate_bf16=False, device=dev)
     nm = np.zeros(len(union), np.int32)
     stop = np.zeros(len(union), np.int8)
-    pending = []
+    pending, f_lists = [], []
     for i, (p, q) in enumerate(union):
         r = lg.match(feats[p][0], feats[p][1], feats[q][0], feats[q][1])
         mm = r["matches"].cpu().numpy()
         nm[i], stop[i] = len(mm), r["stop"]
-        pending.append(pool.apply_async(_ransac_job, ((i, feats[p][2][mm[:, 0]], feats[q][2][mm[:, 1]]),)))
+        f_lists.append((feats[p][2][mm[:, 0]], feats[q][2][mm[:, 1]]))
+        pending.append(pool.apply_async(_ransac_job, ((i,) + f_lists[-1],)))
         if i % 2000 == 0:
             log(phase="fp32_lightglue", done=i, s=round(time.time() - t0, 1))
     inl = np.zeros(len(union), np.int32)
+    f_masks = [None] * len(union)
     for job in pending:
-        i, g = job.get()
+        i, g, pm = job.get()
         inl[i] = g
+        f_masks[i] = pm
+    # (2) the fp32 chain's lists through the product's GPU RANSAC (batched as the gate
+    # calls it) against the C twin's counts / masks just computed
+    from mlgate import geometry as mgeo
+    g_inl = np.zeros(len(union), np.int32)
+    g_eq_m = 0
+    for c0 in range(0, len(union), 4096):
+        rs = mgeo.epipolar_ransac([x[0] for x in f_lists[c0:c0 + 4096]], [x[1] for x in f_lists[c0:c0 + 4096]],
+                                  bench.ISEC_K, 3.0, device=str(dev))
+        for j, r in enumerate(rs):
+            g_inl[c0 + j] = r.inliers
+            g_eq_m += np.array_equal(np.packbits(r.mask), f_masks[c0 + j])
+    twin_fp32 = {"check": "fp32 chain lists: GPU RANSAC vs C twin", "pairs": len(union),
+                 "inliers_equal_c_twin": float((g_inl == inl).mean()) if len(union) else 1.0,
+                 "masks_equal_c_twin": g_eq_m / max(len(union), 1),
+                 "differ": [{"pair": int(i), "matches": int(nm[i]), "gpu": int(g_inl[i]), "twin": int(inl[i])}
+                            for i in np.flatnonzero(g_inl != inl)[:20]]}
+    log(**twin_fp32)
+    del f_lists, f_masks
     pool.close()
     ratio = inl / np.maximum(nm, 1)
     fvalid = (nm >= 5) & (inl >= 20) & (ratio >= 0.25)
@@ -264,7 +337,8 @@ def chain(a):
            "gpu_valid": int(gv[in_gpu].sum()), "decision_flips_on_common": len(flips),
            "flips": [{"a": union[i][0], "b": union[i][1], "gpu": [int(gm[i]), int(gin[i]), bool(gv[i])],
                       "fp32": [int(nm[i]), int(inl[i]), bool(fvalid[i])]} for i in flips[:50]],
-           "counts_fp32": counts_fp, "counts_gpu": counts_gpu, "s": round(time.time() - t0, 1)}
+           "counts_fp32": counts_fp, "counts_gpu": counts_gpu, "twin_product": twin_product, "twin_fp32": twin_fp32,
+           "s": round(time.time() - t0, 1)}
     log(**rep)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     np.savez_compressed(a.out, keyframes=N, places=a.places, k=k, labels=labels, count32=np.bincount(q32, minlength=N)
