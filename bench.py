@@ -430,7 +430,19 @@ def main():
     dt_t = torch.tensor([dt], dtype=torch.float64, device=dev)
     keys = sorted(counts)
     cv = torch.tensor([counts[k_] for k_ in keys], dtype=torch.int64, device=dev)
+    per_rank = None
     if world > 1:
+        # per-rank view (the slowest rank sets the step): this rank's wall time, its share
+        # of the verification pairs and its profiled warmup step's stage times
+        mine = torch.tensor([dt / max(args.steps, 1) * 1e3, counts.get("pairs_verified", 0) / max(args.steps, 1),
+                             counts.get("pairs_matched_lightglue", 0) / max(args.steps, 1)]
+                            + [tot[s_] for s_ in SLOTS], dtype=torch.float64, device=dev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [{"rank": r_, "ms_per_step": round(float(v[0]), 1), "pairs_verified": int(v[1]),
+                     "pairs_matched_lightglue": int(v[2]),
+                     "stage_ms_warmup_step": {SLOTS[s_]: round(float(v[3 + s_]), 1) for s_ in SLOTS}}
+                    for r_, v in enumerate(x.cpu().numpy() for x in allr)]
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(cv)
     dt = dt_t.item()
@@ -494,13 +506,17 @@ def main():
                              for s in SLOTS if s not in HBM_SLOTS},
                          "vit_mfma_products_per_flop": 3 if args.vit == "split" else 1},
         }
+        if per_rank:
+            line["per_rank"] = per_rank
         if lft:
             line["loftr"] = lft
         if c0:
             line["configs0"] = c0
         if ing:
             line["ingest"] = ing
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:
+            # rank 0 only, after the timed region (at world > 1 the other ranks wait at the
+            # final barrier, so their processes leave the host cores to it)
             line["cpu_baseline"] = cpu_baseline(pairs_per_kf=(counts["pairs_verified"] / N) if gate.verify else 0.0)
         print(json.dumps(line), flush=True)
     if world > 1:
