@@ -127,7 +127,13 @@ def test_bench_step_decisions_match_fp32_chain(chain, gate_run):
     dinl = np.asarray(dinl)
     assert np.median(dinl) <= DINL_MEDIAN and np.percentile(dinl, 99) <= DINL_P99, \
         (float(np.median(dinl)), float(np.percentile(dinl, 99)))
-    # the fp32 chain's four-term count, to within the flips
-    want = int(np.sum(~chain["v32"])) + int(np.sum(chain["in_fp32"] & ~v_fp))
-    got = gate_run["counts"]["retrieval_floor_rejected"] + gate_run["counts"]["verifier_invalid"]
-    assert abs(got - want) <= 1 + len(flips), (got, want, len(flips))
+    # the fp32 chain's four-term count, term by term: the retrieval term within
+    # its own bar; the verifier term within the flips plus the pairs only one chain verified
+    # (near-tie retrieval rows: each may add one invalid pair to its side)
+    want_vi = int(np.sum(chain["in_fp32"] & ~v_fp))
+    fp32_only = int(np.sum(chain["in_fp32"] & ~chain["in_gpu"]))
+    got_vi = gate_run["counts"]["verifier_invalid"]
+    assert abs(got_vi - want_vi) <= len(flips) + missing + fp32_only, (got_vi, want_vi, len(flips), missing, fp32_only)
+    want = int(np.sum(~chain["v32"])) + want_vi
+    got = gate_run["counts"]["retrieval_floor_rejected"] + got_vi
+    assert abs(got - want) <= MAX_FLOOR_REJ + len(flips) + missing + fp32_only, (got, want)
