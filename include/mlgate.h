@@ -34,8 +34,18 @@ extern "C" {
 #define MLG_VIT_EMBED 768
 #define MLG_VIT_PATCH_K 768 /* 3*14*14 = 588 patch inputs, zero-padded to 12 K-tiles of 64 */
 
-/* 2: mlg_vit_weights.packing and mlg_loftr_weights.coarse_tails appended (round 5) */
-int mlg_abi_version(void);
+/* Struct arguments.  Every struct an entry point takes (mlg_vit_weights, mlg_salad_weights,
+ * mlg_rn_weights, mlg_sp_weights, mlg_lg_weights, mlg_sg_weights, mlg_loftr_weights,
+ * mlg_orb_params) begins with a head: struct_size = sizeof(the struct) and abi_version =
+ * MLG_ABI_VERSION, both set by initialising it with MLG_STRUCT_INIT(type).  A struct whose
+ * head disagrees -- built against another version of this header (a shorter or longer
+ * struct), truncated, or not initialised -- is rejected with MLG_EINVAL (size queries
+ * taking one return 0) before any field past the head is read.
+ * Versions: 2 (round 5) appended mlg_vit_weights.packing and mlg_loftr_weights.coarse_tails;
+ * 3 (round 6) added the heads. */
+#define MLG_ABI_VERSION 3
+#define MLG_STRUCT_INIT(T) {(uint32_t)sizeof(T), (uint32_t)MLG_ABI_VERSION}
+int mlg_abi_version(void); /* MLG_ABI_VERSION of the library */
 const char* mlg_strerror(int status);
 
 /* ------------------------------------------------------------------ ViT-B/14 --
@@ -58,6 +68,7 @@ typedef struct mlg_vit_block {
 } mlg_vit_block;
 
 typedef struct mlg_vit_weights {
+    uint32_t struct_size, abi_version; /* MLG_STRUCT_INIT(mlg_vit_weights) */
     const uint16_t* patch_w; /* [768, MLG_VIT_PATCH_K], k = c*196 + ky*14 + kx */
     const float* patch_b;
     const float* cls;        /* [768] */
@@ -113,6 +124,7 @@ int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, 
  *   dust_bin             the learned dust-bin score
  */
 typedef struct mlg_salad_weights {
+    uint32_t struct_size, abi_version; /* MLG_STRUCT_INIT(mlg_salad_weights) */
     const uint16_t* w1;
     const float* b1;
     const uint16_t* w2;
@@ -295,6 +307,7 @@ typedef struct mlg_rn_block {
     const uint16_t* wd; const float* bd;  /* downsample 1x1: bf16 [4 width][Cin], or NULL */
 } mlg_rn_block;
 typedef struct mlg_rn_weights {
+    uint32_t struct_size, abi_version; /* MLG_STRUCT_INIT(mlg_rn_weights) */
     const float* stem_w;  /* f32 [64][7][7][3] */
     const float* stem_b;  /* f32 [64] */
     mlg_rn_block blocks[16];
@@ -320,6 +333,7 @@ int mlg_op_pillow_resize_224(const uint8_t* frames, int B, int H, int W, int C, 
  * the same in bf16, counts int32 [B].  Keypoint order: raster order when at most
  * max_kp pass the threshold, else score-descending (raster index ascending on ties). */
 typedef struct mlg_sp_weights {
+    uint32_t struct_size, abi_version; /* MLG_STRUCT_INIT(mlg_sp_weights) */
     const float* conv1a_w;  /* f32 [64][3][3] */
     const float* conv1a_b;  /* f32 [64] */
     const uint16_t* w[11];  /* bf16: conv1b conv2a conv2b conv3a conv3b conv4a conv4b convPa
@@ -355,6 +369,7 @@ typedef struct mlg_lg_block {
     const uint16_t* Wf2;  const float* bf2;   /* ffn.3 [256][512]             } [k/16][n][k%16] */
 } mlg_lg_block;
 typedef struct mlg_lg_weights {
+    uint32_t struct_size, abi_version;                     /* MLG_STRUCT_INIT(mlg_lg_weights) */
     const float* Wr;                                       /* posenc.Wr [32][2] f32 */
     mlg_lg_block self[9], cross[9];                        /* bf16 weights, f32 biases */
     const uint16_t* Wfinal[9]; const float* bfinal[9];     /* log_assignment.i.final_proj */
@@ -425,6 +440,7 @@ int mlg_dbg_att_trace(void* host, size_t bytes);
  * Wfinal bf16 [out][in] (not k-step-major).  Outputs as mlg_lightglue (matches
  * ascending in the image0 index).  Synchronises `stream`. */
 typedef struct mlg_sg_weights {
+    uint32_t struct_size, abi_version; /* MLG_STRUCT_INIT(mlg_sg_weights) */
     const float* kenc_w[3]; const float* kenc_b[3];
     const uint16_t* kenc_w4; const float* kenc_b4;
     const uint16_t* kenc_w5; const float* kenc_b5;
@@ -480,7 +496,8 @@ typedef struct {
     const uint16_t* w2;     /* mlp.2 [d][2d] */
     const float *ln1_g, *ln1_b, *ln2_g, *ln2_b;
 } mlg_loftr_layer;
-typedef struct {
+typedef struct mlg_loftr_weights {
+    uint32_t struct_size, abi_version; /* MLG_STRUCT_INIT(mlg_loftr_weights) */
     const float* stem_w; /* conv1 7x7 (BN folded) f32 [49][128] */
     const float* stem_b; /* [128] */
     const uint16_t* conv_w[MLG_LOFTR_NCONV];
@@ -558,6 +575,7 @@ int mlg_prof_read_work(int slot, double* flops);
  */
 #define MLG_ORB_LEVELS 8
 typedef struct mlg_orb_params {
+    uint32_t struct_size, abi_version; /* MLG_STRUCT_INIT(mlg_orb_params) */
     int level_w[MLG_ORB_LEVELS], level_h[MLG_ORB_LEVELS];
     int level_features[MLG_ORB_LEVELS]; /* nfeaturesPerLevel */
     float level_scale[MLG_ORB_LEVELS];

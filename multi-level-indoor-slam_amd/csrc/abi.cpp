@@ -8,6 +8,8 @@
 #include <vector>
 
 #include "../../include/mlgate.h"
+#include <cstddef>
+
 #include "kernels.h"
 
 namespace {
@@ -115,7 +117,7 @@ MlgProfScope::~MlgProfScope() {
 
 extern "C" {
 
-int mlg_abi_version(void) { return 2; }
+int mlg_abi_version(void) { return MLG_ABI_VERSION; }
 
 const char* mlg_strerror(int status) {
     switch (status) {
@@ -212,7 +214,8 @@ extern "C" {
 int mlg_vit_forward(const mlg_vit_weights* w, const uint8_t* frames, int batch, int H, int W, int C,
                     long frame_stride, int image_size, int flags, void* workspace, size_t workspace_bytes,
                     float* desc_out, float* local_out, void* stream) {
-    if (!w || !frames || !workspace || !desc_out || batch <= 0 || image_size % PATCH) return MLG_EINVAL;
+    if (!mlg_head_ok(w, MLG_ABI_VERSION) || !frames || !workspace || !desc_out || batch <= 0 || image_size % PATCH)
+        return MLG_EINVAL;
     // the split forward reads 2x-wide weight rows: plain weights with the flag would be read out of bounds
     if (w->packing != ((flags & MLG_VIT_SPLIT) ? MLG_VIT_SPLIT : 0)) return MLG_EINVAL;
     const VitGeom g(batch, image_size);
@@ -235,7 +238,9 @@ size_t mlg_salad_workspace_bytes(int batch, int image_size) {
 int mlg_salad_forward(const mlg_vit_weights* w, const mlg_salad_weights* sw, const uint8_t* frames, int batch,
                       int H, int W, int C, long frame_stride, int image_size, void* workspace,
                       size_t workspace_bytes, float* desc_out, void* stream) {
-    if (!w || !sw || !frames || !workspace || !desc_out || batch <= 0 || image_size % PATCH) return MLG_EINVAL;
+    if (!mlg_head_ok(w, MLG_ABI_VERSION) || !mlg_head_ok(sw, MLG_ABI_VERSION) || !frames || !workspace || !desc_out ||
+        batch <= 0 || image_size % PATCH)
+        return MLG_EINVAL;
     if (w->packing != 0) return MLG_EINVAL;  // SALAD's trunk runs the plain bf16 forward
     const VitGeom g(batch, image_size);
     VitWorkspace ws;
@@ -355,14 +360,18 @@ int mlg_proximity_emit(const double* pos, const int64_t* floor, int N, int row0,
                                   pairs, dist, valid, (hipStream_t)stream);
 }
 
-static_assert(sizeof(mlg_rn_weights) == sizeof(mlg_rn_weights_i), "ResNet weight tables must match");
+// the internal tables are the public structs past their 8-byte head
+static_assert(offsetof(mlg_rn_weights, stem_w) == 8 &&
+                  sizeof(mlg_rn_weights) - offsetof(mlg_rn_weights, stem_w) == sizeof(mlg_rn_weights_i),
+              "ResNet weight tables must match");
 
 size_t mlg_resnet50_workspace_bytes(int B, int H, int W) { return mlg_resnet50_ws_bytes(B, H, W); }
 
 int mlg_resnet50_forward(const mlg_rn_weights* w, const uint8_t* frames, int B, int H, int W, int C,
                          long frame_stride, int descriptor_dim, void* workspace, size_t workspace_bytes,
                          float* desc, void* stream) {
-    if (!w || !frames || !workspace || !desc || !w->stem_w || !w->stem_b) return MLG_EINVAL;
+    if (!mlg_head_ok(w, MLG_ABI_VERSION) || !frames || !workspace || !desc || !w->stem_w || !w->stem_b)
+        return MLG_EINVAL;
     for (int i = 0; i < 16; ++i) {
         const mlg_rn_block& b = w->blocks[i];
         if (!b.w1 || !b.b1 || !b.w2 || !b.b2 || !b.w3 || !b.b3) return MLG_EINVAL;
@@ -370,7 +379,7 @@ int mlg_resnet50_forward(const mlg_rn_weights* w, const uint8_t* frames, int B, 
         if (first != (b.wd != nullptr) || (b.wd && !b.bd)) return MLG_EINVAL;
     }
     if (frame_stride < (long)H * W * C) return MLG_EINVAL;
-    return mlg_resnet50_run(*reinterpret_cast<const mlg_rn_weights_i*>(w), frames, B, H, W, C, frame_stride,
+    return mlg_resnet50_run(*reinterpret_cast<const mlg_rn_weights_i*>(&w->stem_w), frames, B, H, W, C, frame_stride,
                             descriptor_dim, workspace, workspace_bytes, desc, nullptr, (hipStream_t)stream);
 }
 
@@ -388,7 +397,8 @@ int mlg_superpoint(const mlg_sp_weights* w, const uint8_t* frames, int B, int H,
                    float detection_threshold, int max_keypoints, int nms_radius, int remove_borders, void* workspace,
                    size_t workspace_bytes, float* keypoints, float* scores, float* descriptors,
                    uint16_t* descriptors_bf16, int32_t* counts, void* stream) {
-    if (!w || !frames || !workspace || !keypoints || !scores || !descriptors || !counts) return MLG_EINVAL;
+    if (!mlg_head_ok(w, MLG_ABI_VERSION) || !frames || !workspace || !keypoints || !scores || !descriptors || !counts)
+        return MLG_EINVAL;
     if (!w->conv1a_w || !w->conv1a_b) return MLG_EINVAL;
     mlg_sp_weights_i wi;
     wi.conv1a_w = w->conv1a_w;
@@ -406,7 +416,9 @@ int mlg_superpoint(const mlg_sp_weights* w, const uint8_t* frames, int B, int H,
                               descriptors_bf16, counts, (hipStream_t)stream);
 }
 
-static_assert(sizeof(mlg_lg_weights) == sizeof(mlg_lg_weights_i), "LightGlue weight tables must match");
+static_assert(offsetof(mlg_lg_weights, Wr) == 8 &&
+                  sizeof(mlg_lg_weights) - offsetof(mlg_lg_weights, Wr) == sizeof(mlg_lg_weights_i),
+              "LightGlue weight tables must match");
 static_assert(sizeof(mlg_lg_block) == sizeof(mlg_lg_block_i), "LightGlue block tables must match");
 
 size_t mlg_lightglue_workspace_bytes(int P, int kmax) { return mlg_lightglue_ws_bytes(P, kmax); }
@@ -416,18 +428,20 @@ int mlg_lightglue(const mlg_lg_weights* w, const float* keypoints, const float* 
                   float width_confidence, float filter_threshold, int pruning_min_kpts, void* workspace,
                   size_t workspace_bytes, int32_t* matches, float* scores, int32_t* num_matches, int32_t* stop_layer,
                   void* stream) {
-    if (!w || !keypoints || !descriptors || !counts || !pair_a || !pair_b || !workspace || !matches || !scores ||
-        !num_matches || F <= 0 || P <= 0)
+    if (!mlg_head_ok(w, MLG_ABI_VERSION) || !keypoints || !descriptors || !counts || !pair_a || !pair_b || !workspace ||
+        !matches || !scores || !num_matches || F <= 0 || P <= 0)
         return MLG_EINVAL;
     for (int p = 0; p < P; ++p)
         if (pair_a[p] < 0 || pair_a[p] >= F || pair_b[p] < 0 || pair_b[p] >= F) return MLG_EINVAL;
-    const mlg_lg_weights_i& wi = *reinterpret_cast<const mlg_lg_weights_i*>(w);
+    const mlg_lg_weights_i& wi = *reinterpret_cast<const mlg_lg_weights_i*>(&w->Wr);
     return mlg_lightglue_run(wi, keypoints, descriptors, counts, kmax, pair_a, pair_b, P, depth_confidence,
                              width_confidence, filter_threshold, pruning_min_kpts, workspace, workspace_bytes,
                              matches, scores, num_matches, stop_layer, (hipStream_t)stream);
 }
 
-static_assert(sizeof(mlg_sg_weights) == sizeof(mlg_sg_weights_i), "SuperGlue weight tables must match");
+static_assert(offsetof(mlg_sg_weights, kenc_w) == 8 &&
+                  sizeof(mlg_sg_weights) - offsetof(mlg_sg_weights, kenc_w) == sizeof(mlg_sg_weights_i),
+              "SuperGlue weight tables must match");
 
 size_t mlg_superglue_workspace_bytes(int P, int kmax) { return mlg_superglue_ws_bytes(P, kmax); }
 
@@ -435,12 +449,12 @@ int mlg_superglue(const mlg_sg_weights* w, const float* keypoints, const float* 
                   const int32_t* counts, int F, int kmax, int W, int H, const int32_t* pair_a, const int32_t* pair_b,
                   int P, int sinkhorn_iterations, float match_threshold, void* workspace, size_t workspace_bytes,
                   int32_t* matches, float* match_scores, int32_t* num_matches, void* stream) {
-    if (!w || !keypoints || !scores || !descriptors || !counts || !pair_a || !pair_b || !workspace || !matches ||
-        !match_scores || !num_matches || F <= 0 || P <= 0 || W <= 0 || H <= 0)
+    if (!mlg_head_ok(w, MLG_ABI_VERSION) || !keypoints || !scores || !descriptors || !counts || !pair_a || !pair_b ||
+        !workspace || !matches || !match_scores || !num_matches || F <= 0 || P <= 0 || W <= 0 || H <= 0)
         return MLG_EINVAL;
     for (int p = 0; p < P; ++p)
         if (pair_a[p] < 0 || pair_a[p] >= F || pair_b[p] < 0 || pair_b[p] >= F) return MLG_EINVAL;
-    const mlg_sg_weights_i& wi = *reinterpret_cast<const mlg_sg_weights_i*>(w);
+    const mlg_sg_weights_i& wi = *reinterpret_cast<const mlg_sg_weights_i*>(&w->kenc_w);
     return mlg_superglue_run(wi, keypoints, scores, descriptors, counts, kmax, W, H, pair_a, pair_b, P,
                              sinkhorn_iterations, match_threshold, workspace, workspace_bytes, matches, match_scores,
                              num_matches, (hipStream_t)stream);

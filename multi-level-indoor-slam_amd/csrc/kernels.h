@@ -9,6 +9,13 @@
 
 typedef uint16_t bf16_t;
 
+// The head every struct argument of the C ABI begins with (include/mlgate.h
+// MLG_STRUCT_INIT): true iff it names this struct's size and the library's ABI version.
+template <class T>
+inline bool mlg_head_ok(const T* p, uint32_t abi_version) {
+    return p && p->struct_size == (uint32_t)sizeof(T) && p->abi_version == abi_version;
+}
+
 // HIP-event profiling scope (abi.cpp): records the launches between construction and
 // destruction on stream s into `slot` with `work` algorithmic FLOPs (or bytes).
 // Slots: 0 fc1, 1 fc2, 2 qkv, 3 proj, 4 ViT attention, 5 LightGlue attention,

@@ -1042,7 +1042,7 @@ size_t mlg_loftr_features_ws_bytes(int B, int H, int W) {
 
 int mlg_loftr_features(const mlg_loftr_weights* wp, const uint8_t* frames_in, int B, int H_in, int W_in, int C,
                        long frame_stride, void* ws, size_t ws_bytes, float* coarse, float* fine, void* stream) {
-    if (!wp || !frames_in || !ws || !coarse || !fine || B <= 0 || H_in < 32 || W_in < 32 ||
+    if (!mlg_head_ok(wp, MLG_ABI_VERSION) || !frames_in || !ws || !coarse || !fine || B <= 0 || H_in < 32 || W_in < 32 ||
         (C != 1 && C != 3 && C != 4))
         return MLG_EINVAL;
     const int H = H_in / 8 * 8, W = W_in / 8 * 8;
@@ -1396,7 +1396,7 @@ size_t mlg_loftr_match_ws_bytes(int P, int H, int W) {
 int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const float* fine, int H, int W,
                     const int32_t* pa, const int32_t* pb, int P, const float* pe, void* ws, size_t ws_bytes,
                     int32_t* counts, float* kpts0, float* kpts1, float* conf, void* stream) {
-    if (!wp || !coarse || !fine || !pa || !pb || !pe || !ws || !counts || !kpts0 || !kpts1 || !conf || P <= 0 ||
+    if (!mlg_head_ok(wp, MLG_ABI_VERSION) || !coarse || !fine || !pa || !pb || !pe || !ws || !counts || !kpts0 || !kpts1 || !conf || P <= 0 ||
         H < 32 || W < 32 || (H % 8) || (W % 8))
         return MLG_EINVAL;
     const int hc = H / 8, wc = W / 8, L = hc * wc, Hf = H / 2, Wf = W / 2;
@@ -1550,7 +1550,7 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
 extern "C" size_t mlg_loftr_tails_bytes(void) { return TAILS_BYTES; }
 
 extern "C" int mlg_loftr_pack_tails(const mlg_loftr_weights* w, void* out, void* stream) {
-    if (!w || !out) return MLG_EINVAL;
+    if (!mlg_head_ok(w, MLG_ABI_VERSION) || !out) return MLG_EINVAL;
     TailW tw[8];
     return pack_tails(*w, (char*)out, tw, (hipStream_t)stream);
 }
@@ -1588,7 +1588,7 @@ extern "C" size_t mlg_op_loftr_coarse_layer_ws_bytes(int nseg, int L) {
 // sequence -- the two arms of the fused-tail parity test (tests/test_loftr_gpu.py).
 extern "C" int mlg_op_loftr_coarse_layer(const mlg_loftr_weights* w, int layer, int fused, float* x, uint16_t* cat,
                                          int nseg, int L, void* ws, size_t ws_bytes, void* stream) {
-    if (!w || !x || !cat || !ws || layer < 0 || layer >= 8 || nseg <= 0 || L <= 0) return MLG_EINVAL;
+    if (!mlg_head_ok(w, MLG_ABI_VERSION) || !x || !cat || !ws || layer < 0 || layer >= 8 || nseg <= 0 || L <= 0) return MLG_EINVAL;
     const CoarseLayerLayout M = coarse_layer_layout(nseg, L);
     if (ws_bytes < M.total) return MLG_ENOMEM;
     char* base = (char*)ws;

@@ -495,7 +495,7 @@ OrbLayout orb_layout(const OrbGeom& g) {
 }
 
 bool make_geom(const mlg_orb_params* p, int F, int H, int W, int max_kp, OrbGeom& g) {
-    if (!p || F <= 0 || H < 16 || W < 16 || max_kp <= 0 || H > 65535 || W > 65535) return false;
+    if (!mlg_head_ok(p, MLG_ABI_VERSION) || F <= 0 || H < 16 || W < 16 || max_kp <= 0 || H > 65535 || W > 65535) return false;
     g = OrbGeom{};
     g.H = H; g.W = W; g.F = F; g.max_kp = max_kp;
     g.fast_t = p->fast_threshold;

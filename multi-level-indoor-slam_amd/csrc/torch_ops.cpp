@@ -81,8 +81,7 @@ mlg_vit_weights vit_weights(const std::vector<Tensor>& w, bool split = false) {
         want_n(b[9], 3072LL * 768, "fc1_w");
         want_n(b[11], 768LL * 3072, "fc2_w");
     }
-    mlg_vit_weights s;
-    std::memset(&s, 0, sizeof(s));
+    mlg_vit_weights s = MLG_STRUCT_INIT(mlg_vit_weights);
     s.patch_w = cp<uint16_t>(w[0]);
     s.patch_b = cp<float>(w[1]);
     s.cls = cp<float>(w[2]);
@@ -152,7 +151,7 @@ Tensor salad_forward(const Tensor& frames, at::TensorList w, at::TensorList sala
         want(salad[i], kinds[i], "salad weight");
         TORCH_CHECK(salad[i].numel() == numel[i], "salad weight ", i, ": expected ", numel[i], " elements");
     }
-    mlg_salad_weights sw;
+    mlg_salad_weights sw = MLG_STRUCT_INIT(mlg_salad_weights);
     sw.w1 = cp<uint16_t>(salad[0]); sw.b1 = cp<float>(salad[1]);
     sw.w2 = cp<uint16_t>(salad[2]); sw.b2 = cp<float>(salad[3]);
     sw.wt1 = cp<float>(salad[4]); sw.bt1 = cp<float>(salad[5]);
@@ -269,7 +268,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> superpoint(const Tensor& fram
     want(frames, at::kByte, "frames");
     TORCH_CHECK(frames.dim() == 4, "frames must be [B, H, W, C]");
     TORCH_CHECK(w.size() == 24, "superpoint weights: expected 24 tensors");
-    mlg_sp_weights s;
+    mlg_sp_weights s = MLG_STRUCT_INIT(mlg_sp_weights);
     s.conv1a_w = cp<float>(w[0]);
     s.conv1a_b = cp<float>(w[1]);
     for (int i = 0; i < 11; ++i) {
@@ -304,8 +303,7 @@ constexpr int kLoftrTensors = 2 + 2 * MLG_LOFTR_NCONV + 10 * 8 + 5;
 mlg_loftr_weights loftr_weights(at::TensorList w) {
     TORCH_CHECK((int)w.size() == kLoftrTensors || (int)w.size() == kLoftrTensors + 1, "loftr weights: expected ",
                 kLoftrTensors, " (+ 1 packed tails) tensors, got ", w.size());
-    mlg_loftr_weights s;
-    std::memset(&s, 0, sizeof(s));
+    mlg_loftr_weights s = MLG_STRUCT_INIT(mlg_loftr_weights);
     int i = 0;
     s.stem_w = cp<float>(w[i++]);
     s.stem_b = cp<float>(w[i++]);
@@ -436,8 +434,7 @@ std::tuple<Tensor, Tensor, Tensor> superglue(const Tensor& kpts, const Tensor& s
     TORCH_CHECK(counts.numel() == F && pair_b.numel() == P && P > 0, "counts [F], pair_a / pair_b [P]");
     const int32_t* cn = cp<int32_t>(counts);
     for (int64_t f = 0; f < F; ++f) TORCH_CHECK(cn[f] >= 0 && cn[f] <= kmax, "counts out of range");
-    mlg_sg_weights s;
-    std::memset(&s, 0, sizeof(s));
+    mlg_sg_weights s = MLG_STRUCT_INIT(mlg_sg_weights);
     int i = 0;
     for (int l = 0; l < 3; ++l) s.kenc_w[l] = cp<float>(w[i++]);
     for (int l = 0; l < 3; ++l) s.kenc_b[l] = cp<float>(w[i++]);
@@ -510,8 +507,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> lightglue(const Tensor& kpts, const T
     for (int64_t p = 0; p < P; ++p)
         TORCH_CHECK(pa[p] >= 0 && pa[p] < F && pb[p] >= 0 && pb[p] < F, "pair frame index out of range");
     for (int64_t f = 0; f < F; ++f) TORCH_CHECK(cn[f] >= 0 && cn[f] <= kmax, "counts out of range");
-    mlg_lg_weights s;
-    std::memset(&s, 0, sizeof(s));
+    mlg_lg_weights s = MLG_STRUCT_INIT(mlg_lg_weights);
     int i = 0;
     s.Wr = cp<float>(w[i++]);
     for (mlg_lg_block* blocks : {s.self, s.cross})
@@ -621,7 +617,7 @@ Tensor resnet50(const Tensor& frames, at::TensorList w, int64_t descriptor_dim) 
     want(frames, at::kByte, "frames");
     TORCH_CHECK(frames.dim() == 4, "frames must be [B, H, W, C]");
     TORCH_CHECK(w.size() == 2 + 16 * 8, "resnet50 weights: expected 130 tensors");
-    mlg_rn_weights s;
+    mlg_rn_weights s = MLG_STRUCT_INIT(mlg_rn_weights);
     s.stem_w = cp<float>(w[0]);
     s.stem_b = cp<float>(w[1]);
     for (int b = 0; b < 16; ++b) {
@@ -729,8 +725,7 @@ mlg_orb_params orb_params(const Tensor& ip, const Tensor& fp) {
                 "orb params: expected 42 ints and 8 scales + 7 Gaussian taps");
     const int32_t* v = ip.data_ptr<int32_t>();
     const float* f = fp.data_ptr<float>();
-    mlg_orb_params p;
-    std::memset(&p, 0, sizeof(p));
+    mlg_orb_params p = MLG_STRUCT_INIT(mlg_orb_params);
     for (int l = 0; l < MLG_ORB_LEVELS; ++l) {
         p.level_w[l] = v[l];
         p.level_h[l] = v[8 + l];

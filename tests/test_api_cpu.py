@@ -182,7 +182,7 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, name), name
     assert set(_native.EXPORTS) <= declared
     L = _native.lib()
-    assert L.mlg_abi_version() == 2
+    assert L.mlg_abi_version() == 3
     assert L.mlg_vit_workspace_bytes(64, 322) > 0
     assert L.mlg_vit_workspace_bytes(64, 300) == 0
     assert L.mlg_strerror(-1).decode().startswith("invalid")
@@ -243,3 +243,48 @@ def test_gate_none_labels_raise_nan_labels_accept():
     valid, rejected = h.gate_candidates([(0, 1, 0.9), (0, 2, 0.8)])
     assert [(c.query_idx, c.match_idx) for c in valid] == [(0, 1)] and len(rejected) == 1
     assert h.gate_candidate(1, 2).is_valid
+
+
+def test_struct_heads_reject_foreign_structs():
+    """every struct argument begins with (struct_size, abi_version)
+    (include/mlgate.h MLG_STRUCT_INIT).  A truncated struct, one from another header
+    version and a version-2 struct (no head: its first 8 bytes are a device pointer) are
+    rejected with MLG_EINVAL before anything past the head is read -- no GPU needed, no
+    device work issued."""
+    import struct as st
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    heads = {"truncated": st.pack("<II", 16, 3), "other_version": st.pack("<II", 8 * 1024, 2),
+             "v2_pointer_first": st.pack("<Q", 0x7F1234567890), "zeros": bytes(8)}
+    dummy = ctypes.create_string_buffer(4096)
+    d = ctypes.cast(dummy, ctypes.c_void_p)
+    vp, i, z, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_float
+    for name, head in heads.items():
+        buf = ctypes.create_string_buffer(head + bytes(64 * 1024))  # room: never read past the head
+        w = ctypes.cast(buf, ctypes.c_void_p)
+        calls = {
+            "mlg_vit_forward": lambda: lib.mlg_vit_forward(w, d, 1, 480, 640, 3, ctypes.c_long(921600), 322, 0, d,
+                                                           z(1 << 30), d, None, None),
+            "mlg_salad_forward": lambda: lib.mlg_salad_forward(w, w, d, 1, 480, 640, 3, ctypes.c_long(921600), 322, d,
+                                                               z(1 << 30), d, None),
+            "mlg_resnet50_forward": lambda: lib.mlg_resnet50_forward(w, d, 1, 480, 640, 3, ctypes.c_long(921600), 4096,
+                                                                     d, z(1 << 30), d, None),
+            "mlg_superpoint": lambda: lib.mlg_superpoint(w, d, 1, 480, 640, 3, ctypes.c_long(921600), f(0.0005), 2048,
+                                                         4, 4, d, z(1 << 30), d, d, d, None, d, None),
+            "mlg_lightglue": lambda: lib.mlg_lightglue(w, d, d, d, 1, 2048, d, d, 1, f(0.95), f(0.99), f(0.1), 1536, d,
+                                                       z(1 << 30), d, d, d, None, None),
+            "mlg_superglue": lambda: lib.mlg_superglue(w, d, d, d, d, 1, 2048, 640, 480, d, d, 1, 20, f(0.2), d,
+                                                       z(1 << 30), d, d, d, None),
+            "mlg_loftr_features": lambda: lib.mlg_loftr_features(w, d, 1, 480, 640, 3, ctypes.c_long(921600), d,
+                                                                 z(1 << 30), d, d, None),
+            "mlg_loftr_match": lambda: lib.mlg_loftr_match(w, d, d, 480, 640, d, d, 1, d, d, z(1 << 30), d, d, d, d,
+                                                           None),
+            "mlg_loftr_pack_tails": lambda: lib.mlg_loftr_pack_tails(w, d, None),
+            "mlg_op_loftr_coarse_layer": lambda: lib.mlg_op_loftr_coarse_layer(w, 0, 1, d, d, 1, 64, d, z(1 << 30),
+                                                                               None),
+            "mlg_orb_detect": lambda: lib.mlg_orb_detect(w, d, d, ctypes.c_long(921600), 1, 480, 640, 3, 500, d,
+                                                         z(1 << 30), d, d, d, d, d, d, None),
+        }
+        for fn, call in calls.items():
+            assert call() == -1, (name, fn)
+        lib.mlg_orb_workspace_bytes.restype = ctypes.c_size_t
+        assert lib.mlg_orb_workspace_bytes(w, 1, 480, 640, 500) == 0, name
