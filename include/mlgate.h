@@ -511,7 +511,9 @@ typedef struct mlg_loftr_weights {
     const float* merge_b;
     /* optional: the coarse layers' block-tail weights in the fused kernel's layout, written
      * once by mlg_loftr_pack_tails (mlg_loftr_tails_bytes() bytes of device memory); NULL:
-     * mlg_loftr_match repacks them into its workspace on every call */
+     * mlg_loftr_match repacks them into its workspace on every call.  The pack is a COPY:
+     * redo it whenever the coarse layers' merge / MLP / LayerNorm weights change, or the
+     * fused tail keeps the old ones while the attention reads the new */
     const void* coarse_tails;
 } mlg_loftr_weights;
 size_t mlg_loftr_tails_bytes(void);
@@ -539,8 +541,18 @@ int mlg_loftr_features(const mlg_loftr_weights* w, const uint8_t* frames, int B,
  * Outputs (device): counts int32 [P]; for pair p, match k < counts[p] (row order of the
  * coarse cell in frame pa[p]): kpts0 / kpts1 f32 [P, L, 2] at [p * L + k], conf f32
  * [P, L] (L = H/8 * W/8).  Synchronises the stream (the fine stage is sized by the
- * coarse counts). */
+ * coarse counts).  Workspace (mlg_loftr_match_ws_bytes): the coarse transformer's token
+ * buffers (~13 KB per token, 2 P L tokens: q / k / v f32 is the largest, and holds the
+ * similarity's split-bf16 operand rows afterwards), the similarity of min(P, 8) pairs at a
+ * time (L x roundup4(L) f32 each: 92 MB at 640 x 480, 145 MB at 720 x 536), and the fine
+ * stage's buffers for 4096 matches at a time. */
 size_t mlg_loftr_match_ws_bytes(int P, int H, int W);
+/* The coarse similarity's arithmetic for the following mlg_loftr_match calls of this
+ * process: exact = 0 (default) the split-bf16 product (hi*hi + hi*lo + lo*hi of the bf16
+ * halves, f32 accumulation, ~6x the exact-f32 MFMA's rate; any frame size, the rows of S
+ * padded to a multiple of 4 floats), exact = 1 the exact-f32 MFMA (A/B and parity tests:
+ * tests/test_loftr_gpu.py compares the two arms pair by pair). */
+int mlg_set_loftr_similarity(int exact);
 int mlg_loftr_match(const mlg_loftr_weights* w, const float* coarse, const float* fine, int H, int W,
                     const int32_t* pa, const int32_t* pb, int P, const float* pe, void* workspace,
                     size_t workspace_bytes, int32_t* counts, float* kpts0, float* kpts1, float* conf, void* stream);

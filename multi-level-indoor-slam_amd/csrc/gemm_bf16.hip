@@ -66,8 +66,10 @@ struct EpiBiasSplitBF16 {
 };
 
 // LoFTR's coarse similarity from the split-bf16 product: S[m][n] = (acc / 256) / 0.1 as
-// the exact-f32 path scales it (mlg_similarity_f32_loftr), columns n < ncols only (the
-// GEMM's N is padded to the 256-column tile)
+// the exact-f32 path scales it (mlg_similarity_f32_loftr), columns n < ncols; rows of lds
+// floats (lds % 4 == 0, >= ncols: the GEMM's N is padded to the 256-column tile), the
+// columns [ncols, lds) written -inf so that 16-B row reads see no similarity there (a
+// frame of L % 4 != 0 cells, e.g. 720 x 536: L = 6030, lds = 6032)
 struct EpiSimLoFTR {
     float* S; int lds; int ncols;
     struct Col {};
@@ -81,11 +83,10 @@ struct EpiSimLoFTR {
         float* row = S + (size_t)m * lds;
         if (n + 3 < ncols) {
             *reinterpret_cast<float4*>(row + n) = make_float4(a, b, c, d);
-        } else {
-            const float v[4] = {a, b, c, d};
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (n + e < ncols) row[n + e] = v[e];
+        } else if (n < lds) {  // n % 4 == 0 and lds % 4 == 0: the quad lies inside the row
+            *reinterpret_cast<float4*>(row + n) =
+                make_float4(n < ncols ? a : -INFINITY, n + 1 < ncols ? b : -INFINITY, n + 2 < ncols ? c : -INFINITY,
+                            n + 3 < ncols ? d : -INFINITY);
         }
     }
     // staged form (k_gemm256s): the scaled products staged as f32 rows, written as whole
@@ -1505,7 +1506,7 @@ int mlg_gemm_patch_split(const bf16_t* A, const bf16_t* W, const float* bias, co
 
 int mlg_gemm_sim_split_loftr(const bf16_t* A, const bf16_t* B, int M, int Npad, int K0, float* S, int lds, int ncols,
                              hipStream_t s) {
-    if (ncols > Npad || (lds % 4)) return MLG_EINVAL;
+    if (ncols > Npad || ncols > lds || lds > Npad || (lds % 4)) return MLG_EINVAL;
     return launch_split(A, B, M, Npad, K0, 2 * K0, 2 * K0, EpiSimLoFTR{S, lds, ncols}, s);
 }
 

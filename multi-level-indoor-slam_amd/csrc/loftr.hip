@@ -521,29 +521,30 @@ __device__ __forceinline__ float lf_conf(float x, float rm, float rz, float cm, 
 
 // one wave per row; the row lives in v[] (lane l: float4 l + 64 k); rows longer than
 // 256 LF_ROWREG cells take the two-pass loop over memory
-__global__ __launch_bounds__(256) void k_lf_rowstats(const float* __restrict__ S, int L, float* __restrict__ rmax,
-                                                     float* __restrict__ rsum, float* __restrict__ rkey) {
+__global__ __launch_bounds__(256) void k_lf_rowstats(const float* __restrict__ S, int L, int lds,
+                                                     float* __restrict__ rmax, float* __restrict__ rsum,
+                                                     float* __restrict__ rkey) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= L) return;
-    S += LF_Z * L * L;
+    S += LF_Z * L * lds;
     rmax += LF_Z * L;
     rsum += LF_Z * L;
     rkey += LF_Z * L;
-    const float* s = S + (size_t)row * L;
+    const float* s = S + (size_t)row * lds;
     float m = -INFINITY, z = 0.f;
-    if ((L & 3) == 0 && L <= 256 * LF_ROWREG) {
+    if ((lds & 3) == 0 && lds <= 256 * LF_ROWREG) {  // columns [L, lds) hold -inf (EpiSimLoFTR)
         const float4* s4 = reinterpret_cast<const float4*>(s);
         float4 v[LF_ROWREG];
 #pragma unroll
         for (int k = 0; k < LF_ROWREG; ++k) {
             const int j = lane + 64 * k;
-            v[k] = j < L / 4 ? s4[j] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+            v[k] = j < lds / 4 ? s4[j] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
             m = fmaxf(m, fmaxf(fmaxf(v[k].x, v[k].y), fmaxf(v[k].z, v[k].w)));
         }
         m = wave_max(m);
 #pragma unroll
         for (int k = 0; k < LF_ROWREG; ++k)
-            if (lane + 64 * k < L / 4) z += expf(v[k].x - m) + expf(v[k].y - m) + expf(v[k].z - m) + expf(v[k].w - m);
+            if (lane + 64 * k < lds / 4) z += expf(v[k].x - m) + expf(v[k].y - m) + expf(v[k].z - m) + expf(v[k].w - m);
     } else {
         for (int j = lane; j < L; j += 64) m = fmaxf(m, s[j]);
         m = wave_max(m);
@@ -561,18 +562,18 @@ __global__ __launch_bounds__(256) void k_lf_rowstats(const float* __restrict__ S
 // 256, row chunks of LF_RCH); thread = column, coalesced 1 KiB row reads, the chunk's 64
 // values in registers.  Chunk c's (max, sum exp(x - max)) -> pm / pz [c][L]; k_lf_colfin
 // merges the chunks (max, then sum_c pz_c exp(pm_c - max)).
-__global__ __launch_bounds__(256) void k_lf_colpart(const float* __restrict__ S, int L, float* __restrict__ pm,
-                                                    float* __restrict__ pz) {
+__global__ __launch_bounds__(256) void k_lf_colpart(const float* __restrict__ S, int L, int lds,
+                                                    float* __restrict__ pm, float* __restrict__ pz) {
     const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
     if (col >= L) return;
-    S += LF_Z * L * L;
+    S += LF_Z * L * lds;
     pm += LF_Z * gridDim.y * L;
     pz += LF_Z * gridDim.y * L;
     const int r0 = c * LF_RCH, n = min(L - r0, LF_RCH);
     float v[LF_RCH], m = -INFINITY, z = 0.f;
 #pragma unroll
     for (int i = 0; i < LF_RCH; ++i) {
-        v[i] = i < n ? S[(size_t)(r0 + i) * L + col] : -INFINITY;
+        v[i] = i < n ? S[(size_t)(r0 + i) * lds + col] : -INFINITY;
         m = fmaxf(m, v[i]);
     }
 #pragma unroll
@@ -588,21 +589,21 @@ __global__ __launch_bounds__(256) void k_lf_colpart(const float* __restrict__ S,
 // the max -- until lane l holds row l's max over the wave's 64 columns; the four waves
 // meet in LDS and prm[column block][row] gets the block's max.  Max is exact in any order,
 // so rmax = max over blocks equals k_lf_rowstats' bit for bit.
-__global__ __launch_bounds__(256) void k_lf_stats(const float* __restrict__ S, int L, float* __restrict__ pm,
+__global__ __launch_bounds__(256) void k_lf_stats(const float* __restrict__ S, int L, int lds, float* __restrict__ pm,
                                                   float* __restrict__ pz, float* __restrict__ prm) {
     __shared__ float red[4][LF_RCH];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
     const int r0 = c * LF_RCH, n = min(L - r0, LF_RCH);
     const bool ok = col < L;
-    S += LF_Z * L * L;
+    S += LF_Z * L * lds;
     pm += LF_Z * gridDim.y * L;
     pz += LF_Z * gridDim.y * L;
     prm += LF_Z * gridDim.x * L;
     float v[LF_RCH], m = -INFINITY, z = 0.f;
 #pragma unroll
     for (int i = 0; i < LF_RCH; ++i) {
-        v[i] = (ok && i < n) ? S[(size_t)(r0 + i) * L + col] : -INFINITY;
+        v[i] = (ok && i < n) ? S[(size_t)(r0 + i) * lds + col] : -INFINITY;
         m = fmaxf(m, v[i]);
     }
 #pragma unroll
@@ -631,7 +632,7 @@ __global__ __launch_bounds__(256) void k_lf_stats(const float* __restrict__ S, i
 // 64 columns x 4 chunk groups per workgroup (group g: chunks g, g + 4, ..): the chunk
 // loads of a column run in parallel; the four partials combine in group order
 __global__ __launch_bounds__(256) void k_lf_colfin(const float* __restrict__ pm, const float* __restrict__ pz, int L,
-                                                   int nch, float* __restrict__ cmax, float* __restrict__ csum,
+                                                   int lds, int nch, float* __restrict__ cmax, float* __restrict__ csum,
                                                    float* __restrict__ ckey) {
     __shared__ float part[4][64];
     const int cl = threadIdx.x & 63, g = threadIdx.x >> 6, col = blockIdx.x * 64 + cl;
@@ -640,7 +641,7 @@ __global__ __launch_bounds__(256) void k_lf_colfin(const float* __restrict__ pm,
     pz += LF_Z * nch * L;
     cmax += LF_Z * L;
     csum += LF_Z * L;
-    ckey += LF_Z * L;
+    ckey += LF_Z * lds;  // rows of lds: k_lf_rowbest reads it as float4 over [0, lds)
     float m = -INFINITY;
     if (ok)
 #pragma unroll 4
@@ -668,7 +669,7 @@ __global__ __launch_bounds__(256) void k_lf_colfin(const float* __restrict__ pm,
 // per-lane order and wave sum as k_lf_rowstats, so the same bits); rmax / rsum / rkey are
 // written for k_lf_colmaxpart.  Otherwise they are read (k_lf_rowstats ran before).
 template <bool SELF>
-__global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S, int L, float* __restrict__ rmax,
+__global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S, int L, int lds, float* __restrict__ rmax,
                                                     float* __restrict__ rsum, float* __restrict__ rkey,
                                                     const float* __restrict__ prm, int ncb,
                                                     const float* __restrict__ cmax, const float* __restrict__ csum,
@@ -676,25 +677,27 @@ __global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S,
                                                     int32_t* __restrict__ bidx) {
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= L) return;
-    S += LF_Z * L * L;
+    S += LF_Z * L * lds;
     rmax += LF_Z * L;
     rsum += LF_Z * L;
     rkey += LF_Z * L;
     if (SELF) prm += LF_Z * ncb * L;
     cmax += LF_Z * L;
     csum += LF_Z * L;
-    ckey += LF_Z * L;
+    ckey += LF_Z * lds;
     bval += LF_Z * L;
     bidx += LF_Z * L;
-    const float* s = S + (size_t)row * L;
+    const float* s = S + (size_t)row * lds;
     float rm, rz;
-    const bool reg = (L & 3) == 0 && L <= 256 * LF_ROWREG;
+    // register rows: 16-B reads over [0, lds); the pad columns [L, lds) hold -inf, so they
+    // add nothing to the max / sum and never pass the key band (2 (-inf) - key = -inf or NaN)
+    const bool reg = (lds & 3) == 0 && lds <= 256 * LF_ROWREG;
     float4 v[LF_ROWREG];
     if (reg) {
         const float4* s4 = reinterpret_cast<const float4*>(s);
 #pragma unroll
         for (int k = 0; k < LF_ROWREG; ++k)
-            if (lane + 64 * k < L / 4) v[k] = s4[lane + 64 * k];
+            if (lane + 64 * k < lds / 4) v[k] = s4[lane + 64 * k];
     }
     if constexpr (SELF) {
         float m = -INFINITY;
@@ -704,7 +707,7 @@ __global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S,
         if (reg) {
 #pragma unroll
             for (int k = 0; k < LF_ROWREG; ++k)
-                if (lane + 64 * k < L / 4)
+                if (lane + 64 * k < lds / 4)
                     z += expf(v[k].x - m) + expf(v[k].y - m) + expf(v[k].z - m) + expf(v[k].w - m);
         } else {
             for (int j = lane; j < L; j += 64) z += expf(s[j] - m);
@@ -733,7 +736,7 @@ __global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S,
 #pragma unroll
         for (int k = 0; k < LF_ROWREG; ++k) {
             const int j = lane + 64 * k;
-            if (j < L / 4) {
+            if (j < lds / 4) {
                 const float4 ck = k4[j];
                 kb = fmaxf(kb, fmaxf(fmaxf(2.f * v[k].x - ck.x, 2.f * v[k].y - ck.y),
                                      fmaxf(2.f * v[k].z - ck.z, 2.f * v[k].w - ck.w)));
@@ -744,7 +747,7 @@ __global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S,
 #pragma unroll
         for (int k = 0; k < LF_ROWREG; ++k) {
             const int j = lane + 64 * k;
-            if (j < L / 4) {
+            if (j < lds / 4) {
                 const float4 ck = k4[j];
                 if (2.f * v[k].x - ck.x >= lim) take(v[k].x, 4 * j);
                 if (2.f * v[k].y - ck.y >= lim) take(v[k].y, 4 * j + 1);
@@ -772,14 +775,14 @@ __global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S,
 }
 
 // column max of conf per row chunk (max is exact in any order)
-__global__ __launch_bounds__(256) void k_lf_colmaxpart(const float* __restrict__ S, int L,
+__global__ __launch_bounds__(256) void k_lf_colmaxpart(const float* __restrict__ S, int L, int lds,
                                                        const float* __restrict__ rmax, const float* __restrict__ rsum,
                                                        const float* __restrict__ rkey, const float* __restrict__ cmax,
                                                        const float* __restrict__ csum, float* __restrict__ pb) {
     __shared__ float rk[LF_RCH];
     const int col = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
     const int r0 = c * LF_RCH, n = min(L - r0, LF_RCH);
-    S += LF_Z * L * L;
+    S += LF_Z * L * lds;
     rmax += LF_Z * L;
     rsum += LF_Z * L;
     rkey += LF_Z * L;
@@ -793,7 +796,7 @@ __global__ __launch_bounds__(256) void k_lf_colmaxpart(const float* __restrict__
     float v[LF_RCH], kb = -INFINITY;
 #pragma unroll
     for (int i = 0; i < LF_RCH; ++i) {
-        v[i] = i < n ? S[(size_t)(r0 + i) * L + col] : 0.f;
+        v[i] = i < n ? S[(size_t)(r0 + i) * lds + col] : 0.f;
         kb = fmaxf(kb, 2.f * v[i] - rk[i]);
     }
     const float lim = kb - lf_band(kb);
@@ -1137,6 +1140,7 @@ namespace {
 #ifndef MLG_LF_SIM_SPLIT
 #define MLG_LF_SIM_SPLIT 1
 #endif
+int g_lf_sim_split = MLG_LF_SIM_SPLIT;  // mlg_set_loftr_similarity
 // Dual softmax in three reads of S: k_lf_stats (column statistics + row block maxima) and
 // a self-normalising k_lf_rowbest replace k_lf_rowstats + k_lf_colpart; 0 builds the
 // four-read sequence (A/B arm).  Both give the same bits.
@@ -1357,16 +1361,19 @@ MatchLayout match_layout(int P, int L) {
     M.cd = take((size_t)2 * FINE_CHUNK * 128 * 2);
     M.cm = take((size_t)2 * FINE_CHUNK * 128 * 4);
     const size_t G = (size_t)std::min(P, MLG_LF_PGRP);  // pairs per dual-softmax group
-    M.S = take(G * L * L * 4);
+    const size_t Lp = (size_t)(L + 3) / 4 * 4;          // S / ckey row stride (split path)
+    M.S = take(G * L * Lp * 4);
     // the coarse features as split-bf16 rows [hi | lo] (+ 256 zero rows: the similarity
-    // GEMM reads B rows up to its 256-column tile)
-    M.csplit = take(((size_t)2 * P * L + 256) * 512 * 2);
+    // GEMM reads B rows up to its 256-column tile), in the q / k / v buffer, which the
+    // coarse transformer no longer needs when the similarity runs (3x larger: 2 P L x 768 f32)
+    const size_t csplit_bytes = ((size_t)2 * P * L + 256) * 512 * 2;
+    M.csplit = csplit_bytes <= rc * 768 * 4 ? M.cqkv : take(csplit_bytes);
     M.rmax = take(G * L * 4);
     M.rsum = take(G * L * 4);
     M.rkey = take(G * L * 4);
     M.cmax = take(G * L * 4);
     M.csum = take(G * L * 4);
-    M.ckey = take(G * L * 4);
+    M.ckey = take(G * Lp * 4);
     const size_t nrch = (size_t)(L + LF_RCH - 1) / LF_RCH;
     M.pm = take(G * nrch * L * 4);
     M.pz = take(G * nrch * L * 4);
@@ -1457,12 +1464,14 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
     }
     LF_TRY(transformer(w.coarse, 8, bc, 256, P, L, s, MLG_LF_FUSED_TAIL ? tails : nullptr));
     // the coarse similarity: split-bf16 operands (3 bf16 MFMA products at ~6x the exact-f32
-    // MFMA's rate) or the exact-f32 MFMA (MLG_LF_SIM_SPLIT=0)
+    // MFMA's rate) or the exact-f32 MFMA (mlg_set_loftr_similarity(1)).  The split GEMM
+    // writes 16-B row pieces, so its S rows are lds = L rounded up to 4 floats, the pad
+    // columns -inf (EpiSimLoFTR): frames of L % 4 != 0 cells -- the ISEC 720 x 536, L =
+    // 6030 -- take the split path too (round 6; before, the exact-f32 one)
     bf16_t* CS = (bf16_t*)at(ML.csplit);
     const int Lpad = (L + 255) / 256 * 256;
-    // (the split GEMM's staged f32 rows are written as 16-B pieces: S rows of L % 4 != 0
-    // cells -- e.g. 720 x 536 frames, L = 6030 -- take the exact-f32 path)
-    const bool split = MLG_LF_SIM_SPLIT && (L % 4) == 0;
+    const bool split = g_lf_sim_split != 0;
+    const int lds = split ? (L + 3) / 4 * 4 : L;
     if (split) {
         const long rows = (long)2 * P * L;
         hipLaunchKernelGGL(k_lf_split_rows, dim3((unsigned)((rows * 64 + 255) / 256)), dim3(256), 0, s, bc.x, rows, CS);
@@ -1475,30 +1484,30 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
         const unsigned g = (unsigned)std::min(G, P - p0);
         for (int q = 0; q < (int)g; ++q) {
             const int p = p0 + q;
-            float* Sq = S + (size_t)q * L * L;
+            float* Sq = S + (size_t)q * L * lds;
             if (split)
                 LF_TRY(mlg_gemm_sim_split_loftr(CS + (size_t)p * L * 512, CS + ((size_t)P + p) * L * 512, L, Lpad, 256,
-                                                Sq, L, L, s));
+                                                Sq, lds, L, s));
             else
                 LF_TRY(mlg_similarity_f32_loftr(bc.x + (size_t)p * L * 256, L, bc.x + ((size_t)P + p) * L * 256, L, 256,
                                                 Sq, L, s));
         }
         if (MLG_LF_STATS1) {  // three reads of S: stats, rowbest, colmaxpart
-            hipLaunchKernelGGL(k_lf_stats, dim3(ncb, nrch, g), dim3(256), 0, s, S, L, pm, pz, prm);
-            hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64, 1, g), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum,
-                               ckey);
-            hipLaunchKernelGGL(k_lf_rowbest<true>, dim3((L + 3) / 4, 1, g), dim3(256), 0, s, S, L, rmax, rsum, rkey,
-                               prm, ncb, cmax, csum, ckey, bval, bidx);
+            hipLaunchKernelGGL(k_lf_stats, dim3(ncb, nrch, g), dim3(256), 0, s, S, L, lds, pm, pz, prm);
+            hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64, 1, g), dim3(256), 0, s, pm, pz, L, lds, nrch, cmax,
+                               csum, ckey);
+            hipLaunchKernelGGL(k_lf_rowbest<true>, dim3((L + 3) / 4, 1, g), dim3(256), 0, s, S, L, lds, rmax, rsum,
+                               rkey, prm, ncb, cmax, csum, ckey, bval, bidx);
         } else {
-            hipLaunchKernelGGL(k_lf_rowstats, dim3((L + 3) / 4, 1, g), dim3(256), 0, s, S, L, rmax, rsum, rkey);
-            hipLaunchKernelGGL(k_lf_colpart, dim3(ncb, nrch, g), dim3(256), 0, s, S, L, pm, pz);
-            hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64, 1, g), dim3(256), 0, s, pm, pz, L, nrch, cmax, csum,
-                               ckey);
-            hipLaunchKernelGGL(k_lf_rowbest<false>, dim3((L + 3) / 4, 1, g), dim3(256), 0, s, S, L, rmax, rsum, rkey,
-                               nullptr, 0, cmax, csum, ckey, bval, bidx);
+            hipLaunchKernelGGL(k_lf_rowstats, dim3((L + 3) / 4, 1, g), dim3(256), 0, s, S, L, lds, rmax, rsum, rkey);
+            hipLaunchKernelGGL(k_lf_colpart, dim3(ncb, nrch, g), dim3(256), 0, s, S, L, lds, pm, pz);
+            hipLaunchKernelGGL(k_lf_colfin, dim3((L + 63) / 64, 1, g), dim3(256), 0, s, pm, pz, L, lds, nrch, cmax,
+                               csum, ckey);
+            hipLaunchKernelGGL(k_lf_rowbest<false>, dim3((L + 3) / 4, 1, g), dim3(256), 0, s, S, L, lds, rmax, rsum,
+                               rkey, nullptr, 0, cmax, csum, ckey, bval, bidx);
         }
-        hipLaunchKernelGGL(k_lf_colmaxpart, dim3((L + 255) / 256, nrch, g), dim3(256), 0, s, S, L, rmax, rsum, rkey,
-                           cmax, csum, pm);
+        hipLaunchKernelGGL(k_lf_colmaxpart, dim3((L + 255) / 256, nrch, g), dim3(256), 0, s, S, L, lds, rmax, rsum,
+                           rkey, cmax, csum, pm);
         hipLaunchKernelGGL(k_lf_colmaxfin, dim3((L + 255) / 256, 1, g), dim3(256), 0, s, pm, L, nrch, cbest);
         hipLaunchKernelGGL(k_lf_select, dim3(1, 1, g), dim3(1024), 0, s, bval, bidx, cbest, L, hc, wc, 0.2f, 2,
                            mi + (size_t)p0 * L, mj + (size_t)p0 * L, mconf + (size_t)p0 * L, cnt + p0);
@@ -1548,6 +1557,12 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
 }
 
 extern "C" size_t mlg_loftr_tails_bytes(void) { return TAILS_BYTES; }
+
+extern "C" int mlg_set_loftr_similarity(int exact) {
+    if (exact != 0 && exact != 1) return MLG_EINVAL;
+    g_lf_sim_split = exact ? 0 : 1;
+    return MLG_OK;
+}
 
 extern "C" int mlg_loftr_pack_tails(const mlg_loftr_weights* w, void* out, void* stream) {
     if (!mlg_head_ok(w, MLG_ABI_VERSION) || !out) return MLG_EINVAL;

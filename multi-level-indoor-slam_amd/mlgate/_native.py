@@ -75,6 +75,7 @@ EXPORTS = {
     "mlg_op_gemm_f32out": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_op_gemm_f32out_variant": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_set_gemm_variant": (c_int, [c_int]),
+    "mlg_set_loftr_similarity": (c_int, [c_int]),
     "mlg_op_gemm_bias_gelu": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "mlg_op_gemm_residual": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                      c_void_p]),

@@ -216,3 +216,48 @@ def test_fused_coarse_tail_equals_unfused_layer(dev, setup, layer):
     print(stats)
     assert not torch.equal(xu, x0.double().cpu())
     assert cell <= 2e-3 and stats["dx_median"] <= 1e-5 * scale and same_cat >= 0.99, stats
+
+
+@pytest.mark.parametrize("hw", [(480, 640), (540, 720)])
+def test_split_similarity_against_exact_arm(dev, setup, hw):
+    """ADVICE r05 / VERDICT r05 next 8: the coarse similarity from split-bf16 operands (the
+    product default) against the exact-f32 arm (mlg_set_loftr_similarity(1)) on the SAME
+    coarse features, 18 revisit pairs (three dual-softmax groups of 8), at the bench frame
+    size (L = 4800) and at the ISEC frame size (720 x 540 -> 536: L = 6030, L % 4 != 0,
+    which took the exact path before round 6; its S rows are now padded to 6032).  The
+    mutual-nearest coarse match sets agree up to near ties, and the shared matches'
+    confidences and fine keypoints agree."""
+    from mlgate import _native
+    sd, lf, orc, _, _, _ = setup
+    H, W = hw
+    seq = synthetic.make_sequence(40, 8, 1)
+    po = seq.place_of
+    pairs = [(a, b) for a in range(40) for b in range(a + 1, 40) if po[a] == po[b]][:18]
+    idx = sorted({i for p in pairs for i in p})
+    fr = torch.from_numpy(synthetic.frames_host(seq, np.array(idx), H, W)).to(dev)
+    coarse, fine = lf.features(fr)
+    H8, W8 = H // 8 * 8, W // 8 * 8
+    pos = {f: k for k, f in enumerate(idx)}
+    pa, pb = [pos[a] for a, _ in pairs], [pos[b] for _, b in pairs]
+    L = _native.lib()
+    out = {}
+    try:
+        for exact in (0, 1):
+            assert L.mlg_set_loftr_similarity(exact) == 0
+            out[exact] = [x.cpu().numpy() for x in lf.match_device(coarse, fine, H8, W8, pa, pb)]
+    finally:
+        L.mlg_set_loftr_similarity(0)
+    (n0, a0, b0, c0), (n1, a1, b1, c1) = out[0], out[1]
+    tot = shared = close = 0
+    for p in range(len(pairs)):
+        m0 = {tuple(np.rint(a0[p, k]).astype(int)): k for k in range(n0[p])}
+        m1 = {tuple(np.rint(a1[p, k]).astype(int)): k for k in range(n1[p])}
+        common = set(m0) & set(m1)
+        tot += max(len(m0), len(m1))
+        shared += len(common)
+        for key in common:
+            i, j = m0[key], m1[key]
+            close += abs(c0[p, i] - c1[p, j]) <= 1e-3 * c1[p, j] and np.abs(b0[p, i] - b1[p, j]).max() < 0.05
+        assert abs(int(n0[p]) - int(n1[p])) <= max(2, 0.01 * n1[p]), (p, n0[p], n1[p])
+    print(f"{hw}: {shared} of {tot} coarse matches shared, {close} within conf 1e-3 / 0.05 px")
+    assert tot > 18 * 50 and shared >= 0.99 * tot and close >= 0.99 * shared, (tot, shared, close)
