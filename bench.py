@@ -364,6 +364,33 @@ def _loftr_kernels(lf, sel, used, pairs, chunk, dev):
             "flops": {"backbone_per_keyframe": bf, "match_per_pair": round(mf, 0)}}
 
 
+def stress_bench(n, k, dev):
+    """SURVEY §8d's stress size: the same gate over an n-keyframe sequence (places scaled as
+    bench.py's 600 per 5000) on one GPU, the LightGlue chunk sized from the free HBM and the
+    local-feature cache (31 GB at 19,163) unmaterialised; one warm-up step, one timed step."""
+    seq, labels = sequence(n, max(1, round(n * 600 / 5000)))
+    frames = synthetic.frames_device(seq, np.arange(n), dev)
+    g = DeviceGate(frames, seq.t, labels, 1, 0, dev, k=k, verify=True, K=ISEC_K, vit_batch=246, lg_chunk="auto",
+                   local_features=False, vit_state_dict=synthetic_state_dict(0))
+    g.step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    c = g.step()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    rej = c["retrieval_floor_rejected"] + c["skipped_floor_mismatch"] + c["verifier_invalid"] + \
+        c["gate_rejected_cross_floor"]
+    out = {"workload": f"configs[3] gate over {n} keyframes (ORB-SLAM3 pose count of the ISEC run, SURVEY §8d), "
+                       "lg_chunk auto, local features not materialised",
+           "keyframes": n, "seconds": round(dt, 3), "keyframes_per_s": round(n / dt, 1),
+           "lg_chunk": g.last_lg_chunk, "pairs_verified": c["pairs_verified"], "verified_valid": c["verified_valid"],
+           "false_loop_closure_rejections": rej,
+           "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)}
+    del g, frames
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -389,6 +416,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ingest", action="store_true", help="skip the f2 ingestion sub-object")
     ap.add_argument("--loftr-pairs", type=int, default=1024, help="configs[4] LoFTR sub-object: gate pairs (0: skip)")
+    ap.add_argument("--stress-keyframes", type=int, default=0,
+                    help="also gate an N-keyframe sequence once warm (SURVEY §8d: 19163, the ORB-SLAM3 pose count) "
+                         "on one GPU and report it as the 'stress' sub-object (0: skip; one rank only)")
     ap.add_argument("--vit", choices=["split", "bf16"], default="split",
                     help="split: split-bf16 ViT (MLG_VIT_SPLIT, fp32-faithful descriptors); bf16: plain bf16 operands")
     args = ap.parse_args()
@@ -463,6 +493,11 @@ def main():
     lft = loftr_bench(frames, seq, labels, lo, dev, world, rank, args.loftr_pairs) if args.loftr_pairs > 0 else None
     c0 = configs0_bench(frames, seq, labels, lo, dev) if rank == 0 else None
     ing = ingest_bench(dev) if rank == 0 and not args.no_ingest else None
+    stress = None
+    if args.stress_keyframes > 0 and world == 1:
+        del gate, frames
+        torch.cuda.empty_cache()
+        stress = stress_bench(args.stress_keyframes, args.k, dev)
 
     if rank == 0:
         avg_s = ms / 1e3 / max(cnt, 1)
@@ -474,7 +509,7 @@ def main():
                                           "gate_rejected_cross_floor")}
         rej["total"] = sum(rej.values())
         line = {
-            "metric": "keyframes gated/sec (VPR+kNN+LightGlue verify)" if gate.verify else
+            "metric": "keyframes gated/sec (VPR+kNN+LightGlue verify)" if args.verify == "all" else
                       "keyframes gated/sec (CricaVPR DINOv2-B/14 descriptor + cosine-kNN floor gate)",
             "value": round(N * args.steps / dt, 2), "unit": "keyframes/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / steps * 1e3, 3),
@@ -490,7 +525,7 @@ def main():
                                       "SuperPoint(2048) + LightGlue + OpenCV-sequenced E-RANSAC (K = ISEC cam1) + "
                                       "decision rule (LightGlue once per unordered pair, RANSAC + decision per ordered pair); "
                                       "floor gate on the geometrically valid pairs"
-                                      if gate.verify else ""),
+                                      if args.verify == "all" else ""),
                        "keyframes": N, "k": args.k, "vit_batch": args.batch, "parallelism": f"frame-sharded x{world}",
                        "matches": counts["matches"], "pairs_verified": counts["pairs_verified"],
                        "pairs_matched_lightglue": counts.get("pairs_matched_lightglue", 0),
@@ -524,10 +559,12 @@ def main():
             line["configs0"] = c0
         if ing:
             line["ingest"] = ing
+        if stress:
+            line["stress"] = stress
         if not args.no_cpu_baseline:
             # rank 0 only, after the timed region (at world > 1 the other ranks wait at the
             # final barrier, so their processes leave the host cores to it)
-            line["cpu_baseline"] = cpu_baseline(pairs_per_kf=(counts["pairs_verified"] / N) if gate.verify else 0.0)
+            line["cpu_baseline"] = cpu_baseline(pairs_per_kf=(counts["pairs_verified"] / N) if args.verify == "all" else 0.0)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

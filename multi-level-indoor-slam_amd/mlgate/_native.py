@@ -149,6 +149,12 @@ def ops():
     return _ops
 
 
+def lightglue_workspace_bytes(pairs, kmax):
+    """mlg_lightglue_workspace_bytes: HBM one LightGlue call of `pairs` pairs needs (a size
+    query: DeviceGate sizes its pair chunks from it)."""
+    return int(lib().mlg_lightglue_workspace_bytes(int(pairs), int(kmax)))
+
+
 def check(rc, what=""):
     if rc != 0:
         msg = lib().mlg_strerror(rc).decode()

@@ -162,7 +162,8 @@ class DeviceGate:
                  similarity_threshold=0.5, min_time_gap=10.0, strict_mode=True, retrieval_floor_gating=True,
                  verifier_floor_gating=True, verify=True, K=None, min_inliers=20, min_inlier_ratio=0.25,
                  vit_batch=123, sp_batch=64, lg_chunk=1024, max_keypoints=2048, vit_state_dict=None, record=False,
-                 vit_precise=True, matcher='lightglue', loftr_chunk=256, max_pairs=None, lg_tail=0):
+                 vit_precise=True, matcher='lightglue', loftr_chunk=256, max_pairs=None, lg_tail=0,
+                 local_features=True):
         import torch
         from . import distributed as mdist
         from .lightglue import LightGlueGPU
@@ -182,6 +183,8 @@ class DeviceGate:
         self.limit = 0 if strict_mode else 1
         self.retrieval_floor_gating, self.verifier_floor_gating = retrieval_floor_gating, verifier_floor_gating
         self.min_inliers, self.min_inlier_ratio = min_inliers, min_inlier_ratio
+        # lg_chunk: pairs per LightGlue call, or 'auto' (sized from the free HBM when the pairs
+        # are known: _lg_chunk_for)
         self.sp_batch, self.lg_chunk, self.kp = sp_batch, lg_chunk, max_keypoints
         self.lg_tail = int(lg_tail)
         self.t_all = torch.as_tensor(np.asarray(timestamps, np.float64), device=self.dev)
@@ -204,7 +207,12 @@ class DeviceGate:
         self.gather = mdist.RowGather(N, EMBED, world, self.dev)
         self.desc_loc = (self.gather.out[self.lo:self.hi] if world == 1
                          else torch.empty(self.n_local, EMBED, device=self.dev))
-        self.local_feats = torch.empty(self.n_local, self.eng.n_local, EMBED, dtype=torch.float32, device=self.dev)
+        # CricaVPR's per-keyframe local features (place_recognition.py:645-667, the input of
+        # rerank_candidates), written by the same ViT forward: [N, 528, 768] f32, 1.6 MB per
+        # keyframe.  local_features=False leaves them unmaterialised (the gate itself never
+        # reads them): the N = 19,163 sequence then fits one GPU with its LightGlue workspace
+        self.local_feats = (torch.empty(self.n_local, self.eng.n_local, EMBED, dtype=torch.float32, device=self.dev)
+                            if local_features else None)
         self.totals = torch.zeros(2, dtype=torch.int64, device=self.dev)
         self.verify = verify
         # matcher: 'lightglue' (SuperPoint + LightGlue, the reference default) or 'loftr'
@@ -378,7 +386,9 @@ class DeviceGate:
         # chunk starts: full chunks, then (lg_tail > 0) the remainder cut so the LAST chunk
         # is 1 / lg_tail of it -- that chunk's RANSAC is the only one with no LightGlue to
         # overlap (per-pair results do not depend on the chunking)
-        starts = list(range(0, len(ua), self.lg_chunk))
+        chunk = self._lg_chunk_for(len(ua))
+        self.last_lg_chunk = chunk
+        starts = list(range(0, len(ua), chunk))
         rem = len(ua) - starts[-1] if starts else 0
         if self.lg_tail > 0 and rem >= 1024:
             starts.append(len(ua) - max(256, rem // self.lg_tail))
@@ -415,6 +425,29 @@ class DeviceGate:
         out["gate_rejected_cross_floor"] = gate_rej
         out["accepted"] = n_valid - gate_rej
         return out
+
+    # HBM per LightGlue pair beside its mlg_lightglue workspace: the pair's RANSAC
+    # workspace at 1000 hypotheses (models, scores, subsets, points: ~0.9 MB), its flat
+    # match coordinates and oriented matches
+    _RANSAC_PAIR_BYTES = 1 << 20
+
+    def _lg_chunk_for(self, n_pairs):
+        """Pairs per LightGlue call: self.lg_chunk, or with 'auto' the largest multiple of 256
+        (<= 5120, bench.py's measured optimum) whose LightGlue + RANSAC workspaces fit in the
+        HBM free now (the caching allocator's reusable blocks included), keeping 6 % of the
+        device and 4 GiB in reserve."""
+        if self.lg_chunk != 'auto':
+            return int(self.lg_chunk)
+        torch = self.torch
+        free, total = torch.cuda.mem_get_info(self.dev)
+        free += torch.cuda.memory_reserved(self.dev) - torch.cuda.memory_allocated(self.dev)
+        avail = free - 0.06 * total - (4 << 30)
+        per = _native.lightglue_workspace_bytes(1024, self.kp) / 1024 + self._RANSAC_PAIR_BYTES
+        chunk = int(max(avail, 0) // per) // 256 * 256
+        if chunk < 256:
+            raise MemoryError(f"LightGlue needs {per * 256 / 2**30:.1f} GiB for 256 pairs; "
+                              f"{max(avail, 0) / 2**30:.1f} GiB free")
+        return min(chunk, 5120, max(256, -(-n_pairs // 256) * 256))
 
     def _extract_side(self, rows):
         """_extract_rows on the SuperPoint side stream, after everything already queued on
