@@ -563,15 +563,37 @@ __device__ __forceinline__ void attention_tile_pipe(unsigned long long* att_tt, 
             for (int qt = 0; qt < QT; ++qt) {
                 const int r = qt * 32 + col;
 #pragma unroll
-                for (int dt = 0; dt < 2; ++dt)
+                for (int dt = 0; dt < 2; ++dt) {
+                    if (MLG_ATT_STAGE_W) {
+                        // lanes l / l + 32 hold the two 8-B halves of chunks (dt, g) and (dt, g + 1)
+                        // of row r: after the swap lane l < 32 holds chunk g whole, lane l + 32
+                        // chunk g + 1 -- one conflict-free b128 write each (8 rows per write
+                        // group) instead of two b64 writes whose rows r and r + 8 shared banks
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        uint2 w, wl;
-                        split_bf16x4(o[qt][dt][4 * g] * inv[qt], o[qt][dt][4 * g + 1] * inv[qt],
-                                     o[qt][dt][4 * g + 2] * inv[qt], o[qt][dt][4 * g + 3] * inv[qt], w, wl);
-                        *reinterpret_cast<uint2*>(st + r * 128 + (((dt * 4 + g) ^ (r & 7)) << 4) + 8 * hh) =
-                            part ? wl : w;
+                        for (int g = 0; g < 4; g += 2) {
+                            uint2 w0, wl0, w1, wl1;
+                            split_bf16x4(o[qt][dt][4 * g] * inv[qt], o[qt][dt][4 * g + 1] * inv[qt],
+                                         o[qt][dt][4 * g + 2] * inv[qt], o[qt][dt][4 * g + 3] * inv[qt], w0, wl0);
+                            split_bf16x4(o[qt][dt][4 * g + 4] * inv[qt], o[qt][dt][4 * g + 5] * inv[qt],
+                                         o[qt][dt][4 * g + 6] * inv[qt], o[qt][dt][4 * g + 7] * inv[qt], w1, wl1);
+                            const uint2 a = part ? wl0 : w0, b = part ? wl1 : w1;
+                            const auto s0 = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+                            const auto s1 = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+                            const int gg = g + hh;
+                            *reinterpret_cast<uint4*>(st + r * 128 + (((dt * 4 + gg) ^ (r & 7)) << 4)) =
+                                make_uint4(s0[0], s1[0], s0[1], s1[1]);
+                        }
+                    } else {
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) {
+                            uint2 w, wl;
+                            split_bf16x4(o[qt][dt][4 * g] * inv[qt], o[qt][dt][4 * g + 1] * inv[qt],
+                                         o[qt][dt][4 * g + 2] * inv[qt], o[qt][dt][4 * g + 3] * inv[qt], w, wl);
+                            *reinterpret_cast<uint2*>(st + r * 128 + (((dt * 4 + g) ^ (r & 7)) << 4) + 8 * hh) =
+                                part ? wl : w;
+                        }
                     }
+                }
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's staging writes landed
             __builtin_amdgcn_wave_barrier();
