@@ -398,13 +398,20 @@ class DeviceGate:
         ua, ub = local(ua), local(ub)  # LightGlue indexes the feature tables
         sp_done = None
         if getattr(self, "_sp_overlap", False):
-            # the first chunk's keyframes now, the rest on a side stream under that chunk
+            # the first chunk's keyframes now, the rest on a side stream under that chunk;
+            # only the finished rows' counts are read here (the side stream is
+            # writing the others), the rest once the side stream's event has passed
             first = np.unique(np.concatenate([ua[:starts[1]], ub[:starts[1]]])) if len(starts) > 1 else \
                 np.zeros(0, np.int64)
             self._extract_rows(first)
+            counts = np.zeros(nf, np.int32)
+            if len(first):
+                fi = self.torch.from_numpy(first.astype(np.int64)).to(self.dev)
+                counts[first] = cnt_c.view(-1).index_select(0, fi).cpu().numpy()
             rest = np.setdiff1d(np.arange(self.n_local), first, assume_unique=True)
             sp_done = self._extract_side(rest)
-        counts = cnt_c.view(-1).cpu().numpy()  # rows of the first chunk's keyframes final
+        else:
+            counts = cnt_c.view(-1).cpu().numpy()
         # RANSAC of chunk c runs on a side stream while LightGlue matches chunk c + 1 on
         # this one (mlg_lightglue waits on its stream once per layer; the side stream
         # fills those gaps and the CUs the small RANSAC / assignment grids leave idle)

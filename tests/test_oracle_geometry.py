@@ -145,3 +145,16 @@ def test_c_fundamental_small_sizes():
     med = np.sort(e)[len(e) // 2]
     sigma = max(2.5 * 1.4826 * (1 + 5.0 / (len(e) - 7)) * np.sqrt(np.float64(med)), 0.001)
     assert np.array_equal(mask, e <= np.float32(sigma * sigma)) and g == int(mask.sum())
+
+
+def test_bench_fixture_records_ransac_twin_equality():
+    """The committed bench-scale fixture (tools/bench_parity.py chain on the GPU box, round 6)
+    records the GPU RANSAC against the C twin on every ordered pair of a bench step, on the
+    product's match lists and on the fp32 chain's: counts and masks equal on all of them."""
+    import json
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "bench_chain_fp32.npz"))
+    rep = json.loads(str(z["report"]))
+    for key in ("twin_product", "twin_fp32"):
+        r = rep[key]
+        assert r["pairs"] > 32000 and r["inliers_equal_c_twin"] == 1.0 and r["masks_equal_c_twin"] == 1.0, r
