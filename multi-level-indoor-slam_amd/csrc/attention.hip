@@ -45,6 +45,12 @@ __device__ unsigned long long g_att_trace[ATT_TRACE_WGS * 8];
 constexpr int KB = 64;                 // keys per block
 constexpr int KTILE_BYTES = KB * 128;  // 64 rows x 64 bf16
 constexpr int VTILE_BYTES = 64 * KB * 2;
+// SPLIT: the lo V^T tile of a ring slot starts 8 B past the hi tile's end.  At exactly
+// VTILE_BYTES (a multiple of 512 B) hipcc fused each hi / lo pair of fragment reads into
+// one ds_read2st64_b64, which banks modulo 32 dwords and 2-way conflicts (the split ViT
+// tile's PMC conflict share 0.67-0.76, round 6); 8200 B apart no ds_read2 form applies, and a
+// uniform 8-B shift keeps the image's bank pattern.
+constexpr int VLO = VTILE_BYTES + 8;
 
 __device__ __forceinline__ int k_off(int key, int chunk) {  // K image [key][d], 16-B chunks
     return key * 128 + ((chunk ^ ((key >> 1) & 7)) << 4);
@@ -167,7 +173,7 @@ typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
 template <bool SPLIT>
 struct Slots {
     static constexpr int K = SPLIT ? 2 * KTILE_BYTES : KTILE_BYTES;
-    static constexpr int V = SPLIT ? 2 * VTILE_BYTES : VTILE_BYTES;
+    static constexpr int V = SPLIT ? 2 * VTILE_BYTES + 16 : VTILE_BYTES;  // + 16: slots stay 16-B aligned
 };
 
 struct PipeCtx {
@@ -325,8 +331,8 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[QT], f32x16 (&nxt
             for (int qt = 0; qt < QT; ++qt)
                 o[qt][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[st][qt], o[qt][dt], 0, 0, 0);
             if (SPLIT) {
-                const s16x4 llo = *reinterpret_cast<const s16x4*>(vb + VTILE_BYTES + c.voff[H][st][2 * dt]);
-                const s16x4 lhi = *reinterpret_cast<const s16x4*>(vb + VTILE_BYTES + c.voff[H][st][2 * dt + 1]);
+                const s16x4 llo = *reinterpret_cast<const s16x4*>(vb + VLO + c.voff[H][st][2 * dt]);
+                const s16x4 lhi = *reinterpret_cast<const s16x4*>(vb + VLO + c.voff[H][st][2 * dt + 1]);
                 const bf16x8 vl = __builtin_shufflevector(llo, lhi, 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt)
@@ -352,7 +358,7 @@ __device__ __forceinline__ void pipe_half(int j, f32x16 (&cur)[QT], f32x16 (&nxt
         if (SPLIT) {
             *reinterpret_cast<uint4*>(kwp + KTILE_BYTES + c.sk0) = stage[2 * SP];
             if (SP == 2) *reinterpret_cast<uint4*>(kwp + KTILE_BYTES + c.sk1) = stage[5];
-            char* vl = vw + VTILE_BYTES;
+            char* vl = vw + VLO;
             *reinterpret_cast<uint2*>(vl + c.sv0a) = make_uint2(stage[3 * SP].x, stage[3 * SP].y);
             *reinterpret_cast<uint2*>(vl + c.sv0b) = make_uint2(stage[3 * SP].z, stage[3 * SP].w);
             if (SP == 2) {
@@ -449,7 +455,7 @@ __device__ __forceinline__ void attention_tile_pipe(unsigned long long* att_tt, 
             if (SP == 2) *reinterpret_cast<uint4*>(smem + KTILE_BYTES + c.sk1) = l1;
             *reinterpret_cast<uint4*>(smem + KS + KTILE_BYTES + c.sk0) = l2;
             if (SP == 2) *reinterpret_cast<uint4*>(smem + KS + KTILE_BYTES + c.sk1) = l3;
-            char* vl = vw + VTILE_BYTES;
+            char* vl = vw + VLO;
             *reinterpret_cast<uint2*>(vl + c.sv0a) = make_uint2(w0.x, w0.y);
             *reinterpret_cast<uint2*>(vl + c.sv0b) = make_uint2(w0.z, w0.w);
             if (SP == 2) {

@@ -954,7 +954,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ 
                             uint2 h, l;
                             epi.stage2(acc[i][j], cols[i], h, l);
                             const int ch = 2 * i + ((lane >> 5) & 1);
-                            const int o = r * 128 + ((ch ^ (r & 7)) << 4) + 8 * ((lane >> 4) & 1);
+                            // 8-B half of the 16-B chunk: flipped for rows r with bit 3 set, so the
+                            // 16 rows of one b64 write group (r and r + 8 share a chunk slot under
+                            // the r & 7 swizzle) fill 16 distinct 8-B banks (the LDS write rule,
+                            // profiles/r05x_lds_calibration.txt); the reader swaps them back
+                            const int o = r * 128 + ((ch ^ (r & 7)) << 4) + 8 * (((lane >> 4) ^ (r >> 3)) & 1);
                             *reinterpret_cast<uint2*>(img + o) = h;
                             *reinterpret_cast<uint2*>(img + 4096 + o) = l;
                         }
@@ -965,7 +969,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ 
                     for (int it = 0; it < 8; ++it) {
                         const int L = it * 64 + lane, q = L >> 8, r = (L >> 3) & 31, ch = L & 7;
                         const int m = m0 + wm * 128 + p * 32 + r;
-                        const uint4 d = *reinterpret_cast<const uint4*>(img + q * 4096 + r * 128 + ((ch ^ (r & 7)) << 4));
+                        uint4 d = *reinterpret_cast<const uint4*>(img + q * 4096 + r * 128 + ((ch ^ (r & 7)) << 4));
+                        if ((r >> 3) & 1) d = make_uint4(d.z, d.w, d.x, d.y);
                         if (m < M) epi.put(m, nw + ch * 8, q, skey[wave][r], d);
                     }
                     __builtin_amdgcn_s_waitcnt(0xc07f);  // image read before the next pass writes it
