@@ -610,14 +610,15 @@ __device__ int real_roots10(double (&c)[11], double (&roots)[10], int r, int gl,
             }
         }
         if (!done) {
-            // p(z), p'(z) by Horner (complex)
+            // p(z), p'(z) by Horner (complex), the complex products as explicit fma chains
+            // (the C twin spells the same ones: this file builds without contraction)
             double pr = 0.0, pi_ = 0.0, dr = 0.0, di = 0.0;
 #pragma unroll
             for (int i = 10; i >= 0; --i) {
                 if (i <= n) {
-                    const double ndr = dr * zr - di * zi + pr, ndi = dr * zi + di * zr + pi_;
+                    const double ndr = fma(dr, zr, fma(-di, zi, pr)), ndi = fma(dr, zi, fma(di, zr, pi_));
                     dr = ndr; di = ndi;
-                    const double npr = pr * zr - pi_ * zi + c[i], npi = pr * zi + pi_ * zr;
+                    const double npr = fma(pr, zr, fma(-pi_, zi, c[i])), npi = fma(pr, zi, pi_ * zr);
                     pr = npr; pi_ = npi;
                 }
             }
@@ -636,9 +637,9 @@ __device__ int real_roots10(double (&c)[11], double (&roots)[10], int r, int gl,
             for (int j = 0; j < 10; ++j) {
                 if (j != r && j < n) {
                     const double ar = zr - xr_[j], ai = zi - xi_[j];
-                    const double tr = nr_ * ar - ni_ * ai + er, ti = nr_ * ai + ni_ * ar + ei;
+                    const double tr = fma(nr_, ar, fma(-ni_, ai, er)), ti = fma(nr_, ai, fma(ni_, ar, ei));
                     nr_ = tr; ni_ = ti;
-                    const double ur = er * ar - ei * ai, ui = er * ai + ei * ar;
+                    const double ur = fma(er, ar, -(ei * ai)), ui = fma(er, ai, ei * ar);
                     er = ur; ei = ui;
                 }
             }

@@ -211,12 +211,12 @@ static int real_roots10(const double cin[11], double roots[10]) {
         for (int r = 0; r < 10; r++) {
             if (done[r]) continue;
             double pr = 0.0, pi_ = 0.0, dr = 0.0, di = 0.0;
-            for (int i = 10; i >= 0; i--) {
+            for (int i = 10; i >= 0; i--) { /* the GPU's explicit fma chains */
                 if (i <= n) {
-                    const double ndr = dr * zr[r] - di * zi[r] + pr, ndi = dr * zi[r] + di * zr[r] + pi_;
+                    const double ndr = fma(dr, zr[r], fma(-di, zi[r], pr)), ndi = fma(dr, zi[r], fma(di, zr[r], pi_));
                     dr = ndr;
                     di = ndi;
-                    const double npr = pr * zr[r] - pi_ * zi[r] + c[i], npi = pr * zi[r] + pi_ * zr[r];
+                    const double npr = fma(pr, zr[r], fma(-pi_, zi[r], c[i])), npi = fma(pr, zi[r], pi_ * zr[r]);
                     pr = npr;
                     pi_ = npi;
                 }
@@ -234,10 +234,10 @@ static int real_roots10(const double cin[11], double roots[10]) {
             for (int j = 0; j < 10; j++) {
                 if (j != r && j < n) {
                     const double ar = zr[r] - xr[j], ai = zi[r] - xi[j];
-                    const double tr = nr_ * ar - ni_ * ai + er, ti = nr_ * ai + ni_ * ar + ei;
+                    const double tr = fma(nr_, ar, fma(-ni_, ai, er)), ti = fma(nr_, ai, fma(ni_, ar, ei));
                     nr_ = tr;
                     ni_ = ti;
-                    const double ur = er * ar - ei * ai, ui = er * ai + ei * ar;
+                    const double ur = fma(er, ar, -(ei * ai)), ui = fma(er, ai, ei * ar);
                     er = ur;
                     ei = ui;
                 }
