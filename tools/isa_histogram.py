@@ -1,9 +1,10 @@
 """Instruction histogram of a kernel's hottest loop from hipcc assembly (CPU only).
 
-    hipcc -O3 -std=c++17 --offload-arch=gfx950 -fno-slp-vectorize --cuda-device-only -S \
-        -o /tmp/attn.s multi-level-indoor-slam_amd/csrc/attention.hip -I include -I multi-level-indoor-slam_amd/csrc
+    hipcc -O3 -std=c++17 --offload-arch=gfx950 -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form \
+        --cuda-device-only -S -o /tmp/attn.s multi-level-indoor-slam_amd/csrc/attention.hip -I include -I multi-level-indoor-slam_amd/csrc
     python tools/isa_histogram.py /tmp/attn.s 'k_attention_varlenILb0ELb0ELi4'
 
+(the flags are the Makefile's rule for attention.hip; use the file's own rule for others.)
 Finds the function whose symbol contains the pattern, every backward branch in it (a
 loop), and for the loop with the most MFMAs prints the instructions per class: the
 per-score softmax work (exp, fma / mul / sub, add, max, cvt / pack), the MFMAs, and the
