@@ -279,6 +279,18 @@ def ingest_bench(dev, n_files=1024, distinct=64):
             "source": "page cache (files repeat)"}
 
 
+def _all_reduce(t, op=dist.ReduceOp.SUM):
+    """in-place all-reduce of a device tensor; through the host under gloo (the one-GPU
+    rehearsal, MLGATE_BENCH_REHEARSE), straight on the device under RCCL"""
+    if dist.get_backend() == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+    return t
+
+
 def loftr_flops_per_pair(L=4800, matches=0.0):
     """Algorithmic FLOPs of LoFTR's matching for one pair at 640x480 (L = 80 x 60 coarse
     cells): 8 coarse encoder layers (4 self + 4 cross) on both sides -- q / k / v, merge,
@@ -320,8 +332,8 @@ def loftr_bench(frames, seq, labels, lo, dev, world, rank, n_pairs=1024, chunk=1
     vt = torch.tensor([g.last_verify_s], dtype=torch.float64, device=dev)
     cnt = torch.tensor([out["pairs_verified"], out["verified_valid"]], dtype=torch.int64, device=dev)
     if world > 1:
-        dist.all_reduce(vt, op=dist.ReduceOp.MAX)
-        dist.all_reduce(cnt)
+        _all_reduce(vt, dist.ReduceOp.MAX)
+        _all_reduce(cnt)
     del g
     torch.cuda.empty_cache()
     res = {"workload": "configs[4] LoFTR 640x480 (seeded synthetic weights) as the gate's matcher: "
@@ -446,10 +458,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MLGATE_BENCH_REHEARSE=1: every rank on cuda:0 over gloo -- a one-GPU rehearsal of the
+    # multi-rank bench flow (collectives, per-rank line, sub-benches); its timing means nothing
+    rehearse = os.environ.get("MLGATE_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     seq, labels = sequence(args.keyframes, args.places)
     lo, hi = mdist.shard(args.keyframes, world, rank)
@@ -498,13 +518,13 @@ def main():
                              counts.get("pairs_matched_lightglue", 0) / max(args.steps, 1)]
                             + [tot[s_] for s_ in SLOTS], dtype=torch.float64, device=dev)
         allr = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(allr, mine)
+        mdist.all_gather_into(allr, mine)
         per_rank = [{"rank": r_, "ms_per_step": round(float(v[0]), 1), "pairs_verified": int(v[1]),
                      "pairs_matched_lightglue": int(v[2]),
                      "stage_ms_warmup_step": {SLOTS[s_]: round(float(v[3 + s_]), 1) for s_ in SLOTS}}
                     for r_, v in enumerate(x.cpu().numpy() for x in allr)]
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(cv)
+        _all_reduce(dt_t, dist.ReduceOp.MAX)
+        _all_reduce(cv)
     dt = dt_t.item()
     steps = max(args.steps, 1)
     counts = {k_: int(v) // steps for k_, v in zip(keys, cv.cpu().tolist())}  # per step, all ranks
