@@ -107,10 +107,18 @@ def frames_host(seq, idx=None, h=H, w=W):
 
 def frames_device(seq, idx, device, h=H, w=W):
     """Same scenes generated on the device (torch noise; for bench-sized sequences, where
-    host generation of 5000 x 921,600 B would dominate start-up)."""
+    host generation of 5000 x 921,600 B would dominate start-up).  Keyframe i's noise is
+    draw i of one seeded Philox stream whichever frames are rendered: the generator offset
+    is set per frame (i x one draw's increment), so a rank's shard arange(lo, hi) equals
+    rows lo..hi of the whole sequence bit for bit (the sharded bench gates the single-rank
+    bench's frames)."""
     import torch
     idx = np.asarray(idx)
     g = torch.Generator(device=device).manual_seed(seq.seed)
+    base = g.get_offset()
+    probe = torch.Generator(device=device).manual_seed(seq.seed)
+    torch.randint(0, 30, (h, w, 3), generator=probe, device=device, dtype=torch.int16)
+    inc = probe.get_offset() - base
     out = torch.empty(len(idx), h, w, 3, dtype=torch.uint8, device=device)
     bases = {}
     for j, i in enumerate(idx):
@@ -118,6 +126,7 @@ def frames_device(seq, idx, device, h=H, w=W):
         if p not in bases:
             bases[p] = torch.from_numpy(_base(p, h, w)).to(device)
         sx, sy = (int(v) for v in seq.shift[i])
+        g.set_offset(base + int(i) * inc)
         fr = torch.roll(bases[p], shifts=(sy, sx), dims=(0, 1)).to(torch.int16)
         fr = fr + torch.randint(0, 30, fr.shape, generator=g, device=device, dtype=torch.int16)
         out[j] = fr.clamp_(0, 255).to(torch.uint8)

@@ -262,3 +262,18 @@ def test_device_gate_float_and_missing_labels(dev, chain):
                                    "gate_rejected_cross_floor")}
         got["total"] = sum(got.values())
         assert got == rep.rejections.as_dict(), (rg, vg, got, rep.rejections.as_dict())
+
+
+def test_synthetic_frames_shard_equal_whole_sequence():
+    """frames_device renders keyframe i from draw i of one seeded stream whichever frames
+    are asked for, so each rank's shard is the same rows of the single-rank workload."""
+    from mlgate import distributed as mdist
+    seq = synthetic.make_sequence(24, 6, 0)
+    dev = torch.device("cuda", 0)
+    whole = synthetic.frames_device(seq, np.arange(24), dev, 64, 96)
+    for world in (2, 3, 4):
+        for r in range(world):
+            lo, hi = mdist.shard(24, world, r)
+            assert torch.equal(synthetic.frames_device(seq, np.arange(lo, hi), dev, 64, 96), whole[lo:hi])
+    odd = np.array([17, 3, 9])
+    assert torch.equal(synthetic.frames_device(seq, odd, dev, 64, 96), whole[torch.from_numpy(odd).to(dev)])
