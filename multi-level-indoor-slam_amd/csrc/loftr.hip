@@ -514,6 +514,15 @@ constexpr int LF_RCH = 64;           // rows per column chunk
 
 __device__ __forceinline__ float lf_band(float k) { return LF_KEY_BAND + 1e-5f * fabsf(k); }
 
+// The softmax SUMS' exponentials (row / column sum of exp(x - max), the chunk merge): the
+// hardware exp2 of x log2 e (__expf: v_mul + v_exp_f32, relative error ~|x| 2^-24 per term)
+// instead of the libm-accurate expf (~10 VALU), as these sums made the statistics passes
+// VALU-bound; the exact conf of a candidate keeps expf.  0 builds the expf sums (A/B arm).
+#ifndef MLG_LF_FAST_EXP
+#define MLG_LF_FAST_EXP 1
+#endif
+__device__ __forceinline__ float lf_sexp(float x) { return MLG_LF_FAST_EXP ? __expf(x) : expf(x); }
+
 // conf as the reference computes it: softmax(sim, 1) * softmax(sim, 2)
 __device__ __forceinline__ float lf_conf(float x, float rm, float rz, float cm, float cz) {
     return (expf(x - cm) / cz) * (expf(x - rm) / rz);
@@ -544,11 +553,12 @@ __global__ __launch_bounds__(256) void k_lf_rowstats(const float* __restrict__ S
         m = wave_max(m);
 #pragma unroll
         for (int k = 0; k < LF_ROWREG; ++k)
-            if (lane + 64 * k < lds / 4) z += expf(v[k].x - m) + expf(v[k].y - m) + expf(v[k].z - m) + expf(v[k].w - m);
+            if (lane + 64 * k < lds / 4)
+                z += lf_sexp(v[k].x - m) + lf_sexp(v[k].y - m) + lf_sexp(v[k].z - m) + lf_sexp(v[k].w - m);
     } else {
         for (int j = lane; j < L; j += 64) m = fmaxf(m, s[j]);
         m = wave_max(m);
-        for (int j = lane; j < L; j += 64) z += expf(s[j] - m);
+        for (int j = lane; j < L; j += 64) z += lf_sexp(s[j] - m);
     }
     z = wave_sum(z);
     if (lane == 0) {
@@ -578,7 +588,7 @@ __global__ __launch_bounds__(256) void k_lf_colpart(const float* __restrict__ S,
     }
 #pragma unroll
     for (int i = 0; i < LF_RCH; ++i)
-        if (i < n) z += expf(v[i] - m);
+        if (i < n) z += lf_sexp(v[i] - m);
     pm[(size_t)c * L + col] = m;
     pz[(size_t)c * L + col] = z;
 }
@@ -608,7 +618,7 @@ __global__ __launch_bounds__(256) void k_lf_stats(const float* __restrict__ S, i
     }
 #pragma unroll
     for (int i = 0; i < LF_RCH; ++i)
-        if (i < n) z += expf(v[i] - m);
+        if (i < n) z += lf_sexp(v[i] - m);
     if (ok) {
         pm[(size_t)c * L + col] = m;
         pz[(size_t)c * L + col] = z;
@@ -653,7 +663,7 @@ __global__ __launch_bounds__(256) void k_lf_colfin(const float* __restrict__ pm,
     float z = 0.f;
     if (ok)
 #pragma unroll 4
-        for (int c = g; c < nch; c += 4) z += pz[(size_t)c * L + col] * expf(pm[(size_t)c * L + col] - m);
+        for (int c = g; c < nch; c += 4) z += pz[(size_t)c * L + col] * lf_sexp(pm[(size_t)c * L + col] - m);
     part[g][cl] = z;
     __syncthreads();
     if (g == 0 && ok) {
@@ -708,9 +718,9 @@ __global__ __launch_bounds__(256) void k_lf_rowbest(const float* __restrict__ S,
 #pragma unroll
             for (int k = 0; k < LF_ROWREG; ++k)
                 if (lane + 64 * k < lds / 4)
-                    z += expf(v[k].x - m) + expf(v[k].y - m) + expf(v[k].z - m) + expf(v[k].w - m);
+                    z += lf_sexp(v[k].x - m) + lf_sexp(v[k].y - m) + lf_sexp(v[k].z - m) + lf_sexp(v[k].w - m);
         } else {
-            for (int j = lane; j < L; j += 64) z += expf(s[j] - m);
+            for (int j = lane; j < L; j += 64) z += lf_sexp(s[j] - m);
         }
         z = wave_sum(z);
         rm = m;
