@@ -783,7 +783,8 @@ struct staged_of<E, std::void_t<decltype(E::STAGED)>> { static constexpr int val
 #endif
 template <class Epi>
 __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
-                                                    int M, int N, int K0, int lda, int ldw, Epi epi) {
+                                                    int M, int N, int K0, int lda, int ldw, Epi epi, int nb,
+                                                    long sA, long sW) {
     constexpr int BK = 32, TM = 256, TN = 256;
     constexpr int PLANE = TM * BK * 2;  // 16 KiB: one 256 x 32 bf16 operand plane
     constexpr int STAGE = 4 * PLANE;    // A_hi, A_lo, W_hi, W_lo
@@ -792,7 +793,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ 
     constexpr int STG = staged_of<Epi>::value;
     __shared__ size_t skey[STG == 1 ? 8 : 1][32];  // staged form: the pass's row keys per wave
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nN = N / TN, nM = (M + TM - 1) / TM, ntiles = nN * nM;
+    // nb > 1 (staged-f32 epilogues only): nb independent products of one shape in one
+    // persistent launch, problem z at A + z sA, W + z sW, its output rows z M + m (the
+    // LoFTR similarity of a pair group: one tile queue instead of a 2-3-tile tail per pair)
+    const int nN = N / TN, nM = (M + TM - 1) / TM, nMN = nN * nM, ntiles = nb * nMN;
     const int xcd = blockIdx.x & 7, per_xcd = gridDim.x >> 3;
     const int tx = (ntiles + 7) >> 3;
     const int tile_end = min((xcd + 1) * tx, ntiles);
@@ -810,15 +814,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ 
         ob[i] = (unsigned)(row * ldw + ((lp ^ ((row >> 1) & 3)) * 8)) * 2u;
     }
     auto a_offsets = [&](int t, unsigned* oa) {
-        const int m0 = (t / nN) * TM;
+        const int m0 = ((t % nMN) / nN) * TM;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int row = (2 * wave + i) * 16 + lr;
             oa[i] = (unsigned)((min(m0 + row, M - 1) - m0) * lda + ((lp ^ ((row >> 1) & 3)) * 8)) * 2u;
         }
     };
-    auto a_base = [&](int t) { return A + (size_t)((t / nN) * TM) * lda; };
-    auto b_base = [&](int t) { return W + (size_t)((t % nN) * TN) * ldw; };
+    auto a_base = [&](int t) { return A + (t / nMN) * sA + (size_t)(((t % nMN) / nN) * TM) * lda; };
+    auto b_base = [&](int t) { return W + (t / nMN) * sW + (size_t)((t % nN) * TN) * ldw; };
     unsigned oa[2];
     const bf16_t* sa = a_base(tile);
     const bf16_t* sb = b_base(tile);
@@ -893,7 +897,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ 
             __builtin_amdgcn_s_waitcnt(0xF70);
             __builtin_amdgcn_s_barrier();
         }
-        const int mt = tile / nN, m0 = mt * TM, n0 = (tile - mt * nN) * TN;
+        const int tz = tile / nMN, lt = tile - tz * nMN, mz = tz * M;
+        const int mt = lt / nN, m0 = mt * TM, n0 = (lt - mt * nN) * TN;
         // batched epilogue: every column's (bias, ...) and every row's index data first, then
         // per column group the 8 fragments' global reads (the residual) before any of their
         // stores -- a fragment-at-a-time epilogue waited one L2 / HBM round trip per
@@ -1006,14 +1011,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm256s(const bf16_t* __restrict__ 
 #pragma unroll
                 for (int it = 0; it < 8; ++it) {
                     const int L = it * 64 + lane, r = L >> 4, ch = L & 15;
-                    xv[it] = epi.load4(min(m0 + wm * 128 + p * 32 + r, M - 1), nw + ch * 4);
+                    xv[it] = epi.load4(mz + min(m0 + wm * 128 + p * 32 + r, M - 1), nw + ch * 4);
                 }
 #pragma unroll
                 for (int it = 0; it < 8; ++it) {
                     const int L = it * 64 + lane, r = L >> 4, ch = L & 15;
                     const int m = m0 + wm * 128 + p * 32 + r;
                     const float4 y = *reinterpret_cast<const float4*>(img + r * 256 + ((ch ^ (r & 15)) << 4));
-                    if (m < M) epi.put4(m, nw + ch * 4, xv[it], y);
+                    if (m < M) epi.put4(mz + m, nw + ch * 4, xv[it], y);
                 }
                 __builtin_amdgcn_s_waitcnt(0xc07f);
                 __builtin_amdgcn_wave_barrier();
@@ -1468,11 +1473,15 @@ template <class Epi>
 #ifndef MLG_SPLIT_TILE
 #define MLG_SPLIT_TILE 256
 #endif
-int launch_split(const bf16_t* A, const bf16_t* W, int M, int N, int K0, int lda, int ldw, Epi epi, hipStream_t s) {
+int launch_split(const bf16_t* A, const bf16_t* W, int M, int N, int K0, int lda, int ldw, Epi epi, hipStream_t s,
+                 int nb = 1, long sA = 0, long sW = 0) {
     g_num_cus = num_cus();
     if (M <= 0 || K0 <= 0 || K0 % 64 || lda < 2 * K0 || ldw < 2 * K0 || (lda % 8) || (ldw % 8)) return MLG_EINVAL;
     if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(W)) & 15) return MLG_EINVAL;
-    if (MLG_SPLIT_TILE == 192 && N % 192 == 0) {
+    // batched products: staged-f32 epilogues only (their row index is the only per-problem
+    // output coordinate), 16-B aligned problem bases
+    if (nb < 1 || (nb > 1 && (dma::staged_of<Epi>::value != 2 || ((sA | sW) & 7)))) return MLG_EINVAL;
+    if (MLG_SPLIT_TILE == 192 && N % 192 == 0 && nb == 1) {
         const long nt = (long)(N / 192) * ((M + 191) / 192);
         const long g = std::min<long>(g_num_cus, (nt + 7) / 8 * 8);
         hipLaunchKernelGGL(dma::k_gemm192s<Epi>, dim3((unsigned)g), dim3(512), 0, s, A, W, M, N, K0, lda, ldw, epi);
@@ -1480,9 +1489,11 @@ int launch_split(const bf16_t* A, const bf16_t* W, int M, int N, int K0, int lda
         return MLG_OK;
     }
     if (N % 256) return MLG_EINVAL;
-    const long ntiles = (long)(N / 256) * ((M + 255) / 256);
+    const long ntiles = (long)nb * (N / 256) * ((M + 255) / 256);
+    if (ntiles > INT32_MAX) return MLG_EINVAL;
     const long grid = std::min<long>(g_num_cus, (ntiles + 7) / 8 * 8);
-    hipLaunchKernelGGL(dma::k_gemm256s<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K0, lda, ldw, epi);
+    hipLaunchKernelGGL(dma::k_gemm256s<Epi>, dim3((unsigned)grid), dim3(512), 0, s, A, W, M, N, K0, lda, ldw, epi, nb,
+                       sA, sW);
     MLG_LAUNCH_CHECK();
     return MLG_OK;
 }
@@ -1510,9 +1521,9 @@ int mlg_gemm_patch_split(const bf16_t* A, const bf16_t* W, const float* bias, co
 }
 
 int mlg_gemm_sim_split_loftr(const bf16_t* A, const bf16_t* B, int M, int Npad, int K0, float* S, int lds, int ncols,
-                             hipStream_t s) {
+                             hipStream_t s, int nb, long pstride) {
     if (ncols > Npad || ncols > lds || lds > Npad || (lds % 4)) return MLG_EINVAL;
-    return launch_split(A, B, M, Npad, K0, 2 * K0, 2 * K0, EpiSimLoFTR{S, lds, ncols}, s);
+    return launch_split(A, B, M, Npad, K0, 2 * K0, 2 * K0, EpiSimLoFTR{S, lds, ncols}, s, nb, pstride, pstride);
 }
 
 int mlg_gemm_f32out(const bf16_t* A, const bf16_t* W, float* C, int M, int N, int K, hipStream_t s) {

@@ -108,9 +108,11 @@ int mlg_similarity_f32(const float* A, int Q, const float* B, int N, int D, floa
 // the same product stored as LoFTR's coarse similarity (S / 256) / 0.1
 int mlg_similarity_f32_loftr(const float* A, int Q, const float* B, int N, int D, float* S, int lds, hipStream_t s);
 // the same similarity from split-bf16 operands (A / B rows [hi | lo], K0 = 256 each; B
-// readable up to Npad = ncols rounded up to 256 rows): 3 bf16 MFMA products per product
+// readable up to Npad = ncols rounded up to 256 rows): 3 bf16 MFMA products per product.
+// nb > 1: nb pairs in one launch, pair z's operands at A / B + z pstride elements and its
+// similarity at S + z M lds (one persistent tile queue for the whole pair group)
 int mlg_gemm_sim_split_loftr(const bf16_t* A, const bf16_t* B, int M, int Npad, int K0, float* S, int lds, int ncols,
-                             hipStream_t s);
+                             hipStream_t s, int nb = 1, long pstride = 0);
 int mlg_similarity_f32_t(const float* A, int Q, const float* B, int N, int D, float* S, int lds, float* St, int ldt,
                          hipStream_t s);
 int mlg_topk_gate(const float* S, int lds, int N, int Q, const double* tq, const double* tdb, const int64_t* fq,

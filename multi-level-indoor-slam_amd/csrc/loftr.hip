@@ -1157,6 +1157,12 @@ int g_lf_sim_split = MLG_LF_SIM_SPLIT;  // mlg_set_loftr_similarity
 #ifndef MLG_LF_STATS1
 #define MLG_LF_STATS1 1
 #endif
+// The split similarity of a dual-softmax group in ONE persistent GEMM launch (round 6): per
+// pair, 576 tiles (720 x 536) or 361 (640 x 480) over 256 workgroups left a 2-3-tile tail;
+// 0 builds one launch per pair (A/B arm).  Same tiles, same per-tile arithmetic: same bits.
+#ifndef MLG_LF_SIM_BATCH
+#define MLG_LF_SIM_BATCH 1
+#endif
 
 // nn.Linear weight [N][K] bf16 -> k-step-major [K / 16][N][16] (lg_ffn.hip's layout)
 __global__ void k_lf_pack_kstep(const bf16_t* __restrict__ w, int N, int K, bf16_t* __restrict__ out) {
@@ -1492,15 +1498,20 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
     const int G = std::min(P, MLG_LF_PGRP);
     for (int p0 = 0; p0 < P; p0 += G) {
         const unsigned g = (unsigned)std::min(G, P - p0);
-        for (int q = 0; q < (int)g; ++q) {
-            const int p = p0 + q;
-            float* Sq = S + (size_t)q * L * lds;
-            if (split)
-                LF_TRY(mlg_gemm_sim_split_loftr(CS + (size_t)p * L * 512, CS + ((size_t)P + p) * L * 512, L, Lpad, 256,
-                                                Sq, lds, L, s));
-            else
-                LF_TRY(mlg_similarity_f32_loftr(bc.x + (size_t)p * L * 256, L, bc.x + ((size_t)P + p) * L * 256, L, 256,
-                                                Sq, L, s));
+        if (split && MLG_LF_SIM_BATCH) {  // the group's g similarities as one tile queue
+            LF_TRY(mlg_gemm_sim_split_loftr(CS + (size_t)p0 * L * 512, CS + ((size_t)P + p0) * L * 512, L, Lpad, 256, S,
+                                            lds, L, s, (int)g, (long)L * 512));
+        } else {
+            for (int q = 0; q < (int)g; ++q) {
+                const int p = p0 + q;
+                float* Sq = S + (size_t)q * L * lds;
+                if (split)
+                    LF_TRY(mlg_gemm_sim_split_loftr(CS + (size_t)p * L * 512, CS + ((size_t)P + p) * L * 512, L, Lpad,
+                                                    256, Sq, lds, L, s));
+                else
+                    LF_TRY(mlg_similarity_f32_loftr(bc.x + (size_t)p * L * 256, L, bc.x + ((size_t)P + p) * L * 256, L,
+                                                    256, Sq, L, s));
+            }
         }
         if (MLG_LF_STATS1) {  // three reads of S: stats, rowbest, colmaxpart
             hipLaunchKernelGGL(k_lf_stats, dim3(ncb, nrch, g), dim3(256), 0, s, S, L, lds, pm, pz, prm);
