@@ -269,7 +269,23 @@ class DeviceGate:
 
     def step(self):
         """Gate the sequence once.  Returns this rank's counts (dict of ints): matches,
-        the four rejection terms, pairs verified, pairs geometrically valid, accepted."""
+        the four rejection terms, pairs verified, pairs geometrically valid, accepted.
+        MLGATE_MAIN_PRIORITY=1 (A/B): the step's own work on a high-priority stream, so the
+        hardware dispatches its workgroups ahead of the side streams' (RANSAC, SuperPoint)."""
+        import os
+        if os.environ.get("MLGATE_MAIN_PRIORITY", "0") != "1":
+            return self._step()
+        torch = self.torch
+        if getattr(self, "_hi", None) is None:
+            self._hi = torch.cuda.Stream(device=self.dev, priority=-1)
+        cur = torch.cuda.current_stream(self.dev)
+        self._hi.wait_stream(cur)
+        with torch.cuda.stream(self._hi):
+            out = self._step()
+        cur.wait_stream(self._hi)
+        return out
+
+    def _step(self):
         torch = self.torch
         from . import geometry, retrieval
         self.eng.forward_into(self.frames, self.desc_loc, self.local_feats)
