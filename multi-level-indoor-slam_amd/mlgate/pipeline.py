@@ -270,10 +270,13 @@ class DeviceGate:
     def step(self):
         """Gate the sequence once.  Returns this rank's counts (dict of ints): matches,
         the four rejection terms, pairs verified, pairs geometrically valid, accepted.
-        MLGATE_MAIN_PRIORITY=1 (A/B): the step's own work on a high-priority stream, so the
-        hardware dispatches its workgroups ahead of the side streams' (RANSAC, SuperPoint)."""
+        The step's own work runs on a high-priority stream, so the hardware dispatches its
+        workgroups ahead of the side streams' (RANSAC, SuperPoint): they fill the gaps and
+        kernel tails instead of taking CUs from the LightGlue kernels (same-box A/B,
+        profiles/r06p_ab_main_priority.txt: attention -2 % per launch, step time equal).
+        MLGATE_MAIN_PRIORITY=0: everything at normal priority (A/B)."""
         import os
-        if os.environ.get("MLGATE_MAIN_PRIORITY", "0") != "1":
+        if os.environ.get("MLGATE_MAIN_PRIORITY", "1") != "1":
             return self._step()
         torch = self.torch
         if getattr(self, "_hi", None) is None:
