@@ -1288,6 +1288,9 @@ __global__ __launch_bounds__(512, 2) void k_gemm256q(const bf16_t* __restrict__ 
 // the zero padding read a 16-B zero line (`zero`).  TN = 256: 8 waves 2 (M) x 4 (N) of
 // 128 x 64; TN = 128: 4 (M) x 2 (N) of 64 x 64.  Same MFMA k order as the explicit
 // im2col GEMM, so the same bits.
+#ifndef MLG_CONV_STAGED
+#define MLG_CONV_STAGED 1
+#endif
 struct ConvGeom {
     const bf16_t* in; const bf16_t* zero; int H, W, C, kw, s, pad, Ho, Wo;
 };
@@ -1398,14 +1401,51 @@ __global__ __launch_bounds__(512, 2) void k_conv256(ConvGeom g, const bf16_t* __
             __builtin_amdgcn_s_barrier();
         }
         const int mt = tile / nN, m0 = mt * TM, n0 = (tile - mt * nN) * TN;
+        if constexpr (MLG_CONV_STAGED) {
+            // Staged epilogue: the wave's RM x 64 accumulators go through its IMG bytes of
+            // the dead stage st1 as f32 rows (PR rows a pass, 16-B chunks swizzled by the row),
+            // then every lane applies the epilogue to a float4 of one row: 16 lanes cover a
+            // row's 64 channels, so the residual reads and the f32 / bf16 stores are whole
+            // 256-B / 128-B row pieces instead of 16 rows x 32-64 B per wave-instruction
+            // (timing probe with the epilogue skipped: the LoFTR backbone 29 % faster,
+            // profiles/r06r_ab_conv_staged_epilogue.txt).  Same per-element math: same bits.
+            constexpr int IMG = STAGE / 8, PR = IMG >= 8192 ? 32 : 16, NP = RM / PR, JP = PR / 16;
+            char* img = st1 + wave * IMG;
+            const int nw = n0 + wn * 64;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int p = 0; p < NP; ++p) {
 #pragma unroll
-            for (int j = 0; j < JM; ++j) {
-                const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4;
-                const int m = m0 + wm * RM + j * 16 + (lane & 15);
-                if (m < M) epi(m, n, acc[i][j]);
+                for (int jj = 0; jj < JP; ++jj) {
+                    const int r = jj * 16 + (lane & 15);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int ch = 4 * i + (lane >> 4);
+                        *reinterpret_cast<f32x4*>(img + r * 256 + ((ch ^ (r & 15)) << 4)) = acc[i][p * JP + jj];
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's image written
+                __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                for (int it = 0; it < PR / 4; ++it) {
+                    const int L = it * 64 + lane, r = L >> 4, ch = L & 15;
+                    const int m = m0 + wm * RM + p * PR + r;
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + ((ch ^ (r & 15)) << 4));
+                    if (m < M) epi(m, nw + ch * 4, v);
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // image read before the next pass writes it
+                __builtin_amdgcn_wave_barrier();
             }
+            __syncthreads();  // every wave's image read: the next tile DMAs into st1
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < JM; ++j) {
+                    const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4;
+                    const int m = m0 + wm * RM + j * 16 + (lane & 15);
+                    if (m < M) epi(m, n, acc[i][j]);
+                }
+        }
         sb = nsb;
     }
     __builtin_amdgcn_s_waitcnt(0xF70);
