@@ -291,6 +291,11 @@ class DeviceGate:
     def _step(self):
         torch = self.torch
         from . import geometry, retrieval
+        # MLGATE_SP_UNDER_VIT=1 (A/B): SuperPoint of every local keyframe on its side stream
+        # (normal priority) while the ViT and the kNN run on this one (high priority)
+        sp_ev = None
+        if self.verify and self.matcher == 'lightglue' and os.environ.get("MLGATE_SP_UNDER_VIT", "0") == "1":
+            sp_ev = self._extract_side(np.arange(self.n_local))
         self.eng.forward_into(self.frames, self.desc_loc, self.local_feats)
         if self.world > 1:
             self.gather(self.desc_loc)  # RCCL all-gather of the descriptors over xGMI
@@ -320,9 +325,11 @@ class DeviceGate:
         # per-stage HIP-event table would then time SuperPoint's launches with the
         # concurrent LightGlue in them (profiles/r05p_ab_superpoint_overlap.txt): off by
         # default.  Several ranks: all keyframes first (FeatureExchange ships finished rows).
-        self._sp_overlap = (self.world == 1 and self.matcher == 'lightglue'
+        self._sp_overlap = (sp_ev is None and self.world == 1 and self.matcher == 'lightglue'
                             and os.environ.get("MLGATE_SP_OVERLAP", "0") == "1")
-        if self.matcher == 'lightglue' and not self._sp_overlap:
+        if sp_ev is not None:
+            torch.cuda.current_stream(self.dev).wait_event(sp_ev)
+        elif self.matcher == 'lightglue' and not self._sp_overlap:
             self._extract_rows(np.arange(self.n_local))
         # matches handed to verify_with_semantics (is_valid ones), skip rule on floors
         qs, js = np.nonzero(live & (h_valid != 0))
