@@ -291,10 +291,13 @@ class DeviceGate:
     def _step(self):
         torch = self.torch
         from . import geometry, retrieval
-        # MLGATE_SP_UNDER_VIT=1 (A/B): SuperPoint of every local keyframe on its side stream
-        # (normal priority) while the ViT and the kNN run on this one (high priority)
+        # SuperPoint of every local keyframe on its side stream (normal priority) while the
+        # ViT and the kNN run on this one (high priority): it fills the ViT kernels' tails and
+        # the CUs its LayerNorm / attention launches leave free (same-box ABAB, profiles/
+        # r06u_ab_sp_under_vit.txt: -0.4 % step time, counts identical).  The LightGlue stage
+        # waits on its event.  MLGATE_SP_UNDER_VIT=0: SuperPoint after them on this stream.
         sp_ev = None
-        if self.verify and self.matcher == 'lightglue' and os.environ.get("MLGATE_SP_UNDER_VIT", "0") == "1":
+        if self.verify and self.matcher == 'lightglue' and os.environ.get("MLGATE_SP_UNDER_VIT", "1") == "1":
             sp_ev = self._extract_side(np.arange(self.n_local))
         self.eng.forward_into(self.frames, self.desc_loc, self.local_feats)
         if self.world > 1:
