@@ -150,7 +150,8 @@ def test_c_fundamental_small_sizes():
 def test_bench_fixture_records_ransac_twin_equality():
     """The committed bench-scale fixture (tools/bench_parity.py chain on the GPU box, round 6)
     records the GPU RANSAC against the C twin on every ordered pair of a bench step, on the
-    product's match lists and on the fp32 chain's: counts and masks equal on all of them."""
+    product's match lists and on the fp32 chain's: counts, masks and (fixtures made since the
+    model check was added) the model bits equal on all of them."""
     import json
     import os
     z = np.load(os.path.join(os.path.dirname(__file__), "golden", "bench_chain_fp32.npz"))
@@ -158,3 +159,4 @@ def test_bench_fixture_records_ransac_twin_equality():
     for key in ("twin_product", "twin_fp32"):
         r = rep[key]
         assert r["pairs"] > 32000 and r["inliers_equal_c_twin"] == 1.0 and r["masks_equal_c_twin"] == 1.0, r
+        assert r.get("models_equal_c_twin", 1.0) == 1.0, r

@@ -163,12 +163,13 @@ def probe(a):
 
 
 def _ransac_job(job):
-    """(key, k1, k2) -> (key, inliers, mask) with the C twin of findEssentialMat (pool worker)."""
+    """(key, k1, k2) -> (key, inliers, packed mask, model or None) with the C twin of
+    findEssentialMat (pool worker)."""
     from oracle import _lib
     from oracle import geometry as ogeo
     key, k1, k2 = job
-    _, mask, g = _lib.essential_ransac(k1, k2, ogeo.ISEC_K, 3.0)
-    return key, g, np.packbits(mask)
+    M, mask, g = _lib.essential_ransac(k1, k2, ogeo.ISEC_K, 3.0)
+    return key, g, np.packbits(mask), (None if M is None else np.asarray(M, np.float64).reshape(3, 3))
 
 
 def _capture_product_ransac(store):
@@ -182,28 +183,39 @@ def _capture_product_ransac(store):
         out = orig(k1, k2, offs, K, k_stride, threshold, **kw)
         o = offs.cpu().numpy()  # on the current (RANSAC side) stream: ordered after the launch
         store.append((k1[:int(o[-1])].cpu().numpy(), k2[:int(o[-1])].cpu().numpy(), o, out[2].cpu().numpy(),
-                      out[1][:int(o[-1])].cpu().numpy()))
+                      out[1][:int(o[-1])].cpu().numpy(), out[0].cpu().numpy(), out[4].cpu().numpy()))
         return out
     mgeo.epipolar_ransac_device = hook
     return orig
 
 
-def _twin_report(pool, lists, gpu_inl, gpu_masks, label):
-    """GPU RANSAC vs the C twin on the same lists: counts and masks, pair by pair."""
+def _same_model(gpu_model, twin_model):
+    """the GPU's model (None when it found none) vs the twin's, bit for bit"""
+    if gpu_model is None or twin_model is None:
+        return gpu_model is None and twin_model is None
+    return np.array_equal(np.asarray(gpu_model, np.float64).reshape(3, 3).view(np.uint64),
+                          np.asarray(twin_model, np.float64).reshape(3, 3).view(np.uint64))
+
+
+def _twin_report(pool, lists, gpu_inl, gpu_masks, gpu_models, label):
+    """GPU RANSAC vs the C twin on the same lists: counts, masks and model bits, pair by pair."""
     jobs = [pool.apply_async(_ransac_job, ((i, k1, k2),)) for i, (k1, k2) in enumerate(lists)]
-    eq_n = eq_m = 0
+    eq_n = eq_m = eq_e = 0
     bad = []
     for job in jobs:
-        i, g, pm = job.get()
+        i, g, pm, M = job.get()
         same_n = int(gpu_inl[i]) == int(g)
         same_m = np.array_equal(np.packbits(gpu_masks[i].astype(bool)), pm)
+        same_e = _same_model(gpu_models[i], M)
         eq_n += same_n
         eq_m += same_m
-        if not (same_n and same_m) and len(bad) < 20:
-            bad.append({"pair": i, "matches": len(lists[i][0]), "gpu": int(gpu_inl[i]), "twin": int(g)})
+        eq_e += same_e
+        if not (same_n and same_m and same_e) and len(bad) < 20:
+            bad.append({"pair": i, "matches": len(lists[i][0]), "gpu": int(gpu_inl[i]), "twin": int(g),
+                        "model_equal": bool(same_e)})
     n = max(len(lists), 1)
     rep = {"check": label, "pairs": len(lists), "inliers_equal_c_twin": eq_n / n, "masks_equal_c_twin": eq_m / n,
-           "differ": bad}
+           "models_equal_c_twin": eq_e / n, "differ": bad}
     log(**rep)
     return rep
 
@@ -233,15 +245,16 @@ def chain(a):
     from mlgate import geometry as mgeo
     mgeo.epipolar_ransac_device = orig_ransac
     # (1) the product's own match lists: its GPU RANSAC vs the C twin, every ordered pair
-    p_lists, p_inl, p_masks = [], [], []
-    for k1c, k2c, o, inl_c, mask_c in captured:
+    p_lists, p_inl, p_masks, p_models = [], [], [], []
+    for k1c, k2c, o, inl_c, mask_c, model_c, status_c in captured:
         for p_ in range(len(o) - 1):
             p_lists.append((k1c[o[p_]:o[p_ + 1]], k2c[o[p_]:o[p_ + 1]]))
             p_inl.append(inl_c[p_])
             p_masks.append(mask_c[o[p_]:o[p_ + 1]])
+            p_models.append(None if int(status_c[p_]) == 1 else model_c[p_])
     del captured
-    twin_product = _twin_report(pool, p_lists, p_inl, p_masks, "product lists: GPU RANSAC vs C twin")
-    del p_lists, p_inl, p_masks
+    twin_product = _twin_report(pool, p_lists, p_inl, p_masks, p_models, "product lists: GPU RANSAC vs C twin")
+    del p_lists, p_inl, p_masks, p_models
     gr = gate.last_pair_results
     g_idx, g_sim, g_valid, g_count = gate.last_retrieval
     del gate
@@ -291,28 +304,32 @@ def chain(a):
             log(phase="fp32_lightglue", done=i, s=round(time.time() - t0, 1))
     inl = np.zeros(len(union), np.int32)
     f_masks = [None] * len(union)
+    f_models = [None] * len(union)
     for job in pending:
-        i, g, pm = job.get()
+        i, g, pm, M = job.get()
         inl[i] = g
         f_masks[i] = pm
+        f_models[i] = M
     # (2) the fp32 chain's lists through the product's GPU RANSAC (batched as the gate
     # calls it) against the C twin's counts / masks just computed
     from mlgate import geometry as mgeo
     g_inl = np.zeros(len(union), np.int32)
-    g_eq_m = 0
+    g_eq_m = g_eq_e = 0
     for c0 in range(0, len(union), 4096):
         rs = mgeo.epipolar_ransac([x[0] for x in f_lists[c0:c0 + 4096]], [x[1] for x in f_lists[c0:c0 + 4096]],
                                   bench.ISEC_K, 3.0, device=str(dev))
         for j, r in enumerate(rs):
             g_inl[c0 + j] = r.inliers
             g_eq_m += np.array_equal(np.packbits(r.mask), f_masks[c0 + j])
+            g_eq_e += _same_model(r.model, f_models[c0 + j])
     twin_fp32 = {"check": "fp32 chain lists: GPU RANSAC vs C twin", "pairs": len(union),
                  "inliers_equal_c_twin": float((g_inl == inl).mean()) if len(union) else 1.0,
                  "masks_equal_c_twin": g_eq_m / max(len(union), 1),
+                 "models_equal_c_twin": g_eq_e / max(len(union), 1),
                  "differ": [{"pair": int(i), "matches": int(nm[i]), "gpu": int(g_inl[i]), "twin": int(inl[i])}
                             for i in np.flatnonzero(g_inl != inl)[:20]]}
     log(**twin_fp32)
-    del f_lists, f_masks
+    del f_lists, f_masks, f_models
     pool.close()
     ratio = inl / np.maximum(nm, 1)
     fvalid = (nm >= 5) & (inl >= 20) & (ratio >= 0.25)
