@@ -335,7 +335,13 @@ struct EpiBiasAddRelu {
 // Generic conv / linear epilogue (LoFTR, loftr.hip): y = acc (+ bias) (+ R[m, n]), then
 // act 1 = ReLU, 2 = LeakyReLU(0.01), 3 = elu + 1 on columns < act_cols; stored as f32
 // (X, ldx) and / or bf16 (C, ldc), either may be null.
+#ifndef MLG_GEMM_ROW_STAGED
+#define MLG_GEMM_ROW_STAGED 1  // 0: EpiConv fragment-at-a-time in k_gemm256 (A/B arm)
+#endif
 struct EpiConv {
+    // row-major outputs / residual: k_gemm256 runs it from an LDS row image (whole-row
+    // accesses) -- see row_staged below
+    static constexpr bool ROW_STAGED = MLG_GEMM_ROW_STAGED;
     const float* bias; const float* R; int ldr; float* X; int ldx; bf16_t* C; int ldc; int act; int act_cols;
     float vdiv = 0.f;  // != 0: columns >= act_cols divided by it (LoFTR's values / v_length)
     __device__ void operator()(int m, int n, const f32x4& v) const {
@@ -640,6 +646,49 @@ __global__ __launch_bounds__(512, BK == 32 ? 4 : 2) void k_gemm(const bf16_t* __
 // so the next tile's first wait overlaps this tile's epilogue, and the epilogue's
 // stores drain while the next tile's MFMAs run.  Twice the MFMAs per barrier and
 // 0.375 fragment reads per MFMA (vs 0.5 at 64 x 64 per wave).
+// Row-staged epilogue of a wave's RM x 64 block of a persistent 256-row tile (k_gemm256,
+// k_conv256): the accumulators (16 x 16 fragments, lane = 4 consecutive columns of one
+// row) go through IMG bytes of the dead LDS stage as f32 rows, PR rows a pass, 16-B chunks
+// swizzled by the row; each lane then applies the epilogue to a float4 of one row, 16
+// lanes per row, so the residual reads and the f32 / bf16 stores are whole 256-B / 128-B
+// row pieces instead of 16 rows x 32-64 B per wave-instruction.  Same per-element math
+// (the same epi() call): the same bits.  The caller syncs the workgroup before the stage
+// is refilled.
+template <class E, class = void>
+struct row_staged { static constexpr bool value = false; };
+template <class E>
+struct row_staged<E, std::void_t<decltype(E::ROW_STAGED)>> { static constexpr bool value = E::ROW_STAGED; };
+
+template <int RM, int IMG, class Epi, int JM>
+__device__ __forceinline__ void gemm256_rows_epilogue(const Epi& epi, const f32x4 (&acc)[4][JM], char* img, int mw,
+                                                      int nw, int M, int lane) {
+    constexpr int PR = IMG >= 8192 ? 32 : 16, NP = RM / PR, JP = PR / 16;
+    static_assert(RM == JM * 16 && RM % PR == 0 && PR * 256 <= IMG, "row-staged epilogue shape");
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+        for (int jj = 0; jj < JP; ++jj) {
+            const int r = jj * 16 + (lane & 15);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int ch = 4 * i + (lane >> 4);
+                *reinterpret_cast<f32x4*>(img + r * 256 + ((ch ^ (r & 15)) << 4)) = acc[i][p * JP + jj];
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's image written
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < PR / 4; ++it) {
+            const int L = it * 64 + lane, r = L >> 4, ch = L & 15;
+            const int m = mw + p * PR + r;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + ((ch ^ (r & 15)) << 4));
+            if (m < M) epi(m, nw + ch * 4, v);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // image read before the next pass writes it
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 template <class Epi>
 __global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
                                                    int M, int N, int K, int lda, int ldw, Epi epi) {
@@ -738,14 +787,20 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(const bf16_t* __restrict__ A
             __builtin_amdgcn_s_barrier();
         }
         const int mt = tile / nN, m0 = mt * TM, n0 = (tile - mt * nN) * TN;
+        if constexpr (row_staged<Epi>::value) {
+            gemm256_rows_epilogue<TM / 2, STAGE / 8>(epi, acc, st1 + wave * (STAGE / 8), m0 + wm * 128, n0 + wn * 64,
+                                                     M, lane);
+            __syncthreads();  // every wave's image read: the next tile DMAs into st1
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4;
-                const int m = m0 + wm * 128 + j * 16 + (lane & 15);
-                if (m < M) epi(m, n, acc[i][j]);
-            }
+                for (int j = 0; j < 8; ++j) {
+                    const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4;
+                    const int m = m0 + wm * 128 + j * 16 + (lane & 15);
+                    if (m < M) epi(m, n, acc[i][j]);
+                }
+        }
 #pragma unroll
         for (int i = 0; i < NA; ++i) oa[i] = na[i];
         sa = nsa;
@@ -1402,39 +1457,11 @@ __global__ __launch_bounds__(512, 2) void k_conv256(ConvGeom g, const bf16_t* __
         }
         const int mt = tile / nN, m0 = mt * TM, n0 = (tile - mt * nN) * TN;
         if constexpr (MLG_CONV_STAGED) {
-            // Staged epilogue: the wave's RM x 64 accumulators go through its IMG bytes of
-            // the dead stage st1 as f32 rows (PR rows a pass, 16-B chunks swizzled by the row),
-            // then every lane applies the epilogue to a float4 of one row: 16 lanes cover a
-            // row's 64 channels, so the residual reads and the f32 / bf16 stores are whole
-            // 256-B / 128-B row pieces instead of 16 rows x 32-64 B per wave-instruction
-            // (timing probe with the epilogue skipped: the LoFTR backbone 29 % faster,
-            // profiles/r06r_ab_conv_staged_epilogue.txt).  Same per-element math: same bits.
-            constexpr int IMG = STAGE / 8, PR = IMG >= 8192 ? 32 : 16, NP = RM / PR, JP = PR / 16;
-            char* img = st1 + wave * IMG;
-            const int nw = n0 + wn * 64;
-#pragma unroll
-            for (int p = 0; p < NP; ++p) {
-#pragma unroll
-                for (int jj = 0; jj < JP; ++jj) {
-                    const int r = jj * 16 + (lane & 15);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int ch = 4 * i + (lane >> 4);
-                        *reinterpret_cast<f32x4*>(img + r * 256 + ((ch ^ (r & 15)) << 4)) = acc[i][p * JP + jj];
-                    }
-                }
-                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's image written
-                __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                for (int it = 0; it < PR / 4; ++it) {
-                    const int L = it * 64 + lane, r = L >> 4, ch = L & 15;
-                    const int m = m0 + wm * RM + p * PR + r;
-                    const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 256 + ((ch ^ (r & 15)) << 4));
-                    if (m < M) epi(m, nw + ch * 4, v);
-                }
-                __builtin_amdgcn_s_waitcnt(0xc07f);  // image read before the next pass writes it
-                __builtin_amdgcn_wave_barrier();
-            }
+            // row-staged (gemm256_rows_epilogue; timing probe with the epilogue skipped: the
+            // LoFTR backbone 29 % faster, the staged form -3 %, profiles/
+            // r06r_ab_conv_staged_epilogue.txt)
+            gemm256_rows_epilogue<RM, STAGE / 8>(epi, acc, st1 + wave * (STAGE / 8), m0 + wm * RM, n0 + wn * 64, M,
+                                                 lane);
             __syncthreads();  // every wave's image read: the next tile DMAs into st1
         } else {
 #pragma unroll
