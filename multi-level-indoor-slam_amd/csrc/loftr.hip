@@ -38,6 +38,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -193,6 +194,38 @@ __global__ void k_lf_tokens(const float* __restrict__ coarse, const int32_t* __r
     const float4 y = make_float4(f.x + p.x, f.y + p.y, f.z + p.z, f.w + p.w);
     reinterpret_cast<float4*>(x + (size_t)row * 256)[c4] = y;
     reinterpret_cast<uint2*>(cat + (size_t)row * 512)[c4] = make_uint2(pack_bf16x2(y.x, y.y), pack_bf16x2(y.z, y.w));
+}
+
+// Layer 0 of the coarse transformer is a self layer: its output rows depend on the frame
+// alone.  k_lf_stash copies the distinct frames' rows (f32 x and its bf16 copy, the first
+// half of cat) aside; k_lf_gather_rows lays them out per pair side (segment g <- frame row
+// block umap[g]) for layers 1.. (MLG_LF_SELF0_DEDUP).
+__global__ void k_lf_stash(const float* __restrict__ x, const bf16_t* __restrict__ cat, long rows,
+                           float* __restrict__ tx, bf16_t* __restrict__ tc) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;  // (row, 16 B of x) then (row, 16 B of cat)
+    if (e < rows * 64) {
+        reinterpret_cast<float4*>(tx)[e] = reinterpret_cast<const float4*>(x)[e];
+    } else if (e < rows * 96) {
+        const long f = e - rows * 64, r = f >> 5;
+        const int c = (int)(f & 31);
+        reinterpret_cast<uint4*>(tc + r * 256)[c] = reinterpret_cast<const uint4*>(cat + r * 512)[c];
+    }
+}
+
+__global__ void k_lf_gather_rows(const float* __restrict__ tx, const bf16_t* __restrict__ tc,
+                                 const int32_t* __restrict__ umap, int L, long rows, float* __restrict__ x,
+                                 bf16_t* __restrict__ cat) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < rows * 64) {
+        const long r = e >> 6;
+        const int c = (int)(e & 63), g = (int)(r / L), t = (int)(r - (long)g * L);
+        reinterpret_cast<float4*>(x + r * 256)[c] =
+            reinterpret_cast<const float4*>(tx + ((long)umap[g] * L + t) * 256)[c];
+    } else if (e < rows * 96) {
+        const long f = e - rows * 64, r = f >> 5;
+        const int c = (int)(f & 31), g = (int)(r / L), t = (int)(r - (long)g * L);
+        reinterpret_cast<uint4*>(cat + r * 512)[c] = reinterpret_cast<const uint4*>(tc + ((long)umap[g] * L + t) * 256)[c];
+    }
 }
 
 // ------------------------------------------------------ linear attention ----
@@ -1163,6 +1196,11 @@ int g_lf_sim_split = MLG_LF_SIM_SPLIT;  // mlg_set_loftr_similarity
 #ifndef MLG_LF_SIM_BATCH
 #define MLG_LF_SIM_BATCH 1
 #endif
+// Layer 0 (self) once per distinct frame of the call, its rows gathered per pair side
+// (round 6); 0 runs it on every pair side (A/B arm).  Row-independent kernels: same bits.
+#ifndef MLG_LF_SELF0_DEDUP
+#define MLG_LF_SELF0_DEDUP 1
+#endif
 
 // nn.Linear weight [N][K] bf16 -> k-step-major [K / 16][N][16] (lg_ffn.hip's layout)
 __global__ void k_lf_pack_kstep(const bf16_t* __restrict__ w, int N, int K, bf16_t* __restrict__ out) {
@@ -1284,9 +1322,9 @@ int encoder_layer(const mlg_loftr_layer& lw, const LayerBufs& b, int d, long x0,
 // then side 1 from the updated side 0.  Side-major rows: side s, segment g at
 // (s * nseg + g) * L.
 int transformer(const mlg_loftr_layer* layers, int nl, const LayerBufs& b, int d, int nseg, int L, hipStream_t s,
-                const TailW* tails = nullptr) {
+                const TailW* tails = nullptr, int first = 0) {
     const long half = (long)nseg * L;
-    for (int i = 0; i < nl; ++i) {
+    for (int i = first; i < nl; ++i) {
         const TailW* tw = tails ? tails + i : nullptr;
         if (i % 2 == 0) {
             LF_TRY(encoder_layer(layers[i], b, d, 0, 0, 2 * nseg, L, s, tw));
@@ -1341,7 +1379,7 @@ struct MatchLayout {
     size_t cx, ccat, cqkv, cmsg, ct, ch, ckv, cks, ckvp;  // coarse transformer (rows 2 P L, d 256)
     size_t fx, fcat, fqkv, fmsg, ft, fh, fkv, fks;  // fine transformer (rows 2 C 25, d 128)
     size_t win, crow, cd, cm, S, csplit, rmax, rsum, rkey, cmax, csum, ckey, pm, pz, prm, bval, bidx, cbest, mi, mj, mconf, cnt,
-        frm, mp, ms, tails, total;
+        frm, ufr, umap, mp, ms, tails, total;
 };
 
 constexpr int FINE_CHUNK = 4096;  // matches per fine-stage pass
@@ -1402,6 +1440,8 @@ MatchLayout match_layout(int P, int L) {
     M.mconf = take((size_t)P * L * 4);
     M.cnt = take((size_t)P * 4);
     M.frm = take((size_t)2 * P * 4);
+    M.ufr = take((size_t)2 * P * 4);
+    M.umap = take((size_t)2 * P * 4);
     M.mp = take((size_t)FINE_CHUNK * 4);
     M.ms = take((size_t)FINE_CHUNK * 4);
     M.tails = take(TAILS_BYTES);
@@ -1468,9 +1508,6 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
     if (hipMemcpyAsync(frm, h_frames.data(), h_frames.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
         return MLG_EHIP;
     const long crows = (long)2 * P * L;
-    hipLaunchKernelGGL(k_lf_tokens, dim3((unsigned)((crows * 64 + 255) / 256)), dim3(256), 0, s, coarse, frm, L, pe,
-                       bc.x, bc.cat, (int)crows);
-    MLG_LAUNCH_CHECK();
     TailW tails[8];
     if (MLG_LF_FUSED_TAIL) {
         if (w.coarse_tails)
@@ -1478,7 +1515,49 @@ int mlg_loftr_match(const mlg_loftr_weights* wp, const float* coarse, const floa
         else
             LF_TRY(pack_tails(w, (char*)at(ML.tails), tails, s));
     }
-    LF_TRY(transformer(w.coarse, 8, bc, 256, P, L, s, MLG_LF_FUSED_TAIL ? tails : nullptr));
+    const TailW* tw = MLG_LF_FUSED_TAIL ? tails : nullptr;
+    // the distinct frames of the call (first-appearance order) and each pair side's index
+    std::vector<int32_t> h_ufr, h_umap(2 * P);
+    {
+        std::unordered_map<int32_t, int32_t> pos;
+        for (int g = 0; g < 2 * P; ++g) {
+            auto it = pos.find(h_frames[g]);
+            if (it == pos.end()) {
+                it = pos.emplace(h_frames[g], (int32_t)h_ufr.size()).first;
+                h_ufr.push_back(h_frames[g]);
+            }
+            h_umap[g] = it->second;
+        }
+    }
+    const int NU = (int)h_ufr.size();
+    if (MLG_LF_SELF0_DEDUP && NU < 2 * P) {
+        int32_t* ufr = (int32_t*)at(ML.ufr);
+        int32_t* umap = (int32_t*)at(ML.umap);
+        if (hipMemcpyAsync(ufr, h_ufr.data(), (size_t)NU * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(umap, h_umap.data(), (size_t)2 * P * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+            return MLG_EHIP;
+        const long urows = (long)NU * L;
+        hipLaunchKernelGGL(k_lf_tokens, dim3((unsigned)((urows * 64 + 255) / 256)), dim3(256), 0, s, coarse, ufr, L,
+                           pe, bc.x, bc.cat, (int)urows);
+        MLG_LAUNCH_CHECK();
+        LF_TRY(encoder_layer(w.coarse[0], bc, 256, 0, 0, NU, L, s, tw));
+        // the NU frames' rows aside in the dead q / k / v buffer (2 P L x 3 KiB >= NU L x
+        // 1.5 KiB), then laid out per pair side
+        float* tx = bc.qkv;
+        bf16_t* tc = (bf16_t*)(bc.qkv + urows * 256);
+        hipLaunchKernelGGL(k_lf_stash, dim3((unsigned)((urows * 96 + 255) / 256)), dim3(256), 0, s, bc.x, bc.cat,
+                           urows, tx, tc);
+        MLG_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_lf_gather_rows, dim3((unsigned)((crows * 96 + 255) / 256)), dim3(256), 0, s, tx, tc,
+                           umap, L, crows, bc.x, bc.cat);
+        MLG_LAUNCH_CHECK();
+        LF_TRY(transformer(w.coarse, 8, bc, 256, P, L, s, tw, 1));
+    } else {
+        hipLaunchKernelGGL(k_lf_tokens, dim3((unsigned)((crows * 64 + 255) / 256)), dim3(256), 0, s, coarse, frm, L,
+                           pe, bc.x, bc.cat, (int)crows);
+        MLG_LAUNCH_CHECK();
+        LF_TRY(transformer(w.coarse, 8, bc, 256, P, L, s, tw));
+    }
     // the coarse similarity: split-bf16 operands (3 bf16 MFMA products at ~6x the exact-f32
     // MFMA's rate) or the exact-f32 MFMA (mlg_set_loftr_similarity(1)).  The split GEMM
     // writes 16-B row pieces, so its S rows are lds = L rounded up to 4 floats, the pad
