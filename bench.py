@@ -291,15 +291,21 @@ def _all_reduce(t, op=dist.ReduceOp.SUM):
     return t
 
 
-def loftr_flops_per_pair(L=4800, matches=0.0):
-    """Algorithmic FLOPs of LoFTR's matching for one pair at 640x480 (L = 80 x 60 coarse
-    cells): 8 coarse encoder layers (4 self + 4 cross) on both sides -- q / k / v, merge,
-    MLP 512 -> 512 -> 256 and the linear attention's KV and apply (8 heads x 32 x 32) per
-    token --, the coarse similarity L x L x 256, and per coarse match the fine stage (2
-    layers over 2 x 25 window tokens at d 128, 8 heads x 16 x 16)."""
-    def layer(d):
-        return 2 * (4 * d * d + 2 * d * 2 * d + 2 * d * d + 2 * 8 * (d // 8) ** 2)
-    return 8 * 2 * L * layer(256) + 2 * L * L * 256 + matches * 2 * 2 * 25 * layer(128)
+def _lf_layer_flops(d):
+    """one LoFTR encoder layer per token: q / k / v, merge, MLP 2d -> 2d -> d, the linear
+    attention's KV and apply (8 heads x (d / 8)^2)"""
+    return 2 * (4 * d * d + 2 * d * 2 * d + 2 * d * d + 2 * 8 * (d // 8) ** 2)
+
+
+def loftr_flops_per_pair(L=4800, matches=0.0, self0_sides=2.0):
+    """FLOPs of LoFTR's matching for one pair at L coarse cells (640x480: 80 x 60): 8 coarse
+    encoder layers (4 self + 4 cross) on both sides, the coarse similarity L x L x 256, and
+    per coarse match the fine stage (2 layers over 2 x 25 window tokens at d 128, 8 heads x
+    16 x 16).  self0_sides: the pair sides layer 0 runs on -- 2 as the reference computes
+    it; the product runs that self layer once per distinct frame of a call (round 6), so
+    the kernel sub-run passes distinct frames / pairs and the rate counts the work done."""
+    return ((7 * 2 + self0_sides) * L * _lf_layer_flops(256) + 2 * L * L * 256
+            + matches * 2 * 2 * 25 * _lf_layer_flops(128))
 
 
 # algorithmic FLOPs per 640x480 keyframe of LoFTR's ResNetFPN_8_2 backbone (196-channel
@@ -384,7 +390,9 @@ def _loftr_kernels(lf, sel, used, pairs, chunk, dev):
     torch.cuda.synchronize(dev)
     t_feat, t_match = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
     m = float(cntm.float().mean())
-    bf, mf = loftr_backbone_flops(H, W), loftr_flops_per_pair((H // 8) * (W // 8), m)
+    # layer 0 runs once per distinct frame of each match_device call
+    nu = sum(len(set(pa[c0:c0 + chunk]) | set(pb[c0:c0 + chunk])) for c0 in range(0, len(pairs), chunk))
+    bf, mf = loftr_backbone_flops(H, W), loftr_flops_per_pair((H // 8) * (W // 8), m, nu / max(len(pairs), 1))
     bt = bf * len(used) / (t_feat * 1e-3) / 1e12
     mt = mf * len(pairs) / (t_match * 1e-3) / 1e12
     return {"frame": f"{int(sel.shape[2])}x{int(sel.shape[1])} (network {W}x{H}, L = {(H // 8) * (W // 8)})",
@@ -393,7 +401,8 @@ def _loftr_kernels(lf, sel, used, pairs, chunk, dev):
             "backbone_frac": round(bt / MFMA_BF16_PEAK_TFLOPS, 4),
             "match_ms_per_pair": round(t_match / len(pairs), 3), "match_tflops": round(mt, 1),
             "match_frac": round(mt / MFMA_BF16_PEAK_TFLOPS, 4),
-            "flops": {"backbone_per_keyframe": bf, "match_per_pair": round(mf, 0)}}
+            "flops": {"backbone_per_keyframe": bf, "match_per_pair": round(mf, 0),
+                      "layer0_sides_per_pair": round(nu / max(len(pairs), 1), 3)}}
 
 
 def stress_bench(n, k, dev):
