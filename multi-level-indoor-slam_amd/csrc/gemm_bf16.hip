@@ -372,6 +372,39 @@ struct EpiConv {
     }
 };
 
+// LoFTR's FPN merge in the lateral 1x1 conv's epilogue: C = bf16((acc + bias) +
+// up(src)), up = bilinear x2 (align_corners=True) of the coarser NHWC f32 map src [B, h,
+// w, N] at output pixel m = (b, oy, ox) of the [B, 2h, 2w] grid -- the same expressions in
+// the same order as k_lf_up_add reading the conv's f32 output, so the same bits, without
+// the f32 lateral map's write and re-read.  Row-staged (whole-row stores).
+struct EpiConvUp {
+    static constexpr bool ROW_STAGED = true;
+    const float* bias; const float* src; int h, w; bf16_t* C; int ldc;
+    __device__ void operator()(int m, int n, const f32x4& v) const {
+        const int Ho = 2 * h, Wo = 2 * w;
+        const int x = m % Wo, r = m / Wo, y = r % Ho, b = r / Ho;
+        const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+        const float l0 = v[0] + bb.x, l1 = v[1] + bb.y, l2 = v[2] + bb.z, l3 = v[3] + bb.w;
+        const float sh = Ho > 1 ? (float)(h - 1) / (float)(Ho - 1) : 0.f;
+        const float sw = Wo > 1 ? (float)(w - 1) / (float)(Wo - 1) : 0.f;
+        const float fy = sh * (float)y, fx = sw * (float)x;
+        const int y0 = (int)fy, x0 = (int)fx;
+        const int y1 = y0 < h - 1 ? y0 + 1 : y0, x1 = x0 < w - 1 ? x0 + 1 : x0;
+        const float ly1 = fy - (float)y0, lx1 = fx - (float)x0, ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+        const float* s0 = src + ((size_t)b * h * w) * ldc + n;
+        const float4 v00 = *reinterpret_cast<const float4*>(s0 + ((size_t)y0 * w + x0) * ldc);
+        const float4 v01 = *reinterpret_cast<const float4*>(s0 + ((size_t)y0 * w + x1) * ldc);
+        const float4 v10 = *reinterpret_cast<const float4*>(s0 + ((size_t)y1 * w + x0) * ldc);
+        const float4 v11 = *reinterpret_cast<const float4*>(s0 + ((size_t)y1 * w + x1) * ldc);
+        auto up = [&](float a, float b_, float c_, float d) {
+            return ly0 * (lx0 * a + lx1 * b_) + ly1 * (lx0 * c_ + lx1 * d);
+        };
+        const float o0 = l0 + up(v00.x, v01.x, v10.x, v11.x), o1 = l1 + up(v00.y, v01.y, v10.y, v11.y);
+        const float o2 = l2 + up(v00.z, v01.z, v10.z, v11.z), o3 = l3 + up(v00.w, v01.w, v10.w, v11.w);
+        *reinterpret_cast<uint2*>(C + (size_t)m * ldc + n) = make_uint2(pack_bf16x2(o0, o1), pack_bf16x2(o2, o3));
+    }
+};
+
 struct EpiPatch {  // patch tokens: X[b, 1 + p, :] = acc + b + pos[1 + p]
     float* X; const float* bias; const float* pos; int P;  // P = patches per image
     struct Col { float4 b; };
@@ -1621,6 +1654,11 @@ int mlg_gemm_conv(const bf16_t* A, int lda, const bf16_t* W, const float* bias, 
                   int ldx, bf16_t* C, int ldc, int act, int act_cols, int M, int N, int K_, hipStream_t s, float vdiv) {
     if ((!X && !C) || act < 0 || act > 3) return MLG_EINVAL;
     return launch(A, W, M, N, K_, lda, K_, EpiConv{bias, R, ldr, X, ldx, C, ldc, act, act_cols, vdiv}, s);
+}
+int mlg_gemm_conv_upadd(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* src, int h, int w,
+                        bf16_t* C, int M, int N, int K_, hipStream_t s) {
+    if (!bias || !src || !C || h < 1 || w < 1 || (N % 4) || M % (4 * h * w)) return MLG_EINVAL;
+    return launch(A, W, M, N, K_, lda, K_, EpiConvUp{bias, src, h, w, C, N}, s);
 }
 int mlg_gemm_set_variant(int variant) {
     if (variant < 1 || variant > 5) return MLG_EINVAL;

@@ -53,6 +53,11 @@ int mlg_gemm_bias_add_relu(const bf16_t* A, int lda, const bf16_t* W, const floa
 int mlg_gemm_conv(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* R, int ldr, float* X,
                   int ldx, bf16_t* C, int ldc, int act, int act_cols, int M, int N, int K_, hipStream_t s,
                   float vdiv = 0.f);
+// LoFTR's FPN merge fused into the lateral 1x1 conv: C = bf16((A W^T + bias) + up(src)),
+// src the coarser NHWC f32 map [B, h, w, N], M = B (2h) (2w) output pixels (k_lf_up_add's
+// arithmetic in the epilogue)
+int mlg_gemm_conv_upadd(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* src, int h, int w,
+                        bf16_t* C, int M, int N, int K_, hipStream_t s);
 // implicit-GEMM k x k (k = 1 or 3, pad k / 2) stride-s convolution over NHWC bf16 [B, H, W, C]
 // (C % 64 == 0), weights [N][tap * C + c], EpiConv epilogue; `zero` = 16 zero bytes
 int mlg_conv_implicit(const bf16_t* in, const bf16_t* zero, int B, int H, int W, int C, int k, int s,

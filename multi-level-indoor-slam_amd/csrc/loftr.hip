@@ -1079,6 +1079,27 @@ int basic_block(const mlg_loftr_weights& w, int c1, int c2, int cds, int B, int 
     return conv(w, c2, yb, B, Ho, Wo, zero, R, x, xb, 1, s);
 }
 
+// FPN merge: bf16(outconv(x) + up2x(coarser)) -> out.  MLG_LF_FPN_FUSED: the upsample-add
+// in the lateral 1x1 conv's epilogue (EpiConvUp, gemm_bf16.hip); 0: the conv's f32 output
+// to `tf`, then k_lf_up_add (A/B arm).  Same expressions: same bits.
+#ifndef MLG_LF_FPN_FUSED
+#define MLG_LF_FPN_FUSED 1
+#endif
+int fpn_merge(const mlg_loftr_weights& w, int idx, const bf16_t* in, int B, int H, int W, const float* coarser,
+              float* tf, bf16_t* out, hipStream_t s) {
+    const ConvSpec sp = CONVS[idx];
+    if (sp.k != 1 || sp.s != 1 || (H % 2) || (W % 2)) return MLG_EINVAL;
+    if (MLG_LF_FPN_FUSED)
+        return mlg_gemm_conv_upadd(in, sp.cin, (const bf16_t*)w.conv_w[idx], w.conv_b[idx], coarser, H / 2, W / 2, out,
+                                   B * H * W, sp.cout, sp.cin, s);
+    LF_TRY(conv(w, idx, in, B, H, W, nullptr, nullptr, tf, nullptr, 0, s));
+    const long n = (long)B * H * W * (sp.cout / 4);
+    hipLaunchKernelGGL(k_lf_up_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tf, coarser, B, H / 2, W / 2,
+                       sp.cout, out);
+    MLG_LAUNCH_CHECK();
+    return MLG_OK;
+}
+
 }  // namespace
 
 size_t mlg_loftr_features_ws_bytes(int B, int H, int W) {
@@ -1144,23 +1165,11 @@ int mlg_loftr_features(const mlg_loftr_weights* wp, const uint8_t* frames_in, in
     // FPN: x3_out = outconv3(x3) -> coarse output (f32)
     LF_TRY(conv(w, 14, xb, B, H8, W8, zero, nullptr, coarse, nullptr, 0, s));
     // x2_out = outconv2(x2) + up(x3_out) -> bf16 -> conv + BN + leaky -> conv
-    LF_TRY(conv(w, 15, x2b, B, H4, W4, zero, nullptr, tf, nullptr, 0, s));
-    {
-        const long n = (long)B * H4 * W4 * 64;
-        hipLaunchKernelGGL(k_lf_up_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tf, coarse, B, H8, W8, 256,
-                           yb);
-        MLG_LAUNCH_CHECK();
-    }
+    LF_TRY(fpn_merge(w, 15, x2b, B, H4, W4, coarse, tf, yb, s));
     LF_TRY(conv(w, 16, yb, B, H4, W4, zero, nullptr, nullptr, xb, 2, s));
     LF_TRY(conv(w, 17, xb, B, H4, W4, zero, nullptr, c2, nullptr, 0, s));  // x2_out f32 (1/4, 256p)
     // x1_out = outconv1(x1) + up(x2_out) -> conv + BN + leaky -> conv -> fine
-    LF_TRY(conv(w, 18, x1b, B, H2, W2, zero, nullptr, tf, nullptr, 0, s));
-    {
-        const long n = (long)B * H2 * W2 * 64;
-        hipLaunchKernelGGL(k_lf_up_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tf, c2, B, H4, W4, 256,
-                           yb);
-        MLG_LAUNCH_CHECK();
-    }
+    LF_TRY(fpn_merge(w, 18, x1b, B, H2, W2, c2, tf, yb, s));
     LF_TRY(conv(w, 19, yb, B, H2, W2, zero, nullptr, nullptr, xb, 2, s));
     LF_TRY(conv(w, 20, xb, B, H2, W2, zero, nullptr, fine, nullptr, 0, s));
     (void)c3;
