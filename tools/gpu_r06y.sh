@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 6: LoFTR FPN merge fused into the lateral 1x1 conv epilogue (EpiConvUp)
-# (tree) vs on every pair side (ab/fpn, -DMLG_LF_SELF0_DEDUP=0): LoFTR GPU tests (incl. the
+# (tree) vs the conv + k_lf_up_add (ab/fpn, -DMLG_LF_FPN_FUSED=0): LoFTR GPU tests (incl. the
 # sharded gate case) on the tree, then same-box ABAB of tools/loftr_bench.py at 480x640 and
 # 540x720 (digests must be equal) and the bench's LoFTR sub-object.
 set -u
