@@ -383,8 +383,14 @@ struct EpiConvUp {
     __device__ void operator()(int m, int n, const f32x4& v) const {
         const int Ho = 2 * h, Wo = 2 * w;
         const int x = m % Wo, r = m / Wo, y = r % Ho, b = r / Ho;
-        const float4 bb = *reinterpret_cast<const float4*>(bias + n);
-        const float l0 = v[0] + bb.x, l1 = v[1] + bb.y, l2 = v[2] + bb.z, l3 = v[3] + bb.w;
+        float l0 = v[0], l1 = v[1], l2 = v[2], l3 = v[3];  // no bias: as EpiConv, no add at all
+        if (bias) {
+            const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+            l0 += bb.x;
+            l1 += bb.y;
+            l2 += bb.z;
+            l3 += bb.w;
+        }
         const float sh = Ho > 1 ? (float)(h - 1) / (float)(Ho - 1) : 0.f;
         const float sw = Wo > 1 ? (float)(w - 1) / (float)(Wo - 1) : 0.f;
         const float fy = sh * (float)y, fx = sw * (float)x;
@@ -1657,7 +1663,7 @@ int mlg_gemm_conv(const bf16_t* A, int lda, const bf16_t* W, const float* bias, 
 }
 int mlg_gemm_conv_upadd(const bf16_t* A, int lda, const bf16_t* W, const float* bias, const float* src, int h, int w,
                         bf16_t* C, int M, int N, int K_, hipStream_t s) {
-    if (!bias || !src || !C || h < 1 || w < 1 || (N % 4) || M % (4 * h * w)) return MLG_EINVAL;
+    if (!src || !C || h < 1 || w < 1 || (N % 4) || M % (4 * h * w)) return MLG_EINVAL;
     return launch(A, W, M, N, K_, lda, K_, EpiConvUp{bias, src, h, w, C, N}, s);
 }
 int mlg_gemm_set_variant(int variant) {
