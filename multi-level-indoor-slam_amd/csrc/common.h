@@ -26,6 +26,16 @@ __device__ __forceinline__ float bf16_to_f32(bf16_t v) {
 // Round-to-nearest-even f32 -> bf16 (v_cvt_pk_bf16_f32; NaN stays NaN).
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 
+// LoFTR FPN merge: lat + bilinear(v00, v01, v10, v11) with explicit rounding (no FMA
+// contraction), shared by k_lf_up_add (loftr.hip) and the fused lateral-conv epilogue
+// EpiConvUp (gemm_bf16.hip), so the two forms give the same bits
+__device__ __forceinline__ float lf_up_add1(float lat, float a, float b, float c, float d, float lx0, float lx1,
+                                            float ly0, float ly1) {
+    const float t0 = __fadd_rn(__fmul_rn(lx0, a), __fmul_rn(lx1, b));
+    const float t1 = __fadd_rn(__fmul_rn(lx0, c), __fmul_rn(lx1, d));
+    return __fadd_rn(lat, __fadd_rn(__fmul_rn(ly0, t0), __fmul_rn(ly1, t1)));
+}
+
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
     bf16x2_t v = {(__bf16)a, (__bf16)b};
     return __builtin_bit_cast(uint32_t, v);

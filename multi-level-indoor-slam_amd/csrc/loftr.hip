@@ -176,9 +176,10 @@ __global__ void k_lf_up_add(const float* __restrict__ lat, const float* __restri
     const float4 v10 = *reinterpret_cast<const float4*>(s0 + ((size_t)y1 * w + x0) * C);
     const float4 v11 = *reinterpret_cast<const float4*>(s0 + ((size_t)y1 * w + x1) * C);
     const float4 l = *reinterpret_cast<const float4*>(lat + r * C + c);
-    auto up = [&](float a, float b_, float c_, float d) { return ly0 * (lx0 * a + lx1 * b_) + ly1 * (lx0 * c_ + lx1 * d); };
-    const float o0 = l.x + up(v00.x, v01.x, v10.x, v11.x), o1 = l.y + up(v00.y, v01.y, v10.y, v11.y);
-    const float o2 = l.z + up(v00.z, v01.z, v10.z, v11.z), o3 = l.w + up(v00.w, v01.w, v10.w, v11.w);
+    const float o0 = lf_up_add1(l.x, v00.x, v01.x, v10.x, v11.x, lx0, lx1, ly0, ly1);
+    const float o1 = lf_up_add1(l.y, v00.y, v01.y, v10.y, v11.y, lx0, lx1, ly0, ly1);
+    const float o2 = lf_up_add1(l.z, v00.z, v01.z, v10.z, v11.z, lx0, lx1, ly0, ly1);
+    const float o3 = lf_up_add1(l.w, v00.w, v01.w, v10.w, v11.w, lx0, lx1, ly0, ly1);
     *reinterpret_cast<uint2*>(out + r * C + c) = make_uint2(pack_bf16x2(o0, o1), pack_bf16x2(o2, o3));
 }
 
