@@ -1080,11 +1080,14 @@ int basic_block(const mlg_loftr_weights& w, int c1, int c2, int cds, int B, int 
     return conv(w, c2, yb, B, Ho, Wo, zero, R, x, xb, 1, s);
 }
 
-// FPN merge: bf16(outconv(x) + up2x(coarser)) -> out.  MLG_LF_FPN_FUSED: the upsample-add
-// in the lateral 1x1 conv's epilogue (EpiConvUp, gemm_bf16.hip); 0: the conv's f32 output
-// to `tf`, then k_lf_up_add (A/B arm).  Same expressions: same bits.
+// FPN merge: bf16(outconv(x) + up2x(coarser)) -> out.  MLG_LF_FPN_FUSED=1: the
+// upsample-add in the lateral 1x1 conv's epilogue (EpiConvUp, gemm_bf16.hip; no f32
+// lateral map written and re-read): backbone -3 % in a same-box A/B and the LoFTR GPU tests
+// pass, but its features are not bit-identical to this two-kernel form for a reason not yet
+// found (profiles/r06y_ab_loftr_fpn_fused.txt), so it stays off; default: the conv's f32
+// output to `tf`, then k_lf_up_add.
 #ifndef MLG_LF_FPN_FUSED
-#define MLG_LF_FPN_FUSED 1
+#define MLG_LF_FPN_FUSED 0
 #endif
 int fpn_merge(const mlg_loftr_weights& w, int idx, const bf16_t* in, int B, int H, int W, const float* coarser,
               float* tf, bf16_t* out, hipStream_t s) {
